@@ -1,0 +1,219 @@
+"""Benchmark: CIFAR-10 UNet DDPM training img/s (BASELINE.json metric), plus DDIM-50 sampling img/s.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+A "step" is one full DiffusionTrainer.train_step of the reference loop (utils/trainer.py:222-265) on a
+synthetic 128 x 3 x 32 x 32 batch already resident in HBM: t ~ randint, q_sample, UNet forward, MSE,
+backward, fused clip_grad_norm(1.0), AdamW step, zero_grad, fused EMA (rank 0, decay 0.9999), with
+dropout 0.1, on the configs/cifar10_unet.py network (37.06 M params, random init), bf16 compute.
+Data parallel: one process per GPU, gradients averaged by RCCL all-reduce overlapped with backward; each
+rank trains its own 128-image shard (weak scaling). value = images of all ranks / max-over-ranks time.
+
+The JSON line also carries:
+  roofline      the dominant kernel (implicit-GEMM 3x3 conv, bf16 MFMA) timed with HIP events on its
+                own stream: achieved = algorithmic FLOPs per launch / average launch time, vs the
+                2.5 PFLOP/s dense bf16 MFMA peak (MI355X_MICROARCH.md)
+  cpu_baseline  the CPU oracle (oracle/unet_oracle.py, fp32, a port of the reference path) running the
+                same train step on the host cores, rank 0 only, bounded sample (B=32, 3 timed steps)
+  ddim50        DDIM-50 sampling img/s (eta 0, B=128 per GPU, replicas)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CIFAR = dict(image_size=(32, 32), in_channels=3, model_channels=128, out_channels=3, num_res_blocks=2,
+             attention_resolutions=(16, 8), dropout=0.1, channel_mult=(1, 2, 2, 2), use_attention=True)
+MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense, MI355X_MICROARCH.md
+TRAIN_GFLOP_PER_IMG = 37.890     # fwd + bwd, = 3 x 12.632 forward
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def conv_roofline(dtype, B=128):
+    """Time the dominant kernel (3x3 ResBlock conv 128->128 @32x32, B=128, GN+SiLU prologue, bias+temb
+    epilogue) with HIP events on the stream it is launched on."""
+    from diffusion_models_collection_amd import _lib as L, kernels as K
+    H = W = 32
+    C = 128
+    dev = "cuda"
+    x = torch.randn(B, H, W, C, device=dev).to(dtype)
+    w = torch.randn(C, C, 3, 3, device=dev) * 0.03
+    Kc = L.kc_for(C, dtype)
+    wp = K.pack_weight(L.PACK_FWD, dtype, w, Kc)
+    sc = torch.rand(B, C, device=dev)
+    sh = torch.randn(B, C, device=dev)
+    bias = torch.randn(C, device=dev)
+    addv = torch.randn(B, C, device=dev)
+    y = torch.empty(B, H, W, C, device=dev, dtype=dtype)
+    d = K.make_desc(dtype, B, H, W, C, 0, C, 0, Kc, H, W, C, K.TAPS3)
+    K.set_prologue(d, L.PRO_AFFINE_SILU, sc, sh, C)
+    K.set_epilogue(d, bias=bias, addvec=addv, ld_add=C, ldy1=C)
+    for _ in range(5):
+        K.conv(d, x, None, wp, y)
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 50
+    e0.record(s)
+    for _ in range(n):
+        K.conv(d, x, None, wp, y)
+    e1.record(s)
+    e1.synchronize()
+    avg_ms = e0.elapsed_time(e1) / n
+    flops = 2.0 * B * H * W * C * C * 9
+    achieved = flops / (avg_ms * 1e-3) / 1e12
+    return {"kernel": "conv_fwd_kernel<bf16,128,128> (ResBlock 3x3 128->128 @32x32, B=128)" if dtype == torch.bfloat16
+            else "conv_fwd_kernel<f32,128,128>",
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+            "flops_per_launch": flops, "avg_launch_ms": round(avg_ms, 4)}
+
+
+def cpu_baseline(B=32, warm=1, steps=3, threads=16):
+    """The CPU oracle (a port of the reference path) doing the same train step on the host cores."""
+    from oracle.unet_oracle import make_oracle
+    from oracle import diffusion_oracle as DO
+    from diffusion_models_collection_amd.models import UNet
+    torch.set_num_threads(threads)
+    torch.manual_seed(42)
+    m = UNet(**CIFAR)
+    orc, sd = make_oracle(m.state_dict(), dict(CIFAR, num_classes=None), requires_grad=True)
+    params = list(sd.values())
+    opt = torch.optim.AdamW(params, lr=2e-4, weight_decay=1e-4)
+    ema = {k: v.detach().clone() for k, v in sd.items()}
+    tab = DO.schedule()
+    x0 = torch.rand(B, 3, 32, 32) * 2 - 1
+
+    def step():
+        t = torch.randint(0, 1000, (B,))
+        noise = torch.randn_like(x0)
+        loss = DO.loss("l2", noise, orc.forward(DO.q_sample(tab, x0, t, noise), t, None, training=True))
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params, 1.0)
+        opt.step()
+        opt.zero_grad()
+        DO.ema_update(ema, {k: v.detach() for k, v in sd.items()}, 0.9999)
+
+    for _ in range(warm):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = time.perf_counter() - t0
+    return {"value": round(B * steps / dt, 3), "unit": "img/s", "cores": threads, "kind": "port",
+            "sample": f"oracle fp32 train step (q_sample, UNet fwd+bwd, clip, AdamW, EMA), B={B}, {steps} timed "
+                      f"steps after {warm} warm-up, torch CPU with {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-sample", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--sample-steps", type=int, default=50)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    from diffusion_models_collection_amd.models import UNet
+    from diffusion_models_collection_amd.diffusion import DDPM, DDIM
+    from diffusion_models_collection_amd.utils.trainer import DiffusionTrainer
+
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    torch.manual_seed(42 + rank)
+    model = UNet(**CIFAR, compute_dtype=args.dtype).to(dev)
+    ddpm = DDPM(1000, 1e-4, 0.02, "linear", device=dev)
+    opt = torch.optim.AdamW(model.parameters(), lr=2e-4, weight_decay=1e-4)
+    cfg = {"epochs": 1, "save_dir": "/tmp/dmc_bench_ckpt", "sample_dir": "/tmp/dmc_bench_smp", "loss_type": "l2",
+           "use_ema": True, "ema_decay": 0.9999, "model_type": "unet", "model_params": dict(CIFAR)}
+    trainer = DiffusionTrainer(model, ddpm, None, opt, None, device=dev, config=cfg, rank=rank, world_size=world)
+    B = args.batch
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    pool = [torch.rand(B, 3, 32, 32, device=dev, generator=gen) * 2 - 1 for _ in range(4)]
+
+    model.train()
+    for i in range(args.warmup):
+        trainer.train_step(pool[i % 4], 0)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        trainer.train_step(pool[i % 4], 0)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        tt = torch.tensor([el], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = tt.item()
+    ms = el / args.steps * 1e3
+    value = world * B * args.steps / el
+    log(f"[bench] rank {rank}: {ms:.2f} ms/step, {value:.1f} img/s aggregate")
+
+    out = {"metric": "CIFAR-10 UNet DDPM train imgs/sec (aggregate over GPUs)", "value": round(value, 2),
+           "unit": "img/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+           "data": "synthetic (U(-1,1) 32x32x3 batches resident in HBM, random-init weights)",
+           "config": {"workload": "configs/cifar10_unet.py UNet DDPM train step (q_sample, fwd, MSE, bwd, clip, "
+                                  "AdamW, EMA), dropout 0.1", "model": "UNet 37.06M (128ch, mult 1,2,2,2, attn 16/8)",
+                      "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
+                      "parallelism": f"dp{world}"},
+           "per_gpu_imgs_per_sec": round(value / world, 2),
+           "train_tflops_per_gpu": round(value / world * TRAIN_GFLOP_PER_IMG / 1e3, 2)}
+
+    if not args.no_sample:
+        model.eval()
+        ddim = DDIM(1000, args.sample_steps, device=dev)
+        with torch.no_grad():
+            ddim.sample(model, (B, 3, 32, 32))   # warm-up (also populates the weight pack cache)
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ddim.sample(model, (B, 3, 32, 32))
+            torch.cuda.synchronize()
+            sel = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([sel], device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            sel = tt.item()
+        out["ddim50"] = {"value": round(world * B / sel, 2), "unit": "img/s", "batch_per_gpu": B,
+                         "steps": args.sample_steps, "seconds": round(sel, 3), "scaling": "replicas"}
+    if rank == 0 and not args.no_roofline:
+        out["roofline"] = conv_roofline(dtype)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            out["cpu_baseline"] = cpu_baseline()
+        except Exception as e:  # the CPU leg must never hide the GPU result
+            out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

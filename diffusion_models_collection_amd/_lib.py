@@ -1,0 +1,133 @@
+"""ctypes binding of libdmc.so (include/dmc.h) plus thin torch-tensor wrappers.
+
+This module is the only place that talks to the native library. It fails loudly: importing it on a
+machine where libdmc.so is missing raises, and there is no Python/PyTorch fallback for any kernel.
+Every wrapper launches on torch's current HIP stream and never synchronises.
+"""
+import ctypes
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (must be loaded first so libdmc binds to torch's libamdhip64.so.7)
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("DMC_LIB", _PKG / "libdmc.so"))
+
+DMC_F32, DMC_BF16 = 0, 1
+MODE_NORMAL, MODE_UPSAMPLE, MODE_DILATE = 0, 1, 2
+PRO_NONE, PRO_AFFINE_SILU, PRO_SILU, PRO_AFFINE = 0, 1, 2, 3
+LOSS = {"l1": 0, "l2": 1, "huber": 2}
+PACK_FWD, PACK_DGRAD, PACK_UPDGRAD = 0, 1, 2
+
+_c_int, _c_p, _c_f, _c_u32, _c_long, _c_size = (ctypes.c_int, ctypes.c_void_p, ctypes.c_float, ctypes.c_uint32,
+                                                ctypes.c_long, ctypes.c_size_t)
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _c_int), ("N", _c_int), ("H", _c_int), ("W", _c_int),
+        ("C1", _c_int), ("C2", _c_int), ("ld1", _c_int), ("ld2", _c_int), ("Kc", _c_int),
+        ("OH", _c_int), ("OW", _c_int), ("Cout", _c_int), ("ntaps", _c_int), ("mode", _c_int), ("stride", _c_int),
+        ("tap_dy", _c_int * 16), ("tap_dx", _c_int * 16),
+        ("prologue", _c_int), ("pro_scale", _c_p), ("pro_shift", _c_p), ("ld_pro", _c_int),
+        ("drop_seed", _c_u32), ("drop_thresh", _c_u32), ("drop_scale", _c_f), ("drop_ld", _c_int),
+        ("bias", _c_p), ("addvec", _c_p), ("ld_add", _c_int), ("resid", _c_p), ("ld_res", _c_int),
+        ("silu_pre", _c_p), ("ld_silu", _c_int), ("Csplit", _c_int), ("ldy1", _c_int), ("ldy2", _c_int),
+        ("out_f32", _c_int), ("out_nchw", _c_int),
+    ]
+
+
+class TensorRef(ctypes.Structure):
+    _fields_ = [("a", _c_p), ("b", _c_p), ("n", _c_long)]
+
+
+def _load():
+    if not LIB_PATH.exists():
+        raise RuntimeError(
+            f"libdmc.so not found at {LIB_PATH}. Build it with `python -m diffusion_models_collection_amd.build` "
+            "(there is no fallback: the diffusion hot path runs only on the gfx950 HIP kernels).")
+    lib = ctypes.CDLL(str(LIB_PATH))
+    sig = {
+        "dmc_version": (_c_int, []),
+        "dmc_last_error": (ctypes.c_char_p, []),
+        "dmc_conv2d": (_c_int, [ctypes.POINTER(ConvDesc), _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+        "dmc_conv2d_wgrad_workspace": (_c_size, [ctypes.POINTER(ConvDesc)]),
+        "dmc_conv2d_wgrad": (_c_int, [ctypes.POINTER(ConvDesc), _c_p, _c_int, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p]),
+        "dmc_pack_weight": (_c_int, [_c_int, _c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p]),
+        "dmc_gn_workspace": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
+        "dmc_gn_stats": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_f,
+                                  _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+        "dmc_gn_silu_bwd": (_c_int, [_c_int, _c_p, _c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int,
+                                     _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_u32, _c_u32, _c_f, _c_p, _c_p,
+                                     _c_int, _c_int, _c_int, _c_int, _c_p, _c_p, _c_p, _c_p]),
+        "dmc_channel_sum_workspace": (_c_size, [_c_int, _c_int, _c_int]),
+        "dmc_channel_sum": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_p, _c_int, _c_p, _c_f, _c_p,
+                                     _c_p]),
+        "dmc_attn_fwd": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_int, _c_p, _c_p]),
+        "dmc_attn_workspace": (_c_size, [_c_int, _c_int, _c_int]),
+        "dmc_attn_bwd": (_c_int, [_c_int, _c_p, _c_int, _c_p, _c_p, _c_int, _c_p, _c_int, _c_int, _c_int, _c_int,
+                                  _c_p, _c_int, _c_p, _c_p]),
+        "dmc_time_embed": (_c_int, [_c_p, _c_int, _c_int, _c_p, _c_p]),
+        "dmc_embed_fwd": (_c_int, [_c_p, _c_int, _c_int, _c_p, _c_int, _c_p, _c_p]),
+        "dmc_embed_bwd": (_c_int, [_c_p, _c_int, _c_int, _c_p, _c_int, _c_p, _c_p]),
+        "dmc_pack_input": (_c_int, [_c_int, _c_p, _c_p, _c_p, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_p,
+                                    _c_int, _c_p]),
+        "dmc_q_sample": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_int, _c_int, _c_p, _c_p]),
+        "dmc_loss_fwd": (_c_int, [_c_int, _c_p, _c_p, _c_long, _c_p, _c_p, _c_p]),
+        "dmc_loss_bwd": (_c_int, [_c_int, _c_p, _c_p, _c_long, _c_p, _c_p, _c_p]),
+        "dmc_ddim_step": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_int, _c_int, _c_f, _c_int, _c_p, _c_p,
+                                   _c_p]),
+        "dmc_ddpm_step": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_int, _c_int, _c_int,
+                                   _c_p, _c_p, _c_p]),
+        "dmc_cfg_x0": (_c_int, [_c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p, _c_int, _c_int, _c_int, _c_f, _c_p, _c_p,
+                                _c_p]),
+        "dmc_ema_update": (_c_int, [_c_p, _c_int, _c_f, _c_p]),
+        "dmc_clip_grad_norm": (_c_int, [_c_p, _c_int, _c_f, _c_p, _c_p, _c_p]),
+        "dmc_silu_fwd": (_c_int, [_c_p, _c_p, _c_long, _c_p]),
+        "dmc_unpack_output": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p]),
+        "dmc_add": (_c_int, [_c_int, _c_p, _c_p, _c_long, _c_p]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib, list(sig)
+
+
+LIB, EXPORTS = _load()
+
+
+class DMCError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise DMCError(f"{what} failed ({rc}): {LIB.dmc_last_error().decode()}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return DMC_F32
+    if dt == torch.bfloat16:
+        return DMC_BF16
+    raise DMCError(f"unsupported storage dtype {dt}")
+
+
+def kc_for(cin: int, dt: torch.dtype) -> int:
+    """Packed K per tap: channel count rounded up to the kernel stage depth (32 fp32 / 64 bf16)."""
+    bk = 32 if dt == torch.float32 else 64
+    return (cin + bk - 1) // bk * bk
+
+
+def chunk_for(dt: torch.dtype) -> int:
+    return 4 if dt == torch.float32 else 8

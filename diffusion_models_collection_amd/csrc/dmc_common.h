@@ -1,0 +1,163 @@
+// Common device helpers for the MI355X (gfx950 / CDNA4) kernels of the diffusion hot path.
+//
+// Layout conventions (see DESIGN.md "Data layout in HBM"):
+//   * activations are NHWC ("pixel rows"): element (n, y, x, c) at ((n*H + y)*W + x)*ld + c
+//   * packed conv weights are [Cout][tap][Cin_pad]  (K-contiguous rows)
+//   * storage type T is float (parity mode) or bf16 (perf mode); accumulation is always fp32
+//
+// MFMA fragment convention used by every kernel (16x16 output tiles, wave64):
+//   lane l, h = l >> 4, r = l & 15
+//   A operand  : A[row r][k = h*KPL + j], j < KPL           (16 bytes per lane)
+//   B operand  : B[k = h*KPL + j][col r]
+//   C/D        : C[row 4h + i][col r], i < 4
+//   bf16: KPL = 8, one v_mfma_f32_16x16x32_bf16 per fragment pair
+//   fp32: KPL = 4, four v_mfma_f32_16x16x4_f32 (element e of both fragments -> k = 4h + e)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v2i __attribute__((ext_vector_type(2)));
+
+#define DMC_DEV __device__ __forceinline__
+#define LDS_AS __attribute__((address_space(3)))
+
+DMC_DEV float bf2f(uint32_t b) { return __uint_as_float(b << 16); }
+DMC_DEV uint32_t f2bf(float f) {
+  // round-to-nearest-even; NaN stays NaN
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+template <typename T> struct TT;
+template <> struct TT<float> {
+  static constexpr int KPL = 4;   // elements per 16-byte chunk
+  static constexpr int SZ = 4;
+};
+template <> struct TT<bf16_t> {
+  static constexpr int KPL = 8;
+  static constexpr int SZ = 2;
+};
+
+// ---- 16-byte chunk <-> 8 floats (bf16) or 4 floats (fp32) ----
+template <typename T> struct Chunk;
+template <> struct Chunk<float> {
+  static DMC_DEV void unpack(const v4i& c, float* f) {
+    f[0] = __int_as_float(c[0]); f[1] = __int_as_float(c[1]);
+    f[2] = __int_as_float(c[2]); f[3] = __int_as_float(c[3]);
+  }
+  static DMC_DEV v4i pack(const float* f) {
+    v4i c; c[0] = __float_as_int(f[0]); c[1] = __float_as_int(f[1]);
+    c[2] = __float_as_int(f[2]); c[3] = __float_as_int(f[3]); return c;
+  }
+};
+template <> struct Chunk<bf16_t> {
+  static DMC_DEV void unpack(const v4i& c, float* f) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t u = (uint32_t)c[i];
+      f[2 * i] = __uint_as_float(u << 16);
+      f[2 * i + 1] = __uint_as_float(u & 0xffff0000u);
+    }
+  }
+  static DMC_DEV v4i pack(const float* f) {
+    v4i c;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c[i] = (int)(f2bf(f[2 * i]) | (f2bf(f[2 * i + 1]) << 16));
+    return c;
+  }
+};
+
+// ---- MFMA over one 16-byte fragment pair ----
+template <typename T> DMC_DEV v4f mma16(v4f acc, const v4i& a, const v4i& b);
+template <> DMC_DEV v4f mma16<float>(v4f acc, const v4i& a, const v4i& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__int_as_float(a[0]), __int_as_float(b[0]), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__int_as_float(a[1]), __int_as_float(b[1]), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__int_as_float(a[2]), __int_as_float(b[2]), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__int_as_float(a[3]), __int_as_float(b[3]), acc, 0, 0, 0);
+  return acc;
+}
+template <> DMC_DEV v4f mma16<bf16_t>(v4f acc, const v4i& a, const v4i& b) {
+  v8s av = __builtin_bit_cast(v8s, a);
+  v8s bv = __builtin_bit_cast(v8s, b);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+}
+
+// ---- fragment loads from LDS ----
+// Row-contiguous image: element (row, k) at base + row*pitch + k*SZ (bytes). Lane reads 16 B.
+DMC_DEV v4i lds_frag_rows(const char* base, int pitch, int row0, int kbyte0) {
+  const int l = threadIdx.x & 63;
+  return *(const v4i*)(base + (row0 + (l & 15)) * pitch + kbyte0 + (l >> 4) * 16);
+}
+
+// Transposed image: element (k, row) at base + k*pitch + row*SZ. Lane needs KPL consecutive k.
+// bf16: two ds_read_b64_tr_b16 (rows k0+8h..+3 and k0+8h+4..+7); fp32: four ds_read_b32.
+template <typename T> DMC_DEV v4i lds_frag_tr(const char* base, int pitch, int k0, int row0);
+template <> DMC_DEV v4i lds_frag_tr<float>(const char* base, int pitch, int k0, int row0) {
+  const int l = threadIdx.x & 63;
+  const char* p = base + (k0 + (l >> 4) * 4) * pitch + (row0 + (l & 15)) * 4;
+  v4i r;
+  r[0] = *(const int*)(p);
+  r[1] = *(const int*)(p + pitch);
+  r[2] = *(const int*)(p + 2 * pitch);
+  r[3] = *(const int*)(p + 3 * pitch);
+  return r;
+}
+// general form for bf16: the two 4-row blocks start at k rows ka and kb (per lane group h)
+DMC_DEV v4i lds_frag_tr_bf16_rows(const char* base, int pitch, int ka, int kb, int row0) {
+  const int l = threadIdx.x & 63;
+  const int q = (l >> 2) & 3, p = l & 3;
+  const char* pa = base + (ka + q) * pitch + (row0 + 4 * p) * 2;
+  const char* pb = base + (kb + q) * pitch + (row0 + 4 * p) * 2;
+  v4s ra = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS v4s*)(uintptr_t)(pa));
+  v4s rb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS v4s*)(uintptr_t)(pb));
+  v2i ia = __builtin_bit_cast(v2i, ra), ib = __builtin_bit_cast(v2i, rb);
+  v4i r; r[0] = ia[0]; r[1] = ia[1]; r[2] = ib[0]; r[3] = ib[1];
+  return r;
+}
+template <> DMC_DEV v4i lds_frag_tr<bf16_t>(const char* base, int pitch, int k0, int row0) {
+  const int h = (threadIdx.x & 63) >> 4;
+  return lds_frag_tr_bf16_rows(base, pitch, k0 + 8 * h, k0 + 8 * h + 4, row0);
+}
+
+// ---- misc ----
+DMC_DEV float silu_f(float z) { return z / (1.0f + __expf(-z)); }
+DMC_DEV float sigmoid_f(float z) { return 1.0f / (1.0f + __expf(-z)); }
+
+// Counter-based hash for dropout masks: recomputable in backward from (seed, element index).
+DMC_DEV uint32_t hash_u32(uint32_t x, uint32_t seed) {
+  x ^= seed;
+  x *= 0x9E3779B1u; x ^= x >> 16;
+  x *= 0x85EBCA6Bu; x ^= x >> 13;
+  x *= 0xC2B2AE35u; x ^= x >> 16;
+  return x;
+}
+DMC_DEV bool drop_keep(uint64_t idx, uint32_t seed, uint32_t thresh) {
+  uint32_t h = hash_u32((uint32_t)idx ^ hash_u32((uint32_t)(idx >> 32), seed * 0x27d4eb2fu + 1u), seed);
+  return h >= thresh;
+}
+
+DMC_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+DMC_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// load / store one element of storage type T as float
+template <typename T> DMC_DEV float ld_as_f(const void* p, size_t i);
+template <> DMC_DEV float ld_as_f<float>(const void* p, size_t i) { return ((const float*)p)[i]; }
+template <> DMC_DEV float ld_as_f<bf16_t>(const void* p, size_t i) { return bf2f(((const bf16_t*)p)[i]); }
+template <typename T> DMC_DEV void st_from_f(void* p, size_t i, float v);
+template <> DMC_DEV void st_from_f<float>(void* p, size_t i, float v) { ((float*)p)[i] = v; }
+template <> DMC_DEV void st_from_f<bf16_t>(void* p, size_t i, float v) { ((bf16_t*)p)[i] = (bf16_t)f2bf(v); }

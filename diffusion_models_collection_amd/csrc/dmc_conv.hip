@@ -1,0 +1,593 @@
+// Implicit-GEMM convolution for gfx950: forward / input-gradient (one kernel) and weight-gradient.
+//
+// Replaces the nn.Conv2d / nn.Linear arithmetic of models/unet.py (ResidualBlock :34-60, AttentionBlock
+// qkv/proj :81-82, Downsample :106, Upsample :116 with F.interpolate, time_embed :167-172, input_conv
+// :188, output :237-241) and the torch.cat skip concat of :284 (two-source virtual concat), with the
+// GroupNorm-apply + SiLU (+ dropout) prologue and the bias + embedding + residual epilogue fused.
+//
+// GEMM orientation (forward): C[co][pix] = sum_k Wp[co][k] * A[pix][k],  k = (tap, channel).
+//   MFMA A operand = weight rows (co), B operand = activation rows (pix); each lane ends up holding 4
+//   consecutive output channels of one pixel, which is one vector store in NHWC.
+// Weight gradient: C[co][kk] = sum_pix dY[pix][co] * A[pix][kk]; both operands are staged as
+//   [pixel][channel] images and read transposed (ds_read_b64_tr_b16 for bf16).
+#include "dmc_common.h"
+#include "dmc_internal.h"
+
+namespace {
+
+struct ConvK {
+  const char* x1; const char* x2; const char* w; char* y1; char* y2;
+  int N, H, W, C1, C2, ld1, ld2, Kc, OH, OW, Cout, ntaps, mode, stride;
+  int tdy[16], tdx[16];
+  int prologue; const float* psc; const float* psh; int ldp;
+  uint32_t dseed, dthresh; float dscale; int dld;
+  const float* bias; const float* addvec; int ld_add;
+  const char* resid; int ld_res; const float* silu_pre; int ld_silu;
+  int Csplit, ldy1, ldy2, out_f32, out_nchw;
+  int M;      // N*OH*OW output pixels
+  int OHW;    // OH*OW
+};
+
+// Source pixel of output pixel (n,oy,ox) under tap; returns -1 if it falls in the zero padding.
+DMC_DEV int src_pixel(const ConvK& a, int n, int oy, int ox, int tap) {
+  int iy = oy * a.stride + a.tdy[tap];
+  int ix = ox * a.stride + a.tdx[tap];
+  if (a.mode == DMC_MODE_UPSAMPLE) {
+    if (iy < 0 || iy >= 2 * a.H || ix < 0 || ix >= 2 * a.W) return -1;
+    iy >>= 1; ix >>= 1;
+  } else if (a.mode == DMC_MODE_DILATE) {
+    if (iy < 0 || ix < 0 || (iy & 1) || (ix & 1)) return -1;
+    iy >>= 1; ix >>= 1;
+    if (iy >= a.H || ix >= a.W) return -1;
+  } else {
+    if (iy < 0 || iy >= a.H || ix < 0 || ix >= a.W) return -1;
+  }
+  return (n * a.H + iy) * a.W + ix;
+}
+
+// One 16-byte chunk of the (prologue-transformed) activation operand: channels [c, c+KPL) of source
+// pixel sp (or zero).
+template <typename T>
+DMC_DEV v4i load_act_chunk(const ConvK& a, int n, int sp, int c) {
+  constexpr int EPC = TT<T>::KPL;
+  v4i v = {0, 0, 0, 0};
+  if (sp < 0) return v;
+  const char* src;
+  if (c < a.C1) src = a.x1 + ((size_t)sp * a.ld1 + c) * sizeof(T);
+  else if (c < a.C1 + a.C2) src = a.x2 + ((size_t)sp * a.ld2 + (c - a.C1)) * sizeof(T);
+  else return v;
+  v = *(const v4i*)src;
+  if (a.prologue != DMC_PRO_NONE) {
+    float f[EPC];
+    Chunk<T>::unpack(v, f);
+    if (a.prologue == DMC_PRO_AFFINE_SILU) {
+      const float* sc = a.psc + (size_t)n * a.ldp + c;
+      const float* sh = a.psh + (size_t)n * a.ldp + c;
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) f[e] = silu_f(fmaf(f[e], sc[e], sh[e]));
+    } else if (a.prologue == DMC_PRO_AFFINE) {
+      const float* sc = a.psc + (size_t)n * a.ldp + c;
+      const float* sh = a.psh + (size_t)n * a.ldp + c;
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) f[e] = fmaf(f[e], sc[e], sh[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) f[e] = silu_f(f[e]);
+    }
+    if (a.dthresh) {
+      const uint64_t base = (uint64_t)sp * a.dld + c;
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) f[e] = drop_keep(base + e, a.dseed, a.dthresh) ? f[e] * a.dscale : 0.f;
+    }
+    v = Chunk<T>::pack(f);
+  }
+  return v;
+}
+
+template <typename T> DMC_DEV void load4(const char* p, size_t idx, float* v, bool f32);
+template <typename T>
+DMC_DEV void load4(const char* p, size_t idx, float* v, bool f32) {
+  if (f32 || sizeof(T) == 4) {
+    v4f x = *(const v4f*)(p + idx * 4);
+    v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+  } else {
+    v2i x = *(const v2i*)(p + idx * 2);
+    v[0] = bf2f((uint32_t)x[0] & 0xffffu); v[1] = bf2f((uint32_t)x[0] >> 16);
+    v[2] = bf2f((uint32_t)x[1] & 0xffffu); v[3] = bf2f((uint32_t)x[1] >> 16);
+  }
+}
+template <typename T>
+DMC_DEV void store4(char* p, size_t idx, const float* v, bool f32) {
+  if (f32 || sizeof(T) == 4) {
+    v4f x = {v[0], v[1], v[2], v[3]};
+    *(v4f*)(p + idx * 4) = x;
+  } else {
+    v2i x;
+    x[0] = (int)(f2bf(v[0]) | (f2bf(v[1]) << 16));
+    x[1] = (int)(f2bf(v[2]) | (f2bf(v[3]) << 16));
+    *(v2i*)(p + idx * 2) = x;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Forward / dgrad kernel. Tile BM pixels x BN output channels, 256 threads = 2x2 waves, stage depth
+// 128 bytes of K per row (BK = 32 fp32 / 64 bf16), register-staged double buffer, one barrier per stage.
+// LDS rows are 128 B, 16-byte chunk ch of row r stored at chunk ch ^ (r & 7) (conflict-free
+// ds_read_b128 for the fragment pattern).
+template <typename T, int BM, int BN>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(ConvK a) {
+  constexpr int EPC = TT<T>::KPL;
+  constexpr int BK = 128 / sizeof(T);
+  constexpr int ACH = BM / 32;   // activation chunks per thread per stage
+  constexpr int BCH = BN / 32;   // weight chunks per thread per stage
+  constexpr int TM = BM / 32;    // 16-pixel tiles per wave
+  constexpr int TN = BN / 32;    // 16-channel tiles per wave
+  __shared__ __attribute__((aligned(16))) char lds[2][(BM + BN) * 128];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int ch = tid & 7;          // fixed 16-byte chunk column of this thread
+  const int rbase = tid >> 3;      // rows rbase + 32*j
+
+  int pn[ACH], poy[ACH], pox[ACH];
+#pragma unroll
+  for (int j = 0; j < ACH; ++j) {
+    int pix = m0 + rbase + 32 * j;
+    if (pix < a.M) {
+      pn[j] = pix / a.OHW;
+      int rem = pix - pn[j] * a.OHW;
+      poy[j] = rem / a.OW;
+      pox[j] = rem - poy[j] * a.OW;
+    } else {
+      pn[j] = -1; poy[j] = 0; pox[j] = 0;
+    }
+  }
+  const size_t wrow = (size_t)a.ntaps * a.Kc;
+  const int nstages = a.ntaps * (a.Kc / BK);
+
+  v4i ra[ACH], rb[BCH];
+  auto load_stage = [&](int s) {
+    const int k0 = s * BK;
+    const int tap = k0 / a.Kc;
+    const int c = k0 - tap * a.Kc + ch * EPC;
+#pragma unroll
+    for (int j = 0; j < ACH; ++j) {
+      int sp = (pn[j] >= 0) ? src_pixel(a, pn[j], poy[j], pox[j], tap) : -1;
+      ra[j] = load_act_chunk<T>(a, pn[j], sp, c);
+    }
+#pragma unroll
+    for (int j = 0; j < BCH; ++j) {
+      int co = n0 + rbase + 32 * j;
+      if (co < a.Cout) rb[j] = *(const v4i*)(a.w + ((size_t)co * wrow + k0 + ch * EPC) * sizeof(T));
+      else rb[j] = v4i{0, 0, 0, 0};
+    }
+  };
+  auto store_stage = [&](int buf) {
+    char* A = lds[buf];
+    char* B = lds[buf] + BM * 128;
+#pragma unroll
+    for (int j = 0; j < ACH; ++j) {
+      int r = rbase + 32 * j;
+      *(v4i*)(A + r * 128 + ((ch ^ (r & 7)) << 4)) = ra[j];
+    }
+#pragma unroll
+    for (int j = 0; j < BCH; ++j) {
+      int r = rbase + 32 * j;
+      *(v4i*)(B + r * 128 + ((ch ^ (r & 7)) << 4)) = rb[j];
+    }
+  };
+
+  v4f acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  load_stage(0);
+  store_stage(0);
+  __syncthreads();
+  const int fr = lane & 15, fh = lane >> 4;
+  for (int s = 0; s < nstages; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nstages) load_stage(s + 1);
+    const char* A = lds[buf];
+    const char* B = lds[buf] + BM * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = ks * 4 + fh;
+      v4i fa[TN], fb[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        int r = wn * (BN / 2) + i * 16 + fr;
+        fa[i] = *(const v4i*)(B + r * 128 + ((chunk ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        int r = wm * (BM / 2) + j * 16 + fr;
+        fb[j] = *(const v4i*)(A + r * 128 + ((chunk ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
+    }
+    if (s + 1 < nstages) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue ----
+  const bool of32 = a.out_f32 != 0;
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    const int pix = m0 + wm * (BM / 2) + j * 16 + fr;
+    if (pix >= a.M) continue;
+    const int n = pix / a.OHW;
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int co = n0 + wn * (BN / 2) + i * 16 + fh * 4;
+      if (co >= a.Cout) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      const bool full = (co + 3 < a.Cout) && ((a.Cout & 3) == 0);
+      if (full && !a.out_nchw) {
+        if (a.bias) { v4f b = *(const v4f*)(a.bias + co); v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3]; }
+        if (a.addvec) { v4f b = *(const v4f*)(a.addvec + (size_t)n * a.ld_add + co); v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3]; }
+        if (a.silu_pre) {
+          v4f z = *(const v4f*)(a.silu_pre + (size_t)pix * a.ld_silu + co);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { float sg = sigmoid_f(z[e]); v[e] *= sg * (1.f + z[e] * (1.f - sg)); }
+        }
+        if (a.resid) { float r[4]; load4<T>(a.resid, (size_t)pix * a.ld_res + co, r, of32); v[0] += r[0]; v[1] += r[1]; v[2] += r[2]; v[3] += r[3]; }
+        if (co < a.Csplit) store4<T>(a.y1, (size_t)pix * a.ldy1 + co, v, of32);
+        else store4<T>(a.y2, (size_t)pix * a.ldy2 + (co - a.Csplit), v, of32);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = co + e;
+          if (c >= a.Cout) break;
+          float x = v[e];
+          if (a.bias) x += a.bias[c];
+          if (a.addvec) x += a.addvec[(size_t)n * a.ld_add + c];
+          if (a.silu_pre) { float z = a.silu_pre[(size_t)pix * a.ld_silu + c]; float sg = sigmoid_f(z); x *= sg * (1.f + z * (1.f - sg)); }
+          if (a.out_nchw) {
+            const int rem = pix - n * a.OHW;
+            float* y = (float*)a.y1 + ((size_t)n * a.Cout + c) * a.OHW + rem;
+            if (a.resid) x += ((const float*)a.resid)[((size_t)n * a.Cout + c) * a.OHW + rem];
+            *y = x;
+          } else {
+            if (a.resid) x += (of32 ? ld_as_f<float>(a.resid, (size_t)pix * a.ld_res + c) : ld_as_f<T>(a.resid, (size_t)pix * a.ld_res + c));
+            if (c < a.Csplit) {
+              if (of32) ((float*)a.y1)[(size_t)pix * a.ldy1 + c] = x; else st_from_f<T>(a.y1, (size_t)pix * a.ldy1 + c, x);
+            } else {
+              if (of32) ((float*)a.y2)[(size_t)pix * a.ldy2 + c - a.Csplit] = x; else st_from_f<T>(a.y2, (size_t)pix * a.ldy2 + c - a.Csplit, x);
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Weight-gradient kernel: C[co][kk] over a pixel range (split-K over grid.z), written as an fp32
+// slab [split][kk][co]. Tile 128 co x 128 kk, stage SP = 128/sizeof(T) pixels.
+// Image layout: [pixel row][channel], 16-byte chunks swizzled so the transposed fragment reads of
+// both operands are bank-conflict-free ("wgrad LDS image").
+template <typename T>
+DMC_DEV int wg_phys(int row, int chk) {
+  if (sizeof(T) == 2) {  // 256-byte rows, 32-byte segments
+    const int f = (row & 3) | (((row >> 3) & 1) << 2);
+    return ((((chk >> 1) ^ f) << 1) | (chk & 1)) << 4;
+  } else {               // 512-byte rows, 64-byte blocks
+    const int f = (row >> 2) & 1;
+    return ((((chk >> 2) ^ f) << 2) | (chk & 3)) << 4;
+  }
+}
+// transposed fragment read from a swizzled [k rows][128 cols] image: col tile `tile` (16 cols)
+template <typename T> DMC_DEV v4i wg_frag(const char* img, int k0, int tile);
+template <> DMC_DEV v4i wg_frag<float>(const char* img, int k0, int tile) {
+  const int l = threadIdx.x & 63;
+  const int h = l >> 4, r = l & 15;
+  v4i out;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int row = k0 + 4 * h + e;
+    const int f = (row >> 2) & 1;
+    out[e] = *(const int*)(img + row * 512 + ((tile ^ f) << 6) + r * 4);
+  }
+  return out;
+}
+template <> DMC_DEV v4i wg_frag<bf16_t>(const char* img, int k0, int tile) {
+  const int l = threadIdx.x & 63;
+  const int h = l >> 4, q = (l >> 2) & 3, p = l & 3;
+  v4i out;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int row = k0 + 8 * h + 4 * half + q;
+    const int f = (row & 3) | (((row >> 3) & 1) << 2);
+    const char* ptr = img + row * 256 + ((tile ^ f) << 5) + p * 8;
+    v4s rr = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS v4s*)(uintptr_t)(ptr));
+    v2i ii = __builtin_bit_cast(v2i, rr);
+    out[2 * half] = ii[0];
+    out[2 * half + 1] = ii[1];
+  }
+  return out;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvK a, const char* dy, int ld_dy, float* slab,
+                                                         int KK, int pix_per_split) {
+  constexpr int EPC = TT<T>::KPL;
+  constexpr int SP = 128 / sizeof(T);      // pixels per stage
+  constexpr int ROWB = 128 * sizeof(T);    // bytes per image row (128 columns)
+  constexpr int CPR = ROWB / 16;           // chunks per row
+  constexpr int NCH = SP * CPR / 256;      // chunks per thread per operand (=4)
+  __shared__ __attribute__((aligned(16))) char lds[2][2 * SP * ROWB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;  // wm: co half, wn: kk half
+  const int co0 = blockIdx.y * 128;
+  const int kk0 = blockIdx.x * 128;
+  const int p_begin = blockIdx.z * pix_per_split;
+  const int p_end = min(a.M, p_begin + pix_per_split);
+  const int chk = tid % CPR;
+  const int rb0 = tid / CPR;
+  constexpr int RSTEP = 256 / CPR;
+
+  // activation column of this thread: kk = kk0 + chk*EPC -> (tap, channel)
+  const int kk = kk0 + chk * EPC;
+  const int tap = kk / a.Kc;
+  const int cch = kk - tap * a.Kc;
+  const bool kk_ok = kk < KK;
+  const int co_c = co0 + chk * EPC;
+
+  v4i rd[NCH], rx[NCH];
+  auto load_stage = [&](int p0) {
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int pix = p0 + rb0 + RSTEP * j;
+      v4i d = {0, 0, 0, 0}, x = {0, 0, 0, 0};
+      if (pix < p_end) {
+        if (co_c < a.Cout) d = *(const v4i*)(dy + ((size_t)pix * ld_dy + co_c) * sizeof(T));
+        if (kk_ok) {
+          const int n = pix / a.OHW;
+          const int rem = pix - n * a.OHW;
+          const int oy = rem / a.OW, ox = rem - (rem / a.OW) * a.OW;
+          const int sp = src_pixel(a, n, oy, ox, tap);
+          x = load_act_chunk<T>(a, n, sp, cch);
+        }
+      }
+      rd[j] = d; rx[j] = x;
+    }
+  };
+  auto store_stage = [&](int buf) {
+    char* D = lds[buf];
+    char* X = lds[buf] + SP * ROWB;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int r = rb0 + RSTEP * j;
+      *(v4i*)(D + r * ROWB + wg_phys<T>(r, chk)) = rd[j];
+      *(v4i*)(X + r * ROWB + wg_phys<T>(r, chk)) = rx[j];
+    }
+  };
+
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int nst = (p_end - p_begin + SP - 1) / SP;
+  if (nst > 0) {
+    load_stage(p_begin);
+    store_stage(0);
+    __syncthreads();
+    for (int s = 0; s < nst; ++s) {
+      const int buf = s & 1;
+      if (s + 1 < nst) load_stage(p_begin + (s + 1) * SP);
+      const char* D = lds[buf];
+      const char* X = lds[buf] + SP * ROWB;
+#pragma unroll
+      for (int ks = 0; ks < SP / (4 * EPC); ++ks) {
+        v4i fa[4], fb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = wg_frag<T>(D, ks * 4 * EPC, wm * 4 + i);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = wg_frag<T>(X, ks * 4 * EPC, wn * 4 + j);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
+      }
+      if (s + 1 < nst) store_stage(buf ^ 1);
+      __syncthreads();
+    }
+  }
+  // slab [z][kk][Cpad] where Cpad = round up Cout to 128 (co is the row of C: co = 4h+i, kk = col r)
+  const int Cpad = gridDim.y * 128;
+  float* out = slab + (size_t)blockIdx.z * KK * Cpad;
+  const int fr = lane & 15, fh = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = kk0 + wn * 64 + j * 16 + fr;
+    if (k >= KK) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = co0 + wm * 64 + i * 16 + fh * 4;
+      *(v4f*)(out + (size_t)k * Cpad + co) = acc[i][j];
+    }
+  }
+}
+
+// dw[co][c][t] = scale * sum_z slab[z][t*Kc + c][co]
+__global__ void wgrad_reduce_kernel(const float* slab, int splits, int KK, int Cpad, int Cout, int Ctot,
+                                    int ntaps, int Kc, float scale, float* dw) {
+  const long total = (long)Cout * Ctot * ntaps;
+  for (long o = blockIdx.x * (long)blockDim.x + threadIdx.x; o < total; o += (long)gridDim.x * blockDim.x) {
+    const int t = o % ntaps;
+    const long r = o / ntaps;
+    const int c = r % Ctot;
+    const int co = r / Ctot;
+    const size_t k = (size_t)t * Kc + c;
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += slab[((size_t)z * KK + k) * Cpad + co];
+    dw[o] = s * scale;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void pack_weight_kernel(int mode, const float* w, int Cout, int Cin, int kh, int kw, int Kc, T* dst) {
+  // FWD: dst[co][t][c]; DGRAD: dst[c][t][co]; UPDGRAD: dst[c][u*4+v][co] (4x4 folded kernel)
+  const int ntaps = (mode == DMC_PACK_UPDGRAD) ? 16 : kh * kw;
+  const int rows = (mode == DMC_PACK_FWD) ? Cout : Cin;
+  const long total = (long)rows * ntaps * Kc;
+  for (long o = blockIdx.x * (long)blockDim.x + threadIdx.x; o < total; o += (long)gridDim.x * blockDim.x) {
+    const int k = o % Kc;
+    const long r = o / Kc;
+    const int t = r % ntaps;
+    const int row = r / ntaps;
+    float v = 0.f;
+    if (mode == DMC_PACK_FWD) {
+      if (k < Cin) v = w[((size_t)row * Cin + k) * kh * kw + t];
+    } else if (mode == DMC_PACK_DGRAD) {
+      if (k < Cout) v = w[((size_t)k * Cin + row) * kh * kw + t];
+    } else {
+      if (k < Cout) {
+        // folded taps: offset u in {-1,0,1,2} <- set of kh with (dj + 1 - kh == u), dj in {0,1}
+        const int u = t >> 2, vv = t & 3;  // u,v index 0..3 <-> offset -1..2
+        const int khs[4][2] = {{2, -1}, {1, 2}, {0, 1}, {0, -1}};
+        const float* base = w + ((size_t)k * Cin + row) * 9;
+        for (int a1 = 0; a1 < 2; ++a1) {
+          const int y = khs[u][a1];
+          if (y < 0) continue;
+          for (int b1 = 0; b1 < 2; ++b1) {
+            const int x = khs[vv][b1];
+            if (x < 0) continue;
+            v += base[y * 3 + x];
+          }
+        }
+      }
+    }
+    if (sizeof(T) == 4) ((float*)dst)[o] = v;
+    else ((bf16_t*)dst)[o] = (bf16_t)f2bf(v);
+  }
+}
+
+int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const void* w, void* y1, void* y2,
+               ConvK& k) {
+  DMC_REQUIRE(d->dtype == DMC_F32 || d->dtype == DMC_BF16, "conv: bad dtype %d", d->dtype);
+  const int epc = d->dtype == DMC_F32 ? 4 : 8;
+  const int bk = d->dtype == DMC_F32 ? 32 : 64;
+  // C1 may be ragged only for a single un-normalised source whose storage pitch is padded with zeros
+  // (the 3-channel network input): a chunk then reads the zero padding channels.
+  DMC_REQUIRE((d->C1 % epc == 0 || (d->C2 == 0 && d->prologue == DMC_PRO_NONE && d->ld1 >= (d->C1 + epc - 1) / epc * epc)) &&
+                  d->C2 % epc == 0,
+              "conv: C1/C2 (%d,%d) must be multiples of %d", d->C1, d->C2, epc);
+  DMC_REQUIRE(d->Kc % bk == 0 && d->Kc >= d->C1 + d->C2, "conv: Kc %d must be a multiple of %d and >= C1+C2", d->Kc, bk);
+  DMC_REQUIRE(d->ntaps >= 1 && d->ntaps <= 16, "conv: ntaps %d", d->ntaps);
+  DMC_REQUIRE(d->ld1 % epc == 0 && (d->C2 == 0 || d->ld2 % epc == 0), "conv: source pitch alignment");
+  DMC_REQUIRE(d->Csplit >= 0 && d->Csplit <= d->Cout && d->Csplit % 4 == 0, "conv: Csplit %d", d->Csplit);
+  k.x1 = (const char*)x1; k.x2 = (const char*)x2; k.w = (const char*)w; k.y1 = (char*)y1; k.y2 = (char*)y2;
+  k.N = d->N; k.H = d->H; k.W = d->W; k.C1 = d->C1; k.C2 = d->C2; k.ld1 = d->ld1; k.ld2 = d->ld2; k.Kc = d->Kc;
+  k.OH = d->OH; k.OW = d->OW; k.Cout = d->Cout; k.ntaps = d->ntaps; k.mode = d->mode; k.stride = d->stride;
+  for (int i = 0; i < 16; ++i) { k.tdy[i] = d->tap_dy[i]; k.tdx[i] = d->tap_dx[i]; }
+  k.prologue = d->prologue; k.psc = d->pro_scale; k.psh = d->pro_shift; k.ldp = d->ld_pro;
+  k.dseed = d->drop_seed; k.dthresh = d->drop_thresh; k.dscale = d->drop_scale; k.dld = d->drop_ld;
+  k.bias = d->bias; k.addvec = d->addvec; k.ld_add = d->ld_add; k.resid = (const char*)d->resid; k.ld_res = d->ld_res;
+  k.silu_pre = d->silu_pre; k.ld_silu = d->ld_silu;
+  k.Csplit = d->Csplit; k.ldy1 = d->ldy1; k.ldy2 = d->ldy2; k.out_f32 = d->out_f32; k.out_nchw = d->out_nchw;
+  k.M = d->N * d->OH * d->OW; k.OHW = d->OH * d->OW;
+  return 0;
+}
+
+template <typename T>
+int launch_fwd(const ConvK& k, hipStream_t s) {
+  // tile choice: big tiles when they still give >= ~2 waves of blocks over 256 CUs
+  const long t128 = (long)dmc::cdiv(k.M, 128) * dmc::cdiv(k.Cout, 128);
+  if (t128 >= 384 && k.Cout >= 128) {
+    dim3 g(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128));
+    conv_fwd_kernel<T, 128, 128><<<g, 256, 0, s>>>(k);
+  } else {
+    dim3 g(dmc::cdiv(k.M, 64), dmc::cdiv(k.Cout, 64));
+    conv_fwd_kernel<T, 64, 64><<<g, 256, 0, s>>>(k);
+  }
+  return dmc::check_launch("dmc_conv2d");
+}
+
+int wgrad_splits(const dmc_conv_desc* d, int* pps) {
+  const int sp = d->dtype == DMC_F32 ? 32 : 64;
+  const long M = (long)d->N * d->OH * d->OW;
+  const long KK = (long)d->ntaps * d->Kc;
+  const long tiles = (long)dmc::cdiv(KK, 128) * dmc::cdiv(d->Cout, 128);
+  long splits = (512 + tiles - 1) / tiles;
+  const long max_splits = (M + 4 * sp - 1) / (4 * sp);  // at least 4 stages per split
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  long per = (M + splits - 1) / splits;
+  per = (per + sp - 1) / sp * sp;
+  splits = (M + per - 1) / per;
+  *pps = (int)per;
+  return (int)splits;
+}
+
+}  // namespace
+
+extern "C" int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2, const void* w, void* y1,
+                          void* y2, void* stream) {
+  ConvK k;
+  if (fill_convk(d, x1, x2, w, y1, y2, k)) return 1;
+  hipStream_t s = dmc::as_stream(stream);
+  if (k.M == 0 || k.Cout == 0) return 0;
+  return d->dtype == DMC_F32 ? launch_fwd<float>(k, s) : launch_fwd<bf16_t>(k, s);
+}
+
+extern "C" size_t dmc_conv2d_wgrad_workspace(const dmc_conv_desc* d) {
+  int pps;
+  const int splits = wgrad_splits(d, &pps);
+  const size_t KK = (size_t)d->ntaps * d->Kc;
+  const size_t Cpad = (size_t)dmc::cdiv(d->Cout, 128) * 128;
+  return (size_t)splits * KK * Cpad * sizeof(float);
+}
+
+extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_dy, const void* x1, const void* x2,
+                                void* workspace, float* dw, float scale, void* stream) {
+  ConvK k;
+  if (fill_convk(d, x1, x2, nullptr, nullptr, nullptr, k)) return 1;
+  const int epc = d->dtype == DMC_F32 ? 4 : 8;
+  DMC_REQUIRE(ld_dy % epc == 0, "wgrad: ld_dy %d alignment", ld_dy);
+  hipStream_t s = dmc::as_stream(stream);
+  int pps;
+  const int splits = wgrad_splits(d, &pps);
+  const int KK = d->ntaps * d->Kc;
+  dim3 g(dmc::cdiv(KK, 128), dmc::cdiv(d->Cout, 128), splits);
+  if (d->dtype == DMC_F32)
+    conv_wgrad_kernel<float><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (float*)workspace, KK, pps);
+  else
+    conv_wgrad_kernel<bf16_t><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (float*)workspace, KK, pps);
+  if (dmc::check_launch("dmc_conv2d_wgrad")) return 2;
+  const int Ctot = d->C1 + d->C2;
+  const long total = (long)d->Cout * Ctot * d->ntaps;
+  const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  wgrad_reduce_kernel<<<blocks, 256, 0, s>>>((const float*)workspace, splits, KK, (int)g.y * 128, d->Cout, Ctot,
+                                             d->ntaps, d->Kc, scale, dw);
+  return dmc::check_launch("dmc_conv2d_wgrad reduce");
+}
+
+extern "C" int dmc_pack_weight(int pack_mode, int dtype, const float* w, int Cout, int Cin, int kh, int kw, int Kc,
+                               void* dst, void* stream) {
+  DMC_REQUIRE(pack_mode >= 0 && pack_mode <= 2, "pack: mode");
+  DMC_REQUIRE(pack_mode != DMC_PACK_UPDGRAD || (kh == 3 && kw == 3), "pack: UPDGRAD needs 3x3");
+  const int ntaps = pack_mode == DMC_PACK_UPDGRAD ? 16 : kh * kw;
+  const long rows = pack_mode == DMC_PACK_FWD ? Cout : Cin;
+  const long total = rows * ntaps * Kc;
+  const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  hipStream_t s = dmc::as_stream(stream);
+  if (dtype == DMC_F32)
+    pack_weight_kernel<float><<<blocks, 256, 0, s>>>(pack_mode, w, Cout, Cin, kh, kw, Kc, (float*)dst);
+  else
+    pack_weight_kernel<bf16_t><<<blocks, 256, 0, s>>>(pack_mode, w, Cout, Cin, kh, kw, Kc, (bf16_t*)dst);
+  return dmc::check_launch("dmc_pack_weight");
+}

@@ -1,0 +1,389 @@
+// GroupNorm statistics / backward and per-channel reductions for gfx950.
+//
+// GroupNorm(8, C, eps=1e-5, affine) of models/unet.py:35, :51, :80, :238 is split in two: the statistics
+// pass below (mean, rstd per (n, group) folded with gamma/beta into a per-(n, c) scale/shift), and the
+// apply, which is fused into the consumer convolution's prologue (dmc_conv.hip). The backward of
+// dropout(SiLU(GroupNorm(x))) is a per-channel reduction pass, a tiny finalize, and an apply pass.
+//
+// Every reduction is a fixed-order tree (no float atomics), so results are bitwise reproducible.
+// Access pattern: a thread owns one 16-byte chunk column of the NHWC rows and walks pixels, so each
+// wave reads whole contiguous rows (coalesced) and per-channel partial sums stay in registers.
+#include "dmc_common.h"
+#include "dmc_internal.h"
+
+namespace {
+
+struct Src2 {
+  const char* x1; const char* x2;
+  int C1, C2, ld1, ld2;
+};
+
+template <typename T>
+DMC_DEV v4i load_chunk2(const Src2& s, int pix, int c) {
+  if (c < s.C1) return *(const v4i*)(s.x1 + ((size_t)pix * s.ld1 + c) * sizeof(T));
+  return *(const v4i*)(s.x2 + ((size_t)pix * s.ld2 + (c - s.C1)) * sizeof(T));
+}
+
+// ---------------- statistics ----------------
+// partial [n][split][g][2] = shifted sums of (x - K_g), (x - K_g)^2 with K_g = x[n, pixel 0, first channel of g]
+template <typename T>
+__global__ __launch_bounds__(256) void gn_stats_partial(Src2 s, int HW, int G, int splits, float* partial) {
+  constexpr int EPC = TT<T>::KPL;
+  const int n = blockIdx.x, sp = blockIdx.y;
+  const int C = s.C1 + s.C2, cpg = C / G;
+  const int CPR = C / EPC;
+  const int rpi = 256 / CPR;                 // rows per iteration
+  const int tid = threadIdx.x;
+  const int col = tid % CPR, r0 = tid / CPR;
+  const bool active = r0 < rpi;
+  const int per = (HW + splits - 1) / splits;
+  const int pb = sp * per, pe = min(HW, pb + per);
+  __shared__ float red[256][2 * 8];
+  float s1[EPC], s2[EPC], K[EPC];
+  const int c0 = col * EPC;
+  for (int e = 0; e < EPC; ++e) {
+    s1[e] = 0.f; s2[e] = 0.f;
+    const int g = (c0 + e) / cpg;
+    const int cg = g * cpg;
+    // shift: first element of the group (same for every block of this n)
+    K[e] = (cg < s.C1) ? ld_as_f<T>(s.x1, (size_t)n * HW * s.ld1 + cg)
+                       : ld_as_f<T>(s.x2, (size_t)n * HW * s.ld2 + (cg - s.C1));
+  }
+  if (active) {
+    for (int p = pb + r0; p < pe; p += rpi) {
+      float f[EPC];
+      Chunk<T>::unpack(load_chunk2<T>(s, n * HW + p, c0), f);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        const float d = f[e] - K[e];
+        s1[e] += d;
+        s2[e] = fmaf(d, d, s2[e]);
+      }
+    }
+  }
+  for (int e = 0; e < EPC; ++e) { red[tid][2 * e] = active ? s1[e] : 0.f; red[tid][2 * e + 1] = active ? s2[e] : 0.f; }
+  __syncthreads();
+  // one thread per group: sum over its channels, then over row-threads (fixed order)
+  for (int g = tid; g < G; g += 256) {
+    float a1 = 0.f, a2 = 0.f;
+    for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+      const int cc = c / EPC, e = c % EPC;
+      float b1 = 0.f, b2 = 0.f;
+      for (int r = 0; r < rpi; ++r) { b1 += red[r * CPR + cc][2 * e]; b2 += red[r * CPR + cc][2 * e + 1]; }
+      a1 += b1; a2 += b2;
+    }
+    float* o = partial + (((size_t)n * splits + sp) * G + g) * 2;
+    o[0] = a1; o[1] = a2;
+  }
+}
+
+template <typename T>
+__global__ void gn_stats_final(Src2 s, int HW, int G, int splits, const float* partial, float eps,
+                               const float* gamma, const float* beta, float* mean_rstd, float* scale, float* shift) {
+  const int n = blockIdx.x;
+  const int C = s.C1 + s.C2, cpg = C / G;
+  const float cnt = (float)cpg * (float)HW;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int g = c / cpg, cg = g * cpg;
+    float a1 = 0.f, a2 = 0.f;
+    for (int sp = 0; sp < splits; ++sp) {
+      const float* p = partial + (((size_t)n * splits + sp) * G + g) * 2;
+      a1 += p[0]; a2 += p[1];
+    }
+    const float K = (cg < s.C1) ? ld_as_f<T>(s.x1, (size_t)n * HW * s.ld1 + cg)
+                                : ld_as_f<T>(s.x2, (size_t)n * HW * s.ld2 + (cg - s.C1));
+    const float m1 = a1 / cnt;
+    float var = a2 / cnt - m1 * m1;
+    var = fmaxf(var, 0.f);
+    const float mean = K + m1;
+    const float rstd = 1.0f / sqrtf(var + eps);
+    if (c == cg && mean_rstd) { mean_rstd[((size_t)n * G + g) * 2] = mean; mean_rstd[((size_t)n * G + g) * 2 + 1] = rstd; }
+    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    const float sc = rstd * gm;
+    scale[(size_t)n * C + c] = sc;
+    shift[(size_t)n * C + c] = bt - mean * sc;
+  }
+}
+
+// ---------------- backward of dropout(SiLU(GN(x))) ----------------
+struct GnBwd {
+  Src2 s;
+  const char* g; int ld_g;
+  int HW, G, splits;
+  const float* mr; const float* gamma; const float* beta;
+  uint32_t dseed, dthresh; float dscale;
+  int silu;
+};
+
+// dz for one element (recomputes the forward)
+DMC_DEV float gn_dz(float x, float gv, float mean, float rstd, float gm, float bt, float& xhat, int silu) {
+  xhat = (x - mean) * rstd;
+  if (!silu) return gv;
+  const float z = fmaf(xhat, gm, bt);
+  const float sg = sigmoid_f(z);
+  return gv * sg * (1.f + z * (1.f - sg));
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gn_bwd_partial(GnBwd b, float* partial /*[n][split][C][2]*/) {
+  constexpr int EPC = TT<T>::KPL;
+  const int n = blockIdx.x, sp = blockIdx.y;
+  const int C = b.s.C1 + b.s.C2, cpg = C / b.G;
+  const int CPR = C / EPC, rpi = 256 / CPR;
+  const int tid = threadIdx.x, col = tid % CPR, r0 = tid / CPR;
+  const bool active = r0 < rpi;
+  const int per = (b.HW + b.splits - 1) / b.splits;
+  const int pb = sp * per, pe = min(b.HW, pb + per);
+  __shared__ float red[256][2 * 8];
+  const int c0 = col * EPC;
+  float mean[EPC], rstd[EPC], gm[EPC], bt[EPC], a1[EPC], a2[EPC];
+  for (int e = 0; e < EPC; ++e) {
+    const int c = c0 + e, g = c / cpg;
+    mean[e] = b.mr[((size_t)n * b.G + g) * 2];
+    rstd[e] = b.mr[((size_t)n * b.G + g) * 2 + 1];
+    gm[e] = b.gamma ? b.gamma[c] : 1.f;
+    bt[e] = b.beta ? b.beta[c] : 0.f;
+    a1[e] = 0.f; a2[e] = 0.f;
+  }
+  if (active) {
+    for (int p = pb + r0; p < pe; p += rpi) {
+      const int pix = n * b.HW + p;
+      float x[EPC], gv[EPC];
+      Chunk<T>::unpack(load_chunk2<T>(b.s, pix, c0), x);
+      Chunk<T>::unpack(*(const v4i*)(b.g + ((size_t)pix * b.ld_g + c0) * sizeof(T)), gv);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        float g = gv[e];
+        if (b.dthresh) g = drop_keep((uint64_t)pix * C + c0 + e, b.dseed, b.dthresh) ? g * b.dscale : 0.f;
+        float xh;
+        const float dz = gn_dz(x[e], g, mean[e], rstd[e], gm[e], bt[e], xh, b.silu);
+        a1[e] += dz;
+        a2[e] = fmaf(dz, xh, a2[e]);
+      }
+    }
+  }
+  for (int e = 0; e < EPC; ++e) { red[tid][2 * e] = active ? a1[e] : 0.f; red[tid][2 * e + 1] = active ? a2[e] : 0.f; }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    const int cc = c / EPC, e = c % EPC;
+    float v1 = 0.f, v2 = 0.f;
+    for (int r = 0; r < rpi; ++r) { v1 += red[r * CPR + cc][2 * e]; v2 += red[r * CPR + cc][2 * e + 1]; }
+    float* o = partial + (((size_t)n * b.splits + sp) * C + c) * 2;
+    o[0] = v1; o[1] = v2;
+  }
+}
+
+// per n: A[n][c] = sum over splits; coef[n][g] = (sum_c gamma*A1 / cnt, sum_c gamma*A2 / cnt)
+__global__ void gn_bwd_final(int C, int G, int HW, int splits, const float* partial, const float* gamma,
+                             float* A /*[n][C][2]*/, float* coef /*[n][G][2]*/) {
+  const int n = blockIdx.x;
+  const int cpg = C / G;
+  __shared__ float sA[1024][2];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float v1 = 0.f, v2 = 0.f;
+    for (int sp = 0; sp < splits; ++sp) {
+      const float* p = partial + (((size_t)n * splits + sp) * C + c) * 2;
+      v1 += p[0]; v2 += p[1];
+    }
+    A[((size_t)n * C + c) * 2] = v1;
+    A[((size_t)n * C + c) * 2 + 1] = v2;
+    const float gm = gamma ? gamma[c] : 1.f;
+    sA[c][0] = v1 * gm; sA[c][1] = v2 * gm;
+  }
+  __syncthreads();
+  const float cnt = (float)cpg * (float)HW;
+  for (int g = threadIdx.x; g < G; g += blockDim.x) {
+    float m1 = 0.f, m2 = 0.f;
+    for (int c = g * cpg; c < (g + 1) * cpg; ++c) { m1 += sA[c][0]; m2 += sA[c][1]; }
+    coef[((size_t)n * G + g) * 2] = m1 / cnt;
+    coef[((size_t)n * G + g) * 2 + 1] = m2 / cnt;
+  }
+}
+
+__global__ void gn_bwd_param(int N, int C, const float* A, float* dgamma, float* dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int n = 0; n < N; ++n) { s1 += A[((size_t)n * C + c) * 2]; s2 += A[((size_t)n * C + c) * 2 + 1]; }
+  if (dbeta) dbeta[c] = s1;
+  if (dgamma) dgamma[c] = s2;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, int N, const float* coef, char* dx1, char* dx2, int ld1,
+                                                    int ld2, int acc1, int acc2) {
+  constexpr int EPC = TT<T>::KPL;
+  const int C = b.s.C1 + b.s.C2, cpg = C / b.G, CPR = C / EPC;
+  const long total = (long)N * b.HW * CPR;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int col = i % CPR;
+    const int pix = i / CPR;
+    const int n = pix / b.HW;
+    const int c0 = col * EPC;
+    float x[EPC], gv[EPC], o[EPC];
+    Chunk<T>::unpack(load_chunk2<T>(b.s, pix, c0), x);
+    Chunk<T>::unpack(*(const v4i*)(b.g + ((size_t)pix * b.ld_g + c0) * sizeof(T)), gv);
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      const int c = c0 + e, g = c / cpg;
+      const float mean = b.mr[((size_t)n * b.G + g) * 2], rstd = b.mr[((size_t)n * b.G + g) * 2 + 1];
+      const float gm = b.gamma ? b.gamma[c] : 1.f, bt = b.beta ? b.beta[c] : 0.f;
+      float gg = gv[e];
+      if (b.dthresh) gg = drop_keep((uint64_t)pix * C + c, b.dseed, b.dthresh) ? gg * b.dscale : 0.f;
+      float xh;
+      const float dz = gn_dz(x[e], gg, mean, rstd, gm, bt, xh, b.silu);
+      const float m1 = coef[((size_t)n * b.G + g) * 2], m2 = coef[((size_t)n * b.G + g) * 2 + 1];
+      o[e] = rstd * (dz * gm - m1 - xh * m2);
+    }
+    char* dst; int acc;
+    size_t off;
+    if (c0 < b.s.C1) { dst = dx1; acc = acc1; off = (size_t)pix * ld1 + c0; }
+    else { dst = dx2; acc = acc2; off = (size_t)pix * ld2 + (c0 - b.s.C1); }
+    v4i* p = (v4i*)(dst + off * sizeof(T));
+    if (acc) {
+      float prev[EPC];
+      Chunk<T>::unpack(*p, prev);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) o[e] += prev[e];
+    }
+    *p = Chunk<T>::pack(o);
+  }
+}
+
+// ---------------- per-channel pixel sums ----------------
+template <typename T>
+__global__ __launch_bounds__(256) void chsum_partial(const char* dy, int HW, int C, int ld, int splits, float* partial) {
+  constexpr int EPC = TT<T>::KPL;
+  const int n = blockIdx.x, sp = blockIdx.y;
+  const int CPR = (C + EPC - 1) / EPC, rpi = 256 / CPR;
+  const int tid = threadIdx.x, col = tid % CPR, r0 = tid / CPR;
+  const bool active = r0 < rpi;
+  const int per = (HW + splits - 1) / splits;
+  const int pb = sp * per, pe = min(HW, pb + per);
+  __shared__ float red[256][8];
+  float a[EPC];
+  for (int e = 0; e < EPC; ++e) a[e] = 0.f;
+  if (active) {
+    for (int p = pb + r0; p < pe; p += rpi) {
+      float f[EPC];
+      Chunk<T>::unpack(*(const v4i*)(dy + (((size_t)n * HW + p) * ld + col * EPC) * sizeof(T)), f);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) a[e] += f[e];
+    }
+  }
+  for (int e = 0; e < EPC; ++e) red[tid][e] = active ? a[e] : 0.f;
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    float v = 0.f;
+    for (int r = 0; r < rpi; ++r) v += red[r * CPR + c / EPC][c % EPC];
+    partial[((size_t)n * splits + sp) * C + c] = v;
+  }
+}
+
+__global__ void chsum_final(int N, int C, int splits, const float* partial, float* out_nc, int ld_out, float* out_c,
+                            float scale) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float tot = 0.f;
+  for (int n = 0; n < N; ++n) {
+    float v = 0.f;
+    for (int sp = 0; sp < splits; ++sp) v += partial[((size_t)n * splits + sp) * C + c];
+    if (out_nc) out_nc[(size_t)n * ld_out + c] = v * scale;
+    tot += v;
+  }
+  if (out_c) out_c[c] = tot * scale;
+}
+
+int host_splits(int N, int HW, int C, int epc) {
+  const int cpr = (C + epc - 1) / epc;
+  const int rpi = 256 / cpr > 0 ? 256 / cpr : 1;
+  int want = (1024 + N - 1) / N;
+  int maxs = HW / (rpi * 2);
+  if (maxs < 1) maxs = 1;
+  return want < maxs ? want : maxs;
+}
+
+}  // namespace
+
+extern "C" size_t dmc_gn_workspace(int N, int C, int G, int HW) {
+  const int splits = host_splits(N, HW, C, 4);  // fp32 chunking gives the largest split count
+  size_t stats = (size_t)N * splits * G * 2;
+  size_t bwd = (size_t)N * splits * C * 2 + (size_t)N * C * 2 + (size_t)N * G * 2;
+  return (stats > bwd ? stats : bwd) * sizeof(float) + 256;
+}
+
+extern "C" int dmc_gn_stats(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1, int ld2,
+                            int G, float eps, const float* gamma, const float* beta, void* workspace, float* mean_rstd,
+                            float* scale, float* shift, void* stream) {
+  const int epc = dtype == DMC_F32 ? 4 : 8;
+  const int C = C1 + C2;
+  DMC_REQUIRE(C % G == 0, "gn_stats: C %d not divisible by G %d", C, G);
+  DMC_REQUIRE(C1 % epc == 0 && C2 % epc == 0 && C / epc <= 256, "gn_stats: channel alignment (C1=%d C2=%d)", C1, C2);
+  DMC_REQUIRE(ld1 % epc == 0 && (C2 == 0 || ld2 % epc == 0), "gn_stats: pitch alignment");
+  hipStream_t s = dmc::as_stream(stream);
+  Src2 src{(const char*)x1, (const char*)x2, C1, C2, ld1, ld2};
+  const int splits = host_splits(N, HW, C, epc);
+  float* partial = (float*)workspace;
+  dim3 g(N, splits);
+  if (dtype == DMC_F32) {
+    gn_stats_partial<float><<<g, 256, 0, s>>>(src, HW, G, splits, partial);
+    gn_stats_final<float><<<N, 256, 0, s>>>(src, HW, G, splits, partial, eps, gamma, beta, mean_rstd, scale, shift);
+  } else {
+    gn_stats_partial<bf16_t><<<g, 256, 0, s>>>(src, HW, G, splits, partial);
+    gn_stats_final<bf16_t><<<N, 256, 0, s>>>(src, HW, G, splits, partial, eps, gamma, beta, mean_rstd, scale, shift);
+  }
+  return dmc::check_launch("dmc_gn_stats");
+}
+
+extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x1, const void* x2, int N, int HW, int C1,
+                               int C2, int ld1, int ld2, int G, const float* mean_rstd, const float* gamma,
+                               const float* beta, int silu, uint32_t drop_seed, uint32_t drop_thresh, float drop_scale, void* dx1,
+                               void* dx2, int ld_dx1, int ld_dx2, int accumulate1, int accumulate2, float* dgamma,
+                               float* dbeta, void* workspace, void* stream) {
+  const int epc = dtype == DMC_F32 ? 4 : 8;
+  const int C = C1 + C2;
+  DMC_REQUIRE(C % G == 0 && C <= 1024, "gn_bwd: C %d / G %d", C, G);
+  DMC_REQUIRE(C1 % epc == 0 && C2 % epc == 0 && C / epc <= 256, "gn_bwd: channel alignment");
+  DMC_REQUIRE(ld_g % epc == 0 && ld_dx1 % epc == 0 && (C2 == 0 || ld_dx2 % epc == 0), "gn_bwd: pitch alignment");
+  hipStream_t s = dmc::as_stream(stream);
+  GnBwd b;
+  b.s = Src2{(const char*)x1, (const char*)x2, C1, C2, ld1, ld2};
+  b.g = (const char*)g; b.ld_g = ld_g; b.HW = HW; b.G = G;
+  b.splits = host_splits(N, HW, C, epc);
+  b.mr = mean_rstd; b.gamma = gamma; b.beta = beta;
+  b.dseed = drop_seed; b.dthresh = drop_thresh; b.dscale = drop_scale;
+  b.silu = silu;
+  float* partial = (float*)workspace;
+  float* A = partial + (size_t)N * b.splits * C * 2;
+  float* coef = A + (size_t)N * C * 2;
+  dim3 gr(N, b.splits);
+  const long total = (long)N * HW * (C / epc);
+  const int ablocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  if (dtype == DMC_F32) gn_bwd_partial<float><<<gr, 256, 0, s>>>(b, partial);
+  else gn_bwd_partial<bf16_t><<<gr, 256, 0, s>>>(b, partial);
+  gn_bwd_final<<<N, 256, 0, s>>>(C, G, HW, b.splits, partial, gamma, A, coef);
+  gn_bwd_param<<<(C + 255) / 256, 256, 0, s>>>(N, C, A, dgamma, dbeta);
+  if (dtype == DMC_F32)
+    gn_bwd_apply<float><<<ablocks, 256, 0, s>>>(b, N, coef, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, accumulate1, accumulate2);
+  else
+    gn_bwd_apply<bf16_t><<<ablocks, 256, 0, s>>>(b, N, coef, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, accumulate1, accumulate2);
+  return dmc::check_launch("dmc_gn_silu_bwd");
+}
+
+extern "C" size_t dmc_channel_sum_workspace(int N, int HW, int C) {
+  return (size_t)N * host_splits(N, HW, C, 4) * C * sizeof(float) + 256;
+}
+
+extern "C" int dmc_channel_sum(int dtype, const void* dy, int N, int HW, int C, int ld, float* out_nc, int ld_out,
+                               float* out_c, float scale, void* workspace, void* stream) {
+  const int epc = dtype == DMC_F32 ? 4 : 8;
+  DMC_REQUIRE(ld % epc == 0 && (C + epc - 1) / epc <= 256, "channel_sum: C %d / ld %d", C, ld);
+  hipStream_t s = dmc::as_stream(stream);
+  const int splits = host_splits(N, HW, C, epc);
+  float* partial = (float*)workspace;
+  dim3 g(N, splits);
+  if (dtype == DMC_F32) chsum_partial<float><<<g, 256, 0, s>>>((const char*)dy, HW, C, ld, splits, partial);
+  else chsum_partial<bf16_t><<<g, 256, 0, s>>>((const char*)dy, HW, C, ld, splits, partial);
+  chsum_final<<<(C + 255) / 256, 256, 0, s>>>(N, C, splits, partial, out_nc, ld_out, out_c, scale);
+  return dmc::check_launch("dmc_channel_sum");
+}

@@ -1,0 +1,264 @@
+"""Tensor-level wrappers over the C ABI (include/dmc.h).
+
+Every function takes torch tensors that already live on the GPU, launches on torch's current stream
+and returns without synchronising. Activations are NHWC tensors [N, H, W, ld] (ld = channel pitch).
+No function here has a CPU or PyTorch-op fallback.
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+from ._lib import LIB, check, ptr
+
+TAPS3 = [(kh - 1, kw - 1) for kh in range(3) for kw in range(3)]      # forward 3x3, pad 1
+TAPS3_DGRAD = [(1 - kh, 1 - kw) for kh in range(3) for kw in range(3)]  # input-gradient of a 3x3 conv
+TAPS1 = [(0, 0)]
+TAPS_UPDGRAD = [(u - 1, v - 1) for u in range(4) for v in range(4)]    # folded nearest-x2 + 3x3 (4x4, s2)
+
+
+class Scratch:
+    """Grow-only device scratch shared by the kernels of one stream (wgrad slabs, GN partials, ...)."""
+
+    def __init__(self):
+        self.buf = None
+
+    def get(self, nbytes: int, device) -> torch.Tensor:
+        nbytes = max(int(nbytes), 256)
+        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
+            self.buf = torch.empty(int(nbytes * 1.25) + 4096, dtype=torch.uint8, device=device)
+        return self.buf
+
+
+SCRATCH = Scratch()
+
+
+def make_desc(dtype, N, H, W, C1, C2, ld1, ld2, Kc, OH, OW, Cout, taps, mode=L.MODE_NORMAL, stride=1):
+    d = L.ConvDesc()
+    d.dtype = L.dtype_code(dtype)
+    d.N, d.H, d.W = N, H, W
+    d.C1, d.C2, d.ld1, d.ld2, d.Kc = C1, C2, ld1, ld2, Kc
+    d.OH, d.OW, d.Cout = OH, OW, Cout
+    d.ntaps, d.mode, d.stride = len(taps), mode, stride
+    for i, (dy, dx) in enumerate(taps):
+        d.tap_dy[i] = dy
+        d.tap_dx[i] = dx
+    d.Csplit = Cout
+    d.drop_scale = 1.0
+    return d
+
+
+def set_prologue(d, kind=L.PRO_NONE, scale=None, shift=None, ld=0, drop=None, drop_ld=0):
+    d.prologue = kind
+    d.pro_scale = ptr(scale)
+    d.pro_shift = ptr(shift)
+    d.ld_pro = ld
+    if drop is not None:
+        d.drop_seed, d.drop_thresh, d.drop_scale = drop
+        d.drop_ld = drop_ld
+    else:
+        d.drop_seed, d.drop_thresh, d.drop_scale, d.drop_ld = 0, 0, 1.0, 0
+
+
+def set_epilogue(d, bias=None, addvec=None, ld_add=0, resid=None, ld_res=0, silu_pre=None, ld_silu=0,
+                 ldy1=0, ldy2=0, Csplit=None, out_f32=False, out_nchw=False):
+    d.bias = ptr(bias)
+    d.addvec = ptr(addvec)
+    d.ld_add = ld_add
+    d.resid = ptr(resid)
+    d.ld_res = ld_res
+    d.silu_pre = ptr(silu_pre)
+    d.ld_silu = ld_silu
+    d.ldy1, d.ldy2 = ldy1, ldy2
+    d.Csplit = d.Cout if Csplit is None else Csplit
+    d.out_f32 = int(out_f32)
+    d.out_nchw = int(out_nchw)
+
+
+def conv(d, x1, x2, w, y1, y2=None):
+    check(LIB.dmc_conv2d(ctypes.byref(d), ptr(x1), ptr(x2), ptr(w), ptr(y1), ptr(y2), L.stream()), "dmc_conv2d")
+
+
+def wgrad(d, dy, ld_dy, x1, x2, dw, scale=1.0):
+    nbytes = LIB.dmc_conv2d_wgrad_workspace(ctypes.byref(d))
+    ws = SCRATCH.get(nbytes, dy.device)
+    check(LIB.dmc_conv2d_wgrad(ctypes.byref(d), ptr(dy), ld_dy, ptr(x1), ptr(x2), ptr(ws), ptr(dw), scale, L.stream()),
+          "dmc_conv2d_wgrad")
+
+
+def pack_weight(mode, dtype, w, Kc, out=None):
+    """fp32 [Cout][Cin][kh][kw] (or [Cout][Cin] Linear) -> packed kernel layout."""
+    w = w.detach()
+    if w.dim() == 2:
+        Cout, Cin, kh, kw = w.shape[0], w.shape[1], 1, 1
+    else:
+        Cout, Cin, kh, kw = w.shape
+    ntaps = 16 if mode == L.PACK_UPDGRAD else kh * kw
+    rows = Cout if mode == L.PACK_FWD else Cin
+    if out is None:
+        out = torch.empty(rows * ntaps * Kc, dtype=dtype, device=w.device)
+    check(LIB.dmc_pack_weight(mode, L.dtype_code(dtype), ptr(w.contiguous()), Cout, Cin, kh, kw, Kc, ptr(out),
+                              L.stream()), "dmc_pack_weight")
+    return out
+
+
+def gn_stats(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, G, eps, gamma, beta):
+    C = C1 + C2
+    dev = x1.device
+    mr = torch.empty(N * G * 2, dtype=torch.float32, device=dev)
+    sc = torch.empty(N * C, dtype=torch.float32, device=dev)
+    sh = torch.empty(N * C, dtype=torch.float32, device=dev)
+    ws = SCRATCH.get(LIB.dmc_gn_workspace(N, C, G, HW), dev)
+    check(LIB.dmc_gn_stats(L.dtype_code(dtype), ptr(x1), ptr(x2), N, HW, C1, C2, ld1, ld2, G, eps, ptr(gamma),
+                           ptr(beta), ptr(ws), ptr(mr), ptr(sc), ptr(sh), L.stream()), "dmc_gn_stats")
+    return sc, sh, mr
+
+
+def gn_bwd(dtype, g, ld_g, x1, x2, N, HW, C1, C2, ld1, ld2, G, mr, gamma, beta, silu, drop, dx1, dx2, ld_dx1,
+           ld_dx2, acc1, acc2, dgamma, dbeta):
+    ws = SCRATCH.get(LIB.dmc_gn_workspace(N, C1 + C2, G, HW), g.device)
+    seed, thresh, scale = drop if drop is not None else (0, 0, 1.0)
+    check(LIB.dmc_gn_silu_bwd(L.dtype_code(dtype), ptr(g), ld_g, ptr(x1), ptr(x2), N, HW, C1, C2, ld1, ld2, G, ptr(mr),
+                              ptr(gamma), ptr(beta), int(silu), seed, thresh, scale, ptr(dx1), ptr(dx2), ld_dx1, ld_dx2,
+                              int(acc1), int(acc2), ptr(dgamma), ptr(dbeta), ptr(ws), L.stream()), "dmc_gn_silu_bwd")
+
+
+def channel_sum(dtype, dy, N, HW, C, ld, out_nc=None, ld_out=0, out_c=None, scale=1.0):
+    """Per-(n,c) and per-c pixel sums; wide tensors are processed in channel slices of <= 256 chunks."""
+    step = 256 * L.chunk_for(dtype)
+    esz = dy.element_size()
+    for c0 in range(0, C, step):
+        cs = min(step, C - c0)
+        ws = SCRATCH.get(LIB.dmc_channel_sum_workspace(N, HW, cs), dy.device)
+        onc = None if out_nc is None else out_nc.data_ptr() + 4 * c0
+        oc = None if out_c is None else out_c.data_ptr() + 4 * c0
+        check(LIB.dmc_channel_sum(L.dtype_code(dtype), dy.data_ptr() + esz * c0, N, HW, cs, ld, onc, ld_out, oc,
+                                  scale, ptr(ws), L.stream()), "dmc_channel_sum")
+
+
+def attn_fwd(dtype, qkv, ld_qkv, N, Lq, heads, hd, out, ld_out, lse):
+    check(LIB.dmc_attn_fwd(L.dtype_code(dtype), ptr(qkv), ld_qkv, N, Lq, heads, hd, ptr(out), ld_out, ptr(lse),
+                           L.stream()), "dmc_attn_fwd")
+
+
+def attn_bwd(dtype, qkv, ld_qkv, out, dout, ld_out, lse, N, Lq, heads, hd, dqkv, ld_dqkv):
+    ws = SCRATCH.get(LIB.dmc_attn_workspace(N, Lq, heads), qkv.device)
+    check(LIB.dmc_attn_bwd(L.dtype_code(dtype), ptr(qkv), ld_qkv, ptr(out), ptr(dout), ld_out, ptr(lse), N, Lq, heads,
+                           hd, ptr(dqkv), ld_dqkv, ptr(ws), L.stream()), "dmc_attn_bwd")
+
+
+def time_embed(t, dim, out):
+    check(LIB.dmc_time_embed(ptr(t), t.shape[0], dim, ptr(out), L.stream()), "dmc_time_embed")
+
+
+def embed_fwd(y, table, out):
+    check(LIB.dmc_embed_fwd(ptr(y), y.shape[0], table.shape[0], ptr(table), table.shape[1], ptr(out), L.stream()),
+          "dmc_embed_fwd")
+
+
+def embed_bwd(y, rows, dout, dtable):
+    check(LIB.dmc_embed_bwd(ptr(y), y.shape[0], rows, ptr(dout), dout.shape[1], ptr(dtable), L.stream()),
+          "dmc_embed_bwd")
+
+
+def pack_input(dtype, x, ld, noise=None, t=None, a=None, b=None, out=None):
+    N, C, H, W = x.shape
+    if out is None:
+        out = torch.empty(N, H, W, ld, dtype=dtype, device=x.device)
+    check(LIB.dmc_pack_input(L.dtype_code(dtype), ptr(x), ptr(noise), ptr(t), ptr(a), ptr(b), N, C, H, W, ptr(out), ld,
+                             L.stream()), "dmc_pack_input")
+    return out
+
+
+def unpack_output(dtype, src, ld, N, C, H, W, out=None):
+    if out is None:
+        out = torch.empty(N, C, H, W, dtype=torch.float32, device=src.device)
+    check(LIB.dmc_unpack_output(L.dtype_code(dtype), ptr(src), ld, N, C, H, W, ptr(out), L.stream()),
+          "dmc_unpack_output")
+    return out
+
+
+def add_(dtype, y, x):
+    check(LIB.dmc_add(L.dtype_code(dtype), ptr(y), ptr(x), y.numel(), L.stream()), "dmc_add")
+
+
+def q_sample(x0, noise, t, a, b, out=None):
+    x0 = x0.contiguous()
+    noise = noise.contiguous()
+    if out is None:
+        out = torch.empty_like(x0, dtype=torch.float32)
+    N = x0.shape[0]
+    check(LIB.dmc_q_sample(ptr(x0), ptr(noise), ptr(t), ptr(a), ptr(b), N, x0.numel() // max(N, 1), ptr(out),
+                           L.stream()), "dmc_q_sample")
+    return out
+
+
+def loss_fwd(loss_type, pred, target):
+    n = pred.numel()
+    loss = torch.empty((), dtype=torch.float32, device=pred.device)
+    ws = SCRATCH.get(4096 * 4, pred.device)
+    check(LIB.dmc_loss_fwd(L.LOSS[loss_type], ptr(pred), ptr(target), n, ptr(loss), ptr(ws), L.stream()),
+          "dmc_loss_fwd")
+    return loss
+
+
+def loss_bwd(loss_type, pred, target, dloss):
+    dpred = torch.empty_like(pred)
+    check(LIB.dmc_loss_bwd(L.LOSS[loss_type], ptr(pred), ptr(target), pred.numel(), ptr(dloss), ptr(dpred),
+                           L.stream()), "dmc_loss_bwd")
+    return dpred
+
+
+def ddim_step(x, eps, t, t_next, alphas_cumprod, eta=0.0, clip=True, x0=None, z=None, out=None):
+    if out is None:
+        out = torch.empty_like(x)
+    N = x.shape[0]
+    check(LIB.dmc_ddim_step(ptr(x), ptr(eps), ptr(x0), ptr(t), ptr(t_next), ptr(alphas_cumprod), N, x.numel() // N,
+                            float(eta), int(clip), ptr(z), ptr(out), L.stream()), "dmc_ddim_step")
+    return out
+
+
+def ddpm_step(x, eps, t, sra, srm1, c1, c2, logvar, clip=True, x0=None, z=None, out=None):
+    if out is None:
+        out = torch.empty_like(x)
+    N = x.shape[0]
+    check(LIB.dmc_ddpm_step(ptr(x), ptr(eps), ptr(x0), ptr(t), ptr(sra), ptr(srm1), ptr(c1), ptr(c2), ptr(logvar), N,
+                            x.numel() // N, int(clip), ptr(z), ptr(out), L.stream()), "dmc_ddpm_step")
+    return out
+
+
+def cfg_x0(x, ec, eu, scale, t, ta, tb, mode, p_threshold):
+    N = x.shape[0]
+    eps = torch.empty_like(x)
+    x0 = torch.empty_like(x)
+    p = float(p_threshold) if p_threshold is not None else -1.0
+    check(LIB.dmc_cfg_x0(ptr(x), ptr(ec), ptr(eu), float(scale), ptr(t), ptr(ta), ptr(tb), int(mode), N,
+                         x.numel() // N, p, ptr(eps), ptr(x0), L.stream()), "dmc_cfg_x0")
+    return eps, x0
+
+
+class TensorRefs:
+    """Device array of dmc_tensor_ref {a, b, n} for the multi-tensor kernels (uploaded once per pointer set)."""
+
+    def __init__(self, pairs, device):
+        self.key = tuple((a.data_ptr(), b.data_ptr() if b is not None else 0, a.numel()) for a, b in pairs)
+        arr = (L.TensorRef * len(pairs))()
+        for i, (a, b) in enumerate(pairs):
+            arr[i].a = a.data_ptr()
+            arr[i].b = b.data_ptr() if b is not None else None
+            arr[i].n = a.numel()
+        host = torch.frombuffer(bytearray(arr), dtype=torch.uint8)
+        self.dev = host.to(device)
+        self.count = len(pairs)
+
+
+def ema_update(refs: TensorRefs, decay):
+    check(LIB.dmc_ema_update(ptr(refs.dev), refs.count, float(decay), L.stream()), "dmc_ema_update")
+
+
+def clip_grad_norm(refs: TensorRefs, max_norm):
+    total = torch.empty((), dtype=torch.float32, device=refs.dev.device)
+    ws = SCRATCH.get((16 * refs.count + 16) * 4, refs.dev.device)
+    check(LIB.dmc_clip_grad_norm(ptr(refs.dev), refs.count, float(max_norm), ptr(total), ptr(ws), L.stream()),
+          "dmc_clip_grad_norm")
+    return total

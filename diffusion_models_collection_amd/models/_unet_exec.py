@@ -1,0 +1,715 @@
+"""Graph executor of the UNet on the gfx950 kernels (forward + hand-scheduled backward).
+
+The reference runs UNet.forward (models/unet.py:243-292) as ~400 PyTorch eager ops and lets autograd
+build the backward (~1000 ops). Here the network is walked once per call in the reference's order and
+every layer is a handful of fused HIP kernels over NHWC activations:
+
+  ResidualBlock   gn_stats(x) -> conv3x3[GN1+SiLU prologue; bias + temb epilogue] -> gn_stats(h1)
+                  -> [1x1 shortcut conv] -> conv3x3[GN2+SiLU+dropout prologue; bias + residual epilogue]
+  AttentionBlock  gn_stats(x) -> 1x1 qkv conv[GN prologue] -> fused flash attention -> 1x1 proj[+x]
+  Downsample      stride-2 conv;  Upsample: conv with nearest-x2 folded into the input indexing
+  up-path concat  never materialised: the consumer conv / GN read two sources (virtual concat)
+  time MLP        sinusoid -> Linear -> SiLU -> Linear, then ONE GEMM for all 22 time_mlp (+label_proj)
+                  projections (their weights are packed side by side)
+
+The backward is hand-scheduled in reverse (a tape of forward records), recomputing GN/SiLU/dropout on the
+fly (dropout masks come from a counter hash, never stored). Every parameter gradient is written straight
+into one flat fp32 buffer (views are handed to autograd), which is also what the data-parallel
+all-reduce works on.
+"""
+import math
+from typing import List, Optional
+
+import torch
+
+from .. import _lib as L
+from .. import kernels as K
+
+
+class Act:
+    """An NHWC activation [N, H, W, C] (contiguous, pitch C) plus its gradient buffer."""
+
+    __slots__ = ("t", "H", "W", "C", "grad")
+
+    def __init__(self, t, H, W, C):
+        self.t, self.H, self.W, self.C = t, H, W, C
+        self.grad = None
+
+
+def _seed_from_torch():
+    # dropout seeds follow torch's CPU generator (torch.manual_seed / set_seed semantics), no device sync
+    return int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+
+
+class _PackCache:
+    """Weights repacked into the kernel layouts, refreshed when the parameter's version changes."""
+
+    def __init__(self):
+        self.entries = {}
+
+    def get(self, key, param, version_src, make):
+        v = (version_src._version, version_src.data_ptr())
+        e = self.entries.get(key)
+        if e is None or e[0] != v:
+            e = (v, make())
+            self.entries[key] = e
+        return e[1]
+
+
+class UNetExecutor:
+    def __init__(self, model):
+        self.m = model
+        self.dt = model.compute_dtype
+        self.cdt = L.dtype_code(self.dt)
+        self.chunk = L.chunk_for(self.dt)
+        self.packs = _PackCache()
+        self.params = list(model.parameters())
+        self.pindex = {id(p): i for i, p in enumerate(self.params)}
+        # time-embedding projection layout: all ResidualBlocks' time_mlp (and label_proj) rows side by side
+        self.res_blocks = [mod for mod in model.modules() if type(mod).__name__ == "ResidualBlock"]
+        self.temb_off = {}
+        off = 0
+        for rb in self.res_blocks:
+            self.temb_off[id(rb)] = off
+            off += rb.out_channels
+        self.temb_total = off
+        self._layout_grads()
+        self.daddvec = None
+        self.training_grad_scale = 1.0
+        self.grad_hook = None       # called as hook(flat_grad, lo, hi) when a range of grads is final
+
+    # ---------------------------------------------------------------------------------------
+    def _layout_grads(self):
+        """Flat fp32 gradient buffer layout.
+
+        Slots follow the order in which the backward finishes them (reverse module order), so a prefix
+        of the buffer is final early (data-parallel all-reduce buckets). The 22 time_mlp weights, their
+        biases and the label_proj weights are placed side by side at the end: the stacked projection
+        GEMM's weight gradient then lands in place with no copy.
+        """
+        m = self.m
+        rbs = [mod for mod in m.modules() if type(mod).__name__ == "ResidualBlock"]
+        tail = [rb.time_mlp[1].weight for rb in rbs] + [rb.time_mlp[1].bias for rb in rbs]
+        if m.num_classes is not None:
+            tail += [rb.label_proj[1].weight for rb in rbs]
+        tail_ids = {id(p) for p in tail}
+        head = [p for p in reversed(self.params) if id(p) not in tail_ids]
+        order = head + tail
+        self.goff = [0] * len(self.params)
+        off = 0
+        for p in order:
+            self.goff[self.pindex[id(p)]] = off
+            off += p.numel()
+        self.gtotal = off
+        self.temb_w_off = self.goff[self.pindex[id(tail[0])]]
+        self.temb_b_off = self.goff[self.pindex[id(tail[len(rbs)])]]
+        self.temb_l_off = self.goff[self.pindex[id(tail[2 * len(rbs)])]] if m.num_classes is not None else None
+
+    def _gview(self, flat, p):
+        i = self.pindex[id(p)]
+        o = self.goff[i]
+        return flat[o:o + p.numel()].view(p.shape)
+
+    # ---------------------------------------------------------------------------------------
+    def _wpack(self, conv, mode, Kc, dtype=None):
+        dtype = dtype or self.dt
+        w = conv.weight
+        return self.packs.get((id(conv), mode, Kc, dtype), conv, w, lambda: K.pack_weight(mode, dtype, w, Kc))
+
+    def _temb_pack(self, which, dtype):
+        """Packed [sum Cout][1][Kc=512] weight of every block's time_mlp (which=0) / label_proj (which=1)."""
+        lins = [(rb.time_mlp[1] if which == 0 else rb.label_proj[1]) for rb in self.res_blocks]
+        dim = lins[0].weight.shape[1]
+        Kc = L.kc_for(dim, torch.float32)
+        ver = tuple((lin.weight._version, lin.weight.data_ptr()) for lin in lins)
+        key = ("temb", which)
+        e = self.packs.entries.get(key)
+        if e is None or e[0] != ver:
+            buf = torch.empty(self.temb_total * Kc, dtype=torch.float32, device=lins[0].weight.device)
+            off = 0
+            for lin in lins:
+                co = lin.weight.shape[0]
+                K.pack_weight(L.PACK_FWD, torch.float32, lin.weight, Kc, out=buf[off * Kc:(off + co) * Kc])
+                off += co
+            e = (ver, buf)
+            self.packs.entries[key] = e
+        return e[1]
+
+    def _temb_pack_dgrad(self, which):
+        """[dim][1][Kc >= sum Cout] dgrad pack of the concatenated projection weight."""
+        lins = [(rb.time_mlp[1] if which == 0 else rb.label_proj[1]) for rb in self.res_blocks]
+        ver = tuple((lin.weight._version, lin.weight.data_ptr()) for lin in lins)
+        key = ("temb_dg", which)
+        e = self.packs.entries.get(key)
+        if e is None or e[0] != ver:
+            wcat = torch.cat([lin.weight.detach() for lin in lins], 0)   # [sumC, dim] fp32, tiny, once per step
+            buf = K.pack_weight(L.PACK_DGRAD, torch.float32, wcat, L.kc_for(self.temb_total, torch.float32))
+            e = (ver, buf)
+            self.packs.entries[key] = e
+        return e[1]
+
+    def _temb_bias(self):
+        lins = [rb.time_mlp[1] for rb in self.res_blocks]
+        ver = tuple((lin.bias._version, lin.bias.data_ptr()) for lin in lins)
+        e = self.packs.entries.get("temb_b")
+        if e is None or e[0] != ver:
+            e = (ver, torch.cat([lin.bias.detach() for lin in lins], 0))
+            self.packs.entries["temb_b"] = e
+        return e[1]
+
+    # ---------------------------------------------------------------------------------------
+    def _conv(self, srcs, conv, taps, OH, OW, Cout, mode=L.MODE_NORMAL, stride=1, pro=None, drop=None,
+              bias=None, addvec=None, ld_add=0, resid=None, out=None, out_f32=False, out_nchw=False,
+              dtype=None, packmode=L.PACK_FWD, w=None, Kc=None, silu_pre=None, ld_silu=0, split=None):
+        """Generic implicit-GEMM conv over 1-2 NHWC sources. pro = (kind, scale, shift)."""
+        dtype = dtype or self.dt
+        a = srcs[0]
+        C1 = a.C
+        C2 = srcs[1].C if len(srcs) > 1 else 0
+        ld1 = a.t.shape[-1]
+        ld2 = srcs[1].t.shape[-1] if len(srcs) > 1 else 0
+        N = a.t.shape[0]
+        if Kc is None:
+            Kc = L.kc_for(C1 + C2, dtype)
+        if w is None:
+            w = self._wpack(conv, packmode, Kc, dtype)
+        d = K.make_desc(dtype, N, a.H, a.W, C1, C2, ld1, ld2, Kc, OH, OW, Cout, taps, mode, stride)
+        if pro is not None:
+            K.set_prologue(d, pro[0], pro[1], pro[2], C1 + C2, drop, C1 + C2)
+        elif drop is not None:
+            raise ValueError("dropout needs a prologue")
+        ldy2 = 0
+        y2 = None
+        if split is not None:
+            (y1, ldy1), (y2, ldy2), csplit = split
+        else:
+            y1 = out
+            ldy1 = 0 if out_nchw else out.shape[-1]
+            csplit = None
+        K.set_epilogue(d, bias=bias, addvec=addvec, ld_add=ld_add, resid=resid,
+                       ld_res=(0 if resid is None or out_nchw else resid.shape[-1]), silu_pre=silu_pre,
+                       ld_silu=ld_silu, ldy1=ldy1, ldy2=ldy2, Csplit=csplit, out_f32=out_f32, out_nchw=out_nchw)
+        K.conv(d, a.t, srcs[1].t if len(srcs) > 1 else None, w, y1, y2)
+        return d
+
+    def _wgrad(self, srcs, dy, ld_dy, taps, OH, OW, Cout, dw, mode=L.MODE_NORMAL, stride=1, pro=None, drop=None,
+               dtype=None):
+        dtype = dtype or self.dt
+        a = srcs[0]
+        C1 = a.C
+        C2 = srcs[1].C if len(srcs) > 1 else 0
+        N = a.t.shape[0]
+        Kc = L.kc_for(C1 + C2, dtype)
+        d = K.make_desc(dtype, N, a.H, a.W, C1, C2, a.t.shape[-1], srcs[1].t.shape[-1] if len(srcs) > 1 else 0, Kc,
+                        OH, OW, Cout, taps, mode, stride)
+        if pro is not None:
+            K.set_prologue(d, pro[0], pro[1], pro[2], C1 + C2, drop, C1 + C2)
+        K.wgrad(d, dy, ld_dy, a.t, srcs[1].t if len(srcs) > 1 else None, dw, self.training_grad_scale)
+
+    def _gn(self, srcs, gn, dtype=None):
+        dtype = dtype or self.dt
+        a = srcs[0]
+        b = srcs[1] if len(srcs) > 1 else None
+        N = a.t.shape[0]
+        return K.gn_stats(dtype, a.t, b.t if b else None, N, a.H * a.W, a.C, b.C if b else 0, a.t.shape[-1],
+                          b.t.shape[-1] if b else 0, gn.num_groups, gn.eps, gn.weight, gn.bias)
+
+    def _new(self, N, H, W, C, dtype=None):
+        return Act(torch.empty(N, H, W, C, dtype=dtype or self.dt, device=self.device), H, W, C)
+
+    def _grad_target(self, act):
+        """(buffer, accumulate) for writing a gradient contribution into act.grad."""
+        if act.grad is None:
+            act.grad = torch.empty_like(act.t)
+            return act.grad, 0
+        return act.grad, 1
+
+    # =========================================================================================
+    def run(self, x, t, y=None):
+        params = self.params
+        need_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))
+        if need_grad:
+            return _UNetFunction.apply(self, x, t, y, *params)
+        out, _ = self.forward(x, t, y, keep=False)
+        return out
+
+    def forward(self, x, t, y, keep):
+        m = self.m
+        self.device = x.device
+        dt = self.dt
+        N, Cin, H, W = x.shape
+        x = x.contiguous().float()
+        t = t.to(device=x.device, dtype=torch.long).contiguous()
+        tape = [] if keep else None
+        drop_on = m.training and m.dropout > 0
+        if drop_on:
+            p = float(m.dropout)
+            self._drop = (min(int(round(p * 4294967296.0)), 4294967295), 1.0 / (1.0 - p) if p < 1 else 0.0)
+            self._seed_base = _seed_from_torch()
+        else:
+            self._drop = None
+        self._blk_idx = 0
+
+        # ---- time embedding (fp32) ----
+        f32 = torch.float32
+        te = m.time_embed
+        mc = te[0].dim
+        tdim = te[1].out_features
+        e0 = torch.empty(N, mc, dtype=f32, device=x.device)
+        K.time_embed(t, mc, e0)
+        A0 = Act(e0.view(N, 1, 1, mc), 1, 1, mc)
+        A1 = self._new(N, 1, 1, tdim, f32)
+        self._conv([A0], te[1], K.TAPS1, 1, 1, tdim, bias=te[1].bias, out=A1.t, dtype=f32)
+        A2 = self._new(N, 1, 1, tdim, f32)
+        self._conv([A1], te[3], K.TAPS1, 1, 1, tdim, pro=(L.PRO_SILU, None, None), bias=te[3].bias, out=A2.t,
+                   dtype=f32)
+        Ay = None
+        if m.num_classes is not None and y is not None:
+            y = y.to(device=x.device, dtype=torch.long).contiguous()
+            ye = torch.empty(N, tdim, dtype=f32, device=x.device)
+            K.embed_fwd(y, m.label_embed.weight, ye)
+            Ay = Act(ye.view(N, 1, 1, tdim), 1, 1, tdim)
+        addvec = torch.empty(N, 1, 1, self.temb_total, dtype=f32, device=x.device)
+        Kt = L.kc_for(tdim, f32)
+        self._conv([A2], None, K.TAPS1, 1, 1, self.temb_total, pro=(L.PRO_SILU, None, None), bias=self._temb_bias(),
+                   out=addvec, dtype=f32, w=self._temb_pack(0, f32), Kc=Kt)
+        if Ay is not None:
+            self._conv([Ay], None, K.TAPS1, 1, 1, self.temb_total, pro=(L.PRO_SILU, None, None), resid=addvec,
+                       out=addvec, dtype=f32, w=self._temb_pack(1, f32), Kc=Kt)
+        self.addvec = addvec
+        if keep:
+            tape.append(("temb", t, y, A0, A1, A2, Ay, addvec))
+
+        # ---- input ----
+        ldx = (Cin + self.chunk - 1) // self.chunk * self.chunk
+        xin = Act(K.pack_input(dt, x, ldx), H, W, Cin)
+        h = self._new(N, H, W, m.model_channels)
+        self._conv([xin], m.input_conv, K.TAPS3, H, W, m.model_channels, bias=m.input_conv.bias, out=h.t)
+        if keep:
+            tape.append(("conv_in", xin, h, x.requires_grad))
+        hs = [h]
+        for block in m.down_blocks:
+            for layer in block:
+                h = self._layer([h], layer, tape)
+            hs.append(h)
+        for layer in m.middle_block:
+            if type(layer).__name__ == "Identity":
+                continue
+            h = self._layer([h], layer, tape)
+        for block in m.up_blocks:
+            srcs = [h, hs.pop()]
+            for layer in block:
+                h = self._layer(srcs, layer, tape)
+                srcs = [h]
+        # ---- output: GN -> SiLU -> conv3x3 -> NCHW fp32 ----
+        gno, convo = m.output[0], m.output[2]
+        sc, sh, mr = self._gn([h], gno)
+        out = torch.empty(N, m.out_channels, H, W, dtype=f32, device=x.device)
+        self._conv([h], convo, K.TAPS3, H, W, m.out_channels, pro=(L.PRO_AFFINE_SILU, sc, sh), bias=convo.bias,
+                   out=out, out_f32=True, out_nchw=True)
+        if keep:
+            tape.append(("out", h, (sc, sh, mr)))
+        return out, tape
+
+    def _layer(self, srcs, layer, tape):
+        name = type(layer).__name__
+        if name == "ResidualBlock":
+            return self._res_fwd(srcs, layer, tape)
+        if name == "AttentionBlock":
+            return self._attn_fwd(srcs[0], layer, tape)
+        if name == "Downsample":
+            a = srcs[0]
+            OH, OW = (a.H + 2 - 3) // 2 + 1, (a.W + 2 - 3) // 2 + 1
+            out = self._new(a.t.shape[0], OH, OW, a.C)
+            self._conv([a], layer.conv, K.TAPS3, OH, OW, a.C, stride=2, bias=layer.conv.bias, out=out.t)
+            if tape is not None:
+                tape.append(("down", layer, a, out))
+            return out
+        if name == "Upsample":
+            a = srcs[0]
+            out = self._new(a.t.shape[0], 2 * a.H, 2 * a.W, a.C)
+            self._conv([a], layer.conv, K.TAPS3, 2 * a.H, 2 * a.W, a.C, mode=L.MODE_UPSAMPLE, bias=layer.conv.bias,
+                       out=out.t)
+            if tape is not None:
+                tape.append(("up", layer, a, out))
+            return out
+        raise TypeError(f"unexpected layer {name}")
+
+    def _res_fwd(self, srcs, rb, tape):
+        a = srcs[0]
+        N, H, W = a.t.shape[0], a.H, a.W
+        Cout = rb.out_channels
+        gn1, conv1, gn2, conv2 = rb.conv1[0], rb.conv1[2], rb.conv2[0], rb.conv2[3]
+        st1 = self._gn(srcs, gn1)
+        h1 = self._new(N, H, W, Cout)
+        off = self.temb_off[id(rb)]
+        self._conv(srcs, conv1, K.TAPS3, H, W, Cout, pro=(L.PRO_AFFINE_SILU, st1[0], st1[1]), bias=conv1.bias,
+                   addvec=self.addvec.view(N, -1)[:, off:], ld_add=self.temb_total, out=h1.t)
+        st2 = self._gn([h1], gn2)
+        if isinstance(rb.shortcut, torch.nn.Conv2d):
+            s = torch.empty(N, H, W, Cout, dtype=self.dt, device=self.device)
+            self._conv(srcs, rb.shortcut, K.TAPS1, H, W, Cout, bias=rb.shortcut.bias, out=s)
+            resid = s
+        else:
+            resid = a.t
+        drop = None
+        if self._drop is not None:
+            drop = ((self._seed_base + 7919 * self._blk_idx) & 0xFFFFFFFF, self._drop[0], self._drop[1])
+        self._blk_idx += 1
+        out = self._new(N, H, W, Cout)
+        self._conv([h1], conv2, K.TAPS3, H, W, Cout, pro=(L.PRO_AFFINE_SILU, st2[0], st2[1]), drop=drop,
+                   bias=conv2.bias, resid=resid, out=out.t)
+        if tape is not None:
+            tape.append(("res", rb, srcs, h1, st1, st2, drop, out))
+        return out
+
+    def _attn_fwd(self, a, ab, tape):
+        N, H, W, C = a.t.shape[0], a.H, a.W, a.C
+        Lq = H * W
+        heads = ab.num_heads
+        hd = C // heads
+        st = self._gn([a], ab.norm)
+        qkv = self._new(N, H, W, 3 * C)
+        self._conv([a], ab.qkv, K.TAPS1, H, W, 3 * C, pro=(L.PRO_AFFINE, st[0], st[1]), bias=ab.qkv.bias, out=qkv.t)
+        o = self._new(N, H, W, C)
+        lse = torch.empty(N * heads * Lq, dtype=torch.float32, device=self.device)
+        K.attn_fwd(self.dt, qkv.t, 3 * C, N, Lq, heads, hd, o.t, C, lse)
+        out = self._new(N, H, W, C)
+        self._conv([o], ab.proj, K.TAPS1, H, W, C, bias=ab.proj.bias, resid=a.t, out=out.t)
+        if tape is not None:
+            tape.append(("attn", ab, a, st, qkv, o, lse, out))
+        return out
+
+    # =========================================================================================
+    def backward(self, tape, dout, x_requires_grad):
+        # The flat gradient buffer is reused across steps when no parameter still holds a gradient view of
+        # it (optimizer.zero_grad(set_to_none=True)); with gradient accumulation a fresh one is used.
+        flat = getattr(self, "_flat", None)
+        if flat is None or flat.device != dout.device or any(p.grad is not None for p in self.params):
+            flat = torch.empty(self.gtotal, dtype=torch.float32, device=dout.device)
+        self._flat = flat
+        self.flat = flat
+        self.daddvec = None
+        self._dx = None
+        gv = lambda p: self._gview(flat, p)  # noqa: E731
+        dx = None
+        hook = self.grad_hook
+        if hook is not None:
+            order = sorted(range(len(self.params)), key=lambda i: self.goff[i])
+            final = [False] * len(self.params)
+            cursor = 0
+        for rec in reversed(tape):
+            kind = rec[0]
+            self._backward_record(rec, dout, gv)
+            if kind == "conv_in" and rec[3]:
+                dx = self._dx
+            if hook is not None:
+                # this record's grads are final: publish the finished prefix of the flat buffer
+                for p in self._record_params(rec):
+                    final[self.pindex[id(p)]] = True
+                while cursor < len(order) and final[order[cursor]]:
+                    cursor += 1
+                hi = self.goff[order[cursor]] if cursor < len(order) else self.gtotal
+                hook(flat, hi, kind == "temb")
+        self.daddvec = None
+        grads = [self._gview(flat, p) for p in self.params]
+        return dx, grads
+
+    def _record_params(self, rec):
+        kind = rec[0]
+        m = self.m
+        if kind == "out":
+            return list(m.output.parameters())
+        if kind == "res":
+            rb = rec[1]
+            skip = {id(p) for p in rb.time_mlp.parameters()}
+            if rb.label_proj is not None:
+                skip |= {id(p) for p in rb.label_proj.parameters()}
+            return [p for p in rb.parameters() if id(p) not in skip]
+        if kind in ("attn", "down", "up"):
+            return list(rec[1].parameters())
+        if kind == "conv_in":
+            return list(m.input_conv.parameters())
+        return list(self.params)   # temb: everything else is final now
+
+    def _backward_record(self, rec, dout, gv):
+        m = self.m
+        dt = self.dt
+        f32 = torch.float32
+        kind = rec[0]
+        if True:
+            if kind == "out":
+                _, h, (sc, sh, mr) = rec
+                gno, convo = m.output[0], m.output[2]
+                N, H, W = h.t.shape[0], h.H, h.W
+                Co = m.out_channels
+                ldo = (Co + self.chunk - 1) // self.chunk * self.chunk
+                dy = K.pack_input(dt, dout.contiguous(), ldo)
+                self._wgrad([h], dy, ldo, K.TAPS3, H, W, Co, gv(convo.weight), pro=(L.PRO_AFFINE_SILU, sc, sh))
+                K.channel_sum(dt, dy, N, H * W, Co, ldo, out_c=gv(convo.bias))
+                g = torch.empty(N, H, W, h.C, dtype=dt, device=dout.device)
+                dya = Act(dy, H, W, Co)
+                self._conv([dya], convo, K.TAPS3_DGRAD, H, W, h.C, out=g, packmode=L.PACK_DGRAD,
+                           Kc=L.kc_for(Co, dt))
+                buf, acc = self._grad_target(h)
+                K.gn_bwd(dt, g, h.C, h.t, None, N, H * W, h.C, 0, h.t.shape[-1], 0, gno.num_groups, mr, gno.weight,
+                         gno.bias, True, None, buf, None, h.C, 0, acc, 0, gv(gno.weight), gv(gno.bias))
+            elif kind == "res":
+                self._res_bwd(rec, gv)
+            elif kind == "attn":
+                self._attn_bwd(rec, gv)
+            elif kind == "down":
+                _, layer, a, out = rec
+                N = a.t.shape[0]
+                dy = out.grad
+                self._wgrad([a], dy, out.C, K.TAPS3, out.H, out.W, out.C, gv(layer.conv.weight), stride=2)
+                K.channel_sum(dt, dy, N, out.H * out.W, out.C, out.C, out_c=gv(layer.conv.bias))
+                buf, acc = self._grad_target(a)
+                dya = Act(dy, out.H, out.W, out.C)
+                self._conv([dya], layer.conv, K.TAPS3_DGRAD, a.H, a.W, a.C, mode=L.MODE_DILATE,
+                           out=buf, resid=buf if acc else None, packmode=L.PACK_DGRAD)
+            elif kind == "up":
+                _, layer, a, out = rec
+                N = a.t.shape[0]
+                dy = out.grad
+                self._wgrad([a], dy, out.C, K.TAPS3, out.H, out.W, out.C, gv(layer.conv.weight),
+                            mode=L.MODE_UPSAMPLE)
+                K.channel_sum(dt, dy, N, out.H * out.W, out.C, out.C, out_c=gv(layer.conv.bias))
+                buf, acc = self._grad_target(a)
+                dya = Act(dy, out.H, out.W, out.C)
+                self._conv([dya], layer.conv, K.TAPS_UPDGRAD, a.H, a.W, a.C, stride=2, out=buf,
+                           resid=buf if acc else None, packmode=L.PACK_UPDGRAD)
+            elif kind == "conv_in":
+                _, xin, h, xg = rec
+                N = h.t.shape[0]
+                dy = h.grad
+                conv = m.input_conv
+                self._wgrad([xin], dy, h.C, K.TAPS3, h.H, h.W, h.C, gv(conv.weight))
+                K.channel_sum(dt, dy, N, h.H * h.W, h.C, h.C, out_c=gv(conv.bias))
+                if xg:
+                    ldx = xin.t.shape[-1]
+                    g = torch.empty(N, h.H, h.W, ldx, dtype=dt, device=dout.device)
+                    self._conv([Act(dy, h.H, h.W, h.C)], conv, K.TAPS3_DGRAD, h.H, h.W, xin.C, out=g,
+                               packmode=L.PACK_DGRAD)
+                    self._dx = K.unpack_output(dt, g, ldx, N, xin.C, h.H, h.W)
+            elif kind == "temb":
+                self._temb_bwd(rec, self.daddvec, gv)
+
+    def _res_bwd(self, rec, gv):
+        _, rb, srcs, h1, st1, st2, drop, out = rec
+        dt = self.dt
+        a = srcs[0]
+        N, H, W = a.t.shape[0], a.H, a.W
+        Cout = rb.out_channels
+        C1 = a.C
+        C2 = srcs[1].C if len(srcs) > 1 else 0
+        gn1, conv1, gn2, conv2 = rb.conv1[0], rb.conv1[2], rb.conv2[0], rb.conv2[3]
+        dout = out.grad
+        HW = H * W
+        # conv2 (weight, bias) and its input gradient
+        self._wgrad([h1], dout, Cout, K.TAPS3, H, W, Cout, gv(conv2.weight), pro=(L.PRO_AFFINE_SILU, st2[0], st2[1]),
+                    drop=drop)
+        K.channel_sum(dt, dout, N, HW, Cout, Cout, out_c=gv(conv2.bias))
+        g2 = torch.empty(N, H, W, Cout, dtype=dt, device=dout.device)
+        self._conv([Act(dout, H, W, Cout)], conv2, K.TAPS3_DGRAD, H, W, Cout, out=g2, packmode=L.PACK_DGRAD)
+        # shortcut
+        if isinstance(rb.shortcut, torch.nn.Conv2d):
+            sc = rb.shortcut
+            self._wgrad(srcs, dout, Cout, K.TAPS1, H, W, Cout, gv(sc.weight))
+            K.channel_sum(dt, dout, N, HW, Cout, Cout, out_c=gv(sc.bias))
+            if len(srcs) == 1:
+                buf, acc = self._grad_target(a)
+                self._conv([Act(dout, H, W, Cout)], sc, K.TAPS1, H, W, C1, out=buf, resid=buf if acc else None,
+                           packmode=L.PACK_DGRAD)
+            else:
+                b = srcs[1]
+                b1, acc1 = self._grad_target(a)
+                b2, acc2 = self._grad_target(b)
+                if acc1 or acc2:
+                    # rare: pre-existing gradient on a concat source; go through a temporary
+                    tmp = torch.empty(N, H, W, C1 + C2, dtype=dt, device=dout.device)
+                    self._conv([Act(dout, H, W, Cout)], sc, K.TAPS1, H, W, C1 + C2, out=tmp, packmode=L.PACK_DGRAD)
+                    self._scatter_add_concat(tmp, b1, acc1, b2, acc2, C1, C2)
+                else:
+                    self._conv([Act(dout, H, W, Cout)], sc, K.TAPS1, H, W, C1 + C2, packmode=L.PACK_DGRAD,
+                               split=((b1, C1), (b2, C2), C1))
+        else:
+            if a.grad is None:
+                a.grad = dout          # identity shortcut: alias (dout is dead after this block)
+            else:
+                K.add_(dt, a.grad, dout)
+        # GN2 + SiLU + dropout backward -> dh1
+        dh1 = torch.empty(N, H, W, Cout, dtype=dt, device=dout.device)
+        K.gn_bwd(dt, g2, Cout, h1.t, None, N, HW, Cout, 0, Cout, 0, gn2.num_groups, st2[2], gn2.weight, gn2.bias, True,
+                 drop, dh1, None, Cout, 0, 0, 0, gv(gn2.weight), gv(gn2.bias))
+        # time-embedding add: per-(n, c) pixel sums -> daddvec slice; conv1 bias
+        off = self.temb_off[id(rb)]
+        if self.daddvec is None:
+            self.daddvec = torch.empty(N, self.temb_total, dtype=torch.float32, device=dout.device)
+        K.channel_sum(dt, dh1, N, HW, Cout, Cout, out_nc=self.daddvec[:, off:], ld_out=self.temb_total,
+                      out_c=gv(conv1.bias))
+        # conv1
+        self._wgrad(srcs, dh1, Cout, K.TAPS3, H, W, Cout, gv(conv1.weight), pro=(L.PRO_AFFINE_SILU, st1[0], st1[1]))
+        g1 = torch.empty(N, H, W, C1 + C2, dtype=dt, device=dout.device)
+        self._conv([Act(dh1, H, W, Cout)], conv1, K.TAPS3_DGRAD, H, W, C1 + C2, out=g1, packmode=L.PACK_DGRAD)
+        b1, acc1 = self._grad_target(a)
+        if len(srcs) > 1:
+            b2, acc2 = self._grad_target(srcs[1])
+            ld2 = srcs[1].t.shape[-1]
+        else:
+            b2, acc2, ld2 = None, 0, 0
+        K.gn_bwd(dt, g1, C1 + C2, a.t, srcs[1].t if len(srcs) > 1 else None, N, HW, C1, C2, a.t.shape[-1], ld2,
+                 gn1.num_groups, st1[2], gn1.weight, gn1.bias, True, None, b1, b2, a.t.shape[-1], ld2, acc1, acc2,
+                 gv(gn1.weight), gv(gn1.bias))
+
+    def _scatter_add_concat(self, tmp, b1, acc1, b2, acc2, C1, C2):
+        t1 = tmp[..., :C1].contiguous()
+        t2 = tmp[..., C1:].contiguous()
+        if acc1:
+            K.add_(self.dt, b1, t1)
+        else:
+            b1.copy_(t1)
+        if acc2:
+            K.add_(self.dt, b2, t2)
+        else:
+            b2.copy_(t2)
+
+    def _attn_bwd(self, rec, gv):
+        _, ab, a, st, qkv, o, lse, out = rec
+        dt = self.dt
+        N, H, W, C = a.t.shape[0], a.H, a.W, a.C
+        HW = H * W
+        heads = ab.num_heads
+        hd = C // heads
+        dout = out.grad
+        # proj
+        self._wgrad([o], dout, C, K.TAPS1, H, W, C, gv(ab.proj.weight))
+        K.channel_sum(dt, dout, N, HW, C, C, out_c=gv(ab.proj.bias))
+        do = torch.empty(N, H, W, C, dtype=dt, device=dout.device)
+        self._conv([Act(dout, H, W, C)], ab.proj, K.TAPS1, H, W, C, out=do, packmode=L.PACK_DGRAD)
+        # residual: x gets dout
+        if a.grad is None:
+            a.grad = dout
+        else:
+            K.add_(dt, a.grad, dout)
+        dqkv = torch.empty(N, H, W, 3 * C, dtype=dt, device=dout.device)
+        K.attn_bwd(dt, qkv.t, 3 * C, o.t, do, C, lse, N, HW, heads, hd, dqkv, 3 * C)
+        self._wgrad([a], dqkv, 3 * C, K.TAPS1, H, W, 3 * C, gv(ab.qkv.weight), pro=(L.PRO_AFFINE, st[0], st[1]))
+        K.channel_sum(dt, dqkv, N, HW, 3 * C, 3 * C, out_c=gv(ab.qkv.bias))
+        g = torch.empty(N, H, W, C, dtype=dt, device=dout.device)
+        self._conv([Act(dqkv, H, W, 3 * C)], ab.qkv, K.TAPS1, H, W, C, out=g, packmode=L.PACK_DGRAD)
+        K.gn_bwd(dt, g, C, a.t, None, N, HW, C, 0, C, 0, ab.norm.num_groups, st[2], ab.norm.weight, ab.norm.bias,
+                 False, None, a.grad, None, C, 0, 1, 0, gv(ab.norm.weight), gv(ab.norm.bias))
+
+    def _temb_bwd(self, rec, daddvec, gv):
+        _, t, y, A0, A1, A2, Ay, addvec = rec
+        m = self.m
+        f32 = torch.float32
+        te = m.time_embed
+        N = daddvec.shape[0]
+        tdim = A2.C
+        T = self.temb_total
+        dA = Act(daddvec.view(N, 1, 1, T), 1, 1, T)
+        # stacked projection weights: dW[sumC][dim] -> the per-block slices are contiguous rows
+        flat = self.flat
+        dw_t = flat[self.temb_w_off:self.temb_w_off + T * tdim]
+        self._wgrad([A2], daddvec, T, K.TAPS1, 1, 1, T, dw_t, pro=(L.PRO_SILU, None, None), dtype=f32)
+        K.channel_sum(f32, daddvec, 1, N, T, T, out_c=flat[self.temb_b_off:self.temb_b_off + T])
+        # d(silu(e2)) * silu'(e2) -> de2 (fused in the dgrad epilogue)
+        de2 = torch.empty(N, 1, 1, tdim, dtype=f32, device=daddvec.device)
+        self._conv([dA], None, K.TAPS1, 1, 1, tdim, out=de2, dtype=f32, w=self._temb_pack_dgrad(0),
+                   Kc=L.kc_for(T, f32), silu_pre=A2.t, ld_silu=tdim)
+        if Ay is not None:
+            dw_l = flat[self.temb_l_off:self.temb_l_off + T * tdim]
+            self._wgrad([Ay], daddvec, T, K.TAPS1, 1, 1, T, dw_l, pro=(L.PRO_SILU, None, None), dtype=f32)
+            dye = torch.empty(N, 1, 1, tdim, dtype=f32, device=daddvec.device)
+            self._conv([dA], None, K.TAPS1, 1, 1, tdim, out=dye, dtype=f32, w=self._temb_pack_dgrad(1),
+                       Kc=L.kc_for(T, f32), silu_pre=Ay.t, ld_silu=tdim)
+            K.embed_bwd(y, m.label_embed.weight.shape[0], dye.view(N, tdim), gv(m.label_embed.weight))
+        # Linear2 (te[3]) on silu(e1)
+        self._wgrad([A1], de2, tdim, K.TAPS1, 1, 1, tdim, gv(te[3].weight), pro=(L.PRO_SILU, None, None), dtype=f32)
+        K.channel_sum(f32, de2, 1, N, tdim, tdim, out_c=gv(te[3].bias))
+        de1 = torch.empty(N, 1, 1, tdim, dtype=f32, device=daddvec.device)
+        self._conv([Act(de2, 1, 1, tdim)], te[3], K.TAPS1, 1, 1, tdim, out=de1, dtype=f32, packmode=L.PACK_DGRAD,
+                   silu_pre=A1.t, ld_silu=tdim)
+        # Linear1 (te[1]) on the sinusoid
+        self._wgrad([A0], de1, tdim, K.TAPS1, 1, 1, tdim, gv(te[1].weight), dtype=f32)
+        K.channel_sum(f32, de1, 1, N, tdim, tdim, out_c=gv(te[1].bias))
+
+
+class _UNetFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ex, x, t, y, *params):
+        out, tape = ex.forward(x, t, y, keep=True)
+        ctx.ex = ex
+        ctx.tape = tape
+        ctx.x_req = x.requires_grad
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        ex = ctx.ex
+        dx, grads = ex.backward(ctx.tape, dout, ctx.x_req)
+        ctx.tape = None
+        return (None, dx, None, None, *grads)
+
+
+def count_forward_flops(model) -> float:
+    """2*MACs per image of the convs, linears and attention matmuls of one forward (for rooflines)."""
+    flops = 0.0
+    H, W = model.image_size
+    mc = model.model_channels
+    te = model.time_embed
+    flops += 2 * (te[1].in_features * te[1].out_features + te[3].in_features * te[3].out_features)
+    nres = 0
+
+    def conv(cin, cout, h, w, k):
+        return 2.0 * cin * cout * h * w * k * k
+
+    flops += conv(model.in_channels, mc, H, W, 3)
+    h, w = H, W
+    chans = []
+
+    def res(rb, h, w):
+        f = conv(rb.in_channels, rb.out_channels, h, w, 3) + conv(rb.out_channels, rb.out_channels, h, w, 3)
+        if rb.in_channels != rb.out_channels:
+            f += conv(rb.in_channels, rb.out_channels, h, w, 1)
+        f += 2 * rb.time_mlp[1].in_features * rb.out_channels
+        return f
+
+    def attn(ab, C, h, w):
+        Lq = h * w
+        return conv(C, 3 * C, h, w, 1) + conv(C, C, h, w, 1) + 2 * 2.0 * Lq * Lq * C
+
+    for block in model.down_blocks:
+        for layer in block:
+            n = type(layer).__name__
+            if n == "ResidualBlock":
+                flops += res(layer, h, w)
+                nres += 1
+                C = layer.out_channels
+            elif n == "AttentionBlock":
+                flops += attn(layer, C, h, w)
+            elif n == "Downsample":
+                flops += conv(C, C, h // 2, w // 2, 3)
+                h, w = h // 2, w // 2
+        chans.append(C)
+    for layer in model.middle_block:
+        n = type(layer).__name__
+        if n == "ResidualBlock":
+            flops += res(layer, h, w)
+        elif n == "AttentionBlock":
+            flops += attn(layer, C, h, w)
+    for block in model.up_blocks:
+        for layer in block:
+            n = type(layer).__name__
+            if n == "ResidualBlock":
+                flops += res(layer, h, w)
+                C = layer.out_channels
+            elif n == "AttentionBlock":
+                flops += attn(layer, C, h, w)
+            elif n == "Upsample":
+                h, w = 2 * h, 2 * w
+                flops += conv(C, C, h, w, 3)
+    flops += conv(model.output[2].in_channels, model.out_channels, H, W, 3)
+    return flops

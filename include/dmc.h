@@ -1,0 +1,188 @@
+/*
+ * dmc.h — C ABI of libdmc.so, the MI355X (gfx950) kernels behind the diffusion hot path.
+ *
+ * The reference (sunyzhi55/Diffusion_Models_Collection) is pure Python over PyTorch and has no
+ * FFI layer of its own; every entry point below replaces a group of PyTorch eager
+ * ops that the reference calls at the cited file:line. The Python host side
+ * (diffusion_models_collection_amd/_lib.py) binds these with ctypes.
+ *
+ * Conventions
+ *   - All pointers are device pointers unless stated; `stream` is a hipStream_t (NULL = default).
+ *   - The library never allocates, never synchronises and keeps no mutable global state: callers
+ *     pass every output and workspace buffer. Calls are graph-capturable.
+ *   - Return 0 on success, nonzero on a bad descriptor or launch error; dmc_last_error() explains.
+ *   - Activations are NHWC (pixel rows, channel pitch `ld`); dtype is DMC_F32 (parity mode) or
+ *     DMC_BF16 (perf mode). Statistics, biases, gradients of weights and reductions are fp32.
+ */
+#ifndef DMC_H
+#define DMC_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { DMC_F32 = 0, DMC_BF16 = 1 };
+enum { DMC_MODE_NORMAL = 0, DMC_MODE_UPSAMPLE = 1, DMC_MODE_DILATE = 2 };
+enum { DMC_PRO_NONE = 0, DMC_PRO_AFFINE_SILU = 1, DMC_PRO_SILU = 2, DMC_PRO_AFFINE = 3 };
+enum { DMC_LOSS_L1 = 0, DMC_LOSS_L2 = 1, DMC_LOSS_HUBER = 2 };
+enum { DMC_PACK_FWD = 0, DMC_PACK_DGRAD = 1, DMC_PACK_UPDGRAD = 2 };
+
+int dmc_version(void);
+const char* dmc_last_error(void);
+
+/* Implicit-GEMM convolution descriptor. Replaces nn.Conv2d / nn.Linear forward and input-gradient
+ * of models/unet.py:34-60 (ResidualBlock), :81-82 (qkv/proj), :106 (Downsample), :116 (Upsample +
+ * F.interpolate nearest), :167-172 (time_embed Linears), :188 (input_conv), :237-241 (output), and
+ * the torch.cat skip concatenation of :284 (two sources = virtual concat).
+ * Input coordinate of output pixel (oy,ox) and tap t: (oy*stride + tap_dy[t], ox*stride + tap_dx[t]),
+ * then mode UPSAMPLE: valid in [0,2H) and >>1 (nearest x2); DILATE: valid iff even, /2 (the
+ * transposed stride-2 conv of a dgrad); NORMAL: valid in [0,H). Invalid taps read zero.
+ */
+typedef struct dmc_conv_desc {
+  int dtype;
+  int N, H, W;               /* source batch and spatial size */
+  int C1, C2, ld1, ld2;      /* channels [0,C1) from x1, [C1,C1+C2) from x2 (virtual concat) */
+  int Kc;                    /* packed K per tap: >= C1+C2, multiple of 32 (fp32) / 64 (bf16) */
+  int OH, OW, Cout;
+  int ntaps, mode, stride;
+  int tap_dy[16], tap_dx[16];
+  int prologue;              /* DMC_PRO_*: applied to the sources while staging (never to padding) */
+  const float* pro_scale;    /* [N][ld_pro] per-(n,c): a = x*scale + shift (GroupNorm folded) */
+  const float* pro_shift;
+  int ld_pro;
+  uint32_t drop_seed;        /* dropout after SiLU: keep iff hash(seed, pix*C + c) >= drop_thresh */
+  uint32_t drop_thresh;      /* 0 = no dropout */
+  float drop_scale;          /* 1/(1-p) */
+  int drop_ld;               /* channel count used in the dropout element index */
+  const float* bias;         /* [Cout] or NULL */
+  const float* addvec;       /* [N][ld_add] added per (n, co) (time/label embedding) or NULL */
+  int ld_add;
+  const void* resid;         /* residual [pix][ld_res] in the output dtype, or NULL */
+  int ld_res;
+  const float* silu_pre;     /* if set, result *= silu'(silu_pre[pix][ld_silu]) (fp32) */
+  int ld_silu;
+  int Csplit;                /* co < Csplit -> y1[pix*ldy1 + co], else y2[pix*ldy2 + co - Csplit] */
+  int ldy1, ldy2;
+  int out_f32;               /* output stored fp32 even in bf16 mode */
+  int out_nchw;              /* y1 is NCHW fp32 [N][Cout][OH][OW] */
+} dmc_conv_desc;
+
+/* y = conv(x) with fused prologue/epilogue. w = packed [Cout][ntaps][Kc] (dtype). */
+int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2, const void* w,
+               void* y1, void* y2, void* stream);
+
+/* Weight gradient of the same convolution: dw[co][c][t] (fp32, reference nn.Conv2d layout,
+ * multiplied by `scale`) = sum over pixels of dy[pix][co] * prologue(x)[coord(pix,t)][c].
+ * dy: [N*OH*OW][ld_dy] dtype. workspace: dmc_conv2d_wgrad_workspace() bytes. */
+size_t dmc_conv2d_wgrad_workspace(const dmc_conv_desc* d);
+int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_dy, const void* x1,
+                     const void* x2, void* workspace, float* dw, float scale, void* stream);
+
+/* Repack an fp32 nn.Conv2d / nn.Linear weight [Cout][Cin][kh][kw] into the kernel layout:
+ * FWD [Cout][t][Kc], DGRAD [Cin][t][Kc>=Cout], UPDGRAD [Cin][16][Kc] (nearest-x2 + 3x3 folded
+ * into a 4x4 stride-2 kernel). Padding is zero-filled. */
+int dmc_pack_weight(int pack_mode, int dtype, const float* w, int Cout, int Cin, int kh, int kw,
+                    int Kc, void* dst, void* stream);
+
+/* GroupNorm statistics (models/unet.py:35,51,80,238; eps 1e-5) over the virtual concat of x1/x2:
+ * mean_rstd [N][G][2]; scale/shift [N][C] = folded affine for the consumer's prologue.
+ * workspace: dmc_gn_workspace() bytes. */
+size_t dmc_gn_workspace(int N, int C, int G, int HW);
+int dmc_gn_stats(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1,
+                 int ld2, int G, float eps, const float* gamma, const float* beta, void* workspace,
+                 float* mean_rstd, float* scale, float* shift, void* stream);
+
+/* Backward of a = dropout(SiLU(GroupNorm(x))) (silu=1) or a = GroupNorm(x) (silu=0, AttentionBlock
+ * norm :80): g = dL/da (dtype, [pix][ld_g]); writes
+ * dx (split into dx1/dx2 by channel like the sources; accumulate_k: add into existing),
+ * dgamma/dbeta (fp32 [C], overwritten). */
+int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x1, const void* x2, int N,
+                    int HW, int C1, int C2, int ld1, int ld2, int G, const float* mean_rstd,
+                    const float* gamma, const float* beta, int silu, uint32_t drop_seed,
+                    uint32_t drop_thresh, float drop_scale, void* dx1, void* dx2, int ld_dx1,
+                    int ld_dx2, int accumulate1, int accumulate2, float* dgamma, float* dbeta,
+                    void* workspace, void* stream);
+
+/* Per-(n,c) pixel sums of dy [N][HW][ld] -> out_nc [N][ld_out] (may be NULL) and per-c
+ * sums over n -> out_c [C] (may be NULL); both fp32, scaled by `scale`. Bias / embedding grads. */
+size_t dmc_channel_sum_workspace(int N, int HW, int C);
+int dmc_channel_sum(int dtype, const void* dy, int N, int HW, int C, int ld, float* out_nc,
+                    int ld_out, float* out_c, float scale, void* workspace, void* stream);
+
+/* Self-attention of AttentionBlock (models/unet.py:84-99): qkv [N][L][ld_qkv] with channel
+ * which*C + head*hd + d (reshape(B,3,heads,hd,HW)), softmax(QK^T/sqrt(hd))V -> out [N][L][ld_out]
+ * channel head*hd + d; lse [N][heads][L] fp32 saved for backward. */
+int dmc_attn_fwd(int dtype, const void* qkv, int ld_qkv, int N, int L, int heads, int hd, void* out,
+                 int ld_out, float* lse, void* stream);
+/* dqkv [N][L][ld_dqkv] (overwritten). workspace: dmc_attn_workspace() bytes. */
+size_t dmc_attn_workspace(int N, int L, int heads);
+int dmc_attn_bwd(int dtype, const void* qkv, int ld_qkv, const void* out, const void* dout,
+                 int ld_out, const float* lse, int N, int L, int heads, int hd, void* dqkv,
+                 int ld_dqkv, void* workspace, void* stream);
+
+/* Sinusoidal TimeEmbedding (models/unet.py:18-25): out [B][dim] fp32 = [sin(t f_i) | cos(t f_i)]. */
+int dmc_time_embed(const int64_t* t, int B, int dim, float* out, void* stream);
+/* Label embedding gather with clamp(y, 0, num_classes) (models/unet.py:256-258) and its backward
+ * (padding_idx 0 receives no gradient; deterministic per-row sums). */
+int dmc_embed_fwd(const int64_t* y, int B, int num_rows, const float* table, int dim, float* out,
+                  void* stream);
+int dmc_embed_bwd(const int64_t* y, int B, int num_rows, const float* dout, int dim, float* dtable,
+                  void* stream);
+
+/* NCHW fp32 -> NHWC dtype with channel pitch ld (zero pad channels C..ld). If t != NULL, fuses
+ * DDPM.q_sample (diffusion/ddpm.py:84-104): x = a[t]*x + b[t]*noise. */
+int dmc_pack_input(int dtype, const float* x, const float* noise, const int64_t* t, const float* a,
+                   const float* b, int N, int C, int H, int W, void* dst, int ld, void* stream);
+/* q_sample alone, NCHW fp32 (diffusion/ddpm.py:84-104). */
+int dmc_q_sample(const float* x0, const float* noise, const int64_t* t, const float* a,
+                 const float* b, int N, int per_sample, float* out, void* stream);
+
+/* p_losses loss (diffusion/ddpm.py:130-139): loss = mean(f(noise - pred)); deterministic.
+ * workspace: >= 4096 floats. dmc_loss_bwd: dpred = dloss[0] * df/dpred / n. */
+int dmc_loss_fwd(int loss_type, const float* pred, const float* target, long n, float* loss,
+                 float* workspace, void* stream);
+int dmc_loss_bwd(int loss_type, const float* pred, const float* target, long n, const float* dloss,
+                 float* dpred, void* stream);
+
+/* DDIM.p_sample update (diffusion/ddim.py:154-208), fused; alpha gathers on device; if any
+ * t_next < 0 the reference uses alpha_next = 1 for the whole batch (:176-179), so does this.
+ * x0_in (optional) replaces the x0 prediction; z (optional) is the eta>0 noise. */
+int dmc_ddim_step(const float* x, const float* eps, const float* x0_in, const int64_t* t,
+                  const int64_t* t_next, const float* alphas_cumprod, int N, int per_sample,
+                  float eta, int clip, const float* z, float* out, void* stream);
+/* DDPM.p_sample (diffusion/ddpm.py:151-220), fused. */
+int dmc_ddpm_step(const float* x, const float* eps, const float* x0_in, const int64_t* t,
+                  const float* sqrt_recip_ac, const float* sqrt_recipm1_ac, const float* coef1,
+                  const float* coef2, const float* logvar, int N, int per_sample, int clip,
+                  const float* z, float* out, void* stream);
+/* CFG + x0 prediction + dynamic threshold (diffusion/ddim.py:300-325, ddpm.py:284-303):
+ * eps = eu + s*(ec - eu) -> eps_out; x0 = mode 0: (x - sqrt(1-a)eps)/sqrt(a) [DDIM]
+ * mode 1: sra*x - srm1*eps [DDPM]; threshold: p in (0,1): per-row quantile of |x0| (linear
+ * interpolation, as torch.quantile), s = max(s,1), x0 = clamp(x0,-s,s)/s; p <= 0: clamp +-1. */
+int dmc_cfg_x0(const float* x, const float* ec, const float* eu, float scale, const int64_t* t,
+               const float* tab_a, const float* tab_b, int mode, int N, int per_sample,
+               float p_threshold, float* eps_out, float* x0_out, void* stream);
+
+/* Multi-tensor ops over a device array of descriptors {dst, src, n} (utils/trainer.py:187-202
+ * EMA; :259 clip_grad_norm_). */
+typedef struct dmc_tensor_ref {
+  float* a;
+  const float* b;
+  long n;
+} dmc_tensor_ref;
+int dmc_ema_update(const dmc_tensor_ref* refs, int count, float decay, void* stream);
+/* total_norm (fp32 scalar) = ||(||g_i||)||; g *= min(1, max_norm/(total_norm+1e-6)).
+ */
+int dmc_clip_grad_norm(const dmc_tensor_ref* refs, int count, float max_norm, float* total_norm,
+                       float* workspace, void* stream);   /* workspace >= 16*count + 16 floats */
+/* y = silu(x) (fp32); NHWC dtype -> NCHW fp32 (the inverse of dmc_pack_input); y += x (dtype). */
+int dmc_silu_fwd(const float* x, float* y, long n, void* stream);
+int dmc_unpack_output(int dtype, const void* src, int ld, int N, int C, int H, int W, float* dst,
+                      void* stream);
+int dmc_add(int dtype, void* y, const void* x, long n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

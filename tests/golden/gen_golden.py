@@ -1,0 +1,238 @@
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE implementation.
+
+Run ONLY in the build container (where /root/reference exists):
+
+    python tests/golden/gen_golden.py
+
+It imports sunyzhi55/Diffusion_Models_Collection from /root/reference (read-only, never shipped),
+runs it on CPU in fp32 and writes small .npz fixtures: inputs and expected outputs only.
+The GPU box never runs this script; the tests only read the .npz files it wrote.
+
+Fixture list (every array is float32 / int64 data, loaded with numpy.load(allow_pickle=False)):
+  schedules.npz      DDPM/DDIM tables for linear/cosine/quadratic (diffusion/ddpm.py:38-71)
+                     and DDIM inference timesteps (diffusion/ddim.py:71-85)
+  unet_tiny_*.npz    tiny UNet (models/unet.py) weights, input, output, and the gradients of
+                     sum(out * cot) w.r.t. every parameter and x
+  diffusion_ops.npz  q_sample, p_losses (l1/l2/huber), DDPM p_sample (injected noise),
+                     DDIM p_sample / sample trajectory (injected x_T), CFG+dynamic-threshold step
+  trainer_traj.npz   5 DiffusionTrainer steps (dropout 0, injected t/noise), per-step loss,
+                     final parameters and EMA
+"""
+import os
+import sys
+import types
+from pathlib import Path
+
+import numpy as np
+import torch
+
+REF = Path("/root/reference")
+OUT = Path(__file__).resolve().parent
+
+# utils/trainer.py imports swanlab and torchvision.utils.save_image (both absent here; ordinary
+# ImportError). Stub them so the trainer module imports.
+sys.modules.setdefault("swanlab", types.ModuleType("swanlab"))
+if "torchvision" not in sys.modules:
+    tv = types.ModuleType("torchvision")
+    tvu = types.ModuleType("torchvision.utils")
+    tvu.save_image = lambda *a, **k: None
+    tv.utils = tvu
+    sys.modules["torchvision"] = tv
+    sys.modules["torchvision.utils"] = tvu
+sys.path.insert(0, str(REF))
+
+from models.unet import UNet  # noqa: E402  (reference)
+from diffusion.ddpm import DDPM  # noqa: E402
+from diffusion.ddim import DDIM  # noqa: E402
+
+torch.set_num_threads(8)
+torch.use_deterministic_algorithms(False)
+
+TINY_CFGS = {
+    # 16x16, 2 levels: covers 3x3/1x1/stride-2/upsample convs, concat with a GN group that
+    # straddles the two sources (96 = 64 + 32 channels, 12 per group), attention at 8x8.
+    "unet_tiny_uncond": dict(image_size=(16, 16), in_channels=3, model_channels=16, out_channels=3,
+                             num_res_blocks=1, attention_resolutions=(8,), dropout=0.0,
+                             channel_mult=(1, 2), num_classes=None, use_attention=True),
+    "unet_tiny_cond": dict(image_size=(16, 16), in_channels=3, model_channels=16, out_channels=3,
+                           num_res_blocks=1, attention_resolutions=(8,), dropout=0.0,
+                           channel_mult=(1, 2), num_classes=10, use_attention=True),
+    # 3 levels down to 4x4 (attention at 8x8 and at 4x4 in the middle), 1 input channel
+    "unet_tiny_l3": dict(image_size=(16, 16), in_channels=1, model_channels=16, out_channels=1,
+                         num_res_blocks=2, attention_resolutions=(8, 4), dropout=0.0,
+                         channel_mult=(1, 2, 2), num_classes=None, use_attention=True),
+}
+
+
+def npz(path, **arrs):
+    clean = {}
+    for k, v in arrs.items():
+        if isinstance(v, torch.Tensor):
+            v = v.detach().cpu().numpy()
+        clean[k] = np.ascontiguousarray(v)
+    np.savez_compressed(path, **clean)
+    print("wrote", path, sum(a.nbytes for a in clean.values()) / 1e6, "MB raw")
+
+
+def gen_schedules():
+    out = {}
+    for sched in ("linear", "cosine", "quadratic"):
+        d = DDPM(1000, 1e-4, 0.02, sched, device="cpu")
+        for name in ("betas", "alphas", "alphas_cumprod", "alphas_cumprod_prev", "sqrt_alphas_cumprod",
+                     "sqrt_one_minus_alphas_cumprod", "sqrt_recip_alphas", "sqrt_recipm1_alphas_cumprod",
+                     "posterior_variance", "posterior_log_variance_clipped", "posterior_mean_coef1",
+                     "posterior_mean_coef2"):
+            out[f"{sched}/{name}"] = getattr(d, name)
+    for T in (1000, 100):
+        for S in (10, 20, 50, 100, 250):
+            if S > T:
+                continue
+            d = DDIM(T, S, device="cpu")
+            out[f"ddim_ts/{T}/{S}"] = d.inference_timesteps
+    npz(OUT / "schedules.npz", **out)
+
+
+def gen_unet(name, cfg, B=2):
+    torch.manual_seed(1234)
+    m = UNet(**cfg).float()
+    m.train()  # dropout 0.0 -> deterministic
+    g = torch.Generator().manual_seed(7)
+    C, (H, W) = cfg["in_channels"], cfg["image_size"]
+    x = torch.randn(B, C, H, W, generator=g).requires_grad_(True)
+    t = torch.tensor([17, 903][:B], dtype=torch.long)
+    y = None
+    if cfg["num_classes"] is not None:
+        # label 0 = null class (CFG); 11 > num_classes exercises the clamp (models/unet.py:256-257)
+        y = torch.tensor([0, 11][:B], dtype=torch.long)
+    out = m(x, t, y)
+    cot = torch.randn(out.shape, generator=g)
+    (out * cot).sum().backward()
+    arrs = {"x": x.detach(), "t": t, "out": out.detach(), "cot": cot}
+    if y is not None:
+        arrs["y"] = y
+    for k, v in m.state_dict().items():
+        arrs["param/" + k] = v
+    for k, p in m.named_parameters():
+        if p.grad is not None:
+            arrs["grad/" + k] = p.grad
+    arrs["grad_x"] = x.grad
+    npz(OUT / f"{name}.npz", **arrs)
+
+
+def gen_diffusion_ops():
+    cfg = TINY_CFGS["unet_tiny_cond"]
+    torch.manual_seed(1234)
+    m = UNet(**cfg).float().eval()
+    g = torch.Generator().manual_seed(11)
+    B, C, H, W = 3, 3, 16, 16
+    x0 = torch.rand(B, C, H, W, generator=g) * 2 - 1
+    noise = torch.randn(B, C, H, W, generator=g)
+    t = torch.tensor([0, 499, 999])
+    y = torch.tensor([1, 5, 0])
+    ddpm = DDPM(1000, 1e-4, 0.02, "linear", device="cpu")
+    arrs = {"x0": x0, "noise": noise, "t": t, "y": y}
+    arrs["q_sample"] = ddpm.q_sample(x0, t, noise)
+    with torch.no_grad():
+        for lt in ("l1", "l2", "huber"):
+            arrs[f"p_losses/{lt}"] = ddpm.p_losses(m, x0, t, y, noise=noise, loss_type=lt).reshape(1)
+    # DDPM p_sample with injected noise: patch randn_like for this one call
+    xt = arrs["q_sample"]
+    z = torch.randn(B, C, H, W, generator=g)
+    arrs["ddpm_z"] = z
+    orig = torch.randn_like
+    torch.randn_like = lambda a, *k, **kw: z.clone()
+    try:
+        with torch.no_grad():
+            arrs["ddpm_p_sample"] = ddpm.p_sample(m, xt, t, y)
+    finally:
+        torch.randn_like = orig
+    # DDIM single step and a full 10-step trajectory from an injected x_T
+    ddim = DDIM(1000, 10, 1e-4, 0.02, "linear", eta=0.0, device="cpu")
+    t_next = torch.tensor([-1, 479, 979])
+    with torch.no_grad():
+        arrs["ddim_p_sample"] = ddim.p_sample(m, xt, t, torch.tensor([-1, -1, -1]), y)
+        # the reference takes the alpha_next branch only when every t_next >= 0
+        arrs["ddim_p_sample_next"] = ddim.p_sample(m, xt, torch.tensor([20, 499, 999]),
+                                                   torch.tensor([0, 479, 979]), y)
+    xT = torch.randn(B, C, H, W, generator=g)
+    arrs["ddim_xT"] = xT
+    orig_randn = torch.randn
+    torch.randn = lambda *a, **kw: xT.clone()
+    try:
+        with torch.no_grad():
+            arrs["ddim_sample"] = ddim.sample(m, (B, C, H, W), y)
+            arrs["ddim_sample_all"] = ddim.sample(m, (B, C, H, W), y, return_all_timesteps=True)
+            arrs["ddim_sample_cfg"] = ddim.sample_with_cfg(m, (B, C, H, W), y, cfg_scale=3.0)
+            arrs["ddim_sample_cfg_nothr"] = ddim.sample_with_cfg(m, (B, C, H, W), y, cfg_scale=2.0,
+                                                                 p_threshold=None)
+    finally:
+        torch.randn = orig_randn
+    # DDIM with eta > 0 (stochastic): inject both x_T and the per-step noise
+    ddim_eta = DDIM(1000, 5, 1e-4, 0.02, "linear", eta=0.5, device="cpu")
+    zs = torch.randn(5, B, C, H, W, generator=g)
+    arrs["ddim_eta_z"] = zs
+    it = iter(list(zs))
+    torch.randn = lambda *a, **kw: xT.clone()
+    torch.randn_like = lambda a, *k, **kw: next(it).clone()
+    try:
+        with torch.no_grad():
+            arrs["ddim_eta_sample"] = ddim_eta.sample(m, (B, C, H, W), y)
+    finally:
+        torch.randn = orig_randn
+        torch.randn_like = orig
+    npz(OUT / "diffusion_ops.npz", **arrs)
+    del t_next
+
+
+def gen_trainer_traj():
+    from utils import trainer as trainer_mod  # reference utils/trainer.py
+    cfg = dict(TINY_CFGS["unet_tiny_uncond"])
+    torch.manual_seed(1234)
+    m = UNet(**cfg).float()
+    init = {k: v.clone() for k, v in m.state_dict().items()}
+    g = torch.Generator().manual_seed(21)
+    steps, B = 5, 4
+    images = [torch.rand(B, 3, 16, 16, generator=g) * 2 - 1 for _ in range(steps)]
+    ts = [torch.randint(0, 1000, (B,), generator=g) for _ in range(steps)]
+    noises = [torch.randn(B, 3, 16, 16, generator=g) for _ in range(steps)]
+    ddpm = DDPM(1000, 1e-4, 0.02, "linear", device="cpu")
+    opt = torch.optim.AdamW(m.parameters(), lr=2e-4, weight_decay=1e-4)
+    config = {"epochs": 1, "save_dir": "/tmp/gg_ckpt", "sample_dir": "/tmp/gg_smp", "loss_type": "l2",
+              "use_ema": True, "ema_decay": 0.9, "model_type": "unet",
+              "model_params": {k: v for k, v in cfg.items() if k != "num_classes"}}
+    tr = trainer_mod.DiffusionTrainer(m, ddpm, images, opt, None, device="cpu", config=config)
+    # inject t and noise in order
+    t_it, n_it = iter(ts), iter(noises)
+    orig_randint, orig_randn_like = torch.randint, torch.randn_like
+    losses = []
+    orig_pl = ddpm.p_losses
+
+    def p_losses(model, x, t, y=None, noise=None, loss_type="l2"):
+        loss = orig_pl(model, x, t, y, noise=noise, loss_type=loss_type)
+        losses.append(loss.item())
+        return loss
+
+    ddpm.p_losses = p_losses
+    torch.randint = lambda *a, **kw: next(t_it)
+    torch.randn_like = lambda a, *k, **kw: next(n_it).clone()
+    try:
+        tr.train_epoch(1)
+    finally:
+        torch.randint, torch.randn_like = orig_randint, orig_randn_like
+    arrs = {"images": torch.stack(images), "ts": torch.stack(ts), "noises": torch.stack(noises),
+            "losses": torch.tensor(losses)}
+    for k, v in init.items():
+        arrs["init/" + k] = v
+    for k, v in m.state_dict().items():
+        arrs["final/" + k] = v
+    for k, v in tr.ema_model.state_dict().items():
+        arrs["ema/" + k] = v
+    npz(OUT / "trainer_traj.npz", **arrs)
+
+
+if __name__ == "__main__":
+    gen_schedules()
+    for n, c in TINY_CFGS.items():
+        gen_unet(n, c)
+    gen_diffusion_ops()
+    gen_trainer_traj()

@@ -1,0 +1,139 @@
+"""CPU tests: the C-ABI library loads and exports every declared symbol; host-side API parity with the
+reference (constructors, tables, timesteps, state_dict layout, error behaviour). No GPU compute here."""
+import re
+from pathlib import Path
+
+import pytest
+import torch
+
+from conftest import ROOT, load_golden
+
+
+def _ensure_lib():
+    lib = ROOT / "diffusion_models_collection_amd" / "libdmc.so"
+    if not lib.exists():
+        from diffusion_models_collection_amd.build import build
+        build()
+    return lib
+
+
+def test_library_exports_header_symbols():
+    _ensure_lib()
+    import ctypes
+    hdr = (ROOT / "include" / "dmc.h").read_text()
+    names = sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(dmc_\w+)\s*\(", hdr, re.M)))
+    assert len(names) >= 29, names
+    lib = ctypes.CDLL(str(ROOT / "diffusion_models_collection_amd" / "libdmc.so"))
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    from diffusion_models_collection_amd import _lib
+    assert set(names) == set(_lib.EXPORTS), set(names) ^ set(_lib.EXPORTS)
+    assert _lib.LIB.dmc_version() == 1
+
+
+def test_descriptor_validation_errors():
+    """Bad descriptors are rejected on the host with a message (no launch happens)."""
+    _ensure_lib()
+    from diffusion_models_collection_amd import kernels as K, _lib as L
+    d = K.make_desc(torch.float32, 1, 4, 4, 6, 0, 8, 0, 32, 4, 4, 8, K.TAPS3)   # C1=6 not multiple of 4
+    K.set_prologue(d, L.PRO_AFFINE_SILU)
+    with pytest.raises(L.DMCError, match="multiples"):
+        L.check(L.LIB.dmc_conv2d(__import__("ctypes").byref(d), None, None, None, None, None, None), "conv")
+    with pytest.raises(L.DMCError, match="head dim"):
+        L.check(L.LIB.dmc_attn_fwd(0, None, 768, 1, 16, 4, 100, None, 256, None, None), "attn")
+
+
+def test_schedule_tables_bit_exact_cpu():
+    from diffusion_models_collection_amd.diffusion import DDPM, DDIM
+    g = load_golden("schedules")
+    for kind in ("linear", "cosine", "quadratic"):
+        d = DDPM(1000, 1e-4, 0.02, kind, device="cpu")
+        for name in ("betas", "alphas_cumprod", "alphas_cumprod_prev", "sqrt_alphas_cumprod",
+                     "sqrt_one_minus_alphas_cumprod", "sqrt_recip_alphas", "sqrt_recipm1_alphas_cumprod",
+                     "posterior_variance", "posterior_log_variance_clipped", "posterior_mean_coef1",
+                     "posterior_mean_coef2"):
+            assert torch.equal(getattr(d, name), g[f"{kind}/{name}"]), (kind, name)
+        dd = DDIM(1000, 50, 1e-4, 0.02, kind, device="cpu")
+        assert torch.equal(dd.alphas_cumprod, g[f"{kind}/alphas_cumprod"])
+    for k, v in g.items():
+        if k.startswith("ddim_ts/"):
+            _, T, S = k.split("/")
+            dd = DDIM(int(T), int(S), device="cpu")
+            assert torch.equal(dd.inference_timesteps, v), k
+    dd = DDIM(1000, 10, device="cpu")
+    dd.set_inference_steps(50)
+    assert dd.inference_timesteps[:3].tolist() == [999, 979, 958]
+
+
+def test_errors_match_reference():
+    from diffusion_models_collection_amd.diffusion import DDPM, DDIM
+    with pytest.raises(ValueError, match="Unknown beta schedule"):
+        DDPM(beta_schedule="sigmoid", device="cpu")
+    with pytest.raises(ValueError, match="Unknown beta schedule"):
+        DDIM(beta_schedule="sigmoid", device="cpu")
+    d = DDIM(device="cpu")
+    with pytest.raises(ValueError, match="requires class labels"):
+        d.sample_with_cfg(None, (1, 3, 8, 8), None)
+    with pytest.raises(ValueError, match="p_threshold"):
+        d.sample_with_cfg(None, (1, 3, 8, 8), torch.zeros(1, dtype=torch.long), p_threshold=1.5)
+    from diffusion_models_collection_amd.diffusion.ddpm import diffusion_loss
+    with pytest.raises(ValueError, match="Unknown loss type"):
+        diffusion_loss(torch.zeros(1), torch.zeros(1), "l3")
+
+
+@pytest.mark.parametrize("name", ["unet_tiny_uncond", "unet_tiny_cond", "unet_tiny_l3"])
+def test_state_dict_layout_matches_reference(name):
+    from test_oracle import TINY
+    from diffusion_models_collection_amd.models import UNet
+    g = load_golden(name)
+    ref = {k[len("param/"):]: v for k, v in g.items() if k.startswith("param/")}
+    torch.manual_seed(1234)   # same seed the fixture generator used -> identical initialisation
+    m = UNet(**TINY[name])
+    sd = m.state_dict()
+    assert list(sd) == list(ref)
+    for k in sd:
+        assert sd[k].shape == ref[k].shape, k
+        assert torch.equal(sd[k], ref[k]), k
+    m.load_state_dict(ref)
+
+
+def test_cifar_unet_param_count_and_flops():
+    from diffusion_models_collection_amd.models import UNet
+    from diffusion_models_collection_amd.models.unet import unet_flops_per_image
+    m = UNet()
+    assert sum(p.numel() for p in m.parameters()) == 37064707
+    assert len(m.state_dict()) == 334
+    assert abs(unet_flops_per_image(m) / 1e9 - 12.632) < 0.01
+
+
+def test_forward_refuses_cpu_tensors():
+    from diffusion_models_collection_amd.models import UNet
+    m = UNet(image_size=(8, 8), model_channels=16, channel_mult=(1,), attention_resolutions=())
+    with pytest.raises(RuntimeError, match="MI355X"):
+        m(torch.zeros(1, 3, 8, 8), torch.zeros(1, dtype=torch.long))
+    with pytest.raises(RuntimeError, match="executed by the UNet HIP executor"):
+        m.input_conv.weight.sum() and m.down_blocks[0][0](torch.zeros(1))
+
+
+def test_dropin_registry_imports():
+    import importlib
+    import sys
+    sys.path.insert(0, str(ROOT / "dropin"))
+    try:
+        for mod in ("models", "diffusion", "utils", "utils.trainer", "utils.helpers"):
+            sys.modules.pop(mod, None)
+        models = importlib.import_module("models")
+        diffusion = importlib.import_module("diffusion")
+        trainer = importlib.import_module("utils.trainer")
+        helpers = importlib.import_module("utils.helpers")
+        assert models.UNet.__module__.startswith("diffusion_models_collection_amd")
+        assert hasattr(models, "DiT") and hasattr(models, "DiM")
+        assert diffusion.DDPM.__module__.startswith("diffusion_models_collection_amd")
+        assert trainer.DiffusionTrainer.__module__.startswith("diffusion_models_collection_amd")
+        assert helpers.resolve_image_size(32) == (32, 32)
+        with pytest.raises(NotImplementedError):
+            models.DiT()
+    finally:
+        sys.path.remove(str(ROOT / "dropin"))
+        for mod in ("models", "diffusion", "utils", "utils.trainer", "utils.helpers"):
+            sys.modules.pop(mod, None)

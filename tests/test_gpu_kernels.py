@@ -1,0 +1,265 @@
+"""GPU numerics of each HIP kernel against a plain PyTorch fp32 CPU reference of the same op.
+
+fp32 mode: the f32-input MFMA path is exact-f32 fma chains; tolerances are summation-order level.
+bf16 mode: inputs are rounded to bf16 first, so the reference sees the same operands; tolerance covers
+bf16 rounding of the output (rel ~4e-3) and of the prologue output (re-rounded to bf16 before the MFMA).
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _lib():
+    from diffusion_models_collection_amd import _lib as L, kernels as K
+    return L, K
+
+
+def nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2).contiguous()
+
+
+def tol(dt):
+    return dict(rtol=1e-4, atol=1e-4) if dt == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+
+
+def rel_err(a, b):
+    return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-12)).item()
+
+
+def q(x, dt):
+    """round to the storage dtype and back to fp32 (what the kernel actually sees)"""
+    return x.to(dt).float()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", ["s1_concat_gn", "s2", "up", "1x1", "ragged_in"])
+def test_conv_forward(dt, case):
+    L, K = _lib()
+    torch.manual_seed(0)
+    N, H, W = 2, 8, 8
+    C1, C2, Cout = 32, 16, 48
+    taps, mode, stride, k, OH, OW = K.TAPS3, L.MODE_NORMAL, 1, 3, H, W
+    if case == "s2":
+        C2, stride, OH, OW = 0, 2, 4, 4
+    elif case == "up":
+        C2, mode, OH, OW = 0, L.MODE_UPSAMPLE, 16, 16
+    elif case == "1x1":
+        taps, k = K.TAPS1, 1
+    elif case == "ragged_in":
+        C1, C2 = 3, 0
+    ld1 = C1 if case != "ragged_in" else L.chunk_for(dt)
+    x1 = torch.randn(N, C1, H, W)
+    x2 = torch.randn(N, C2, H, W) if C2 else None
+    w = torch.randn(Cout, C1 + C2, k, k) / math.sqrt((C1 + C2) * k * k)
+    bias = torch.randn(Cout)
+    addv = torch.randn(N, Cout)
+    use_gn = case == "s1_concat_gn"
+    sc = torch.rand(N, C1 + C2) + 0.5
+    sh = torch.randn(N, C1 + C2) * 0.1
+    # reference (fp32 CPU) on dtype-rounded inputs
+    xr = q(x1, dt) if x2 is None else torch.cat([q(x1, dt), q(x2, dt)], 1)
+    if use_gn:
+        xr = q(F.silu(xr * sc[:, :, None, None] + sh[:, :, None, None]), dt)
+    if mode == L.MODE_UPSAMPLE:
+        xr = F.interpolate(xr, scale_factor=2, mode="nearest")
+    yr = F.conv2d(xr, q(w, dt), bias, stride=stride, padding=k // 2)
+    yr = yr + addv[:, :, None, None]
+    resid = torch.randn(N, Cout, OH, OW)
+    yr = yr + q(resid, dt)
+    # kernel
+    x1d = torch.zeros(N, H, W, ld1, dtype=dt, device=DEV)
+    x1d[..., :C1] = nhwc(x1).to(dt).to(DEV)
+    x2d = nhwc(x2).to(dt).to(DEV) if x2 is not None else None
+    Kc = L.kc_for(C1 + C2, dt)
+    wp = K.pack_weight(L.PACK_FWD, dt, w.to(DEV), Kc)
+    d = K.make_desc(dt, N, H, W, C1, C2, ld1, C2, Kc, OH, OW, Cout, taps, mode, stride)
+    if use_gn:
+        K.set_prologue(d, L.PRO_AFFINE_SILU, sc.to(DEV), sh.to(DEV), C1 + C2)
+    y = torch.empty(N, OH, OW, Cout, dtype=dt, device=DEV)
+    rd = nhwc(resid).to(dt).to(DEV)
+    K.set_epilogue(d, bias=bias.to(DEV), addvec=addv.to(DEV), ld_add=Cout, resid=rd, ld_res=Cout, ldy1=Cout)
+    K.conv(d, x1d, x2d, wp, y)
+    torch.cuda.synchronize()
+    got = nchw(y.float().cpu())
+    assert rel_err(got, yr) < (1e-5 if dt == torch.float32 else 2e-2), rel_err(got, yr)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", ["s1", "s2", "up", "1x1_concat_split"])
+def test_conv_dgrad_wgrad(dt, case):
+    """input- and weight-gradient kernels vs autograd of F.conv2d (fp32 CPU)."""
+    L, K = _lib()
+    torch.manual_seed(1)
+    N, H, W, Cin, Cout = 2, 8, 8, 32, 48
+    k, stride, OH, OW, mode = 3, 1, H, W, L.MODE_NORMAL
+    if case == "s2":
+        stride, OH, OW = 2, 4, 4
+    elif case == "up":
+        OH, OW, mode = 16, 16, L.MODE_UPSAMPLE
+    elif case.startswith("1x1"):
+        k = 1
+    x = q(torch.randn(N, Cin, H, W), dt).requires_grad_(True)
+    w = q(torch.randn(Cout, Cin, k, k) / math.sqrt(Cin * k * k), dt).requires_grad_(True)
+    xi = F.interpolate(x, scale_factor=2, mode="nearest") if mode == L.MODE_UPSAMPLE else x
+    y = F.conv2d(xi, w, stride=stride, padding=k // 2)
+    g = q(torch.randn_like(y), dt)
+    y.backward(g)
+    gd = nhwc(g).to(dt).to(DEV)
+    xd = nhwc(x.detach()).to(dt).to(DEV)
+    # dgrad
+    dx = torch.zeros(N, H, W, Cin, dtype=dt, device=DEV)
+    src = K.Act if hasattr(K, "Act") else None
+    if case == "s1" or case.startswith("1x1"):
+        pm, taps, dmode, dstride = L.PACK_DGRAD, (K.TAPS3_DGRAD if k == 3 else K.TAPS1), L.MODE_NORMAL, 1
+    elif case == "s2":
+        pm, taps, dmode, dstride = L.PACK_DGRAD, K.TAPS3_DGRAD, L.MODE_DILATE, 1
+    else:
+        pm, taps, dmode, dstride = L.PACK_UPDGRAD, K.TAPS_UPDGRAD, L.MODE_NORMAL, 2
+    Kc = L.kc_for(Cout, dt)
+    wp = K.pack_weight(pm, dt, w.detach().to(DEV), Kc)
+    d = K.make_desc(dt, N, OH, OW, Cout, 0, Cout, 0, Kc, H, W, Cin, taps, dmode, dstride)
+    if case == "1x1_concat_split":
+        d1 = torch.empty(N, H, W, 24, dtype=dt, device=DEV)
+        d2 = torch.empty(N, H, W, 8, dtype=dt, device=DEV)
+        K.set_epilogue(d, ldy1=24, ldy2=8, Csplit=24)
+        K.conv(d, gd, None, wp, d1, d2)
+        dx = torch.cat([d1, d2], -1)
+    else:
+        K.set_epilogue(d, ldy1=Cin)
+        K.conv(d, gd, None, wp, dx)
+    # wgrad
+    dw = torch.empty_like(w, device=DEV)
+    dw_desc = K.make_desc(dt, N, H, W, Cin, 0, Cin, 0, L.kc_for(Cin, dt), OH, OW, Cout,
+                          K.TAPS3 if k == 3 else K.TAPS1, mode, stride)
+    K.wgrad(dw_desc, gd, Cout, xd, None, dw)
+    torch.cuda.synchronize()
+    e1 = rel_err(nchw(dx.float().cpu()), x.grad)
+    e2 = rel_err(dw.cpu(), w.grad)
+    lim = 1e-5 if dt == torch.float32 else 2e-2
+    assert e1 < lim and e2 < (1e-5 if dt == torch.float32 else 1e-2), (e1, e2)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_groupnorm_stats_and_backward(dt):
+    L, K = _lib()
+    torch.manual_seed(2)
+    N, H, W, C1, C2, G = 3, 8, 8, 48, 48, 8    # group 3 straddles the two sources (12 ch/group)
+    x = q(torch.randn(N, C1 + C2, H, W) * 2 + 0.5, dt).requires_grad_(True)
+    gamma = torch.rand(C1 + C2).requires_grad_(True)
+    beta = torch.randn(C1 + C2).requires_grad_(True)
+    z = F.group_norm(x, G, gamma, beta, 1e-5)
+    a = F.silu(z)
+    gout = q(torch.randn_like(a), dt)
+    a.backward(gout)
+    xd = nhwc(x.detach()).to(dt).to(DEV)
+    x1, x2 = xd[..., :C1].contiguous(), xd[..., C1:].contiguous()
+    sc, sh, mr = K.gn_stats(dt, x1, x2, N, H * W, C1, C2, C1, C2, G, 1e-5, gamma.detach().to(DEV),
+                            beta.detach().to(DEV))
+    torch.cuda.synchronize()
+    zr = z.detach()
+    mean = x.detach().view(N, G, -1).mean(-1)
+    torch.testing.assert_close(mr.view(N, G, 2)[..., 0].cpu(), mean, rtol=1e-5, atol=1e-5)
+    zk = xd.float().cpu().permute(0, 3, 1, 2) * sc.view(N, -1, 1, 1).cpu() + sh.view(N, -1, 1, 1).cpu()
+    torch.testing.assert_close(zk, zr, rtol=1e-4, atol=1e-4)
+    dx1 = torch.empty_like(x1)
+    dx2 = torch.empty_like(x2)
+    dg = torch.empty(C1 + C2, device=DEV)
+    db = torch.empty(C1 + C2, device=DEV)
+    K.gn_bwd(dt, nhwc(gout).to(dt).to(DEV), C1 + C2, x1, x2, N, H * W, C1, C2, C1, C2, G, mr, gamma.detach().to(DEV),
+             beta.detach().to(DEV), True, None, dx1, dx2, C1, C2, 0, 0, dg, db)
+    torch.cuda.synchronize()
+    dxk = nchw(torch.cat([dx1, dx2], -1).float().cpu())
+    assert rel_err(dxk, x.grad) < (1e-4 if dt == torch.float32 else 2e-2)
+    assert rel_err(dg.cpu(), gamma.grad) < 1e-4 and rel_err(db.cpu(), beta.grad) < 1e-4
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Lq,hd", [(16, 64), (64, 64), (256, 64), (1024, 64), (64, 8), (100, 16)])
+def test_attention_fwd_bwd(dt, Lq, hd):
+    L, K = _lib()
+    torch.manual_seed(3)
+    N, heads = 2, 4
+    C = heads * hd
+    qkv = q(torch.randn(N, Lq, 3 * C), dt).requires_grad_(True)
+    # reference: models/unet.py:88-96 channel layout
+    t = qkv.view(N, Lq, 3, heads, hd).permute(2, 0, 3, 1, 4)
+    qq, kk, vv = t[0], t[1], t[2]
+    p = torch.softmax(qq @ kk.transpose(-2, -1) / math.sqrt(hd), -1)
+    o = (p @ vv).permute(0, 2, 1, 3).reshape(N, Lq, C)
+    do = q(torch.randn_like(o), dt)
+    o.backward(do)
+    qd = qkv.detach().to(dt).to(DEV).contiguous()
+    od = torch.empty(N, Lq, C, dtype=dt, device=DEV)
+    lse = torch.empty(N * heads * Lq, device=DEV)
+    K.attn_fwd(dt, qd, 3 * C, N, Lq, heads, hd, od, C, lse)
+    dq = torch.empty_like(qd)
+    K.attn_bwd(dt, qd, 3 * C, od, do.to(dt).to(DEV), C, lse, N, Lq, heads, hd, dq, 3 * C)
+    torch.cuda.synchronize()
+    lim = 1e-4 if dt == torch.float32 else 3e-2
+    assert rel_err(od.float().cpu(), o.detach()) < lim
+    assert rel_err(dq.float().cpu(), qkv.grad) < (2e-4 if dt == torch.float32 else 5e-2)
+
+
+def test_elementwise_and_multitensor():
+    L, K = _lib()
+    torch.manual_seed(4)
+    # loss fwd/bwd
+    pred = torch.randn(4, 3, 8, 8, device=DEV)
+    tgt = torch.randn(4, 3, 8, 8, device=DEV)
+    for lt, fn in (("l2", F.mse_loss), ("l1", F.l1_loss), ("huber", F.smooth_l1_loss)):
+        pc = pred.cpu().requires_grad_(True)
+        ref = fn(tgt.cpu(), pc)
+        ref.backward()
+        got = K.loss_fwd(lt, pred, tgt)
+        g = K.loss_bwd(lt, pred, tgt, torch.ones((), device=DEV))
+        torch.testing.assert_close(got.cpu(), ref.detach(), rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(g.cpu(), pc.grad, rtol=1e-5, atol=1e-7)
+    # EMA + clip
+    ps = [torch.randn(n, device=DEV) for n in (10, 1000, 33333)]
+    es = [torch.randn_like(p) for p in ps]
+    es_ref = [e.clone().cpu() for e in es]
+    refs = K.TensorRefs(list(zip(es, ps)), DEV)
+    K.ema_update(refs, 0.999)
+    for e, p, r in zip(es, ps, es_ref):
+        r.mul_(0.999).add_(p.cpu(), alpha=1 - 0.999)
+        torch.testing.assert_close(e.cpu(), r, rtol=1e-6, atol=1e-7)
+    gs = [torch.randn(n, device=DEV) for n in (10, 1000, 33333)]
+    gref = [g.cpu().clone().requires_grad_(False) for g in gs]
+    tot = K.clip_grad_norm(K.TensorRefs([(g, None) for g in gs], DEV), 1.0)
+    params = [torch.zeros_like(g, requires_grad=True) for g in gref]
+    for p, g in zip(params, gref):
+        p.grad = g
+    tr = torch.nn.utils.clip_grad_norm_(params, 1.0)
+    torch.testing.assert_close(tot.cpu(), tr, rtol=1e-5, atol=1e-6)
+    for g, p in zip(gs, params):
+        torch.testing.assert_close(g.cpu(), p.grad, rtol=1e-5, atol=1e-7)
+
+
+def test_quantile_threshold_matches_torch():
+    L, K = _lib()
+    torch.manual_seed(5)
+    N = 5
+    x = torch.randn(N, 3, 32, 32, device=DEV) * 2
+    ec = torch.randn_like(x)
+    eu = torch.randn_like(x)
+    t = torch.tensor([999, 500, 10, 0, 250], device=DEV)
+    ac = torch.cumprod(1 - torch.linspace(1e-4, 0.02, 1000), 0).to(DEV)
+    eps, x0 = K.cfg_x0(x, ec, eu, 3.0, t, ac, None, 0, 0.995)
+    e_ref = eu.cpu() + 3.0 * (ec.cpu() - eu.cpu())
+    at = ac.cpu()[t.cpu()].view(N, 1, 1, 1)
+    x0r = (x.cpu() - torch.sqrt(1 - at) * e_ref) / torch.sqrt(at)
+    s = torch.quantile(x0r.reshape(N, -1).abs(), 0.995, dim=1)
+    s = torch.maximum(s, torch.ones_like(s)).view(N, 1, 1, 1)
+    x0r = torch.clamp(x0r, -s, s) / s
+    torch.testing.assert_close(eps.cpu(), e_ref, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(x0.cpu(), x0r, rtol=1e-5, atol=1e-5)

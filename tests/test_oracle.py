@@ -1,0 +1,122 @@
+"""Pin the CPU oracle (oracle/) against the golden fixtures produced by the reference (tests/golden/)."""
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle import diffusion_oracle as DO
+from oracle.unet_oracle import make_oracle
+
+TINY = {
+    "unet_tiny_uncond": dict(image_size=(16, 16), in_channels=3, model_channels=16, out_channels=3,
+                             num_res_blocks=1, attention_resolutions=(8,), dropout=0.0, channel_mult=(1, 2),
+                             num_classes=None, use_attention=True),
+    "unet_tiny_cond": dict(image_size=(16, 16), in_channels=3, model_channels=16, out_channels=3,
+                           num_res_blocks=1, attention_resolutions=(8,), dropout=0.0, channel_mult=(1, 2),
+                           num_classes=10, use_attention=True),
+    "unet_tiny_l3": dict(image_size=(16, 16), in_channels=1, model_channels=16, out_channels=1,
+                         num_res_blocks=2, attention_resolutions=(8, 4), dropout=0.0, channel_mult=(1, 2, 2),
+                         num_classes=None, use_attention=True),
+}
+
+
+def split_params(g, prefix):
+    return {k[len(prefix):]: v for k, v in g.items() if k.startswith(prefix)}
+
+
+def test_schedules_bit_exact():
+    g = load_golden("schedules")
+    for kind in ("linear", "cosine", "quadratic"):
+        tab = DO.schedule(1000, 1e-4, 0.02, kind)
+        for name, v in tab.items():
+            assert torch.equal(v, g[f"{kind}/{name}"]), (kind, name)
+
+
+def test_ddim_timesteps_bit_exact():
+    g = load_golden("schedules")
+    for k, v in g.items():
+        if k.startswith("ddim_ts/"):
+            _, T, S = k.split("/")
+            assert torch.equal(DO.ddim_timesteps(int(T), int(S)), v), k
+    assert DO.ddim_timesteps(1000, 50)[:4].tolist() == [999, 979, 958, 938]
+
+
+@pytest.mark.parametrize("name", list(TINY))
+def test_oracle_unet_fwd_bwd(name):
+    g = load_golden(name)
+    params = split_params(g, "param/")
+    orc, sd = make_oracle(params, TINY[name], requires_grad=True)
+    x = g["x"].clone().requires_grad_(True)
+    out = orc.forward(x, g["t"], g.get("y"))
+    torch.testing.assert_close(out, g["out"], rtol=1e-5, atol=1e-5)
+    (out * g["cot"]).sum().backward()
+    torch.testing.assert_close(x.grad, g["grad_x"], rtol=1e-4, atol=1e-5)
+    grads = split_params(g, "grad/")
+    for k, ref in grads.items():
+        torch.testing.assert_close(sd[k].grad, ref, rtol=1e-4, atol=1e-5, msg=k)
+
+
+def test_oracle_diffusion_ops():
+    g = load_golden("diffusion_ops")
+    params = split_params(load_golden("unet_tiny_cond"), "param/")
+    orc, _ = make_oracle(params, TINY["unet_tiny_cond"])
+    tab = DO.schedule()
+    f = lambda x, t, y: orc.forward(x, t, y)  # noqa: E731
+    x0, noise, t, y = g["x0"], g["noise"], g["t"], g["y"]
+    xt = DO.q_sample(tab, x0, t, noise)
+    assert torch.equal(xt, g["q_sample"])
+    with torch.no_grad():
+        pred = f(xt, t, y)
+        for lt in ("l1", "l2", "huber"):
+            torch.testing.assert_close(DO.loss(lt, noise, pred).reshape(1), g[f"p_losses/{lt}"], rtol=1e-5,
+                                       atol=1e-6)
+        torch.testing.assert_close(DO.ddpm_step(tab, xt, pred, t, g["ddpm_z"]), g["ddpm_p_sample"], rtol=1e-5,
+                                   atol=1e-5)
+        ac = tab["alphas_cumprod"]
+        torch.testing.assert_close(DO.ddim_step(ac, xt, pred, t, torch.tensor([-1, -1, -1])), g["ddim_p_sample"],
+                                   rtol=1e-5, atol=1e-5)
+        t2, tn2 = torch.tensor([20, 499, 999]), torch.tensor([0, 479, 979])
+        torch.testing.assert_close(DO.ddim_step(ac, xt, f(xt, t2, y), t2, tn2), g["ddim_p_sample_next"], rtol=1e-5,
+                                   atol=1e-5)
+        ts = DO.ddim_timesteps(1000, 10)
+        torch.testing.assert_close(DO.ddim_sample(f, ac, ts, g["ddim_xT"], y), g["ddim_sample"], rtol=1e-4,
+                                   atol=1e-4)
+        torch.testing.assert_close(DO.ddim_sample(f, ac, ts, g["ddim_xT"], y, cfg_scale=3.0), g["ddim_sample_cfg"],
+                                   rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(DO.ddim_sample(f, ac, ts, g["ddim_xT"], y, cfg_scale=2.0, p_threshold=None),
+                                   g["ddim_sample_cfg_nothr"], rtol=1e-4, atol=1e-4)
+        ts5 = DO.ddim_timesteps(1000, 5)
+        torch.testing.assert_close(DO.ddim_sample(f, ac, ts5, g["ddim_xT"], y, eta=0.5, zs=g["ddim_eta_z"]),
+                                   g["ddim_eta_sample"], rtol=1e-4, atol=1e-4)
+
+
+def train_oracle(g, cfg, steps, ema_decay=0.9):
+    """utils/trainer.py:221-265 step order on the oracle UNet."""
+    init = split_params(g, "init/")
+    orc, sd = make_oracle(init, cfg, requires_grad=True)
+    params = list(sd.values())
+    opt = torch.optim.AdamW(params, lr=2e-4, weight_decay=1e-4)
+    ema = {k: v.detach().clone() for k, v in sd.items()}
+    tab = DO.schedule()
+    losses = []
+    for i in range(steps):
+        x0, t, noise = g["images"][i], g["ts"][i], g["noises"][i]
+        xt = DO.q_sample(tab, x0, t, noise)
+        loss = DO.loss("l2", noise, orc.forward(xt, t, None, training=True))
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params, 1.0)
+        opt.step()
+        opt.zero_grad()
+        DO.ema_update(ema, {k: v.detach() for k, v in sd.items()}, ema_decay)
+        losses.append(loss.item())
+    return losses, sd, ema
+
+
+def test_oracle_trainer_trajectory():
+    g = load_golden("trainer_traj")
+    cfg = dict(TINY["unet_tiny_uncond"])
+    losses, sd, ema = train_oracle(g, cfg, g["losses"].numel())
+    torch.testing.assert_close(torch.tensor(losses), g["losses"].float(), rtol=1e-5, atol=1e-6)
+    for k, v in split_params(g, "final/").items():
+        torch.testing.assert_close(sd[k].detach(), v, rtol=1e-4, atol=1e-6, msg=k)
+    for k, v in split_params(g, "ema/").items():
+        torch.testing.assert_close(ema[k], v, rtol=1e-4, atol=1e-6, msg=k)
