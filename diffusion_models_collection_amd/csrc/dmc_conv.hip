@@ -489,7 +489,8 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
   DMC_REQUIRE(d->Kc % bk == 0 && d->Kc >= d->C1 + d->C2, "conv: Kc %d must be a multiple of %d and >= C1+C2", d->Kc, bk);
   DMC_REQUIRE(d->ntaps >= 1 && d->ntaps <= 16, "conv: ntaps %d", d->ntaps);
   DMC_REQUIRE(d->ld1 % epc == 0 && (d->C2 == 0 || d->ld2 % epc == 0), "conv: source pitch alignment");
-  DMC_REQUIRE(d->Csplit >= 0 && d->Csplit <= d->Cout && d->Csplit % 4 == 0, "conv: Csplit %d", d->Csplit);
+  DMC_REQUIRE(d->Csplit >= 0 && d->Csplit <= d->Cout && (d->Csplit == d->Cout || d->Csplit % 4 == 0),
+              "conv: Csplit %d", d->Csplit);
   k.x1 = (const char*)x1; k.x2 = (const char*)x2; k.w = (const char*)w; k.y1 = (char*)y1; k.y2 = (char*)y2;
   k.N = d->N; k.H = d->H; k.W = d->W; k.C1 = d->C1; k.C2 = d->C2; k.ld1 = d->ld1; k.ld2 = d->ld2; k.Kc = d->Kc;
   k.OH = d->OH; k.OW = d->OW; k.Cout = d->Cout; k.ntaps = d->ntaps; k.mode = d->mode; k.stride = d->stride;
