@@ -57,6 +57,8 @@ def _load():
         "dmc_gn_workspace": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
         "dmc_gn_stats": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_f,
                                   _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+        "dmc_gn_apply": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p,
+                                  _c_int, _c_u32, _c_u32, _c_f, _c_p, _c_int, _c_p]),
         "dmc_gn_silu_bwd": (_c_int, [_c_int, _c_p, _c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int,
                                      _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_u32, _c_u32, _c_f, _c_p, _c_p,
                                      _c_int, _c_int, _c_int, _c_int, _c_p, _c_p, _c_p, _c_p]),

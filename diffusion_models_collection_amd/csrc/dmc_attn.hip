@@ -22,7 +22,7 @@ constexpr float kLog2e = 1.4426950408889634f;
 struct AttnK {
   const char* qkv; int ld_qkv;
   const char* o; const char* dout; int ld_o;
-  const float* lse; const float* delta;
+  const float* lse; const float* delta; float* delta_out;
   char* out; int ld_out;        // fwd: O;   dq kernel: dqkv;   dkdv kernel: dqkv
   float* lse_out;
   int N, L, heads, hd;
@@ -169,21 +169,6 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnK a) {
   }
 }
 
-// delta[nh][q] = sum_d dO * O
-template <typename T>
-__global__ void attn_delta_kernel(AttnK a, float* delta) {
-  const long total = (long)a.N * a.heads * a.L;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int q = i % a.L;
-    const int nh = i / a.L;
-    const int n = nh / a.heads, hh = nh % a.heads;
-    float s = 0.f;
-    const size_t base = (size_t)(n * a.L + q) * a.ld_o + hh * a.hd;
-    for (int d = 0; d < a.hd; ++d) s += ld_as_f<T>(a.dout, base + d) * ld_as_f<T>(a.o, base + d);
-    delta[i] = s;
-  }
-}
-
 template <typename T, int HDP>
 __global__ __launch_bounds__(256) void attn_dq_kernel(AttnK a) {
   constexpr int KPL = TT<T>::KPL;
@@ -202,7 +187,19 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnK a) {
   load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, q, hh * a.hd, qf);
   load_tok_frags<T, DC>(a, a.dout, a.ld_o, n, q, hh * a.hd, df);
   const float lse2 = q < a.L ? a.lse[(size_t)nh * a.L + q] * kLog2e : 0.f;
-  const float dl = q < a.L ? a.delta[(size_t)nh * a.L + q] : 0.f;
+  // delta_q = rowsum(dO * O), computed here (every lane for its own query) and published for dK/dV
+  float dl = 0.f;
+  if (q < a.L) {
+    const size_t row = (size_t)(n * a.L + q) * a.ld_o + hh * a.hd;
+    for (int d0 = 0; d0 < a.hd; d0 += KPL) {
+      float fo[KPL], fd[KPL];
+      Chunk<T>::unpack(*(const v4i*)(a.o + (row + d0) * sizeof(T)), fo);
+      Chunk<T>::unpack(*(const v4i*)(a.dout + (row + d0) * sizeof(T)), fd);
+#pragma unroll
+      for (int e = 0; e < KPL; ++e) dl = fmaf(fo[e], fd[e], dl);
+    }
+    if (h == 0) a.delta_out[(size_t)nh * a.L + q] = dl;
+  }
   const float sl2 = a.scale * kLog2e;
   v4f dq[DT];
 #pragma unroll
@@ -325,9 +322,8 @@ int launch_all(bool fwd, AttnK a, float* delta, hipStream_t s) {
     attn_fwd_kernel<T, HDP><<<g, 256, 0, s>>>(a);
     return dmc::check_launch("dmc_attn_fwd");
   }
-  const long total = (long)a.N * a.heads * a.L;
-  attn_delta_kernel<T><<<(int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096), 256, 0, s>>>(a, delta);
   a.delta = delta;
+  a.delta_out = delta;
   attn_dq_kernel<T, HDP><<<g, 256, 0, s>>>(a);
   attn_dkdv_kernel<T, HDP><<<g, 256, 0, s>>>(a);
   return dmc::check_launch("dmc_attn_bwd");

@@ -405,7 +405,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvK a, const char* dy
       __syncthreads();
     }
   }
-  // slab [z][kk][Cpad] where Cpad = round up Cout to 128 (co is the row of C: co = 4h+i, kk = col r)
+  // slab [z][Cpad][KK], Cpad = Cout rounded up to 128 (co is the row of C: co = 4h+i, kk = col r):
+  // for each register i, 16 lanes store 16 consecutive kk of one co row (64-byte segments)
   const int Cpad = gridDim.y * 128;
   float* out = slab + (size_t)blockIdx.z * KK * Cpad;
   const int fr = lane & 15, fh = lane >> 4;
@@ -416,24 +417,25 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvK a, const char* dy
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int co = co0 + wm * 64 + i * 16 + fh * 4;
-      *(v4f*)(out + (size_t)k * Cpad + co) = acc[i][j];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[(size_t)(co + e) * KK + k] = acc[i][j][e];
     }
   }
 }
 
-// dw[co][c][t] = scale * sum_z slab[z][t*Kc + c][co]
+// dw[co][c][t] = scale * sum_z slab[z][co][t*Kc + c]; threads walk the slab contiguously (k fastest)
 __global__ void wgrad_reduce_kernel(const float* slab, int splits, int KK, int Cpad, int Cout, int Ctot,
                                     int ntaps, int Kc, float scale, float* dw) {
-  const long total = (long)Cout * Ctot * ntaps;
+  const long total = (long)Cout * KK;
+  const size_t zstride = (size_t)Cpad * KK;
   for (long o = blockIdx.x * (long)blockDim.x + threadIdx.x; o < total; o += (long)gridDim.x * blockDim.x) {
-    const int t = o % ntaps;
-    const long r = o / ntaps;
-    const int c = r % Ctot;
-    const int co = r / Ctot;
-    const size_t k = (size_t)t * Kc + c;
+    const int k = o % KK;
+    const int co = o / KK;
+    const int t = k / Kc, c = k - t * Kc;
+    if (c >= Ctot) continue;
     float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += slab[((size_t)z * KK + k) * Cpad + co];
-    dw[o] = s * scale;
+    for (int z = 0; z < splits; ++z) s += slab[(size_t)z * zstride + o];
+    dw[((size_t)co * Ctot + c) * ntaps + t] = s * scale;
   }
 }
 
@@ -570,8 +572,8 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
     conv_wgrad_kernel<bf16_t><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (float*)workspace, KK, pps);
   if (dmc::check_launch("dmc_conv2d_wgrad")) return 2;
   const int Ctot = d->C1 + d->C2;
-  const long total = (long)d->Cout * Ctot * d->ntaps;
-  const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  const long total = (long)d->Cout * KK;
+  const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
   wgrad_reduce_kernel<<<blocks, 256, 0, s>>>((const float*)workspace, splits, KK, (int)g.y * 128, d->Cout, Ctot,
                                              d->ntaps, d->Kc, scale, dw);
   return dmc::check_launch("dmc_conv2d_wgrad reduce");

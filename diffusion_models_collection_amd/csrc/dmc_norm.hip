@@ -200,13 +200,59 @@ __global__ void gn_bwd_final(int C, int G, int HW, int splits, const float* part
   }
 }
 
-__global__ void gn_bwd_param(int N, int C, const float* A, float* dgamma, float* dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s1 = 0.f, s2 = 0.f;
-  for (int n = 0; n < N; ++n) { s1 += A[((size_t)n * C + c) * 2]; s2 += A[((size_t)n * C + c) * 2 + 1]; }
-  if (dbeta) dbeta[c] = s1;
-  if (dgamma) dgamma[c] = s2;
+// Column sums of a row-major fp32 matrix: out0[c] = scale * sum_r in[r*ld + c*stride], out1 likewise at +1.
+// 1024 threads = 64 columns x 16 row slices; slices combined in fixed order (deterministic).
+__global__ __launch_bounds__(1024) void colsum_kernel(const float* in, int R, int C, long ld, int stride, float* out0,
+                                                     float* out1, float scale) {
+  const int lane = threadIdx.x & 63, slice = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < C) {
+    const float* p = in + (size_t)c * stride;
+    for (int r = slice; r < R; r += 16) {
+      s0 += p[(size_t)r * ld];
+      if (out1) s1 += p[(size_t)r * ld + 1];
+    }
+  }
+  __shared__ float red[2][16][64];
+  red[0][slice][lane] = s0;
+  red[1][slice][lane] = s1;
+  __syncthreads();
+  if (slice == 0 && c < C) {
+    float t0 = 0.f, t1 = 0.f;
+    for (int k = 0; k < 16; ++k) { t0 += red[0][k][lane]; t1 += red[1][k][lane]; }
+    if (out0) out0[c] = t0 * scale;
+    if (out1) out1[c] = t1 * scale;
+  }
+}
+
+// GroupNorm-apply (+SiLU, +dropout) materialised once per element: a = drop(silu(x*scale[n,c] + shift[n,c])).
+// Used where the consumer re-reads the activation many times (3x3 implicit GEMM reads each pixel 9x) and
+// by the backward (weight gradients read `a` directly, dropout masks never stored).
+template <typename T>
+__global__ __launch_bounds__(256) void gn_apply_kernel(Src2 s, int HW, const float* scale, const float* shift,
+                                                       int silu, uint32_t seed, uint32_t thresh, float dscale, char* out,
+                                                       int ldo, long total) {
+  constexpr int EPC = TT<T>::KPL;
+  const int C = s.C1 + s.C2, CPR = C / EPC;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int col = i % CPR;
+    const long pix = i / CPR;
+    const int n = pix / HW;
+    const int c0 = col * EPC;
+    float f[EPC];
+    Chunk<T>::unpack(load_chunk2<T>(s, (int)pix, c0), f);
+    const float* sc = scale + (size_t)n * C + c0;
+    const float* sh = shift + (size_t)n * C + c0;
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      float v = fmaf(f[e], sc[e], sh[e]);
+      if (silu) v = silu_f(v);
+      if (thresh) v = drop_keep((uint64_t)pix * C + c0 + e, seed, thresh) ? v * dscale : 0.f;
+      f[e] = v;
+    }
+    *(v4i*)(out + ((size_t)pix * ldo + c0) * sizeof(T)) = Chunk<T>::pack(f);
+  }
 }
 
 template <typename T>
@@ -280,18 +326,16 @@ __global__ __launch_bounds__(256) void chsum_partial(const char* dy, int HW, int
   }
 }
 
-__global__ void chsum_final(int N, int C, int splits, const float* partial, float* out_nc, int ld_out, float* out_c,
-                            float scale) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float tot = 0.f;
-  for (int n = 0; n < N; ++n) {
+// out_nc[n][c] = scale * sum_split partial[n][split][c]   (one thread per (n, c))
+__global__ void chsum_nc(int N, int C, int splits, const float* partial, float* out_nc, int ld_out, float scale) {
+  const long total = (long)N * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = i % C;
+    const int n = i / C;
     float v = 0.f;
     for (int sp = 0; sp < splits; ++sp) v += partial[((size_t)n * splits + sp) * C + c];
-    if (out_nc) out_nc[(size_t)n * ld_out + c] = v * scale;
-    tot += v;
+    out_nc[(size_t)n * ld_out + c] = v * scale;
   }
-  if (out_c) out_c[c] = tot * scale;
 }
 
 int host_splits(int N, int HW, int C, int epc) {
@@ -362,7 +406,8 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
   if (dtype == DMC_F32) gn_bwd_partial<float><<<gr, 256, 0, s>>>(b, partial);
   else gn_bwd_partial<bf16_t><<<gr, 256, 0, s>>>(b, partial);
   gn_bwd_final<<<N, 256, 0, s>>>(C, G, HW, b.splits, partial, gamma, A, coef);
-  gn_bwd_param<<<(C + 255) / 256, 256, 0, s>>>(N, C, A, dgamma, dbeta);
+  // dbeta[c] = sum_n A[n][c][0], dgamma[c] = sum_n A[n][c][1]
+  colsum_kernel<<<(C + 63) / 64, 1024, 0, s>>>(A, N, C, (long)C * 2, 2, dbeta, dgamma, 1.0f);
   if (dtype == DMC_F32)
     gn_bwd_apply<float><<<ablocks, 256, 0, s>>>(b, N, coef, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, accumulate1, accumulate2);
   else
@@ -384,6 +429,29 @@ extern "C" int dmc_channel_sum(int dtype, const void* dy, int N, int HW, int C, 
   dim3 g(N, splits);
   if (dtype == DMC_F32) chsum_partial<float><<<g, 256, 0, s>>>((const char*)dy, HW, C, ld, splits, partial);
   else chsum_partial<bf16_t><<<g, 256, 0, s>>>((const char*)dy, HW, C, ld, splits, partial);
-  chsum_final<<<(C + 255) / 256, 256, 0, s>>>(N, C, splits, partial, out_nc, ld_out, out_c, scale);
+  if (out_nc) {
+    const long tot = (long)N * C;
+    chsum_nc<<<(int)((tot + 255) / 256 < 4096 ? (tot + 255) / 256 : 4096), 256, 0, s>>>(N, C, splits, partial, out_nc,
+                                                                                          ld_out, scale);
+  }
+  if (out_c) colsum_kernel<<<(C + 63) / 64, 1024, 0, s>>>(partial, N * splits, C, C, 1, out_c, nullptr, scale);
   return dmc::check_launch("dmc_channel_sum");
+}
+
+extern "C" int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1, int ld2,
+                            const float* scale, const float* shift, int silu, uint32_t drop_seed, uint32_t drop_thresh,
+                            float drop_scale, void* out, int ld_out, void* stream) {
+  const int epc = dtype == DMC_F32 ? 4 : 8;
+  DMC_REQUIRE(C1 % epc == 0 && C2 % epc == 0 && ld_out % epc == 0, "gn_apply: channel alignment");
+  const long total = (long)N * HW * ((C1 + C2) / epc);
+  const int blocks = (int)((total + 255) / 256 < 16384 ? (total + 255) / 256 : 16384);
+  hipStream_t s = dmc::as_stream(stream);
+  Src2 src{(const char*)x1, (const char*)x2, C1, C2, ld1, ld2};
+  if (dtype == DMC_F32)
+    gn_apply_kernel<float><<<blocks, 256, 0, s>>>(src, HW, scale, shift, silu, drop_seed, drop_thresh, drop_scale,
+                                                  (char*)out, ld_out, total);
+  else
+    gn_apply_kernel<bf16_t><<<blocks, 256, 0, s>>>(src, HW, scale, shift, silu, drop_seed, drop_thresh, drop_scale,
+                                                   (char*)out, ld_out, total);
+  return dmc::check_launch("dmc_gn_apply");
 }

@@ -114,6 +114,17 @@ def gn_stats(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, G, eps, gamma, beta):
     return sc, sh, mr
 
 
+def gn_apply(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, scale, shift, silu=True, drop=None, out=None):
+    """a = dropout(silu(x*scale + shift)) materialised as [N*HW][C1+C2] (dtype)."""
+    C = C1 + C2
+    if out is None:
+        out = torch.empty(N * HW * C, dtype=dtype, device=x1.device)
+    seed, thresh, dscale = drop if drop is not None else (0, 0, 1.0)
+    check(LIB.dmc_gn_apply(L.dtype_code(dtype), ptr(x1), ptr(x2), N, HW, C1, C2, ld1, ld2, ptr(scale), ptr(shift),
+                           int(silu), seed, thresh, dscale, ptr(out), C, L.stream()), "dmc_gn_apply")
+    return out
+
+
 def gn_bwd(dtype, g, ld_g, x1, x2, N, HW, C1, C2, ld1, ld2, G, mr, gamma, beta, silu, drop, dx1, dx2, ld_dx1,
            ld_dx2, acc1, acc2, dgamma, dbeta):
     ws = SCRATCH.get(LIB.dmc_gn_workspace(N, C1 + C2, G, HW), g.device)

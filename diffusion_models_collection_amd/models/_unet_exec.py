@@ -214,6 +214,16 @@ class UNetExecutor:
         return K.gn_stats(dtype, a.t, b.t if b else None, N, a.H * a.W, a.C, b.C if b else 0, a.t.shape[-1],
                           b.t.shape[-1] if b else 0, gn.num_groups, gn.eps, gn.weight, gn.bias)
 
+    def _apply(self, srcs, st, silu=True, drop=None):
+        """Act of dropout(silu(GN(concat(srcs)))) materialised with dmc_gn_apply."""
+        a = srcs[0]
+        b = srcs[1] if len(srcs) > 1 else None
+        N = a.t.shape[0]
+        C = a.C + (b.C if b else 0)
+        out = K.gn_apply(self.dt, a.t, b.t if b else None, N, a.H * a.W, a.C, b.C if b else 0, a.t.shape[-1],
+                         b.t.shape[-1] if b else 0, st[0], st[1], silu=silu, drop=drop)
+        return Act(out.view(N, a.H, a.W, C), a.H, a.W, C)
+
     def _new(self, N, H, W, C, dtype=None):
         return Act(torch.empty(N, H, W, C, dtype=dtype or self.dt, device=self.device), H, W, C)
 
@@ -304,11 +314,11 @@ class UNetExecutor:
         # ---- output: GN -> SiLU -> conv3x3 -> NCHW fp32 ----
         gno, convo = m.output[0], m.output[2]
         sc, sh, mr = self._gn([h], gno)
+        ao = self._apply([h], (sc, sh, mr), silu=True)
         out = torch.empty(N, m.out_channels, H, W, dtype=f32, device=x.device)
-        self._conv([h], convo, K.TAPS3, H, W, m.out_channels, pro=(L.PRO_AFFINE_SILU, sc, sh), bias=convo.bias,
-                   out=out, out_f32=True, out_nchw=True)
+        self._conv([ao], convo, K.TAPS3, H, W, m.out_channels, bias=convo.bias, out=out, out_f32=True, out_nchw=True)
         if keep:
-            tape.append(("out", h, (sc, sh, mr)))
+            tape.append(("out", h, (sc, sh, mr), ao))
         return out, tape
 
     def _layer(self, srcs, layer, tape):
@@ -340,10 +350,13 @@ class UNetExecutor:
         N, H, W = a.t.shape[0], a.H, a.W
         Cout = rb.out_channels
         gn1, conv1, gn2, conv2 = rb.conv1[0], rb.conv1[2], rb.conv2[0], rb.conv2[3]
+        # a1 = SiLU(GN1(x)) materialised once (the 3x3 implicit GEMM reads every pixel 9x; the weight
+        # gradient re-reads it in backward)
         st1 = self._gn(srcs, gn1)
+        a1 = self._apply(srcs, st1, silu=True)
         h1 = self._new(N, H, W, Cout)
         off = self.temb_off[id(rb)]
-        self._conv(srcs, conv1, K.TAPS3, H, W, Cout, pro=(L.PRO_AFFINE_SILU, st1[0], st1[1]), bias=conv1.bias,
+        self._conv([a1], conv1, K.TAPS3, H, W, Cout, bias=conv1.bias,
                    addvec=self.addvec.view(N, -1)[:, off:], ld_add=self.temb_total, out=h1.t)
         st2 = self._gn([h1], gn2)
         if isinstance(rb.shortcut, torch.nn.Conv2d):
@@ -356,9 +369,11 @@ class UNetExecutor:
         if self._drop is not None:
             drop = ((self._seed_base + 7919 * self._blk_idx) & 0xFFFFFFFF, self._drop[0], self._drop[1])
         self._blk_idx += 1
+        a2 = self._apply([h1], st2, silu=True, drop=drop)
         out = self._new(N, H, W, Cout)
-        self._conv([h1], conv2, K.TAPS3, H, W, Cout, pro=(L.PRO_AFFINE_SILU, st2[0], st2[1]), drop=drop,
-                   bias=conv2.bias, resid=resid, out=out.t)
+        self._conv([a2], conv2, K.TAPS3, H, W, Cout, bias=conv2.bias, resid=resid, out=out.t)
+        st1 = (st1, a1)
+        st2 = (st2, a2)
         if tape is not None:
             tape.append(("res", rb, srcs, h1, st1, st2, drop, out))
         return out
@@ -439,13 +454,13 @@ class UNetExecutor:
         kind = rec[0]
         if True:
             if kind == "out":
-                _, h, (sc, sh, mr) = rec
+                _, h, (sc, sh, mr), ao = rec
                 gno, convo = m.output[0], m.output[2]
                 N, H, W = h.t.shape[0], h.H, h.W
                 Co = m.out_channels
                 ldo = (Co + self.chunk - 1) // self.chunk * self.chunk
                 dy = K.pack_input(dt, dout.contiguous(), ldo)
-                self._wgrad([h], dy, ldo, K.TAPS3, H, W, Co, gv(convo.weight), pro=(L.PRO_AFFINE_SILU, sc, sh))
+                self._wgrad([ao], dy, ldo, K.TAPS3, H, W, Co, gv(convo.weight))
                 K.channel_sum(dt, dy, N, H * W, Co, ldo, out_c=gv(convo.bias))
                 g = torch.empty(N, H, W, h.C, dtype=dt, device=dout.device)
                 dya = Act(dy, H, W, Co)
@@ -496,7 +511,7 @@ class UNetExecutor:
                 self._temb_bwd(rec, self.daddvec, gv)
 
     def _res_bwd(self, rec, gv):
-        _, rb, srcs, h1, st1, st2, drop, out = rec
+        _, rb, srcs, h1, (st1, a1), (st2, a2), drop, out = rec
         dt = self.dt
         a = srcs[0]
         N, H, W = a.t.shape[0], a.H, a.W
@@ -506,9 +521,8 @@ class UNetExecutor:
         gn1, conv1, gn2, conv2 = rb.conv1[0], rb.conv1[2], rb.conv2[0], rb.conv2[3]
         dout = out.grad
         HW = H * W
-        # conv2 (weight, bias) and its input gradient
-        self._wgrad([h1], dout, Cout, K.TAPS3, H, W, Cout, gv(conv2.weight), pro=(L.PRO_AFFINE_SILU, st2[0], st2[1]),
-                    drop=drop)
+        # conv2 (weight, bias) and its input gradient; a2 = dropout(SiLU(GN2(h1))) was kept from forward
+        self._wgrad([a2], dout, Cout, K.TAPS3, H, W, Cout, gv(conv2.weight))
         K.channel_sum(dt, dout, N, HW, Cout, Cout, out_c=gv(conv2.bias))
         g2 = torch.empty(N, H, W, Cout, dtype=dt, device=dout.device)
         self._conv([Act(dout, H, W, Cout)], conv2, K.TAPS3_DGRAD, H, W, Cout, out=g2, packmode=L.PACK_DGRAD)
@@ -549,7 +563,7 @@ class UNetExecutor:
         K.channel_sum(dt, dh1, N, HW, Cout, Cout, out_nc=self.daddvec[:, off:], ld_out=self.temb_total,
                       out_c=gv(conv1.bias))
         # conv1
-        self._wgrad(srcs, dh1, Cout, K.TAPS3, H, W, Cout, gv(conv1.weight), pro=(L.PRO_AFFINE_SILU, st1[0], st1[1]))
+        self._wgrad([a1], dh1, Cout, K.TAPS3, H, W, Cout, gv(conv1.weight))
         g1 = torch.empty(N, H, W, C1 + C2, dtype=dt, device=dout.device)
         self._conv([Act(dh1, H, W, Cout)], conv1, K.TAPS3_DGRAD, H, W, C1 + C2, out=g1, packmode=L.PACK_DGRAD)
         b1, acc1 = self._grad_target(a)

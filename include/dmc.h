@@ -93,6 +93,12 @@ int dmc_gn_stats(int dtype, const void* x1, const void* x2, int N, int HW, int C
                  int ld2, int G, float eps, const float* gamma, const float* beta, void* workspace,
                  float* mean_rstd, float* scale, float* shift, void* stream);
 
+/* a = dropout(SiLU(x*scale[n,c] + shift[n,c])) (silu=1) or the affine alone (silu=0), materialised once
+ * (dtype, [pix][ld_out]); dropout keeps element (pix, c) iff hash(seed, pix*C + c) >= drop_thresh. */
+int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1,
+                 int ld2, const float* scale, const float* shift, int silu, uint32_t drop_seed,
+                 uint32_t drop_thresh, float drop_scale, void* out, int ld_out, void* stream);
+
 /* Backward of a = dropout(SiLU(GroupNorm(x))) (silu=1) or a = GroupNorm(x) (silu=0, AttentionBlock
  * norm :80): g = dL/da (dtype, [pix][ld_g]); writes
  * dx (split into dx1/dx2 by channel like the sources; accumulate_k: add into existing),
