@@ -57,7 +57,6 @@ def conv_roofline(dtype, B=128):
     addv = torch.randn(B, C, device=dev)
     y = torch.empty(B, H, W, C, device=dev, dtype=dtype)
     d = K.make_desc(dtype, B, H, W, C, 0, C, 0, Kc, H, W, C, K.TAPS3)
-    K.set_prologue(d, L.PRO_AFFINE_SILU, sc, sh, C)
     K.set_epilogue(d, bias=bias, addvec=addv, ld_add=C, ldy1=C)
     for _ in range(5):
         K.conv(d, x, None, wp, y)
@@ -72,8 +71,8 @@ def conv_roofline(dtype, B=128):
     avg_ms = e0.elapsed_time(e1) / n
     flops = 2.0 * B * H * W * C * C * 9
     achieved = flops / (avg_ms * 1e-3) / 1e12
-    return {"kernel": "conv_fwd_kernel<bf16,128,128> (ResBlock 3x3 128->128 @32x32, B=128)" if dtype == torch.bfloat16
-            else "conv_fwd_kernel<f32,128,128>",
+    return {"kernel": "conv_fwd_glds_kernel<4,2> bf16 implicit GEMM (ResBlock 3x3 128->128 @32x32, B=128, "
+                      "bias+temb epilogue)" if dtype == torch.bfloat16 else "conv_fwd_kernel<f32,128,128>",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
             "flops_per_launch": flops, "avg_launch_ms": round(avg_ms, 4)}

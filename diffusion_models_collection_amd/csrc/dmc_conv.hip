@@ -18,7 +18,7 @@ namespace {
 struct ConvK {
   const char* x1; const char* x2; const char* w; char* y1; char* y2;
   int N, H, W, C1, C2, ld1, ld2, Kc, OH, OW, Cout, ntaps, mode, stride;
-  int tdy[16], tdx[16];
+  int tkw, tdy0, tdx0, tsy, tsx;   // tap grid: tap t -> (tdy0 + tsy*(t / tkw), tdx0 + tsx*(t % tkw))
   int prologue; const float* psc; const float* psh; int ldp;
   uint32_t dseed, dthresh; float dscale; int dld;
   const float* bias; const float* addvec; int ld_add;
@@ -30,8 +30,9 @@ struct ConvK {
 
 // Source pixel of output pixel (n,oy,ox) under tap; returns -1 if it falls in the zero padding.
 DMC_DEV int src_pixel(const ConvK& a, int n, int oy, int ox, int tap) {
-  int iy = oy * a.stride + a.tdy[tap];
-  int ix = ox * a.stride + a.tdx[tap];
+  const int tr = tap / a.tkw;
+  int iy = oy * a.stride + a.tdy0 + a.tsy * tr;
+  int ix = ox * a.stride + a.tdx0 + a.tsx * (tap - tr * a.tkw);
   if (a.mode == DMC_MODE_UPSAMPLE) {
     if (iy < 0 || iy >= 2 * a.H || ix < 0 || ix >= 2 * a.W) return -1;
     iy >>= 1; ix >>= 1;
@@ -108,6 +109,11 @@ DMC_DEV void store4(char* p, size_t idx, const float* v, bool f32) {
     *(v2i*)(p + idx * 2) = x;
   }
 }
+
+template <typename T, int TN, int TM>
+DMC_DEV void conv_epilogue(const ConvK& a, v4f (&acc)[TN][TM], int pix_base, int co_base);
+template <typename T>
+DMC_DEV void conv_store_tile(const ConvK& a, const v4f accv, const int pix, const int co);
 
 // ---------------------------------------------------------------------------------------------
 // Forward / dgrad kernel. Tile BM pixels x BN output channels, 256 threads = 2x2 waves, stage depth
@@ -217,19 +223,30 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvK a) {
     if (s + 1 < nstages) store_stage(buf ^ 1);
     __syncthreads();
   }
+  conv_epilogue<T, TN, TM>(a, acc, m0 + wm * (BM / 2), n0 + wn * (BN / 2));
+}
 
-  // ---- epilogue ----
+// Epilogue shared by the forward kernels: accumulator acc[i][j] holds output channels
+// co_base + 16i + 4h + e of pixel pix_base + 16j + r (lane = 16h + r).
+template <typename T, int TN, int TM>
+DMC_DEV void conv_epilogue(const ConvK& a, v4f (&acc)[TN][TM], int pix_base, int co_base) {
+  const int lane = threadIdx.x & 63;
+  const int fr = lane & 15, fh = lane >> 4;
+  // tiles are visited with compile-time indices and handed over by value, so the accumulator array
+  // stays in registers (a data-dependent early exit inside these loops made hipcc demote it to scratch)
+#pragma unroll
+  for (int j = 0; j < TM; ++j)
+#pragma unroll
+    for (int i = 0; i < TN; ++i) conv_store_tile<T>(a, acc[i][j], pix_base + j * 16 + fr, co_base + i * 16 + fh * 4);
+}
+
+template <typename T>
+DMC_DEV void conv_store_tile(const ConvK& a, const v4f accv, const int pix, const int co) {
   const bool of32 = a.out_f32 != 0;
-#pragma unroll
-  for (int j = 0; j < TM; ++j) {
-    const int pix = m0 + wm * (BM / 2) + j * 16 + fr;
-    if (pix >= a.M) continue;
+  if (pix < a.M && co < a.Cout) {
     const int n = pix / a.OHW;
-#pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      const int co = n0 + wn * (BN / 2) + i * 16 + fh * 4;
-      if (co >= a.Cout) continue;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+    {
+      float v[4] = {accv[0], accv[1], accv[2], accv[3]};
       const bool full = (co + 3 < a.Cout) && ((a.Cout & 3) == 0);
       if (full && !a.out_nchw) {
         if (a.bias) { v4f b = *(const v4f*)(a.bias + co); v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3]; }
@@ -267,6 +284,143 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvK a) {
         }
       }
     }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// bf16 forward / dgrad kernel without prologue: global->LDS DMA (global_load_lds_dwordx4) into a
+// 3-stage LDS ring, counted vmcnt + one raw barrier per stage, 64x64 output per wave.
+// Tile = (64*WM pixels) x (64*WN channels), WM*WN waves.
+// Each glds wave-instruction writes 8 consecutive 128-byte LDS rows, lane l -> row l>>3, physical chunk
+// l&7; the lane loads LOGICAL chunk (l&7) ^ (row&7) so the image carries the same XOR swizzle the
+// fragment reads use (swizzle applied on the source address, MI355X guide rule 21).
+// Zero padding (halo taps, rows past M / Cout, channels past C1+C2) is read from a zero page.
+__device__ v4i g_zero_page[64];
+
+DMC_DEV constexpr int waitcnt_vm(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
+
+// Issue one K-stage (64 channels of one tap) of A (pixels) and B (weights) as LDS-DMA pieces.
+template <int AI, int BI, int BM>
+DMC_DEV void glds_issue(const ConvK& a, char* base, int s, int wave, int lrow, int lc, int n0, const int* pn,
+                        const int* poy, const int* pox) {
+  const int k0 = s * 64;
+  const int tap = k0 / a.Kc;
+  const int c = k0 - tap * a.Kc + lc * 8;
+  const int Ctot = a.C1 + a.C2;
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const void* src = g_zero_page;
+    if (pn[j] >= 0 && c < Ctot) {
+      const int sp = src_pixel(a, pn[j], poy[j], pox[j], tap);
+      if (sp >= 0) src = (c < a.C1) ? (const void*)(a.x1 + ((size_t)sp * a.ld1 + c) * 2)
+                                    : (const void*)(a.x2 + ((size_t)sp * a.ld2 + (c - a.C1)) * 2);
+    }
+    __builtin_amdgcn_global_load_lds(src, (LDS_AS void*)(base + (wave * AI + j) * 8 * 128), 16, 0, 0);
+  }
+  const size_t wrow = (size_t)a.ntaps * a.Kc;
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int co = n0 + (wave * BI + j) * 8 + lrow;
+    const void* src = (co < a.Cout) ? (const void*)(a.w + ((size_t)co * wrow + k0 + lc * 8) * 2) : g_zero_page;
+    __builtin_amdgcn_global_load_lds(src, (LDS_AS void*)(base + BM * 128 + (wave * BI + j) * 8 * 128), 16, 0, 0);
+  }
+}
+
+template <int WM, int WN>
+__global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
+  using T = bf16_t;
+  constexpr int NW = WM * WN;
+  constexpr int BM = 64 * WM, BN = 64 * WN;
+  constexpr int STAGES = 3;
+  constexpr int SB = (BM + BN) * 128;           // bytes per stage
+  constexpr int AI = BM / 8 / NW;               // A glds instructions per wave per stage
+  constexpr int BI = BN / 8 / NW;               // B glds instructions per wave per stage
+  static_assert(AI >= 1 && BI >= 1, "tile too small for the wave count");
+  __shared__ __attribute__((aligned(16))) char lds[STAGES * SB];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int lrow = lane >> 3;
+  const int lc = (lane & 7) ^ lrow;             // logical 16-byte chunk this lane fetches
+
+  int pn[AI], poy[AI], pox[AI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int pix = m0 + (wave * AI + j) * 8 + lrow;
+    if (pix < a.M) {
+      pn[j] = pix / a.OHW;
+      const int rem = pix - pn[j] * a.OHW;
+      poy[j] = rem / a.OW;
+      pox[j] = rem - poy[j] * a.OW;
+    } else {
+      pn[j] = -1; poy[j] = 0; pox[j] = 0;
+    }
+  }
+  const int nstages = a.ntaps * (a.Kc / 64);
+
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+#define DMC_GLDS_ISSUE(S) glds_issue<AI, BI, BM>(a, lds + ((S) % STAGES) * SB, (S), wave, lrow, lc, n0, pn, poy, pox)
+  DMC_GLDS_ISSUE(0);
+  if (nstages > 1) DMC_GLDS_ISSUE(1);
+  const int fr = lane & 15, fh = lane >> 4;
+  for (int s = 0; s < nstages; ++s) {
+    // stage s has landed once at most the next stage's instructions are still outstanding
+    if (s + 1 < nstages) __builtin_amdgcn_s_waitcnt(waitcnt_vm(AI + BI));
+    else __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    // every wave has finished reading stage s-1's buffer: refill it with stage s+2
+    if (s + 2 < nstages) DMC_GLDS_ISSUE(s + 2);
+    const char* A = lds + (s % STAGES) * SB;
+    const char* B = A + BM * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = ks * 4 + fh;
+      v4i fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wn * 64 + i * 16 + fr;
+        fa[i] = *(const v4i*)(B + r * 128 + ((chunk ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = wm * 64 + j * 16 + fr;
+        fb[j] = *(const v4i*)(A + r * 128 + ((chunk ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
+    }
+  }
+#undef DMC_GLDS_ISSUE
+  // Epilogue through LDS: the block's fp32 tile is parked in the (now free) staging ring, then every
+  // thread finishes 4-channel groups of consecutive channels (coalesced NHWC stores; the epilogue loop is
+  // a runtime loop, which keeps hipcc from spilling the accumulators to scratch).
+  constexpr int EP = BN * 4 + 16;
+  static_assert(BM * EP <= STAGES * SB, "epilogue tile must fit the staging ring");
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *(v4f*)(lds + (wm * 64 + j * 16 + fr) * EP + (wn * 64 + i * 16 + fh * 4) * 4) = acc[i][j];
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < BM * BN / 4; idx += NW * 64) {
+    const int pl = idx / (BN / 4), cg = idx - pl * (BN / 4);
+    const v4f v = *(const v4f*)(lds + pl * EP + cg * 16);
+    conv_store_tile<T>(a, v, m0 + pl, n0 + cg * 4);
   }
 }
 
@@ -496,7 +650,20 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
   k.x1 = (const char*)x1; k.x2 = (const char*)x2; k.w = (const char*)w; k.y1 = (char*)y1; k.y2 = (char*)y2;
   k.N = d->N; k.H = d->H; k.W = d->W; k.C1 = d->C1; k.C2 = d->C2; k.ld1 = d->ld1; k.ld2 = d->ld2; k.Kc = d->Kc;
   k.OH = d->OH; k.OW = d->OW; k.Cout = d->Cout; k.ntaps = d->ntaps; k.mode = d->mode; k.stride = d->stride;
-  for (int i = 0; i < 16; ++i) { k.tdy[i] = d->tap_dy[i]; k.tdx[i] = d->tap_dx[i]; }
+  // the kernels take the taps as a regular grid (no dynamically indexed kernel-argument arrays, which
+  // would spill the argument struct to scratch): recover (kw, origin, step) and verify every tap
+  {
+    int kw = 1;
+    while (kw < d->ntaps && d->tap_dy[kw] == d->tap_dy[0]) ++kw;
+    k.tkw = kw;
+    k.tdy0 = d->tap_dy[0]; k.tdx0 = d->tap_dx[0];
+    k.tsx = kw > 1 ? d->tap_dx[1] - d->tap_dx[0] : 1;
+    k.tsy = d->ntaps > kw ? d->tap_dy[kw] - d->tap_dy[0] : 1;
+    bool ok = d->ntaps % kw == 0;
+    for (int t = 0; ok && t < d->ntaps; ++t)
+      ok = d->tap_dy[t] == k.tdy0 + k.tsy * (t / kw) && d->tap_dx[t] == k.tdx0 + k.tsx * (t % kw);
+    DMC_REQUIRE(ok, "conv: taps must form a regular grid");
+  }
   k.prologue = d->prologue; k.psc = d->pro_scale; k.psh = d->pro_shift; k.ldp = d->ld_pro;
   k.dseed = d->drop_seed; k.dthresh = d->drop_thresh; k.dscale = d->drop_scale; k.dld = d->drop_ld;
   k.bias = d->bias; k.addvec = d->addvec; k.ld_add = d->ld_add; k.resid = (const char*)d->resid; k.ld_res = d->ld_res;
@@ -508,6 +675,19 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
 
 template <typename T>
 int launch_fwd(const ConvK& k, hipStream_t s) {
+  if (sizeof(T) == 2 && k.prologue == DMC_PRO_NONE && !getenv_flag("DMC_NO_GLDS")) {
+    // bf16, plain operands: LDS-DMA pipelined kernel; largest tile that still fills the chip
+    const long b42 = (long)dmc::cdiv(k.M, 256) * dmc::cdiv(k.Cout, 128);
+    const long b22 = (long)dmc::cdiv(k.M, 128) * dmc::cdiv(k.Cout, 128);
+    if (b42 >= 240) {
+      conv_fwd_glds_kernel<4, 2><<<dim3(dmc::cdiv(k.M, 256), dmc::cdiv(k.Cout, 128)), 512, 0, s>>>(k);
+    } else if (b22 >= 240) {
+      conv_fwd_glds_kernel<2, 2><<<dim3(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128)), 256, 0, s>>>(k);
+    } else {
+      conv_fwd_glds_kernel<1, 2><<<dim3(dmc::cdiv(k.M, 64), dmc::cdiv(k.Cout, 128)), 128, 0, s>>>(k);
+    }
+    return dmc::check_launch("dmc_conv2d");
+  }
   // tile choice: big tiles when they still give >= ~2 waves of blocks over 256 CUs
   const long t128 = (long)dmc::cdiv(k.M, 128) * dmc::cdiv(k.Cout, 128);
   if (t128 >= 384 && k.Cout >= 128) {

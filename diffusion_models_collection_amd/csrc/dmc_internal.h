@@ -19,6 +19,13 @@ inline int check_launch(const char* what) {
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 }  // namespace dmc
 
+// A/B switches for measurement (read once per process, never on the device).
+#include <stdlib.h>
+inline bool getenv_flag(const char* name) {
+  const char* v = getenv(name);
+  return v && v[0] && v[0] != '0';
+}
+
 #define DMC_REQUIRE(cond, ...)       \
   do {                               \
     if (!(cond)) {                   \

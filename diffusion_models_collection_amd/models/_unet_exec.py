@@ -385,7 +385,9 @@ class UNetExecutor:
         hd = C // heads
         st = self._gn([a], ab.norm)
         qkv = self._new(N, H, W, 3 * C)
-        self._conv([a], ab.qkv, K.TAPS1, H, W, 3 * C, pro=(L.PRO_AFFINE, st[0], st[1]), bias=ab.qkv.bias, out=qkv.t)
+        an = self._apply([a], st, silu=False)          # GroupNorm output (no SiLU in AttentionBlock, :86)
+        self._conv([an], ab.qkv, K.TAPS1, H, W, 3 * C, bias=ab.qkv.bias, out=qkv.t)
+        st = (st, an)
         o = self._new(N, H, W, C)
         lse = torch.empty(N * heads * Lq, dtype=torch.float32, device=self.device)
         K.attn_fwd(self.dt, qkv.t, 3 * C, N, Lq, heads, hd, o.t, C, lse)
@@ -589,7 +591,7 @@ class UNetExecutor:
             b2.copy_(t2)
 
     def _attn_bwd(self, rec, gv):
-        _, ab, a, st, qkv, o, lse, out = rec
+        _, ab, a, (st, an), qkv, o, lse, out = rec
         dt = self.dt
         N, H, W, C = a.t.shape[0], a.H, a.W, a.C
         HW = H * W
@@ -608,7 +610,7 @@ class UNetExecutor:
             K.add_(dt, a.grad, dout)
         dqkv = torch.empty(N, H, W, 3 * C, dtype=dt, device=dout.device)
         K.attn_bwd(dt, qkv.t, 3 * C, o.t, do, C, lse, N, HW, heads, hd, dqkv, 3 * C)
-        self._wgrad([a], dqkv, 3 * C, K.TAPS1, H, W, 3 * C, gv(ab.qkv.weight), pro=(L.PRO_AFFINE, st[0], st[1]))
+        self._wgrad([an], dqkv, 3 * C, K.TAPS1, H, W, 3 * C, gv(ab.qkv.weight))
         K.channel_sum(dt, dqkv, N, HW, 3 * C, 3 * C, out_c=gv(ab.qkv.bias))
         g = torch.empty(N, H, W, C, dtype=dt, device=dout.device)
         self._conv([Act(dqkv, H, W, 3 * C)], ab.qkv, K.TAPS1, H, W, C, out=g, packmode=L.PACK_DGRAD)
