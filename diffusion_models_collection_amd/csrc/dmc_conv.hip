@@ -26,6 +26,9 @@ struct ConvK {
   int Csplit, ldy1, ldy2, out_f32, out_nchw;
   int M;      // N*OH*OW output pixels
   int OHW;    // OH*OW
+  float* sk;  // split-K partial slab (nullptr: no split)
+  int sk_per; // K stages per split
+  int x1_bytes, x2_bytes, w_bytes;  // operand extents for buffer resources (0: too large / absent)
 };
 
 // Source pixel of output pixel (n,oy,ox) under tap; returns -1 if it falls in the zero padding.
@@ -299,22 +302,19 @@ __device__ v4i g_zero_page[64];
 
 DMC_DEV constexpr int waitcnt_vm(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
 
-// Issue one K-stage (64 channels of one tap) of A (pixels) and B (weights) as LDS-DMA pieces.
+// Issue one K-stage (channels [c0, c0+64) of one tap, flat K offset k0) of A (pixels) and B (weights) as
+// LDS-DMA pieces. sp[j] = source pixel of this lane's A row under the stage's tap (-1: zero padding).
 template <int AI, int BI, int BM>
-DMC_DEV void glds_issue(const ConvK& a, char* base, int s, int wave, int lrow, int lc, int n0, const int* pn,
-                        const int* poy, const int* pox) {
-  const int k0 = s * 64;
-  const int tap = k0 / a.Kc;
-  const int c = k0 - tap * a.Kc + lc * 8;
+DMC_DEV void glds_issue(const ConvK& a, char* base, int k0, int c0, int wave, int lrow, int lc, int n0,
+                        const int* sp) {
+  const int c = c0 + lc * 8;
   const int Ctot = a.C1 + a.C2;
 #pragma unroll
   for (int j = 0; j < AI; ++j) {
     const void* src = g_zero_page;
-    if (pn[j] >= 0 && c < Ctot) {
-      const int sp = src_pixel(a, pn[j], poy[j], pox[j], tap);
-      if (sp >= 0) src = (c < a.C1) ? (const void*)(a.x1 + ((size_t)sp * a.ld1 + c) * 2)
-                                    : (const void*)(a.x2 + ((size_t)sp * a.ld2 + (c - a.C1)) * 2);
-    }
+    if (sp[j] >= 0 && c < Ctot)
+      src = (c < a.C1) ? (const void*)(a.x1 + ((size_t)sp[j] * a.ld1 + c) * 2)
+                       : (const void*)(a.x2 + ((size_t)sp[j] * a.ld2 + (c - a.C1)) * 2);
     __builtin_amdgcn_global_load_lds(src, (LDS_AS void*)(base + (wave * AI + j) * 8 * 128), 16, 0, 0);
   }
   const size_t wrow = (size_t)a.ntaps * a.Kc;
@@ -326,7 +326,37 @@ DMC_DEV void glds_issue(const ConvK& a, char* base, int s, int wave, int lrow, i
   }
 }
 
-template <int WM, int WN>
+constexpr unsigned kOOB = 0x80000000u;  // buffer offset past every num_records: the load returns zeros
+
+// Buffer-resource form of glds_issue: o1/o2 = per-row byte offsets into x1/x2 for the current tap (kOOB for
+// padding rows), ob = per-row byte offsets into the packed weights, k2 = byte offset of this K stage.
+template <int AI, int BI, int BM>
+DMC_DEV void glds_issue_buf(const ConvK& a, char* base, int c0, unsigned k2, int wave, const unsigned* o1,
+                            const unsigned* o2, const unsigned* ob) {
+  if (c0 < a.C1) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)a.x1, (short)0, a.x1_bytes, 0x00020000);
+    const unsigned c2 = (unsigned)c0 * 2u;
+#pragma unroll
+    for (int j = 0; j < AI; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(base + (wave * AI + j) * 1024), 16, o1[j] + c2, 0, 0, 0);
+  } else {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)a.x2, (short)0, a.x2_bytes, 0x00020000);
+    const unsigned c2 = (unsigned)(c0 - a.C1) * 2u;
+#pragma unroll
+    for (int j = 0; j < AI; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(base + (wave * AI + j) * 1024), 16, o2[j] + c2, 0, 0, 0);
+  }
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.w_bytes, 0x00020000);
+#pragma unroll
+  for (int j = 0; j < BI; ++j)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (LDS_AS void*)(base + BM * 128 + (wave * BI + j) * 1024), 16, ob[j] + k2, 0, 0, 0);
+}
+
+// BUF = true: all operands through buffer resources (raw_ptr_buffer_load_lds), zero padding by the
+// hardware range check, per-row offsets precomputed once per tap -> one VALU add per DMA instruction.
+// Requires C1 % 64 == 0, C2 % 64 == 0, Kc == C1 + C2 (a stage never straddles the concat boundary).
+// BUF = false: generic (any channel split) with flat global_load_lds and a zero page.
+template <int WM, int WN, bool BUF>
 __global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
   using T = bf16_t;
   constexpr int NW = WM * WN;
@@ -367,13 +397,54 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-#define DMC_GLDS_ISSUE(S) glds_issue<AI, BI, BM>(a, lds + ((S) % STAGES) * SB, (S), wave, lrow, lc, n0, pn, poy, pox)
-  DMC_GLDS_ISSUE(0);
-  if (nstages > 1) DMC_GLDS_ISSUE(1);
+  // split-K (grid.z): this block accumulates stages [s_begin, s_end) and writes fp32 partials
+  const int s_begin = a.sk ? blockIdx.z * a.sk_per : 0;
+  const int s_end = a.sk ? min(nstages, s_begin + a.sk_per) : nstages;
+  const int ns = s_end - s_begin;
+  // stages are issued in order, so the tap / channel offset advance incrementally and the per-row
+  // source pixels are recomputed only when the tap changes (once per Kc/64 stages)
+  const int kst = a.Kc / 64;
+  int is_tap = s_begin / kst, is_c0 = (s_begin - is_tap * kst) * 64;
+  int sp[AI];
+  unsigned o1[AI], o2[AI], ob[BI];
+  if constexpr (BUF) {
+    const unsigned wrow = (unsigned)(a.ntaps * a.Kc);
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const int co = n0 + (wave * BI + j) * 8 + lrow;
+      ob[j] = co < a.Cout ? ((unsigned)co * wrow + lc * 8) * 2u : kOOB;
+    }
+  }
+  auto tap_rows = [&]() {
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const int p = pn[j] >= 0 ? src_pixel(a, pn[j], poy[j], pox[j], is_tap) : -1;
+      if constexpr (BUF) {
+        o1[j] = p >= 0 ? ((unsigned)p * a.ld1 + lc * 8) * 2u : kOOB;
+        o2[j] = p >= 0 ? ((unsigned)p * a.ld2 + lc * 8) * 2u : kOOB;
+      } else {
+        sp[j] = p;
+      }
+    }
+  };
+  tap_rows();
+  auto issue = [&](int S) {
+    char* base = lds + (S % STAGES) * SB;
+    if constexpr (BUF) {
+      glds_issue_buf<AI, BI, BM>(a, base, is_c0, (unsigned)(s_begin + S) * 128u, wave, o1, o2, ob);
+    } else {
+      glds_issue<AI, BI, BM>(a, base, (s_begin + S) * 64, is_c0, wave, lrow, lc, n0, sp);
+    }
+    is_c0 += 64;
+    if (is_c0 == a.Kc) { is_c0 = 0; ++is_tap; if (is_tap < a.ntaps) tap_rows(); }
+  };
+#define DMC_GLDS_ISSUE(S) issue(S)
+  if (ns > 0) DMC_GLDS_ISSUE(0);
+  if (ns > 1) DMC_GLDS_ISSUE(1);
   const int fr = lane & 15, fh = lane >> 4;
-  for (int s = 0; s < nstages; ++s) {
+  for (int s = 0; s < ns; ++s) {
     // stage s has landed once at most the next stage's instructions are still outstanding
-    if (s + 1 < nstages) __builtin_amdgcn_s_waitcnt(waitcnt_vm(AI + BI));
+    if (s + 1 < ns) __builtin_amdgcn_s_waitcnt(waitcnt_vm(AI + BI));
     else __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -381,7 +452,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
     // every wave has finished reading stage s-1's buffer: refill it with stage s+2
-    if (s + 2 < nstages) DMC_GLDS_ISSUE(s + 2);
+    if (s + 2 < ns) DMC_GLDS_ISSUE(s + 2);
     const char* A = lds + (s % STAGES) * SB;
     const char* B = A + BM * 128;
 #pragma unroll
@@ -417,10 +488,37 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
     for (int i = 0; i < 4; ++i)
       *(v4f*)(lds + (wm * 64 + j * 16 + fr) * EP + (wn * 64 + i * 16 + fh * 4) * 4) = acc[i][j];
   __syncthreads();
+  if (a.sk) {
+    // raw partial sums -> slab [z][M][Cpad]
+    const int Cpad = gridDim.y * BN;
+    float* slab = a.sk + (size_t)blockIdx.z * a.M * Cpad;
+    for (int idx = threadIdx.x; idx < BM * BN / 4; idx += NW * 64) {
+      const int pl = idx / (BN / 4), cg = idx - pl * (BN / 4);
+      if (m0 + pl < a.M) *(v4f*)(slab + (size_t)(m0 + pl) * Cpad + n0 + cg * 4) = *(const v4f*)(lds + pl * EP + cg * 16);
+    }
+    return;
+  }
   for (int idx = threadIdx.x; idx < BM * BN / 4; idx += NW * 64) {
     const int pl = idx / (BN / 4), cg = idx - pl * (BN / 4);
     const v4f v = *(const v4f*)(lds + pl * EP + cg * 16);
     conv_store_tile<T>(a, v, m0 + pl, n0 + cg * 4);
+  }
+}
+
+// split-K reduction + the regular epilogue: out(pix, co..co+3) = epilogue(sum_z slab[z][pix][co..])
+template <typename T>
+__global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvK a, int splits, int Cpad) {
+  const int cg_per_row = Cpad / 4;
+  const long total = (long)a.M * cg_per_row;
+  const size_t zs = (size_t)a.M * Cpad;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int pix = idx / cg_per_row;
+    const int co = (idx - (long)pix * cg_per_row) * 4;
+    if (co >= a.Cout) continue;
+    const float* p = a.sk + (size_t)pix * Cpad + co;
+    v4f v = *(const v4f*)p;
+    for (int z = 1; z < splits; ++z) v += *(const v4f*)(p + z * zs);
+    conv_store_tile<T>(a, v, pix, co);
   }
 }
 
@@ -670,25 +768,83 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
   k.silu_pre = d->silu_pre; k.ld_silu = d->ld_silu;
   k.Csplit = d->Csplit; k.ldy1 = d->ldy1; k.ldy2 = d->ldy2; k.out_f32 = d->out_f32; k.out_nchw = d->out_nchw;
   k.M = d->N * d->OH * d->OW; k.OHW = d->OH * d->OW;
+  k.sk = nullptr; k.sk_per = 0;
+  {
+    const size_t esz = d->dtype == DMC_F32 ? 4 : 2;
+    const size_t b1 = (size_t)d->N * d->H * d->W * d->ld1 * esz;
+    const size_t b2 = d->C2 ? (size_t)d->N * d->H * d->W * d->ld2 * esz : 0;
+    const size_t bw = (size_t)d->Cout * d->ntaps * d->Kc * esz;
+    const size_t lim = 0x7fff0000u;  // offsets (+ kOOB marker) must stay 32-bit
+    k.x1_bytes = b1 < lim ? (int)b1 : 0;
+    k.x2_bytes = b2 < lim ? (int)b2 : 0;
+    k.w_bytes = bw < lim ? (int)bw : 0;
+  }
   return 0;
 }
 
+// Launch plan of the bf16 LDS-DMA kernel: tile config and split-K factor.
+struct FwdPlan {
+  int cfg;      // 0: 256x128 (8 waves)  1: 128x128 (4 waves)  2: 64x128 (2 waves)
+  int splits;   // 1 = no split-K
+  int per;      // stages per split
+  size_t ws;    // slab bytes
+};
+
+FwdPlan plan_glds(const ConvK& k) {
+  FwdPlan p{0, 1, 0, 0};
+  const int nst = k.ntaps * (k.Kc / 64);
+  const long b42 = (long)dmc::cdiv(k.M, 256) * dmc::cdiv(k.Cout, 128);
+  const long b22 = (long)dmc::cdiv(k.M, 128) * dmc::cdiv(k.Cout, 128);
+  if (b42 >= 240) { p.cfg = 0; return p; }
+  // small M: split K over grid.z (>= 4 stages per split) rather than shrinking the tile below 128x128
+  long blocks = b22;
+  p.cfg = 1;
+  int sp = (int)((240 + blocks - 1) / blocks);
+  const int maxs = nst / 4;
+  if (sp > maxs) sp = maxs;
+  if (sp > 8) sp = 8;
+  if (sp >= 2) {
+    p.splits = sp;
+    p.per = (nst + sp - 1) / sp;
+    p.splits = (nst + p.per - 1) / p.per;
+    p.ws = (size_t)p.splits * k.M * (size_t)dmc::cdiv(k.Cout, 128) * 128 * sizeof(float);
+  } else if (b22 < 120) {
+    p.cfg = 2;
+  }
+  return p;
+}
+
+template <bool BUF>
+void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
+  if (p.splits > 1) {
+    conv_fwd_glds_kernel<2, 2, BUF><<<dim3(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128), p.splits), 256, 0, s>>>(k);
+    const int Cpad = dmc::cdiv(k.Cout, 128) * 128;
+    const long total = (long)k.M * Cpad / 4;
+    const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+    conv_splitk_epilogue_kernel<bf16_t><<<blocks, 256, 0, s>>>(k, p.splits, Cpad);
+  } else if (p.cfg == 0) {
+    conv_fwd_glds_kernel<4, 2, BUF><<<dim3(dmc::cdiv(k.M, 256), dmc::cdiv(k.Cout, 128)), 512, 0, s>>>(k);
+  } else if (p.cfg == 1) {
+    conv_fwd_glds_kernel<2, 2, BUF><<<dim3(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128)), 256, 0, s>>>(k);
+  } else {
+    conv_fwd_glds_kernel<1, 2, BUF><<<dim3(dmc::cdiv(k.M, 64), dmc::cdiv(k.Cout, 128)), 128, 0, s>>>(k);
+  }
+}
+
 template <typename T>
-int launch_fwd(const ConvK& k, hipStream_t s) {
+int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
   if (sizeof(T) == 2 && k.prologue == DMC_PRO_NONE && !getenv_flag("DMC_NO_GLDS")) {
-    // bf16, plain operands: LDS-DMA pipelined kernel; largest tile that still fills the chip
-    const long b42 = (long)dmc::cdiv(k.M, 256) * dmc::cdiv(k.Cout, 128);
-    const long b22 = (long)dmc::cdiv(k.M, 128) * dmc::cdiv(k.Cout, 128);
-    if (b42 >= 240) {
-      conv_fwd_glds_kernel<4, 2><<<dim3(dmc::cdiv(k.M, 256), dmc::cdiv(k.Cout, 128)), 512, 0, s>>>(k);
-    } else if (b22 >= 240) {
-      conv_fwd_glds_kernel<2, 2><<<dim3(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128)), 256, 0, s>>>(k);
-    } else {
-      conv_fwd_glds_kernel<1, 2><<<dim3(dmc::cdiv(k.M, 64), dmc::cdiv(k.Cout, 128)), 128, 0, s>>>(k);
-    }
+    // bf16, plain operands: LDS-DMA pipelined kernel
+    FwdPlan p = plan_glds(k);
+    if (p.splits > 1 && (ws == nullptr || ws_bytes < p.ws || getenv_flag("DMC_NO_SPLITK"))) { p.splits = 1; p.cfg = 2; }
+    if (p.splits > 1) { k.sk = (float*)ws; k.sk_per = p.per; }
+    const bool buf = k.C1 % 64 == 0 && k.C2 % 64 == 0 && k.Kc == k.C1 + k.C2 && k.x1_bytes > 0 &&
+                     (k.C2 == 0 || k.x2_bytes > 0) && k.w_bytes > 0 && !getenv_flag("DMC_NO_BUFLDS");
+    if (buf) launch_glds<true>(k, p, s);
+    else launch_glds<false>(k, p, s);
     return dmc::check_launch("dmc_conv2d");
   }
-  // tile choice: big tiles when they still give >= ~2 waves of blocks over 256 CUs
+  // register-staged kernel (fp32 parity mode, or a fused prologue)
   const long t128 = (long)dmc::cdiv(k.M, 128) * dmc::cdiv(k.Cout, 128);
   if (t128 >= 384 && k.Cout >= 128) {
     dim3 g(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128));
@@ -718,13 +874,21 @@ int wgrad_splits(const dmc_conv_desc* d, int* pps) {
 
 }  // namespace
 
+extern "C" size_t dmc_conv2d_workspace(const dmc_conv_desc* d) {
+  ConvK k;
+  if (fill_convk(d, nullptr, nullptr, nullptr, nullptr, nullptr, k)) return 0;
+  if (d->dtype != DMC_BF16 || d->prologue != DMC_PRO_NONE || k.M == 0) return 0;
+  return plan_glds(k).ws;
+}
+
 extern "C" int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2, const void* w, void* y1,
-                          void* y2, void* stream) {
+                          void* y2, void* workspace, size_t ws_bytes, void* stream) {
   ConvK k;
   if (fill_convk(d, x1, x2, w, y1, y2, k)) return 1;
   hipStream_t s = dmc::as_stream(stream);
   if (k.M == 0 || k.Cout == 0) return 0;
-  return d->dtype == DMC_F32 ? launch_fwd<float>(k, s) : launch_fwd<bf16_t>(k, s);
+  return d->dtype == DMC_F32 ? launch_fwd<float>(k, workspace, ws_bytes, s)
+                             : launch_fwd<bf16_t>(k, workspace, ws_bytes, s);
 }
 
 extern "C" size_t dmc_conv2d_wgrad_workspace(const dmc_conv_desc* d) {

@@ -229,21 +229,31 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float* in, int R, in
 // GroupNorm-apply (+SiLU, +dropout) materialised once per element: a = drop(silu(x*scale[n,c] + shift[n,c])).
 // Used where the consumer re-reads the activation many times (3x3 implicit GEMM reads each pixel 9x) and
 // by the backward (weight gradients read `a` directly, dropout masks never stored).
+// Grid (N, pixel splits); a thread owns one 16-byte channel chunk column (its scale/shift stay in
+// registers) and walks pixels of one sample, so each wave streams whole contiguous rows.
 template <typename T>
 __global__ __launch_bounds__(256) void gn_apply_kernel(Src2 s, int HW, const float* scale, const float* shift,
                                                        int silu, uint32_t seed, uint32_t thresh, float dscale, char* out,
-                                                       int ldo, long total) {
+                                                       int ldo, int splits) {
   constexpr int EPC = TT<T>::KPL;
   const int C = s.C1 + s.C2, CPR = C / EPC;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int col = i % CPR;
-    const long pix = i / CPR;
-    const int n = pix / HW;
-    const int c0 = col * EPC;
+  const int rpi = 256 / CPR;
+  const int col = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
+  if (r0 >= rpi) return;
+  const int n = blockIdx.x;
+  const int per = (HW + splits - 1) / splits;
+  const int pb = blockIdx.y * per, pe = min(HW, pb + per);
+  const int c0 = col * EPC;
+  float sc[EPC], sh[EPC];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) {
+    sc[e] = scale[(size_t)n * C + c0 + e];
+    sh[e] = shift[(size_t)n * C + c0 + e];
+  }
+  for (int p = pb + r0; p < pe; p += rpi) {
+    const int pix = n * HW + p;
     float f[EPC];
-    Chunk<T>::unpack(load_chunk2<T>(s, (int)pix, c0), f);
-    const float* sc = scale + (size_t)n * C + c0;
-    const float* sh = shift + (size_t)n * C + c0;
+    Chunk<T>::unpack(load_chunk2<T>(s, pix, c0), f);
 #pragma unroll
     for (int e = 0; e < EPC; ++e) {
       float v = fmaf(f[e], sc[e], sh[e]);
@@ -442,16 +452,20 @@ extern "C" int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, in
                             const float* scale, const float* shift, int silu, uint32_t drop_seed, uint32_t drop_thresh,
                             float drop_scale, void* out, int ld_out, void* stream) {
   const int epc = dtype == DMC_F32 ? 4 : 8;
-  DMC_REQUIRE(C1 % epc == 0 && C2 % epc == 0 && ld_out % epc == 0, "gn_apply: channel alignment");
-  const long total = (long)N * HW * ((C1 + C2) / epc);
-  const int blocks = (int)((total + 255) / 256 < 16384 ? (total + 255) / 256 : 16384);
+  DMC_REQUIRE(C1 % epc == 0 && C2 % epc == 0 && ld_out % epc == 0 && (C1 + C2) / epc <= 256,
+              "gn_apply: channel alignment");
+  const int cpr = (C1 + C2) / epc, rpi = 256 / cpr;
+  int splits = (2048 + N - 1) / N;                       // ~2048 blocks in flight
+  const int maxs = (HW + rpi - 1) / rpi;
+  splits = splits < maxs ? splits : maxs;
   hipStream_t s = dmc::as_stream(stream);
   Src2 src{(const char*)x1, (const char*)x2, C1, C2, ld1, ld2};
+  dim3 g(N, splits);
   if (dtype == DMC_F32)
-    gn_apply_kernel<float><<<blocks, 256, 0, s>>>(src, HW, scale, shift, silu, drop_seed, drop_thresh, drop_scale,
-                                                  (char*)out, ld_out, total);
+    gn_apply_kernel<float><<<g, 256, 0, s>>>(src, HW, scale, shift, silu, drop_seed, drop_thresh, drop_scale,
+                                             (char*)out, ld_out, splits);
   else
-    gn_apply_kernel<bf16_t><<<blocks, 256, 0, s>>>(src, HW, scale, shift, silu, drop_seed, drop_thresh, drop_scale,
-                                                   (char*)out, ld_out, total);
+    gn_apply_kernel<bf16_t><<<g, 256, 0, s>>>(src, HW, scale, shift, silu, drop_seed, drop_thresh, drop_scale,
+                                              (char*)out, ld_out, splits);
   return dmc::check_launch("dmc_gn_apply");
 }

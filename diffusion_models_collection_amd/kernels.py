@@ -50,6 +50,7 @@ def make_desc(dtype, N, H, W, C1, C2, ld1, ld2, Kc, OH, OW, Cout, taps, mode=L.M
 
 def set_prologue(d, kind=L.PRO_NONE, scale=None, shift=None, ld=0, drop=None, drop_ld=0):
     d.prologue = kind
+    d._keep_pro = (scale, shift)   # the descriptor holds raw pointers: keep the tensors alive with it
     d.pro_scale = ptr(scale)
     d.pro_shift = ptr(shift)
     d.ld_pro = ld
@@ -62,6 +63,7 @@ def set_prologue(d, kind=L.PRO_NONE, scale=None, shift=None, ld=0, drop=None, dr
 
 def set_epilogue(d, bias=None, addvec=None, ld_add=0, resid=None, ld_res=0, silu_pre=None, ld_silu=0,
                  ldy1=0, ldy2=0, Csplit=None, out_f32=False, out_nchw=False):
+    d._keep_epi = (bias, addvec, resid, silu_pre)   # keep the tensors behind the raw pointers alive
     d.bias = ptr(bias)
     d.addvec = ptr(addvec)
     d.ld_add = ld_add
@@ -76,7 +78,10 @@ def set_epilogue(d, bias=None, addvec=None, ld_add=0, resid=None, ld_res=0, silu
 
 
 def conv(d, x1, x2, w, y1, y2=None):
-    check(LIB.dmc_conv2d(ctypes.byref(d), ptr(x1), ptr(x2), ptr(w), ptr(y1), ptr(y2), L.stream()), "dmc_conv2d")
+    nbytes = LIB.dmc_conv2d_workspace(ctypes.byref(d))
+    ws = SCRATCH.get(nbytes, y1.device) if nbytes else None
+    check(LIB.dmc_conv2d(ctypes.byref(d), ptr(x1), ptr(x2), ptr(w), ptr(y1), ptr(y2), ptr(ws), nbytes, L.stream()),
+          "dmc_conv2d")
 
 
 def wgrad(d, dy, ld_dy, x1, x2, dw, scale=1.0):

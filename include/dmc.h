@@ -68,9 +68,12 @@ typedef struct dmc_conv_desc {
   int out_nchw;              /* y1 is NCHW fp32 [N][Cout][OH][OW] */
 } dmc_conv_desc;
 
-/* y = conv(x) with fused prologue/epilogue. w = packed [Cout][ntaps][Kc] (dtype). */
+/* y = conv(x) with fused prologue/epilogue. w = packed [Cout][ntaps][Kc] (dtype).
+ * workspace (dmc_conv2d_workspace() bytes, may be 0) enables split-K for small-M shapes; with a NULL
+ * or too small workspace the call still succeeds without split-K. */
+size_t dmc_conv2d_workspace(const dmc_conv_desc* d);
 int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2, const void* w,
-               void* y1, void* y2, void* stream);
+               void* y1, void* y2, void* workspace, size_t ws_bytes, void* stream);
 
 /* Weight gradient of the same convolution: dw[co][c][t] (fp32, reference nn.Conv2d layout,
  * multiplied by `scale`) = sum over pixels of dy[pix][co] * prologue(x)[coord(pix,t)][c].

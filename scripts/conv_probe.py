@@ -1,0 +1,67 @@
+"""Time the bf16 forward conv on the UNet's layer shapes (HIP events on the launch stream).
+
+Used standalone and under `rocprofv3 --pmc ...` to read counters for one kernel at a time:
+    python scripts/conv_probe.py [--shape NAME] [--iters N]
+"""
+import argparse
+import ctypes
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from diffusion_models_collection_amd import _lib as L, kernels as K  # noqa: E402
+
+# name: (B, H, W, C1, C2, Cout, taps)
+SHAPES = {
+    "r128_32": (128, 32, 32, 128, 0, 128, "3"),      # ResBlock 128->128 @32x32 (the bench roofline kernel)
+    "r384_32": (128, 32, 32, 256, 128, 128, "3"),    # decoder concat 384->128 @32x32
+    "r256_16": (128, 16, 16, 256, 0, 256, "3"),
+    "r512_8": (128, 8, 8, 256, 256, 256, "3"),       # small M: split-K
+    "r512_4": (128, 4, 4, 256, 256, 256, "3"),
+    "qkv_16": (128, 16, 16, 256, 0, 768, "1"),
+}
+
+
+def run(name, iters):
+    B, H, W, C1, C2, Cout, kind = SHAPES[name]
+    dt = torch.bfloat16
+    dev = "cuda"
+    taps = K.TAPS3 if kind == "3" else K.TAPS1
+    kk = 3 if kind == "3" else 1
+    x1 = torch.randn(B, H, W, C1, device=dev).to(dt)
+    x2 = torch.randn(B, H, W, C2, device=dev).to(dt) if C2 else None
+    w = torch.randn(Cout, C1 + C2, kk, kk, device=dev) * 0.03
+    Kc = L.kc_for(C1 + C2, dt)
+    wp = K.pack_weight(L.PACK_FWD, dt, w, Kc)
+    y = torch.empty(B, H, W, Cout, device=dev, dtype=dt)
+    d = K.make_desc(dt, B, H, W, C1, C2, C1, C2, Kc, H, W, Cout, taps)
+    K.set_epilogue(d, bias=torch.randn(Cout, device=dev), ldy1=Cout)
+    ws = L.LIB.dmc_conv2d_workspace(ctypes.byref(d))
+    for _ in range(3):
+        K.conv(d, x1, x2, wp, y)
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        K.conv(d, x1, x2, wp, y)
+    e1.record(s)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    flops = 2.0 * B * H * W * Cout * (C1 + C2) * kk * kk
+    print(f"{name:8s} M={B*H*W:7d} K={(C1+C2)*kk*kk:5d} N={Cout:4d} splitk_ws={ws/2**20:6.1f}MiB "
+          f"{ms*1e3:8.1f} us  {flops/ms/1e9:7.1f} TFLOP/s", flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="all")
+    ap.add_argument("--iters", type=int, default=50)
+    a = ap.parse_args()
+    for name in (SHAPES if a.shape == "all" else [a.shape]):
+        run(name, a.iters)
+
+
+if __name__ == "__main__":
+    main()

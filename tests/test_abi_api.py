@@ -38,7 +38,8 @@ def test_descriptor_validation_errors():
     d = K.make_desc(torch.float32, 1, 4, 4, 6, 0, 8, 0, 32, 4, 4, 8, K.TAPS3)   # C1=6 not multiple of 4
     K.set_prologue(d, L.PRO_AFFINE_SILU)
     with pytest.raises(L.DMCError, match="multiples"):
-        L.check(L.LIB.dmc_conv2d(__import__("ctypes").byref(d), None, None, None, None, None, None), "conv")
+        L.check(L.LIB.dmc_conv2d(__import__("ctypes").byref(d), None, None, None, None, None, None, 0, None),
+                    "conv")
     with pytest.raises(L.DMCError, match="head dim"):
         L.check(L.LIB.dmc_attn_fwd(0, None, 768, 1, 16, 4, 100, None, 256, None, None), "attn")
 

@@ -42,14 +42,19 @@ def q(x, dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("case", ["s1_concat_gn", "s2", "up", "1x1", "ragged_in"])
+@pytest.mark.parametrize("case", ["s1_concat_gn", "s2", "up", "1x1", "ragged_in", "splitk_concat", "splitk_ragged"])
 def test_conv_forward(dt, case):
+    """splitk_*: small M with deep K, which the bf16 planner runs as split-K over grid.z + epilogue kernel."""
     L, K = _lib()
     torch.manual_seed(0)
     N, H, W = 2, 8, 8
     C1, C2, Cout = 32, 16, 48
     taps, mode, stride, k, OH, OW = K.TAPS3, L.MODE_NORMAL, 1, 3, H, W
-    if case == "s2":
+    if case == "splitk_concat":
+        N, C1, C2, Cout = 4, 192, 64, 256
+    elif case == "splitk_ragged":
+        N, C1, C2, Cout = 3, 320, 0, 200
+    elif case == "s2":
         C2, stride, OH, OW = 0, 2, 4, 4
     elif case == "up":
         C2, mode, OH, OW = 0, L.MODE_UPSAMPLE, 16, 16
@@ -88,6 +93,9 @@ def test_conv_forward(dt, case):
     y = torch.empty(N, OH, OW, Cout, dtype=dt, device=DEV)
     rd = nhwc(resid).to(dt).to(DEV)
     K.set_epilogue(d, bias=bias.to(DEV), addvec=addv.to(DEV), ld_add=Cout, resid=rd, ld_res=Cout, ldy1=Cout)
+    if case.startswith("splitk") and dt == torch.bfloat16:
+        import ctypes
+        assert L.LIB.dmc_conv2d_workspace(ctypes.byref(d)) > 0   # the planner does choose split-K here
     K.conv(d, x1d, x2d, wp, y)
     torch.cuda.synchronize()
     got = nchw(y.float().cpu())
