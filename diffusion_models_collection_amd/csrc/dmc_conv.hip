@@ -505,6 +505,186 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// 3x3 stride-1 conv (forward, or dgrad with the flipped tap grid) with the activation HALO resident in
+// LDS. A block computes 256 output pixels (whole rows: R rows x OW of nimg image segments) x 128
+// channels. Per 64-channel chunk, the (R+2) x (OW+2) halo of every segment is DMA'd into LDS once and
+// all 9 taps read their A fragments from it at a tap-dependent pixel shift; only the [128 co][64 ch]
+// weight slice streams per tap. L2->LDS bytes per chunk: halo (<= 48 KB) + 9 x 16 KB, against
+// 9 x 48 KB for per-tap operand tiles (the per-tap kernel above is bound by that fill rate).
+// Pipeline: stage s = (chunk s/9, tap s%9); 3-slot weight ring (W(s+2) issued at stage s); halo double
+// buffer, chunk c+1's halo issued in three parts during stages 9c..9c+2. Each wave waits with a
+// counted vmcnt for everything but what it issued in the previous slot.
+DMC_DEV void wait_vm_dyn(int n) {
+  switch (n) {
+    case 0: __builtin_amdgcn_s_waitcnt(waitcnt_vm(0)); break;
+    case 1: __builtin_amdgcn_s_waitcnt(waitcnt_vm(1)); break;
+    case 2: __builtin_amdgcn_s_waitcnt(waitcnt_vm(2)); break;
+    case 3: __builtin_amdgcn_s_waitcnt(waitcnt_vm(3)); break;
+    case 4: __builtin_amdgcn_s_waitcnt(waitcnt_vm(4)); break;
+    default: __builtin_amdgcn_s_waitcnt(waitcnt_vm(5)); break;  // n >= 5: waiting for more is still correct
+  }
+}
+
+constexpr int kHaloHP = 6;                       // halo DMA pieces (8 pixels each) per wave: <= 384 pixels
+
+DMC_DEV void halo_issue(const ConvK& a, char* buf, int c0, int wave, int pb, int pe, const unsigned* h1,
+                        const unsigned* h2) {
+  const bool first = c0 < a.C1;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      first ? (void*)a.x1 : (void*)a.x2, (short)0, first ? a.x1_bytes : a.x2_bytes, 0x00020000);
+  const unsigned c2 = (unsigned)(first ? c0 : c0 - a.C1) * 2u;
+#pragma unroll
+  for (int p = 0; p < kHaloHP; ++p)
+    if (p >= pb && p < pe)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(buf + (wave * kHaloHP + p) * 1024), 16,
+                                               (first ? h1[p] : h2[p]) + c2, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int nimg) {
+  using T = bf16_t;
+  constexpr int NW = 8, WM = 4, BM = 256, BN = 128, HP = kHaloHP;
+  constexpr int HB = HP * NW * 1024;             // bytes per halo buffer
+  constexpr int WB = BN * 128;                   // bytes per weight slot
+  constexpr int EP = BN * 4 + 16;                // epilogue row pitch (fp32)
+  constexpr int LDS_BYTES = (2 * HB + 3 * WB) > BM * EP ? (2 * HB + 3 * WB) : BM * EP;
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  char* const wring = lds + 2 * HB;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int lrow = lane >> 3;
+  const int lc = (lane & 7) ^ lrow;
+  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
+  const int n_first = m0 / a.OHW;
+  const int r0 = (m0 - n_first * a.OHW) / OW;
+
+  // halo DMA source offsets per piece (chunk-independent; kOOB = zero padding / past the halo)
+  unsigned h1[HP], h2[HP];
+#pragma unroll
+  for (int p = 0; p < HP; ++p) {
+    const int h = (wave * HP + p) * 8 + lrow;
+    h1[p] = kOOB; h2[p] = kOOB;
+    if (h < npix) {
+      const int img = h / segpix, rem = h - img * segpix;
+      const int hr = rem / HW, hc = rem - hr * HW;
+      const int iy = r0 + hr - 1, ix = hc - 1;
+      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
+        const unsigned sp = (unsigned)(((n_first + img) * a.H + iy) * a.W + ix);
+        h1[p] = (sp * a.ld1 + lc * 8) * 2u;
+        h2[p] = (sp * a.ld2 + lc * 8) * 2u;
+      }
+    }
+  }
+  // weight slice offsets: 2 pieces per wave per stage
+  const unsigned wrow = (unsigned)(a.ntaps * a.Kc);
+  unsigned ob[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int co = n0 + (wave * 2 + j) * 8 + lrow;
+    ob[j] = co < a.Cout ? ((unsigned)co * wrow + lc * 8) * 2u : kOOB;
+  }
+  // halo index of each fragment row for tap (0,0)
+  const int fr = lane & 15, fh = lane >> 4;
+  int hb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = wm * 64 + j * 16 + fr;
+    const int img = m / (R * OW), rem = m - img * (R * OW);
+    const int r = rem / OW, col = rem - r * OW;
+    hb[j] = img * segpix + (r + 1) * HW + col + 1;
+  }
+
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int nch = a.Kc / 64, nst = nch * 9;
+  auto issue_w = [&](int s) {
+    const int c = s / 9, t = s - c * 9;
+    const unsigned koff = (unsigned)(t * a.Kc + c * 64) * 2u;
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.w_bytes, 0x00020000);
+    char* slot = wring + (s % 3) * WB;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (LDS_AS void*)(slot + (wave * 2 + j) * 1024), 16, ob[j] + koff, 0, 0, 0);
+  };
+  auto part_b = [](int k) { return k * HP / 3; };
+  // vector-memory instructions a wave issues in slot t (after the barrier of stage t)
+  auto slot_count = [&](int t) {
+    const int c = t / 9, k = t - c * 9;
+    return (t + 2 < nst ? 2 : 0) + ((k < 3 && c + 1 < nch) ? part_b(k + 1) - part_b(k) : 0);
+  };
+
+  halo_issue(a, lds, 0, wave, 0, HP, h1, h2);
+  issue_w(0);
+  if (nst > 1) issue_w(1);
+  for (int s = 0; s < nst; ++s) {
+    wait_vm_dyn(s == 0 ? (nst > 1 ? 2 : 0) : slot_count(s - 1));
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    const int c = s / 9, t = s - c * 9;
+    if (s + 2 < nst) issue_w(s + 2);
+    if (t < 3 && c + 1 < nch) halo_issue(a, lds + ((c + 1) & 1) * HB, (c + 1) * 64, wave, part_b(t), part_b(t + 1), h1, h2);
+    const char* A = lds + (c & 1) * HB;
+    const char* Bw = wring + (s % 3) * WB;
+    const int ty = t / 3, tx = t - ty * 3;
+    const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = ks * 4 + fh;
+      v4i fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wn * 64 + i * 16 + fr;
+        fa[i] = *(const v4i*)(Bw + r * 128 + ((chunk ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int h = hb[j] + delta;
+        fb[j] = *(const v4i*)(A + h * 128 + ((chunk ^ (h & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *(v4f*)(lds + (wm * 64 + j * 16 + fr) * EP + (wn * 64 + i * 16 + fh * 4) * 4) = acc[i][j];
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < BM * BN / 4; idx += NW * 64) {
+    const int pl = idx / (BN / 4), cg = idx - pl * (BN / 4);
+    const v4f v = *(const v4f*)(lds + pl * EP + cg * 16);
+    conv_store_tile<T>(a, v, m0 + pl, n0 + cg * 4);
+  }
+}
+
+// Geometry of the halo kernel for this conv, or false if it does not apply.
+bool halo_plan(const ConvK& k, int* R, int* nimg) {
+  if (k.mode != DMC_MODE_NORMAL || k.stride != 1 || k.ntaps != 9 || k.tkw != 3) return false;
+  if (!((k.tdy0 == -1 && k.tsy == 1) || (k.tdy0 == 1 && k.tsy == -1))) return false;
+  if (!((k.tdx0 == -1 && k.tsx == 1) || (k.tdx0 == 1 && k.tsx == -1))) return false;
+  if (k.OH != k.H || k.OW != k.W) return false;
+  const int ohw = k.OH * k.OW;
+  if (ohw % 256 == 0 && 256 % k.OW == 0) { *nimg = 1; *R = 256 / k.OW; }
+  else if (256 % ohw == 0 && k.N % (256 / ohw) == 0) { *nimg = 256 / ohw; *R = k.OH; }
+  else return false;
+  const int npix = *nimg * (*R + 2) * (k.OW + 2);
+  return npix <= kHaloHP * 8 * 8;
+}
+
 // split-K reduction + the regular epilogue: out(pix, co..co+3) = epilogue(sum_z slab[z][pix][co..])
 template <typename T>
 __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvK a, int splits, int Cpad) {
@@ -840,7 +1020,10 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     if (p.splits > 1) { k.sk = (float*)ws; k.sk_per = p.per; }
     const bool buf = k.C1 % 64 == 0 && k.C2 % 64 == 0 && k.Kc == k.C1 + k.C2 && k.x1_bytes > 0 &&
                      (k.C2 == 0 || k.x2_bytes > 0) && k.w_bytes > 0 && !getenv_flag("DMC_NO_BUFLDS");
-    if (buf) launch_glds<true>(k, p, s);
+    int R, nimg;
+    if (buf && p.splits == 1 && !getenv_flag("DMC_NO_HALO") && halo_plan(k, &R, &nimg))
+      conv3x3_halo_kernel<<<dim3(k.M / 256, dmc::cdiv(k.Cout, 128)), 512, 0, s>>>(k, R, nimg);
+    else if (buf) launch_glds<true>(k, p, s);
     else launch_glds<false>(k, p, s);
     return dmc::check_launch("dmc_conv2d");
   }

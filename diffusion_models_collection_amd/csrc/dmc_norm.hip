@@ -208,10 +208,24 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float* in, int R, in
   const int c = blockIdx.x * 64 + lane;
   float s0 = 0.f, s1 = 0.f;
   if (c < C) {
+    // 4 rows in flight per thread (the row count is small: the loop is latency-, not bandwidth-bound)
     const float* p = in + (size_t)c * stride;
-    for (int r = slice; r < R; r += 16) {
+    const bool two = out1 != nullptr;
+    int r = slice;
+    for (; r + 48 < R; r += 64) {
+      float a[4], b[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] = p[(size_t)(r + 16 * u) * ld];
+      if (two) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[u] = p[(size_t)(r + 16 * u) * ld + 1];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { s0 += a[u]; s1 += b[u]; }
+    }
+    for (; r < R; r += 16) {
       s0 += p[(size_t)r * ld];
-      if (out1) s1 += p[(size_t)r * ld + 1];
+      if (two) s1 += p[(size_t)r * ld + 1];
     }
   }
   __shared__ float red[2][16][64];
@@ -265,44 +279,56 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(Src2 s, int HW, const flo
   }
 }
 
+// dx = rstd * (dz * gamma - m1 - xhat * m2) per element. Grid (N, pixel splits) like gn_apply_kernel: a
+// thread owns one 16-byte channel chunk column of one sample, so every per-channel coefficient is computed
+// once into registers and the pixel walk is pure streaming (x, g in; dx out).
 template <typename T>
-__global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, int N, const float* coef, char* dx1, char* dx2, int ld1,
+__global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* coef, char* dx1, char* dx2, int ld1,
                                                     int ld2, int acc1, int acc2) {
   constexpr int EPC = TT<T>::KPL;
-  const int C = b.s.C1 + b.s.C2, cpg = C / b.G, CPR = C / EPC;
-  const long total = (long)N * b.HW * CPR;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int col = i % CPR;
-    const int pix = i / CPR;
-    const int n = pix / b.HW;
-    const int c0 = col * EPC;
+  const int C = b.s.C1 + b.s.C2, cpg = C / b.G, CPR = C / EPC, rpi = 256 / CPR;
+  const int col = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
+  if (r0 >= rpi) return;
+  const int n = blockIdx.x;
+  const int per = (b.HW + gridDim.y - 1) / gridDim.y;
+  const int pb = blockIdx.y * per, pe = min(b.HW, pb + per);
+  const int c0 = col * EPC;
+  float mean[EPC], rstd[EPC], gm[EPC], bt[EPC], ka[EPC], kb[EPC], kc[EPC];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) {
+    const int c = c0 + e, g = c / cpg;
+    mean[e] = b.mr[((size_t)n * b.G + g) * 2];
+    rstd[e] = b.mr[((size_t)n * b.G + g) * 2 + 1];
+    gm[e] = b.gamma ? b.gamma[c] : 1.f;
+    bt[e] = b.beta ? b.beta[c] : 0.f;
+    ka[e] = rstd[e] * gm[e];
+    kb[e] = rstd[e] * coef[((size_t)n * b.G + g) * 2];
+    kc[e] = rstd[e] * coef[((size_t)n * b.G + g) * 2 + 1];
+  }
+  const bool first = c0 < b.s.C1;
+  char* const dst = first ? dx1 : dx2;
+  const int ldd = first ? ld1 : ld2, cd = first ? c0 : c0 - b.s.C1, acc = first ? acc1 : acc2;
+  for (int p = pb + r0; p < pe; p += rpi) {
+    const int pix = n * b.HW + p;
     float x[EPC], gv[EPC], o[EPC];
     Chunk<T>::unpack(load_chunk2<T>(b.s, pix, c0), x);
     Chunk<T>::unpack(*(const v4i*)(b.g + ((size_t)pix * b.ld_g + c0) * sizeof(T)), gv);
 #pragma unroll
     for (int e = 0; e < EPC; ++e) {
-      const int c = c0 + e, g = c / cpg;
-      const float mean = b.mr[((size_t)n * b.G + g) * 2], rstd = b.mr[((size_t)n * b.G + g) * 2 + 1];
-      const float gm = b.gamma ? b.gamma[c] : 1.f, bt = b.beta ? b.beta[c] : 0.f;
       float gg = gv[e];
-      if (b.dthresh) gg = drop_keep((uint64_t)pix * C + c, b.dseed, b.dthresh) ? gg * b.dscale : 0.f;
+      if (b.dthresh) gg = drop_keep((uint64_t)pix * C + c0 + e, b.dseed, b.dthresh) ? gg * b.dscale : 0.f;
       float xh;
-      const float dz = gn_dz(x[e], gg, mean, rstd, gm, bt, xh, b.silu);
-      const float m1 = coef[((size_t)n * b.G + g) * 2], m2 = coef[((size_t)n * b.G + g) * 2 + 1];
-      o[e] = rstd * (dz * gm - m1 - xh * m2);
+      const float dz = gn_dz(x[e], gg, mean[e], rstd[e], gm[e], bt[e], xh, b.silu);
+      o[e] = ka[e] * dz - kb[e] - kc[e] * xh;
     }
-    char* dst; int acc;
-    size_t off;
-    if (c0 < b.s.C1) { dst = dx1; acc = acc1; off = (size_t)pix * ld1 + c0; }
-    else { dst = dx2; acc = acc2; off = (size_t)pix * ld2 + (c0 - b.s.C1); }
-    v4i* p = (v4i*)(dst + off * sizeof(T));
+    v4i* q = (v4i*)(dst + ((size_t)pix * ldd + cd) * sizeof(T));
     if (acc) {
       float prev[EPC];
-      Chunk<T>::unpack(*p, prev);
+      Chunk<T>::unpack(*q, prev);
 #pragma unroll
       for (int e = 0; e < EPC; ++e) o[e] += prev[e];
     }
-    *p = Chunk<T>::pack(o);
+    *q = Chunk<T>::pack(o);
   }
 }
 
@@ -411,17 +437,15 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
   float* A = partial + (size_t)N * b.splits * C * 2;
   float* coef = A + (size_t)N * C * 2;
   dim3 gr(N, b.splits);
-  const long total = (long)N * HW * (C / epc);
-  const int ablocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
   if (dtype == DMC_F32) gn_bwd_partial<float><<<gr, 256, 0, s>>>(b, partial);
   else gn_bwd_partial<bf16_t><<<gr, 256, 0, s>>>(b, partial);
   gn_bwd_final<<<N, 256, 0, s>>>(C, G, HW, b.splits, partial, gamma, A, coef);
   // dbeta[c] = sum_n A[n][c][0], dgamma[c] = sum_n A[n][c][1]
   colsum_kernel<<<(C + 63) / 64, 1024, 0, s>>>(A, N, C, (long)C * 2, 2, dbeta, dgamma, 1.0f);
   if (dtype == DMC_F32)
-    gn_bwd_apply<float><<<ablocks, 256, 0, s>>>(b, N, coef, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, accumulate1, accumulate2);
+    gn_bwd_apply<float><<<gr, 256, 0, s>>>(b, coef, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, accumulate1, accumulate2);
   else
-    gn_bwd_apply<bf16_t><<<ablocks, 256, 0, s>>>(b, N, coef, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, accumulate1, accumulate2);
+    gn_bwd_apply<bf16_t><<<gr, 256, 0, s>>>(b, coef, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, accumulate1, accumulate2);
   return dmc::check_launch("dmc_gn_silu_bwd");
 }
 

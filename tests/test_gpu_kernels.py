@@ -157,6 +157,49 @@ def test_conv_dgrad_wgrad(dt, case):
     assert e1 < lim and e2 < (1e-5 if dt == torch.float32 else 1e-2), (e1, e2)
 
 
+@pytest.mark.parametrize("case", ["fwd32_concat", "fwd16_ragged_cout", "dgrad32", "fallback_4x4"])
+def test_conv3x3_halo_kernel(case, monkeypatch):
+    """bf16 3x3 stride-1 convs on the LDS-halo kernel (whole-row 256-pixel tiles) vs an fp32 reference and
+    vs the per-tap kernel (DMC_NO_HALO) on the same inputs."""
+    L, K = _lib()
+    dt = torch.bfloat16
+    torch.manual_seed(5)
+    N, H, C1, C2, Cout, taps, pm = 2, 32, 64, 64, 128, K.TAPS3, L.PACK_FWD
+    if case == "fwd16_ragged_cout":
+        N, H, C1, C2, Cout = 3, 16, 128, 0, 200
+    elif case == "dgrad32":
+        N, H, C1, C2, Cout, taps, pm = 1, 32, 192, 0, 64, K.TAPS3_DGRAD, L.PACK_DGRAD
+    elif case == "fallback_4x4":
+        N, H, C1, C2, Cout = 8, 4, 64, 0, 128     # halo of 16 images exceeds the LDS budget: per-tap kernel
+    W = H
+    Cin = C1 + C2
+    x = q(torch.randn(N, Cin, H, W), dt)
+    if pm == L.PACK_DGRAD:
+        # dgrad of a conv Cout<-Cin is a conv over the gradient with flipped/transposed weights
+        w = q(torch.randn(Cin, Cout, 3, 3) / math.sqrt(Cin * 9), dt)   # forward weight [C_fwd_out=Cin][Cout]
+        yr = torch.nn.grad.conv2d_input((N, Cout, H, W), w, x, padding=1)
+        wp = K.pack_weight(pm, dt, w.to(DEV), L.kc_for(Cin, dt))
+    else:
+        w = q(torch.randn(Cout, Cin, 3, 3) / math.sqrt(Cin * 9), dt)
+        yr = F.conv2d(x, w, padding=1)
+        wp = K.pack_weight(pm, dt, w.to(DEV), L.kc_for(Cin, dt))
+    bias = torch.randn(Cout)
+    yr = yr + bias[:, None, None]
+    xd = nhwc(x).to(dt).to(DEV)
+    x1d, x2d = (xd[..., :C1].contiguous(), xd[..., C1:].contiguous()) if C2 else (xd, None)
+    d = K.make_desc(dt, N, H, W, C1, C2, C1, C2, L.kc_for(Cin, dt), H, W, Cout, taps)
+    K.set_epilogue(d, bias=bias.to(DEV), ldy1=Cout)
+    outs = []
+    for no_halo in ("0", "1"):
+        monkeypatch.setenv("DMC_NO_HALO", no_halo)
+        y = torch.full((N, H, W, Cout), float("nan"), dtype=dt, device=DEV)
+        K.conv(d, x1d, x2d, wp, y)
+        torch.cuda.synchronize()
+        outs.append(nchw(y.float().cpu()))
+    assert rel_err(outs[0], yr) < 2e-2, rel_err(outs[0], yr)
+    assert rel_err(outs[0], outs[1]) < 1e-2
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_groupnorm_stats_and_backward(dt):
     L, K = _lib()
