@@ -855,6 +855,191 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvK a, const char* dy
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Weight gradient of a 3x3 stride-1 conv with the activation HALO resident in LDS (the wgrad twin of
+// conv3x3_halo_kernel): dW[co][t][c] = sum_p dy[p][co] * x[p + shift(t)][c].
+// Block = (64-channel chunk of x, 128 output channels, a range of 256-pixel tiles). Per tile the x halo
+// is DMA'd once and serves all 9 taps; dy streams in 64-pixel stages. 8 waves: 2 (co halves of 64) x 4
+// (quarters of the 9 taps x 4 column tiles = 36 16-wide n tiles, 9 per wave) -> 36 MFMA accumulators
+// per wave, fed by 4 dy fragments + 9 x fragments per 32-pixel k-step. Both operands are read
+// transposed (ds_read_b64_tr_b16) from [pixel][channel] images whose 32-byte segments are XOR-swizzled
+// per row (swizzle applied on the DMA source address), conflict-free for any tap shift.
+// Output: partial sums over the block's tiles -> fp32 slab [z][Cpad][9*Kc] (wgrad_reduce_kernel).
+DMC_DEV int swz_dy(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }        // 8 segments / 256-B row
+DMC_DEV int swz_x(int row) { return ((row >> 1) & 1) | (((row >> 3) & 1) << 1); }   // 4 segments / 128-B row
+
+// Transposed MFMA fragment (16 columns of segment `seg` x 8 k rows): the lane's k rows are
+// row0 + 4*half + q, q = (lane>>2)&3; RB = row pitch in bytes.
+template <int RB, bool DY>
+DMC_DEV v4i tr_frag(const char* img, int row0, int seg) {
+  const int l = threadIdx.x & 63;
+  const int q = (l >> 2) & 3, p = l & 3;
+  v4i out;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int row = row0 + 4 * half + q;
+    const int f = DY ? swz_dy(row) : swz_x(row);
+    v4s rr = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS v4s*)(uintptr_t)(img + row * RB + ((seg ^ f) << 5) + p * 8));
+    v2i ii = __builtin_bit_cast(v2i, rr);
+    out[2 * half] = ii[0];
+    out[2 * half + 1] = ii[1];
+  }
+  return out;
+}
+
+__global__ __launch_bounds__(512) void wgrad3x3_halo_kernel(ConvK a, const char* dy, int ld_dy, int dy_bytes,
+                                                            float* slab, int R, int nimg, int tiles_per_split) {
+  using T = bf16_t;
+  constexpr int HP = kHaloHP;
+  constexpr int HB = HP * 8 * 1024;      // halo buffer bytes
+  constexpr int DB = 64 * 256;           // dy stage: 64 pixels x 128 co
+  __shared__ __attribute__((aligned(16))) char lds[2 * HB + 3 * DB];
+  char* const dring = lds + 2 * HB;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave & 1, wq = wave >> 1;              // co half, n quarter
+  const int c0 = blockIdx.x * 64, co0 = blockIdx.y * 128;
+  const int ntiles = a.M / 256;
+  const int t_begin = blockIdx.z * tiles_per_split, t_end = min(ntiles, t_begin + tiles_per_split);
+  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
+  const bool first = c0 < a.C1;
+  const int cs = first ? c0 : c0 - a.C1;                // channel offset inside its source
+  const int lds_x = first ? a.ld1 : a.ld2;
+
+  // dy DMA: 2 pieces per wave per stage, piece = 4 pixel rows x 256 B; chunk-level source swizzle
+  unsigned od[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = (wave * 2 + j) * 4 + (lane >> 4);
+    const int pc = lane & 15;
+    const int lseg = (pc >> 1) ^ swz_dy(row);
+    const int co = co0 + lseg * 16 + (pc & 1) * 8;
+    od[j] = co < a.Cout ? ((unsigned)row * ld_dy + co) * 2u : kOOB;
+  }
+  // x halo DMA: lane -> (halo row, physical chunk), logical chunk from the segment swizzle of that row
+  unsigned hx[HP];
+  auto halo_offsets = [&](int tile) {
+    const int m0 = tile * 256;
+    const int n_first = m0 / a.OHW;
+    const int r0 = (m0 - n_first * a.OHW) / OW;
+#pragma unroll
+    for (int p = 0; p < HP; ++p) {
+      const int h = (wave * HP + p) * 8 + (lane >> 3);
+      hx[p] = kOOB;
+      if (h < npix) {
+        const int img = h / segpix, rem = h - img * segpix;
+        const int hr = rem / HW, hc = rem - hr * HW;
+        const int iy = r0 + hr - 1, ix = hc - 1;
+        const int lc = ((((lane & 7) >> 1) ^ swz_x(h)) << 1) | (lane & 1);
+        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+          hx[p] = ((unsigned)(((n_first + img) * a.H + iy) * a.W + ix) * lds_x + cs + lc * 8) * 2u;
+      }
+    }
+  };
+  auto halo_issue_w = [&](int buf, int pb, int pe) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        first ? (void*)a.x1 : (void*)a.x2, (short)0, first ? a.x1_bytes : a.x2_bytes, 0x00020000);
+#pragma unroll
+    for (int p = 0; p < HP; ++p)
+      if (p >= pb && p < pe)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(lds + buf * HB + (wave * HP + p) * 1024), 16, hx[p], 0, 0, 0);
+  };
+  auto dy_issue = [&](int st) {  // global stage index -> pixels [st*64, st*64+64) of the block's tile range
+    const int tile = t_begin + (st >> 2);
+    const unsigned base = (unsigned)(tile * 256 + (st & 3) * 64) * (unsigned)ld_dy * 2u;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)dy, (short)0, dy_bytes, 0x00020000);
+    char* slot = dring + (st % 3) * DB;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(slot + (wave * 2 + j) * 1024), 16, od[j] + base, 0, 0, 0);
+  };
+
+  // halo row of output pixel pl (tile-local) for tap (0,0); the lane's 8-pixel groups: pl = 32j + 8h
+  const int fh = lane >> 4;
+  int hb8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int pl = 32 * j + 8 * fh;
+    const int img = pl / (R * OW), rem = pl - img * (R * OW);
+    const int r = rem / OW, col = rem - r * OW;
+    hb8[j] = img * segpix + (r + 1) * HW + col + 1;
+  }
+  // this wave's 9 n tiles: u -> (tap, 16-channel column tile)
+  int dl[9];
+#pragma unroll
+  for (int u = 0; u < 9; ++u) {
+    const int nt = wq * 9 + u, t = nt >> 2;
+    const int ty = t / 3, tx = t - ty * 3;
+    dl[u] = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
+  }
+
+  v4f acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int u = 0; u < 9; ++u) acc[i][u] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int nt_blk = t_end - t_begin, nst = nt_blk * 4;
+  auto slot_count = [&](int st) {   // vector-memory instructions issued in slot st
+    const int k = st & 3;
+    return (st + 2 < nst ? 2 : 0) + ((k < 3 && (st >> 2) + 1 < nt_blk) ? 2 : 0);
+  };
+  if (nst > 0) {
+    halo_offsets(t_begin);
+    halo_issue_w(0, 0, HP);
+    if (nt_blk > 1) halo_offsets(t_begin + 1);
+    dy_issue(0);
+    if (nst > 1) dy_issue(1);
+  }
+  for (int st = 0; st < nst; ++st) {
+    wait_vm_dyn(st == 0 ? (nst > 1 ? 2 : 0) : slot_count(st - 1));
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    const int tl = st >> 2, k = st & 3;
+    if (st + 2 < nst) dy_issue(st + 2);
+    if (k < 3 && tl + 1 < nt_blk) {
+      halo_issue_w((tl + 1) & 1, 2 * k, 2 * k + 2);
+      if (k == 2 && tl + 2 < nt_blk) halo_offsets(t_begin + tl + 2);
+    }
+    const char* X = lds + (tl & 1) * HB;
+    const char* D = dring + (st % 3) * DB;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int j = k * 2 + ks;                          // 32-pixel group inside the tile
+      v4i fa[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = tr_frag<256, true>(D, ks * 32 + 8 * fh, wm * 4 + i);
+#pragma unroll
+      for (int u = 0; u < 9; ++u) {
+        const int nt = wq * 9 + u;
+        const v4i fb = tr_frag<128, false>(X, hb8[j] + dl[u], nt & 3);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][u] = mma16<T>(acc[i][u], fa[i], fb);
+      }
+    }
+  }
+  // partial dW -> slab [z][Cpad][9*Kc]: C[co = 4h+e][n = r]
+  const int Cpad = gridDim.y * 128;
+  const int KK = 9 * a.Kc;
+  float* out = slab + (size_t)blockIdx.z * Cpad * KK;
+  const int fr = lane & 15;
+#pragma unroll
+  for (int u = 0; u < 9; ++u) {
+    const int nt = wq * 9 + u, t = nt >> 2;
+    const int kk = t * a.Kc + c0 + (nt & 3) * 16 + fr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = co0 + wm * 64 + i * 16 + fh * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[(size_t)(co + e) * KK + kk] = acc[i][u][e];
+    }
+  }
+}
+
 // dw[co][c][t] = scale * sum_z slab[z][co][t*Kc + c]; threads walk the slab contiguously (k fastest)
 __global__ void wgrad_reduce_kernel(const float* slab, int splits, int KK, int Cpad, int Cout, int Ctot,
                                     int ntaps, int Kc, float scale, float* dw) {
@@ -1074,9 +1259,36 @@ extern "C" int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2
                              : launch_fwd<bf16_t>(k, workspace, ws_bytes, s);
 }
 
+// Halo weight-gradient plan: applies to bf16 3x3 stride-1 convs the halo forward kernel handles, with
+// 64-aligned channel sources. Splits the 256-pixel tiles so that ~256 blocks run (one per CU).
+struct WgHaloPlan {
+  bool ok;
+  int R, nimg, splits, tps;
+};
+
+WgHaloPlan wgrad_halo_plan(const dmc_conv_desc* d) {
+  WgHaloPlan p{false, 0, 0, 1, 0};
+  if (d->dtype != DMC_BF16 || getenv_flag("DMC_NO_HALO")) return p;
+  ConvK k;
+  if (fill_convk(d, nullptr, nullptr, nullptr, nullptr, nullptr, k)) return p;
+  if (k.C1 % 64 || k.C2 % 64 || k.Kc != k.C1 + k.C2 || k.x1_bytes == 0 || (k.C2 && k.x2_bytes == 0)) return p;
+  if (!halo_plan(k, &p.R, &p.nimg)) return p;
+  const int ntiles = k.M / 256;
+  const int base = (k.Kc / 64) * dmc::cdiv(k.Cout, 128);
+  int sp = (256 + base - 1) / base;
+  if (sp > ntiles) sp = ntiles;
+  if (sp < 1) sp = 1;
+  p.tps = (ntiles + sp - 1) / sp;
+  p.splits = (ntiles + p.tps - 1) / p.tps;
+  p.ok = true;
+  return p;
+}
+
 extern "C" size_t dmc_conv2d_wgrad_workspace(const dmc_conv_desc* d) {
   int pps;
-  const int splits = wgrad_splits(d, &pps);
+  int splits = wgrad_splits(d, &pps);
+  const WgHaloPlan hp = wgrad_halo_plan(d);
+  if (hp.ok && hp.splits > splits) splits = hp.splits;
   const size_t KK = (size_t)d->ntaps * d->Kc;
   const size_t Cpad = (size_t)dmc::cdiv(d->Cout, 128) * 128;
   return (size_t)splits * KK * Cpad * sizeof(float);
@@ -1090,10 +1302,16 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   DMC_REQUIRE(ld_dy % epc == 0, "wgrad: ld_dy %d alignment", ld_dy);
   hipStream_t s = dmc::as_stream(stream);
   int pps;
-  const int splits = wgrad_splits(d, &pps);
+  int splits = wgrad_splits(d, &pps);
   const int KK = d->ntaps * d->Kc;
   dim3 g(dmc::cdiv(KK, 128), dmc::cdiv(d->Cout, 128), splits);
-  if (d->dtype == DMC_F32)
+  const WgHaloPlan hp = wgrad_halo_plan(d);
+  const size_t dyb = (size_t)k.M * ld_dy * 2;
+  if (hp.ok && dyb < 0x7fff0000u) {
+    splits = hp.splits;
+    g = dim3(d->Kc / 64, dmc::cdiv(d->Cout, 128), splits);
+    wgrad3x3_halo_kernel<<<g, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
+  } else if (d->dtype == DMC_F32)
     conv_wgrad_kernel<float><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (float*)workspace, KK, pps);
   else
     conv_wgrad_kernel<bf16_t><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (float*)workspace, KK, pps);

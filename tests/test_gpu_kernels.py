@@ -198,6 +198,20 @@ def test_conv3x3_halo_kernel(case, monkeypatch):
         outs.append(nchw(y.float().cpu()))
     assert rel_err(outs[0], yr) < 2e-2, rel_err(outs[0], yr)
     assert rel_err(outs[0], outs[1]) < 1e-2
+    if pm == L.PACK_FWD:
+        # weight gradient of the same conv: halo wgrad kernel vs autograd and vs the per-tap wgrad kernel
+        g = q(torch.randn(N, Cout, H, W), dt)
+        wr = torch.nn.grad.conv2d_weight(x, w.shape, g, padding=1)
+        gd = nhwc(g).to(dt).to(DEV)
+        dws = []
+        for no_halo in ("0", "1"):
+            monkeypatch.setenv("DMC_NO_HALO", no_halo)
+            dw = torch.full(tuple(w.shape), float("nan"), device=DEV)
+            K.wgrad(d, gd, Cout, x1d, x2d, dw)
+            torch.cuda.synchronize()
+            dws.append(dw.cpu())
+        assert rel_err(dws[0], wr) < 1e-2, rel_err(dws[0], wr)
+        assert rel_err(dws[0], dws[1]) < 1e-3, rel_err(dws[0], dws[1])
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
