@@ -29,6 +29,7 @@ struct ConvK {
   float* sk;  // split-K partial slab (nullptr: no split)
   int sk_per; // K stages per split
   int x1_bytes, x2_bytes, w_bytes;  // operand extents for buffer resources (0: too large / absent)
+  int dbg;    // probe-only ablation bits of the halo kernel (env DMC_HALO_DBG; 0 in production)
 };
 
 // Source pixel of output pixel (n,oy,ox) under tap; returns -1 if it falls in the zero padding.
@@ -526,8 +527,21 @@ DMC_DEV void wait_vm_dyn(int n) {
   }
 }
 
-constexpr int kHaloHP = 6;                       // halo DMA pieces (8 pixels each) per wave: <= 384 pixels
+// N LDS-DMA pieces of 1 KB (64 lanes x 16 B) into consecutive 1-KB LDS slots dst + p*1024, lane source
+// offsets off[p] + add (kOOB-based offsets read zeros); pieces outside [pb, pe) are skipped. The buffer
+// resource is built here, not in the kernels' lambdas (hipcc drops host stubs of template kernels whose
+// lambdas capture an __amdgpu_buffer_rsrc_t).
+template <int N>
+DMC_DEV void dma_pieces(const void* base, int nbytes, char* dst, const unsigned* off, unsigned add, int pb, int pe) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nbytes, 0x00020000);
+#pragma unroll
+  for (int p = 0; p < N; ++p)
+    if (p >= pb && p < pe)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(dst + p * 1024), 16, off[p] + add, 0, 0, 0);
+}
 
+// halo DMA pieces (8 pixels each) per wave: HP = 6 covers <= 384 halo pixels, HP = 7 <= 448 (LDS-bound)
+template <int HP>
 DMC_DEV void halo_issue(const ConvK& a, char* buf, int c0, int wave, int pb, int pe, const unsigned* h1,
                         const unsigned* h2) {
   const bool first = c0 < a.C1;
@@ -535,15 +549,16 @@ DMC_DEV void halo_issue(const ConvK& a, char* buf, int c0, int wave, int pb, int
       first ? (void*)a.x1 : (void*)a.x2, (short)0, first ? a.x1_bytes : a.x2_bytes, 0x00020000);
   const unsigned c2 = (unsigned)(first ? c0 : c0 - a.C1) * 2u;
 #pragma unroll
-  for (int p = 0; p < kHaloHP; ++p)
+  for (int p = 0; p < HP; ++p)
     if (p >= pb && p < pe)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(buf + (wave * kHaloHP + p) * 1024), 16,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(buf + (wave * HP + p) * 1024), 16,
                                                (first ? h1[p] : h2[p]) + c2, 0, 0, 0);
 }
 
+template <int HP>
 __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int nimg) {
   using T = bf16_t;
-  constexpr int NW = 8, WM = 4, BM = 256, BN = 128, HP = kHaloHP;
+  constexpr int NW = 8, WM = 4, BM = 256, BN = 128;
   constexpr int HB = HP * NW * 1024;             // bytes per halo buffer
   constexpr int WB = BN * 128;                   // bytes per weight slot
   constexpr int EP = BN * 4 + 16;                // epilogue row pitch (fp32)
@@ -607,11 +622,7 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
   auto issue_w = [&](int s) {
     const int c = s / 9, t = s - c * 9;
     const unsigned koff = (unsigned)(t * a.Kc + c * 64) * 2u;
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.w_bytes, 0x00020000);
-    char* slot = wring + (s % 3) * WB;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (LDS_AS void*)(slot + (wave * 2 + j) * 1024), 16, ob[j] + koff, 0, 0, 0);
+    dma_pieces<2>(a.w, a.w_bytes, wring + (s % 3) * WB + wave * 2 * 1024, ob, koff, 0, 2);
   };
   auto part_b = [](int k) { return k * HP / 3; };
   // vector-memory instructions a wave issues in slot t (after the barrier of stage t)
@@ -620,7 +631,7 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
     return (t + 2 < nst ? 2 : 0) + ((k < 3 && c + 1 < nch) ? part_b(k + 1) - part_b(k) : 0);
   };
 
-  halo_issue(a, lds, 0, wave, 0, HP, h1, h2);
+  halo_issue<HP>(a, lds, 0, wave, 0, HP, h1, h2);
   issue_w(0);
   if (nst > 1) issue_w(1);
   for (int s = 0; s < nst; ++s) {
@@ -631,8 +642,11 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
     const int c = s / 9, t = s - c * 9;
-    if (s + 2 < nst) issue_w(s + 2);
-    if (t < 3 && c + 1 < nch) halo_issue(a, lds + ((c + 1) & 1) * HB, (c + 1) * 64, wave, part_b(t), part_b(t + 1), h1, h2);
+    if (!(a.dbg & 2)) {
+      if (s + 2 < nst) issue_w(s + 2);
+      if (t < 3 && c + 1 < nch) halo_issue<HP>(a, lds + ((c + 1) & 1) * HB, (c + 1) * 64, wave, part_b(t), part_b(t + 1), h1, h2);
+    }
+    if (a.dbg & 4) continue;
     const char* A = lds + (c & 1) * HB;
     const char* Bw = wring + (s % 3) * WB;
     const int ty = t / 3, tx = t - ty * 3;
@@ -651,10 +665,17 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
         const int h = hb[j] + delta;
         fb[j] = *(const v4i*)(A + h * 128 + ((chunk ^ (h & 7)) << 4));
       }
+      if (a.dbg & 1) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
+          for (int j = 0; j < 4; ++j) acc[i][j][0] += __builtin_bit_cast(float, fa[i][0] ^ fb[j][0]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
+      }
     }
   }
   __syncthreads();
@@ -664,6 +685,7 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
     for (int i = 0; i < 4; ++i)
       *(v4f*)(lds + (wm * 64 + j * 16 + fr) * EP + (wn * 64 + i * 16 + fh * 4) * 4) = acc[i][j];
   __syncthreads();
+  if (a.dbg & 8) return;
   for (int idx = threadIdx.x; idx < BM * BN / 4; idx += NW * 64) {
     const int pl = idx / (BN / 4), cg = idx - pl * (BN / 4);
     const v4f v = *(const v4f*)(lds + pl * EP + cg * 16);
@@ -672,17 +694,18 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
 }
 
 // Geometry of the halo kernel for this conv, or false if it does not apply.
-bool halo_plan(const ConvK& k, int* R, int* nimg) {
-  if (k.mode != DMC_MODE_NORMAL || k.stride != 1 || k.ntaps != 9 || k.tkw != 3) return false;
-  if (!((k.tdy0 == -1 && k.tsy == 1) || (k.tdy0 == 1 && k.tsy == -1))) return false;
-  if (!((k.tdx0 == -1 && k.tsx == 1) || (k.tdx0 == 1 && k.tsx == -1))) return false;
-  if (k.OH != k.H || k.OW != k.W) return false;
+// Returns the DMA pieces per wave (6 or 7) the halo needs, 0 if the halo kernels do not apply.
+int halo_plan(const ConvK& k, int* R, int* nimg) {
+  if (k.mode != DMC_MODE_NORMAL || k.stride != 1 || k.ntaps != 9 || k.tkw != 3) return 0;
+  if (!((k.tdy0 == -1 && k.tsy == 1) || (k.tdy0 == 1 && k.tsy == -1))) return 0;
+  if (!((k.tdx0 == -1 && k.tsx == 1) || (k.tdx0 == 1 && k.tsx == -1))) return 0;
+  if (k.OH != k.H || k.OW != k.W) return 0;
   const int ohw = k.OH * k.OW;
   if (ohw % 256 == 0 && 256 % k.OW == 0) { *nimg = 1; *R = 256 / k.OW; }
   else if (256 % ohw == 0 && k.N % (256 / ohw) == 0) { *nimg = 256 / ohw; *R = k.OH; }
-  else return false;
+  else return 0;
   const int npix = *nimg * (*R + 2) * (k.OW + 2);
-  return npix <= kHaloHP * 8 * 8;
+  return npix <= 6 * 64 ? 6 : npix <= 7 * 64 ? 7 : 0;
 }
 
 // split-K reduction + the regular epilogue: out(pix, co..co+3) = epilogue(sum_z slab[z][pix][co..])
@@ -887,10 +910,10 @@ DMC_DEV v4i tr_frag(const char* img, int row0, int seg) {
   return out;
 }
 
+template <int HP>
 __global__ __launch_bounds__(512) void wgrad3x3_halo_kernel(ConvK a, const char* dy, int ld_dy, int dy_bytes,
                                                             float* slab, int R, int nimg, int tiles_per_split) {
   using T = bf16_t;
-  constexpr int HP = kHaloHP;
   constexpr int HB = HP * 8 * 1024;      // halo buffer bytes
   constexpr int DB = 64 * 256;           // dy stage: 64 pixels x 128 co
   __shared__ __attribute__((aligned(16))) char lds[2 * HB + 3 * DB];
@@ -938,33 +961,25 @@ __global__ __launch_bounds__(512) void wgrad3x3_halo_kernel(ConvK a, const char*
     }
   };
   auto halo_issue_w = [&](int buf, int pb, int pe) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        first ? (void*)a.x1 : (void*)a.x2, (short)0, first ? a.x1_bytes : a.x2_bytes, 0x00020000);
-#pragma unroll
-    for (int p = 0; p < HP; ++p)
-      if (p >= pb && p < pe)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(lds + buf * HB + (wave * HP + p) * 1024), 16, hx[p], 0, 0, 0);
+    dma_pieces<HP>(first ? (const void*)a.x1 : (const void*)a.x2, first ? a.x1_bytes : a.x2_bytes,
+                   lds + buf * HB + wave * HP * 1024, hx, 0u, pb, pe);
   };
   auto dy_issue = [&](int st) {  // global stage index -> pixels [st*64, st*64+64) of the block's tile range
     const int tile = t_begin + (st >> 2);
     const unsigned base = (unsigned)(tile * 256 + (st & 3) * 64) * (unsigned)ld_dy * 2u;
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)dy, (short)0, dy_bytes, 0x00020000);
-    char* slot = dring + (st % 3) * DB;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(slot + (wave * 2 + j) * 1024), 16, od[j] + base, 0, 0, 0);
+    dma_pieces<2>(dy, dy_bytes, dring + (st % 3) * DB + wave * 2 * 1024, od, base, 0, 2);
   };
 
-  // halo row of output pixel pl (tile-local) for tap (0,0); the lane's 8-pixel groups: pl = 32j + 8h
+  // halo row of tile-local output pixel pl for tap (0,0). The lane's 8-pixel group of k-step j is
+  // pl = 32j + 8h; since 32j moves by whole rows / images, hrow(32j + 8h) = hrow(8h) + hrow(32j) - hrow(0)
+  // (a wave-uniform shift).
   const int fh = lane >> 4;
-  int hb8[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int pl = 32 * j + 8 * fh;
+  auto hrow = [&](int pl) {
     const int img = pl / (R * OW), rem = pl - img * (R * OW);
     const int r = rem / OW, col = rem - r * OW;
-    hb8[j] = img * segpix + (r + 1) * HW + col + 1;
-  }
+    return img * segpix + (r + 1) * HW + col + 1;
+  };
+  const int hb0 = hrow(8 * fh), hz = hrow(0);
   // this wave's 9 n tiles: u -> (tap, 16-channel column tile)
   int dl[9];
 #pragma unroll
@@ -1010,13 +1025,14 @@ __global__ __launch_bounds__(512) void wgrad3x3_halo_kernel(ConvK a, const char*
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int j = k * 2 + ks;                          // 32-pixel group inside the tile
+      const int hj = __builtin_amdgcn_readfirstlane(hrow(32 * j) - hz);
       v4i fa[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) fa[i] = tr_frag<256, true>(D, ks * 32 + 8 * fh, wm * 4 + i);
 #pragma unroll
       for (int u = 0; u < 9; ++u) {
         const int nt = wq * 9 + u;
-        const v4i fb = tr_frag<128, false>(X, hb8[j] + dl[u], nt & 3);
+        const v4i fb = tr_frag<128, false>(X, hb0 + hj + dl[u], nt & 3);
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i][u] = mma16<T>(acc[i][u], fa[i], fb);
       }
@@ -1043,15 +1059,24 @@ __global__ __launch_bounds__(512) void wgrad3x3_halo_kernel(ConvK a, const char*
 // dw[co][c][t] = scale * sum_z slab[z][co][t*Kc + c]; threads walk the slab contiguously (k fastest)
 __global__ void wgrad_reduce_kernel(const float* slab, int splits, int KK, int Cpad, int Cout, int Ctot,
                                     int ntaps, int Kc, float scale, float* dw) {
-  const long total = (long)Cout * KK;
+  const int total = Cout * KK;   // < 2^31: weights of one conv
   const size_t zstride = (size_t)Cpad * KK;
-  for (long o = blockIdx.x * (long)blockDim.x + threadIdx.x; o < total; o += (long)gridDim.x * blockDim.x) {
-    const int k = o % KK;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
     const int co = o / KK;
+    const int k = o - co * KK;
     const int t = k / Kc, c = k - t * Kc;
     if (c >= Ctot) continue;
     float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += slab[(size_t)z * zstride + o];
+    // 8 independent loads in flight (fixed order: deterministic)
+    int z = 0;
+    for (; z + 8 <= splits; z += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = slab[(size_t)(z + u) * zstride + o];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; z < splits; ++z) s += slab[(size_t)z * zstride + o];
     dw[((size_t)co * Ctot + c) * ntaps + t] = s * scale;
   }
 }
@@ -1134,6 +1159,7 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
   k.Csplit = d->Csplit; k.ldy1 = d->ldy1; k.ldy2 = d->ldy2; k.out_f32 = d->out_f32; k.out_nchw = d->out_nchw;
   k.M = d->N * d->OH * d->OW; k.OHW = d->OH * d->OW;
   k.sk = nullptr; k.sk_per = 0;
+  k.dbg = 0;
   {
     const size_t esz = d->dtype == DMC_F32 ? 4 : 2;
     const size_t b1 = (size_t)d->N * d->H * d->W * d->ld1 * esz;
@@ -1206,8 +1232,15 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     const bool buf = k.C1 % 64 == 0 && k.C2 % 64 == 0 && k.Kc == k.C1 + k.C2 && k.x1_bytes > 0 &&
                      (k.C2 == 0 || k.x2_bytes > 0) && k.w_bytes > 0 && !getenv_flag("DMC_NO_BUFLDS");
     int R, nimg;
-    if (buf && p.splits == 1 && !getenv_flag("DMC_NO_HALO") && halo_plan(k, &R, &nimg))
-      conv3x3_halo_kernel<<<dim3(k.M / 256, dmc::cdiv(k.Cout, 128)), 512, 0, s>>>(k, R, nimg);
+    const int hp = (buf && p.splits == 1 && !getenv_flag("DMC_NO_HALO")) ? halo_plan(k, &R, &nimg) : 0;
+    if (hp) {
+      const char* dbg = getenv("DMC_HALO_DBG");
+      k.dbg = dbg ? atoi(dbg) : 0;
+    }
+    if (hp == 6)
+      conv3x3_halo_kernel<6><<<dim3(k.M / 256, dmc::cdiv(k.Cout, 128)), 512, 0, s>>>(k, R, nimg);
+    else if (hp == 7)
+      conv3x3_halo_kernel<7><<<dim3(k.M / 256, dmc::cdiv(k.Cout, 128)), 512, 0, s>>>(k, R, nimg);
     else if (buf) launch_glds<true>(k, p, s);
     else launch_glds<false>(k, p, s);
     return dmc::check_launch("dmc_conv2d");
@@ -1263,16 +1296,17 @@ extern "C" int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2
 // 64-aligned channel sources. Splits the 256-pixel tiles so that ~256 blocks run (one per CU).
 struct WgHaloPlan {
   bool ok;
-  int R, nimg, splits, tps;
+  int R, nimg, splits, tps, hp;
 };
 
 WgHaloPlan wgrad_halo_plan(const dmc_conv_desc* d) {
-  WgHaloPlan p{false, 0, 0, 1, 0};
+  WgHaloPlan p{false, 0, 0, 1, 0, 0};
   if (d->dtype != DMC_BF16 || getenv_flag("DMC_NO_HALO")) return p;
   ConvK k;
   if (fill_convk(d, nullptr, nullptr, nullptr, nullptr, nullptr, k)) return p;
   if (k.C1 % 64 || k.C2 % 64 || k.Kc != k.C1 + k.C2 || k.x1_bytes == 0 || (k.C2 && k.x2_bytes == 0)) return p;
-  if (!halo_plan(k, &p.R, &p.nimg)) return p;
+  p.hp = halo_plan(k, &p.R, &p.nimg);
+  if (!p.hp) return p;
   const int ntiles = k.M / 256;
   const int base = (k.Kc / 64) * dmc::cdiv(k.Cout, 128);
   int sp = (256 + base - 1) / base;
@@ -1310,7 +1344,10 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   if (hp.ok && dyb < 0x7fff0000u) {
     splits = hp.splits;
     g = dim3(d->Kc / 64, dmc::cdiv(d->Cout, 128), splits);
-    wgrad3x3_halo_kernel<<<g, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
+    if (hp.hp == 6)
+      wgrad3x3_halo_kernel<6><<<g, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
+    else
+      wgrad3x3_halo_kernel<7><<<g, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
   } else if (d->dtype == DMC_F32)
     conv_wgrad_kernel<float><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (float*)workspace, KK, pps);
   else

@@ -157,7 +157,7 @@ def test_conv_dgrad_wgrad(dt, case):
     assert e1 < lim and e2 < (1e-5 if dt == torch.float32 else 1e-2), (e1, e2)
 
 
-@pytest.mark.parametrize("case", ["fwd32_concat", "fwd16_ragged_cout", "dgrad32", "fallback_4x4"])
+@pytest.mark.parametrize("case", ["fwd32_concat", "fwd16_ragged_cout", "dgrad32", "fwd8_multi_image", "fallback_4x4"])
 def test_conv3x3_halo_kernel(case, monkeypatch):
     """bf16 3x3 stride-1 convs on the LDS-halo kernel (whole-row 256-pixel tiles) vs an fp32 reference and
     vs the per-tap kernel (DMC_NO_HALO) on the same inputs."""
@@ -169,6 +169,8 @@ def test_conv3x3_halo_kernel(case, monkeypatch):
         N, H, C1, C2, Cout = 3, 16, 128, 0, 200
     elif case == "dgrad32":
         N, H, C1, C2, Cout, taps, pm = 1, 32, 192, 0, 64, K.TAPS3_DGRAD, L.PACK_DGRAD
+    elif case == "fwd8_multi_image":
+        N, H, C1, C2, Cout = 8, 8, 128, 64, 128   # 4 whole 8x8 images per 256-pixel tile (7 halo pieces/wave)
     elif case == "fallback_4x4":
         N, H, C1, C2, Cout = 8, 4, 64, 0, 128     # halo of 16 images exceeds the LDS budget: per-tap kernel
     W = H
