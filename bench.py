@@ -34,6 +34,7 @@ CIFAR = dict(image_size=(32, 32), in_channels=3, model_channels=128, out_channel
              attention_resolutions=(16, 8), dropout=0.1, channel_mult=(1, 2, 2, 2), use_attention=True)
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense, MI355X_MICROARCH.md
 TRAIN_GFLOP_PER_IMG = 37.890     # fwd + bwd, = 3 x 12.632 forward
+PMC_FILE = "r1_pmc_roofline_conv.json"
 
 
 def log(*a):
@@ -71,11 +72,23 @@ def conv_roofline(dtype, B=128):
     avg_ms = e0.elapsed_time(e1) / n
     flops = 2.0 * B * H * W * C * C * 9
     achieved = flops / (avg_ms * 1e-3) / 1e12
-    return {"kernel": "conv_fwd_glds_kernel<4,2> bf16 implicit GEMM (ResBlock 3x3 128->128 @32x32, B=128, "
+    return {"kernel": "conv3x3_halo_kernel bf16 implicit GEMM (ResBlock 3x3 128->128 @32x32, B=128, "
                       "bias+temb epilogue)" if dtype == torch.bfloat16 else "conv_fwd_kernel<f32,128,128>",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
-            "flops_per_launch": flops, "avg_launch_ms": round(avg_ms, 4)}
+            "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic(),
+            "flops_per_launch": flops, "avg_launch_ms": round(avg_ms, 4),
+            "algorithmic_bytes_per_launch": 2 * (2 * B * H * W * C) + 2 * C * 9 * C}
+
+
+def pmc_traffic():
+    """HBM bytes per launch of the roofline conv from the committed rocprofv3 --pmc passes
+    (profiles/PMC_FILE, written by scripts/pmc_to_json.py: FETCH_SIZE doubled per the gfx950 correction of
+    MI355X_MICROARCH.md + WRITE_SIZE, averaged over the dispatches of the kernel), or None if absent."""
+    f = os.path.join(ROOT, "profiles", PMC_FILE)
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        return json.load(fh).get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(B=32, warm=1, steps=3, threads=16):
@@ -125,7 +138,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--sample-steps", type=int, default=50)
+    ap.add_argument("--roofline-only", action="store_true", help="time only the roofline conv (PMC passes)")
     args = ap.parse_args()
+    if args.roofline_only:
+        print(json.dumps(conv_roofline(torch.bfloat16 if args.dtype == "bf16" else torch.float32)), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -1,0 +1,29 @@
+#!/bin/bash
+# One GPU session: parity tests, the bench line, a kernel-trace profile of the bench, PMC traffic of the
+# roofline conv. Every GPU step has its own time limit; the first failure ends the script.
+set -e -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/${1:-round}
+mkdir -p "$O"
+STAGES=${STAGES:-tbpm}
+if [[ $STAGES == *t* ]]; then
+  timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$O/pytest_gpu.log" 2>&1 \
+    || { tail -30 "$O/pytest_gpu.log"; exit 1; }
+  tail -3 "$O/pytest_gpu.log"
+fi
+if [[ $STAGES == *b* ]]; then
+  timeout -k 10 500 python -u bench.py > "$O/bench.json" 2> "$O/bench.err" || { tail -30 "$O/bench.err"; exit 1; }
+  cat "$O/bench.json"
+fi
+if [[ $STAGES == *p* ]]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o prof --output-format csv -- \
+    python3 bench.py --steps 10 --warmup 3 --no-cpu > "$O/prof_bench.json" 2> "$O/prof_bench.err" \
+    || { tail -30 "$O/prof_bench.err"; exit 1; }
+  f=$(find "$O/prof" -name '*kernel_stats.csv' | head -1); python3 scripts/prof_summary.py "$f" 10 20
+fi
+if [[ $STAGES == *m* ]]; then
+  P="python3 bench.py --roofline-only"
+  timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d "$O/fetch" -o fetch --output-format csv -- $P > /dev/null
+  timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d "$O/write" -o write --output-format csv -- $P > /dev/null
+  python3 scripts/pmc_to_json.py "$O/fetch" "$O/write" conv3x3_halo_kernel "$O/pmc_roofline_conv.json"
+fi
