@@ -138,6 +138,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--sample-steps", type=int, default=50)
+    ap.add_argument("--no-train", action="store_true", help="sampling only (profiling)")
     ap.add_argument("--roofline-only", action="store_true", help="time only the roofline conv (PMC passes)")
     args = ap.parse_args()
     if args.roofline_only:
@@ -170,13 +171,15 @@ def main():
     pool = [torch.rand(B, 3, 32, 32, device=dev, generator=gen) * 2 - 1 for _ in range(4)]
 
     model.train()
+    if args.no_train:
+        args.warmup, args.steps = 0, 1
     for i in range(args.warmup):
         trainer.train_step(pool[i % 4], 0)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(args.steps if not args.no_train else 0):
         trainer.train_step(pool[i % 4], 0)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0

@@ -37,6 +37,11 @@ class ConvDesc(ctypes.Structure):
     ]
 
 
+class PackJob(ctypes.Structure):
+    _fields_ = [("w", _c_p), ("dst", _c_p), ("dtype", _c_int), ("mode", _c_int), ("Cout", _c_int), ("Cin", _c_int),
+                ("kh", _c_int), ("kw", _c_int), ("Kc", _c_int), ("koff", _c_int)]
+
+
 class TensorRef(ctypes.Structure):
     _fields_ = [("a", _c_p), ("b", _c_p), ("n", _c_long)]
 
@@ -55,6 +60,8 @@ def _load():
         "dmc_conv2d_wgrad_workspace": (_c_size, [ctypes.POINTER(ConvDesc)]),
         "dmc_conv2d_wgrad": (_c_int, [ctypes.POINTER(ConvDesc), _c_p, _c_int, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p]),
         "dmc_pack_weight": (_c_int, [_c_int, _c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p]),
+        "dmc_pack_tiles": (_c_int, [ctypes.POINTER(PackJob), _c_int, _c_p, _c_int]),
+        "dmc_pack_weights": (_c_int, [_c_p, _c_p, _c_int, _c_p]),
         "dmc_gn_workspace": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
         "dmc_gn_stats": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_f,
                                   _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
@@ -86,6 +93,8 @@ def _load():
                                 _c_p]),
         "dmc_ema_update": (_c_int, [_c_p, _c_int, _c_f, _c_p]),
         "dmc_clip_grad_norm": (_c_int, [_c_p, _c_int, _c_f, _c_p, _c_p, _c_p]),
+        "dmc_grad_norm_flat": (_c_int, [_c_p, _c_long, _c_f, _c_p, _c_p, _c_p, _c_p]),
+        "dmc_adamw_flat": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_long, _c_p] + [_c_f] * 9 + [_c_p]),
         "dmc_silu_fwd": (_c_int, [_c_p, _c_p, _c_long, _c_p]),
         "dmc_unpack_output": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p]),
         "dmc_add": (_c_int, [_c_int, _c_p, _c_p, _c_long, _c_p]),

@@ -1082,41 +1082,111 @@ __global__ void wgrad_reduce_kernel(const float* slab, int splits, int KK, int C
 }
 
 // ---------------------------------------------------------------------------------------------
+// Value of packed element (row, tap t, column k) of an fp32 master weight [Cout][Cin][kh][kw].
+// FWD: dst[co][t][c]; DGRAD: dst[c][t][co]; UPDGRAD: dst[c][u*4+v][co] (nearest-x2 upsample folded into a
+// 4x4 stride-2 kernel). Columns past the source extent are the zero padding of Kc.
+DMC_DEV float pack_value(int mode, const float* w, int Cout, int Cin, int kh, int kw, int row, int t, int k) {
+  if (mode == DMC_PACK_FWD) return k < Cin ? w[((size_t)row * Cin + k) * kh * kw + t] : 0.f;
+  if (k >= Cout) return 0.f;
+  if (mode == DMC_PACK_DGRAD) return w[((size_t)k * Cin + row) * kh * kw + t];
+  // folded taps: offset u in {-1,0,1,2} <- set of kh with (dj + 1 - kh == u), dj in {0,1}
+  const int u = t >> 2, vv = t & 3;  // u,v index 0..3 <-> offset -1..2
+  const int khs[4][2] = {{2, -1}, {1, 2}, {0, 1}, {0, -1}};
+  const float* base = w + ((size_t)k * Cin + row) * 9;
+  float v = 0.f;
+  for (int a1 = 0; a1 < 2; ++a1) {
+    const int y = khs[u][a1];
+    if (y < 0) continue;
+    for (int b1 = 0; b1 < 2; ++b1) {
+      const int x = khs[vv][b1];
+      if (x < 0) continue;
+      v += base[y * 3 + x];
+    }
+  }
+  return v;
+}
+
 template <typename T>
 __global__ void pack_weight_kernel(int mode, const float* w, int Cout, int Cin, int kh, int kw, int Kc, T* dst) {
-  // FWD: dst[co][t][c]; DGRAD: dst[c][t][co]; UPDGRAD: dst[c][u*4+v][co] (4x4 folded kernel)
   const int ntaps = (mode == DMC_PACK_UPDGRAD) ? 16 : kh * kw;
   const int rows = (mode == DMC_PACK_FWD) ? Cout : Cin;
   const long total = (long)rows * ntaps * Kc;
   for (long o = blockIdx.x * (long)blockDim.x + threadIdx.x; o < total; o += (long)gridDim.x * blockDim.x) {
     const int k = o % Kc;
     const long r = o / Kc;
-    const int t = r % ntaps;
-    const int row = r / ntaps;
+    const float v = pack_value(mode, w, Cout, Cin, kh, kw, r / ntaps, r % ntaps, k);
+    if (sizeof(T) == 4) ((float*)dst)[o] = v;
+    else ((bf16_t*)dst)[o] = (bf16_t)f2bf(v);
+  }
+}
+
+// Every stale weight pack of a step in ONE launch (was one launch per conv and mode). The host cuts each
+// job into tiles (dmc_pack_tiles); a block packs one tile through LDS so that both the read of the fp32
+// master weight and the write of the packed rows are contiguous:
+//   FWD     tile = (row co, 256 columns k0..): reads w[co][k0..k0+255][taps] (one contiguous run),
+//           writes dst[co][t][k0..] per tap;
+//   DGRAD / UPDGRAD  tile = (8 input channels c0.., 64 output channels co0..): reads w[co][c0..c0+7][taps]
+//           (64 runs of 8*taps floats), writes dst[c][t][co0..co0+63] (64 consecutive columns).
+constexpr int kPackFwdK = 256, kPackDgC = 8, kPackDgCo = 64;
+__global__ __launch_bounds__(256) void pack_tiles_kernel(const dmc_pack_job* jobs, const int* tiles) {
+  __shared__ float sw[kPackDgCo * kPackDgC * 9 > kPackFwdK * 9 ? kPackDgCo * kPackDgC * 9 : kPackFwdK * 9];
+  const int* tl = tiles + 3 * blockIdx.x;
+  const dmc_pack_job J = jobs[tl[0]];
+  const int khkw = J.kh * J.kw;
+  const int koff = J.koff >= 0 ? J.koff : 0;
+  const bool f32 = J.dtype == DMC_F32;
+  auto store = [&](long di, float v) {
+    if (f32) ((float*)J.dst)[di] = v;
+    else ((bf16_t*)J.dst)[di] = (bf16_t)f2bf(v);
+  };
+  if (J.mode == DMC_PACK_FWD) {
+    const int co = tl[1], k0 = tl[2];
+    const int KW = J.koff >= 0 ? J.Cin : J.Kc;
+    const int kn = min(kPackFwdK, KW - k0);
+    const int kv = max(0, min(kn, J.Cin - k0));          // columns backed by the weight (rest: zero padding)
+    const float* src = J.w + ((size_t)co * J.Cin + k0) * khkw;
+    for (int i = threadIdx.x; i < kv * khkw; i += 256) sw[i] = src[i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < khkw * kn; i += 256) {
+      const int t = i / kn, k = i - t * kn;
+      store(((long)co * khkw + t) * J.Kc + koff + k0 + k, k < kv ? sw[k * khkw + t] : 0.f);
+    }
+    return;
+  }
+  const int c0 = tl[1], co0 = tl[2];
+  const int KW = J.koff >= 0 ? J.Cout : J.Kc;              // columns this job writes
+  const int cn = min(kPackDgC, J.Cin - c0), con = min(kPackDgCo, KW - co0);
+  const int cov = max(0, min(con, J.Cout - co0));           // columns backed by the weight
+  const int run = cn * khkw;
+  for (int i = threadIdx.x; i < cov * run; i += 256) {
+    const int r = i / run, j = i - r * run;
+    sw[r * kPackDgC * 9 + j] = J.w[((size_t)(co0 + r) * J.Cin + c0) * khkw + j];
+  }
+  __syncthreads();
+  const int ntaps = J.mode == DMC_PACK_UPDGRAD ? 16 : khkw;
+  for (int i = threadIdx.x; i < cn * ntaps * con; i += 256) {
+    const int q = i / con, co = i - q * con;
+    const int c = q / ntaps, t = q - c * ntaps;
     float v = 0.f;
-    if (mode == DMC_PACK_FWD) {
-      if (k < Cin) v = w[((size_t)row * Cin + k) * kh * kw + t];
-    } else if (mode == DMC_PACK_DGRAD) {
-      if (k < Cout) v = w[((size_t)k * Cin + row) * kh * kw + t];
-    } else {
-      if (k < Cout) {
-        // folded taps: offset u in {-1,0,1,2} <- set of kh with (dj + 1 - kh == u), dj in {0,1}
-        const int u = t >> 2, vv = t & 3;  // u,v index 0..3 <-> offset -1..2
+    if (co < cov) {
+      const float* wv = sw + co * kPackDgC * 9 + c * khkw;
+      if (J.mode == DMC_PACK_DGRAD) {
+        v = wv[t];
+      } else {
+        // folded nearest-x2 taps (see pack_value)
+        const int u = t >> 2, vv = t & 3;
         const int khs[4][2] = {{2, -1}, {1, 2}, {0, 1}, {0, -1}};
-        const float* base = w + ((size_t)k * Cin + row) * 9;
         for (int a1 = 0; a1 < 2; ++a1) {
           const int y = khs[u][a1];
           if (y < 0) continue;
           for (int b1 = 0; b1 < 2; ++b1) {
             const int x = khs[vv][b1];
-            if (x < 0) continue;
-            v += base[y * 3 + x];
+            if (x >= 0) v += wv[y * 3 + x];
           }
         }
       }
     }
-    if (sizeof(T) == 4) ((float*)dst)[o] = v;
-    else ((bf16_t*)dst)[o] = (bf16_t)f2bf(v);
+    store(((long)(c0 + c) * ntaps + t) * J.Kc + koff + co0 + co, v);
   }
 }
 
@@ -1375,4 +1445,30 @@ extern "C" int dmc_pack_weight(int pack_mode, int dtype, const float* w, int Cou
   else
     pack_weight_kernel<bf16_t><<<blocks, 256, 0, s>>>(pack_mode, w, Cout, Cin, kh, kw, Kc, (bf16_t*)dst);
   return dmc::check_launch("dmc_pack_weight");
+}
+
+extern "C" int dmc_pack_tiles(const dmc_pack_job* j, int job_index, int* tiles, int cap) {
+  // host helper: the tile list of one job ({job, a, b} triples), returns the count (or the needed count
+  // when tiles == NULL / cap is too small)
+  int n = 0;
+  auto put = [&](int a, int b) {
+    if (tiles && n < cap) { tiles[3 * n] = job_index; tiles[3 * n + 1] = a; tiles[3 * n + 2] = b; }
+    ++n;
+  };
+  if (j->mode == DMC_PACK_FWD) {
+    const int KW = j->koff >= 0 ? j->Cin : j->Kc;
+    for (int co = 0; co < j->Cout; ++co)
+      for (int k0 = 0; k0 < KW; k0 += kPackFwdK) put(co, k0);
+  } else {
+    const int KW = j->koff >= 0 ? j->Cout : j->Kc;
+    for (int c0 = 0; c0 < j->Cin; c0 += kPackDgC)
+      for (int co0 = 0; co0 < KW; co0 += kPackDgCo) put(c0, co0);
+  }
+  return n;
+}
+
+extern "C" int dmc_pack_weights(const dmc_pack_job* jobs, const int* tiles, int ntiles, void* stream) {
+  DMC_REQUIRE(ntiles > 0, "pack_weights: empty tile list");
+  pack_tiles_kernel<<<ntiles, 256, 0, dmc::as_stream(stream)>>>(jobs, tiles);
+  return dmc::check_launch("dmc_pack_weights");
 }

@@ -346,6 +346,90 @@ __global__ void scale_kernel(const dmc_tensor_ref* refs, const float* coef) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < r.n; i += (long)gridDim.x * blockDim.x) r.a[i] *= c;
 }
 
+// ---------------- flat optimizer step ----------------
+// Parameters, gradients, AdamW moments and the EMA copy live in flat fp32 buffers with one common layout
+// (the executor's gradient order), so clip + AdamW + EMA are one streaming pass over 37 M elements.
+constexpr int kNormBlocks = 1024;
+__global__ __launch_bounds__(256) void flat_sumsq_kernel(const float* g, long n, float* partial) {
+  // block b sums the contiguous range [b*per, (b+1)*per): fixed order, deterministic
+  const long per = ((n + kNormBlocks - 1) / kNormBlocks + 3) & ~3L;
+  const long b0 = blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
+  float s = 0.f;
+  long i = b0 + threadIdx.x * 4;
+  for (; i + 3 < b1; i += 1024) {
+    const v4f v = *(const v4f*)(g + i);
+    s = fmaf(v[0], v[0], s); s = fmaf(v[1], v[1], s); s = fmaf(v[2], v[2], s); s = fmaf(v[3], v[3], s);
+  }
+  for (; i < b1; ++i) s = fmaf(g[i], g[i], s);
+  __shared__ float red[4];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void flat_norm_final(const float* partial, float max_norm, float* total_norm,
+                                                       float* coef) {
+  float s = 0.f;
+  for (int k = threadIdx.x; k < kNormBlocks; k += 256) s += partial[k];
+  __shared__ float red[4];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float tot = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
+    total_norm[0] = tot;
+    const float c = max_norm / (tot + 1e-6f);
+    coef[0] = max_norm > 0.f ? (c < 1.0f ? c : 1.0f) : 1.0f;
+  }
+}
+
+// torch.optim.AdamW (foreach, non-amsgrad) per element, in torch's operation order:
+//   g *= clip;  p *= 1 - lr*wd;  m = lerp(m, g, 1-b1);  v = v*b2 + (1-b2)*g*g;
+//   p += -step_size * m / (sqrt(v)/bc2_sqrt + eps);  then ema = ema*d + (1-d)*p  (utils/trainer.py:198-202)
+struct AdamWArgs {
+  float* p; const float* g; float* m; float* v; float* ema;
+  const float* coef;
+  long n;
+  float wd_mul, w1, b2, omb2, neg_step, bc2_sqrt, eps, ema_d, ema_om;   // host-computed like torch (double -> float)
+};
+
+DMC_DEV void adamw_elem(const AdamWArgs& a, float c, float& p, float g, float& m, float& v, float* e) {
+  g = g * c;
+  p = p * a.wd_mul;
+  m = (a.w1 < 0.5f) ? m + a.w1 * (g - m) : g - (g - m) * (1.0f - a.w1);
+  v = v * a.b2;
+  v = v + a.omb2 * (g * g);
+  const float den = sqrtf(v) / a.bc2_sqrt + a.eps;
+  p = p + a.neg_step * (m / den);
+  if (e) *e = *e * a.ema_d + a.ema_om * p;
+}
+
+__global__ __launch_bounds__(256) void adamw_flat_kernel(AdamWArgs a) {
+  const float c = a.coef ? a.coef[0] : 1.0f;
+  const long n4 = a.n / 4;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n4; q += (long)gridDim.x * blockDim.x) {
+    const long i = q * 4;
+    v4f p = *(v4f*)(a.p + i), m = *(v4f*)(a.m + i), v = *(v4f*)(a.v + i);
+    const v4f g = *(const v4f*)(a.g + i);
+    v4f e;
+    if (a.ema) e = *(v4f*)(a.ema + i);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float pk = p[k], mk = m[k], vk = v[k], ek = e[k];
+      adamw_elem(a, c, pk, g[k], mk, vk, a.ema ? &ek : nullptr);
+      p[k] = pk; m[k] = mk; v[k] = vk; e[k] = ek;
+    }
+    *(v4f*)(a.p + i) = p; *(v4f*)(a.m + i) = m; *(v4f*)(a.v + i) = v;
+    if (a.ema) *(v4f*)(a.ema + i) = e;
+  }
+  // ragged tail (n % 4) handled by the first threads of block 0
+  if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) {
+    const long i = n4 * 4 + threadIdx.x;
+    adamw_elem(a, c, a.p[i], a.g[i], a.m[i], a.v[i], a.ema ? a.ema + i : nullptr);
+  }
+}
+
 template <typename T>
 __global__ void unpack_kernel(const T* src, int ld, int N, int C, int H, int W, float* dst) {
   const long total = (long)N * C * H * W;
@@ -492,4 +576,24 @@ extern "C" int dmc_add(int dtype, void* y, const void* x, long n, void* stream) 
 extern "C" int dmc_silu_fwd(const float* x, float* y, long n, void* stream) {
   silu_kernel<<<grid_for(n), 256, 0, dmc::as_stream(stream)>>>(x, y, n);
   return dmc::check_launch("dmc_silu_fwd");
+}
+
+extern "C" int dmc_grad_norm_flat(const float* g, long n, float max_norm, float* total_norm, float* coef, float* ws,
+                                  void* stream) {
+  DMC_REQUIRE(((uintptr_t)g & 15) == 0, "grad_norm_flat: buffer must be 16-byte aligned");
+  hipStream_t s = dmc::as_stream(stream);
+  flat_sumsq_kernel<<<kNormBlocks, 256, 0, s>>>(g, n, ws);
+  flat_norm_final<<<1, 256, 0, s>>>(ws, max_norm, total_norm, coef);
+  return dmc::check_launch("dmc_grad_norm_flat");
+}
+
+extern "C" int dmc_adamw_flat(float* p, const float* g, float* m, float* v, float* ema, long n, const float* coef,
+                              float wd_mul, float lerp_w, float beta2, float one_minus_beta2, float eps,
+                              float neg_step_size, float bc2_sqrt, float ema_decay, float ema_one_minus, void* stream) {
+  DMC_REQUIRE((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v | (uintptr_t)ema) & 15) == 0,
+              "adamw_flat: buffers must be 16-byte aligned");
+  AdamWArgs a{p, g, m, v, ema, coef, n, wd_mul, lerp_w, beta2, one_minus_beta2, neg_step_size, bc2_sqrt, eps,
+              ema_decay, ema_one_minus};
+  adamw_flat_kernel<<<grid_for(n / 4 + 1, 256, 4096), 256, 0, dmc::as_stream(stream)>>>(a);
+  return dmc::check_launch("dmc_adamw_flat");
 }

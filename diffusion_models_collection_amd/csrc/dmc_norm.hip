@@ -13,6 +13,8 @@
 
 namespace {
 
+constexpr int UNR = 4;   // pixel rows in flight per thread in the streaming walks
+
 struct Src2 {
   const char* x1; const char* x2;
   int C1, C2, ld1, ld2;
@@ -50,28 +52,40 @@ __global__ __launch_bounds__(256) void gn_stats_partial(Src2 s, int HW, int G, i
                        : ld_as_f<T>(s.x2, (size_t)n * HW * s.ld2 + (cg - s.C1));
   }
   if (active) {
-    for (int p = pb + r0; p < pe; p += rpi) {
-      float f[EPC];
-      Chunk<T>::unpack(load_chunk2<T>(s, n * HW + p, c0), f);
+    // UNR independent 16-byte loads in flight per thread (the walk is latency-bound otherwise)
+    for (int p0 = pb + r0; p0 < pe; p0 += UNR * rpi) {
+      v4i buf[UNR];
 #pragma unroll
-      for (int e = 0; e < EPC; ++e) {
-        const float d = f[e] - K[e];
-        s1[e] += d;
-        s2[e] = fmaf(d, d, s2[e]);
+      for (int u = 0; u < UNR; ++u)
+        if (p0 + u * rpi < pe) buf[u] = load_chunk2<T>(s, n * HW + p0 + u * rpi, c0);
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (p0 + u * rpi >= pe) break;
+        float f[EPC];
+        Chunk<T>::unpack(buf[u], f);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+          const float d = f[e] - K[e];
+          s1[e] += d;
+          s2[e] = fmaf(d, d, s2[e]);
+        }
       }
     }
   }
   for (int e = 0; e < EPC; ++e) { red[tid][2 * e] = active ? s1[e] : 0.f; red[tid][2 * e + 1] = active ? s2[e] : 0.f; }
   __syncthreads();
-  // one thread per group: sum over its channels, then over row-threads (fixed order)
+  // two parallel stages, fixed order: channel sums over the row-threads, then group sums over channels
+  __shared__ float csum[1024][2];
+  for (int c = tid; c < C; c += 256) {
+    const int cc = c / EPC, e = c % EPC;
+    float b1 = 0.f, b2 = 0.f;
+    for (int r = 0; r < rpi; ++r) { b1 += red[r * CPR + cc][2 * e]; b2 += red[r * CPR + cc][2 * e + 1]; }
+    csum[c][0] = b1; csum[c][1] = b2;
+  }
+  __syncthreads();
   for (int g = tid; g < G; g += 256) {
     float a1 = 0.f, a2 = 0.f;
-    for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
-      const int cc = c / EPC, e = c % EPC;
-      float b1 = 0.f, b2 = 0.f;
-      for (int r = 0; r < rpi; ++r) { b1 += red[r * CPR + cc][2 * e]; b2 += red[r * CPR + cc][2 * e + 1]; }
-      a1 += b1; a2 += b2;
-    }
+    for (int c = g * cpg; c < (g + 1) * cpg; ++c) { a1 += csum[c][0]; a2 += csum[c][1]; }
     float* o = partial + (((size_t)n * splits + sp) * G + g) * 2;
     o[0] = a1; o[1] = a2;
   }
@@ -136,6 +150,18 @@ __global__ __launch_bounds__(256) void gn_bwd_partial(GnBwd b, float* partial /*
   const int pb = sp * per, pe = min(b.HW, pb + per);
   __shared__ float red[256][2 * 8];
   const int c0 = col * EPC;
+  v4i bx[UNR], bg[UNR];
+  auto issue = [&](int p0) {
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int pix = n * b.HW + p0 + u * rpi;
+      if (p0 + u * rpi < pe) {
+        bx[u] = load_chunk2<T>(b.s, pix, c0);
+        bg[u] = *(const v4i*)(b.g + ((size_t)pix * b.ld_g + c0) * sizeof(T));
+      }
+    }
+  };
+  if (active && pb + r0 < pe) issue(pb + r0);   // in flight while the statistics load
   float mean[EPC], rstd[EPC], gm[EPC], bt[EPC], a1[EPC], a2[EPC];
   for (int e = 0; e < EPC; ++e) {
     const int c = c0 + e, g = c / cpg;
@@ -146,11 +172,15 @@ __global__ __launch_bounds__(256) void gn_bwd_partial(GnBwd b, float* partial /*
     a1[e] = 0.f; a2[e] = 0.f;
   }
   if (active) {
-    for (int p = pb + r0; p < pe; p += rpi) {
-      const int pix = n * b.HW + p;
+    for (int p0 = pb + r0; p0 < pe; p0 += UNR * rpi) {
+      if (p0 != pb + r0) issue(p0);
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+      if (p0 + u * rpi >= pe) break;
+      const int pix = n * b.HW + p0 + u * rpi;
       float x[EPC], gv[EPC];
-      Chunk<T>::unpack(load_chunk2<T>(b.s, pix, c0), x);
-      Chunk<T>::unpack(*(const v4i*)(b.g + ((size_t)pix * b.ld_g + c0) * sizeof(T)), gv);
+      Chunk<T>::unpack(bx[u], x);
+      Chunk<T>::unpack(bg[u], gv);
 #pragma unroll
       for (int e = 0; e < EPC; ++e) {
         float g = gv[e];
@@ -159,6 +189,7 @@ __global__ __launch_bounds__(256) void gn_bwd_partial(GnBwd b, float* partial /*
         const float dz = gn_dz(x[e], g, mean[e], rstd[e], gm[e], bt[e], xh, b.silu);
         a1[e] += dz;
         a2[e] = fmaf(dz, xh, a2[e]);
+      }
       }
     }
   }
@@ -258,24 +289,36 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(Src2 s, int HW, const flo
   const int per = (HW + splits - 1) / splits;
   const int pb = blockIdx.y * per, pe = min(HW, pb + per);
   const int c0 = col * EPC;
+  v4i buf[UNR];
+  auto issue = [&](int p0) {
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      if (p0 + u * rpi < pe) buf[u] = load_chunk2<T>(s, n * HW + p0 + u * rpi, c0);
+  };
+  if (pb + r0 < pe) issue(pb + r0);   // in flight while scale/shift load
   float sc[EPC], sh[EPC];
 #pragma unroll
   for (int e = 0; e < EPC; ++e) {
     sc[e] = scale[(size_t)n * C + c0 + e];
     sh[e] = shift[(size_t)n * C + c0 + e];
   }
-  for (int p = pb + r0; p < pe; p += rpi) {
-    const int pix = n * HW + p;
-    float f[EPC];
-    Chunk<T>::unpack(load_chunk2<T>(s, pix, c0), f);
+  for (int p0 = pb + r0; p0 < pe; p0 += UNR * rpi) {
+    if (p0 != pb + r0) issue(p0);
 #pragma unroll
-    for (int e = 0; e < EPC; ++e) {
-      float v = fmaf(f[e], sc[e], sh[e]);
-      if (silu) v = silu_f(v);
-      if (thresh) v = drop_keep((uint64_t)pix * C + c0 + e, seed, thresh) ? v * dscale : 0.f;
-      f[e] = v;
+    for (int u = 0; u < UNR; ++u) {
+      if (p0 + u * rpi >= pe) break;
+      const int pix = n * HW + p0 + u * rpi;
+      float f[EPC];
+      Chunk<T>::unpack(buf[u], f);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        float v = fmaf(f[e], sc[e], sh[e]);
+        if (silu) v = silu_f(v);
+        if (thresh) v = drop_keep((uint64_t)pix * C + c0 + e, seed, thresh) ? v * dscale : 0.f;
+        f[e] = v;
+      }
+      *(v4i*)(out + ((size_t)pix * ldo + c0) * sizeof(T)) = Chunk<T>::pack(f);
     }
-    *(v4i*)(out + ((size_t)pix * ldo + c0) * sizeof(T)) = Chunk<T>::pack(f);
   }
 }
 
@@ -293,6 +336,23 @@ __global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* coef, 
   const int per = (b.HW + gridDim.y - 1) / gridDim.y;
   const int pb = blockIdx.y * per, pe = min(b.HW, pb + per);
   const int c0 = col * EPC;
+  const bool first = c0 < b.s.C1;
+  char* const dst = first ? dx1 : dx2;
+  const int ldd = first ? ld1 : ld2, cd = first ? c0 : c0 - b.s.C1, acc = first ? acc1 : acc2;
+  v4i bx[UNR], bg[UNR], bp[UNR];
+  auto issue = [&](int p0) {
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int pix = n * b.HW + p0 + u * rpi;
+      if (p0 + u * rpi < pe) {
+        bx[u] = load_chunk2<T>(b.s, pix, c0);
+        bg[u] = *(const v4i*)(b.g + ((size_t)pix * b.ld_g + c0) * sizeof(T));
+        if (acc) bp[u] = *(const v4i*)(dst + ((size_t)pix * ldd + cd) * sizeof(T));
+      }
+    }
+  };
+  // the first rows are in flight while the per-channel coefficients load
+  if (pb + r0 < pe) issue(pb + r0);
   float mean[EPC], rstd[EPC], gm[EPC], bt[EPC], ka[EPC], kb[EPC], kc[EPC];
 #pragma unroll
   for (int e = 0; e < EPC; ++e) {
@@ -305,14 +365,15 @@ __global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* coef, 
     kb[e] = rstd[e] * coef[((size_t)n * b.G + g) * 2];
     kc[e] = rstd[e] * coef[((size_t)n * b.G + g) * 2 + 1];
   }
-  const bool first = c0 < b.s.C1;
-  char* const dst = first ? dx1 : dx2;
-  const int ldd = first ? ld1 : ld2, cd = first ? c0 : c0 - b.s.C1, acc = first ? acc1 : acc2;
-  for (int p = pb + r0; p < pe; p += rpi) {
-    const int pix = n * b.HW + p;
+  for (int p0 = pb + r0; p0 < pe; p0 += UNR * rpi) {
+    if (p0 != pb + r0) issue(p0);
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+    if (p0 + u * rpi >= pe) break;
+    const int pix = n * b.HW + p0 + u * rpi;
     float x[EPC], gv[EPC], o[EPC];
-    Chunk<T>::unpack(load_chunk2<T>(b.s, pix, c0), x);
-    Chunk<T>::unpack(*(const v4i*)(b.g + ((size_t)pix * b.ld_g + c0) * sizeof(T)), gv);
+    Chunk<T>::unpack(bx[u], x);
+    Chunk<T>::unpack(bg[u], gv);
 #pragma unroll
     for (int e = 0; e < EPC; ++e) {
       float gg = gv[e];
@@ -324,11 +385,12 @@ __global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* coef, 
     v4i* q = (v4i*)(dst + ((size_t)pix * ldd + cd) * sizeof(T));
     if (acc) {
       float prev[EPC];
-      Chunk<T>::unpack(*q, prev);
+      Chunk<T>::unpack(bp[u], prev);
 #pragma unroll
       for (int e = 0; e < EPC; ++e) o[e] += prev[e];
     }
     *q = Chunk<T>::pack(o);
+    }
   }
 }
 
@@ -346,11 +408,19 @@ __global__ __launch_bounds__(256) void chsum_partial(const char* dy, int HW, int
   float a[EPC];
   for (int e = 0; e < EPC; ++e) a[e] = 0.f;
   if (active) {
-    for (int p = pb + r0; p < pe; p += rpi) {
-      float f[EPC];
-      Chunk<T>::unpack(*(const v4i*)(dy + (((size_t)n * HW + p) * ld + col * EPC) * sizeof(T)), f);
+    for (int p0 = pb + r0; p0 < pe; p0 += UNR * rpi) {
+      v4i buf[UNR];
 #pragma unroll
-      for (int e = 0; e < EPC; ++e) a[e] += f[e];
+      for (int u = 0; u < UNR; ++u)
+        if (p0 + u * rpi < pe) buf[u] = *(const v4i*)(dy + (((size_t)n * HW + p0 + u * rpi) * ld + col * EPC) * sizeof(T));
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (p0 + u * rpi >= pe) break;
+        float f[EPC];
+        Chunk<T>::unpack(buf[u], f);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) a[e] += f[e];
+      }
     }
   }
   for (int e = 0; e < EPC; ++e) red[tid][e] = active ? a[e] : 0.f;
@@ -398,7 +468,7 @@ extern "C" int dmc_gn_stats(int dtype, const void* x1, const void* x2, int N, in
   const int epc = dtype == DMC_F32 ? 4 : 8;
   const int C = C1 + C2;
   DMC_REQUIRE(C % G == 0, "gn_stats: C %d not divisible by G %d", C, G);
-  DMC_REQUIRE(C1 % epc == 0 && C2 % epc == 0 && C / epc <= 256, "gn_stats: channel alignment (C1=%d C2=%d)", C1, C2);
+  DMC_REQUIRE(C1 % epc == 0 && C2 % epc == 0 && C / epc <= 256 && C <= 1024, "gn_stats: channel alignment (C1=%d C2=%d)", C1, C2);
   DMC_REQUIRE(ld1 % epc == 0 && (C2 == 0 || ld2 % epc == 0), "gn_stats: pitch alignment");
   hipStream_t s = dmc::as_stream(stream);
   Src2 src{(const char*)x1, (const char*)x2, C1, C2, ld1, ld2};

@@ -107,6 +107,39 @@ def pack_weight(mode, dtype, w, Kc, out=None):
     return out
 
 
+class PackBatch:
+    """Device arrays of dmc_pack_job + their tiles for one dmc_pack_weights launch.
+
+    jobs: list of (w fp32 tensor, dst tensor, dst element offset, mode, Cout, Cin, kh, kw, Kc, koff)."""
+
+    def __init__(self, jobs, device):
+        arr = (L.PackJob * len(jobs))()
+        self.keep = []
+        tiles = []
+        for i, (w, dst, off, mode, Cout, Cin, kh, kw, Kc, koff) in enumerate(jobs):
+            w = w.detach()
+            if not w.is_contiguous():
+                raise L.DMCError("pack job: master weight must be contiguous")
+            self.keep.append(w)
+            j = arr[i]
+            j.w = w.data_ptr()
+            j.dst = dst.data_ptr() + off * dst.element_size()
+            j.dtype = L.dtype_code(dst.dtype)
+            j.mode, j.Cout, j.Cin, j.kh, j.kw, j.Kc, j.koff = mode, Cout, Cin, kh, kw, Kc, koff
+            n = LIB.dmc_pack_tiles(ctypes.byref(j), i, None, 0)
+            buf = (ctypes.c_int * (3 * n))()
+            LIB.dmc_pack_tiles(ctypes.byref(j), i, buf, n)
+            tiles.append(torch.frombuffer(bytearray(buf), dtype=torch.int32))
+        self.count = len(jobs)
+        t = torch.cat(tiles)
+        self.ntiles = t.numel() // 3
+        self.jobs = torch.frombuffer(bytearray(arr), dtype=torch.uint8).to(device)
+        self.tiles = t.to(device)
+
+    def launch(self):
+        check(LIB.dmc_pack_weights(ptr(self.jobs), ptr(self.tiles), self.ntiles, L.stream()), "dmc_pack_weights")
+
+
 def gn_stats(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, G, eps, gamma, beta):
     C = C1 + C2
     dev = x1.device
@@ -278,3 +311,17 @@ def clip_grad_norm(refs: TensorRefs, max_norm):
     check(LIB.dmc_clip_grad_norm(ptr(refs.dev), refs.count, float(max_norm), ptr(total), ptr(ws), L.stream()),
           "dmc_clip_grad_norm")
     return total
+
+
+def grad_norm_flat(g, max_norm):
+    """(total_norm, clip coef) of a flat fp32 gradient buffer, both device scalars; no host sync."""
+    out = torch.empty(2, dtype=torch.float32, device=g.device)
+    ws = SCRATCH.get(1024 * 4, g.device)
+    check(LIB.dmc_grad_norm_flat(ptr(g), g.numel(), float(max_norm), ptr(out), out.data_ptr() + 4, ptr(ws),
+                                 L.stream()), "dmc_grad_norm_flat")
+    return out[0], out[1:]
+
+
+def adamw_flat(p, g, m, v, ema, coef, wd_mul, lerp_w, beta2, omb2, eps, neg_step, bc2_sqrt, ema_decay, ema_om):
+    check(LIB.dmc_adamw_flat(ptr(p), ptr(g), ptr(m), ptr(v), ptr(ema), p.numel(), ptr(coef), wd_mul, lerp_w, beta2,
+                             omb2, eps, neg_step, bc2_sqrt, ema_decay, ema_om, L.stream()), "dmc_adamw_flat")

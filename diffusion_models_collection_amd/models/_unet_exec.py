@@ -42,18 +42,51 @@ def _seed_from_torch():
 
 
 class _PackCache:
-    """Weights repacked into the kernel layouts, refreshed when the parameter's version changes."""
+    """Weights repacked into the kernel layouts.
 
-    def __init__(self):
+    An entry is (version, buffer, sources, jobs): `jobs` are dmc_pack_job specs writing `buffer` from the
+    fp32 master `sources`. The version is the sources' torch version counters and pointers plus the
+    executor's weight generation (bumped by the flat optimizer step, whose kernel writes the parameters
+    behind torch's back). `refresh()` repacks every stale entry in ONE dmc_pack_weights launch; `get()`
+    repacks a single stale entry (first use, or a weight changed outside a step).
+    """
+
+    def __init__(self, owner):
+        self.owner = owner
         self.entries = {}
+        self._batch = None
 
-    def get(self, key, param, version_src, make):
-        v = (version_src._version, version_src.data_ptr())
+    def _ver(self, srcs):
+        return (self.owner.wgen,) + tuple((s._version, s.data_ptr()) for s in srcs)
+
+    def get(self, key, srcs, make_buf, make_jobs):
+        v = self._ver(srcs)
         e = self.entries.get(key)
         if e is None or e[0] != v:
-            e = (v, make())
+            buf = e[1] if e is not None and e[2] == tuple(id(s) for s in srcs) else make_buf()
+            jobs = make_jobs(buf)
+            K.PackBatch(jobs, buf.device).launch()
+            e = (v, buf, tuple(id(s) for s in srcs), srcs, jobs)
             self.entries[key] = e
         return e[1]
+
+    def refresh(self):
+        stale = []
+        for k, e in self.entries.items():
+            v = self._ver(e[3])
+            if e[0] != v:
+                stale.append((k, e, v))
+        if not stale:
+            return
+        # the cached job array holds raw source/destination pointers: key it on them
+        key = tuple((k, e[1].data_ptr(), v[1:]) for k, e, v in stale)
+        if self._batch is None or self._batch[0] != tuple((k, b, tuple(p for _, p in vv)) for k, b, vv in key):
+            jobs = [j for _, e, _ in stale for j in e[4]]
+            self._batch = (tuple((k, b, tuple(p for _, p in vv)) for k, b, vv in key),
+                           K.PackBatch(jobs, stale[0][1][1].device))
+        self._batch[1].launch()
+        for k, e, v in stale:
+            self.entries[k] = (v,) + e[1:]
 
 
 class UNetExecutor:
@@ -62,7 +95,8 @@ class UNetExecutor:
         self.dt = model.compute_dtype
         self.cdt = L.dtype_code(self.dt)
         self.chunk = L.chunk_for(self.dt)
-        self.packs = _PackCache()
+        self.wgen = 0               # weight generation: bumped when a fused step rewrote the parameters
+        self.packs = _PackCache(self)
         self.params = list(model.parameters())
         self.pindex = {id(p): i for i, p in enumerate(self.params)}
         # time-embedding projection layout: all ResidualBlocks' time_mlp (and label_proj) rows side by side
@@ -114,48 +148,74 @@ class UNetExecutor:
     def _wpack(self, conv, mode, Kc, dtype=None):
         dtype = dtype or self.dt
         w = conv.weight
-        return self.packs.get((id(conv), mode, Kc, dtype), conv, w, lambda: K.pack_weight(mode, dtype, w, Kc))
+        if w.dim() == 2:
+            Cout, Cin, kh, kw = w.shape[0], w.shape[1], 1, 1
+        else:
+            Cout, Cin, kh, kw = w.shape
+        ntaps = 16 if mode == L.PACK_UPDGRAD else kh * kw
+        rows = Cout if mode == L.PACK_FWD else Cin
+
+        def make_buf():
+            return torch.empty(rows * ntaps * Kc, dtype=dtype, device=w.device)
+
+        return self.packs.get((id(conv), mode, Kc, dtype), (w,), make_buf,
+                              lambda buf: [(w, buf, 0, mode, Cout, Cin, kh, kw, Kc, -1)])
+
+    def _temb_lins(self, which):
+        return [(rb.time_mlp[1] if which == 0 else rb.label_proj[1]) for rb in self.res_blocks]
 
     def _temb_pack(self, which, dtype):
         """Packed [sum Cout][1][Kc=512] weight of every block's time_mlp (which=0) / label_proj (which=1)."""
-        lins = [(rb.time_mlp[1] if which == 0 else rb.label_proj[1]) for rb in self.res_blocks]
+        lins = self._temb_lins(which)
         dim = lins[0].weight.shape[1]
         Kc = L.kc_for(dim, torch.float32)
-        ver = tuple((lin.weight._version, lin.weight.data_ptr()) for lin in lins)
-        key = ("temb", which)
-        e = self.packs.entries.get(key)
-        if e is None or e[0] != ver:
-            buf = torch.empty(self.temb_total * Kc, dtype=torch.float32, device=lins[0].weight.device)
-            off = 0
+
+        def jobs(buf):
+            out, off = [], 0
             for lin in lins:
                 co = lin.weight.shape[0]
-                K.pack_weight(L.PACK_FWD, torch.float32, lin.weight, Kc, out=buf[off * Kc:(off + co) * Kc])
+                out.append((lin.weight, buf, off * Kc, L.PACK_FWD, co, dim, 1, 1, Kc, -1))
                 off += co
-            e = (ver, buf)
-            self.packs.entries[key] = e
-        return e[1]
+            return out
+
+        return self.packs.get(("temb", which), tuple(lin.weight for lin in lins),
+                              lambda: torch.zeros(self.temb_total * Kc, dtype=torch.float32,
+                                                  device=lins[0].weight.device), jobs)
 
     def _temb_pack_dgrad(self, which):
-        """[dim][1][Kc >= sum Cout] dgrad pack of the concatenated projection weight."""
-        lins = [(rb.time_mlp[1] if which == 0 else rb.label_proj[1]) for rb in self.res_blocks]
-        ver = tuple((lin.weight._version, lin.weight.data_ptr()) for lin in lins)
-        key = ("temb_dg", which)
-        e = self.packs.entries.get(key)
-        if e is None or e[0] != ver:
-            wcat = torch.cat([lin.weight.detach() for lin in lins], 0)   # [sumC, dim] fp32, tiny, once per step
-            buf = K.pack_weight(L.PACK_DGRAD, torch.float32, wcat, L.kc_for(self.temb_total, torch.float32))
-            e = (ver, buf)
-            self.packs.entries[key] = e
-        return e[1]
+        """[dim][1][Kc >= sum Cout] dgrad pack of the row-concatenated projection weight: each Linear writes
+        its own column block (koff) of the shared rows; the padding columns stay zero from allocation."""
+        lins = self._temb_lins(which)
+        dim = lins[0].weight.shape[1]
+        Kt = L.kc_for(self.temb_total, torch.float32)
+
+        def jobs(buf):
+            out, off = [], 0
+            for lin in lins:
+                co = lin.weight.shape[0]
+                out.append((lin.weight, buf, 0, L.PACK_DGRAD, co, dim, 1, 1, Kt, off))
+                off += co
+            return out
+
+        return self.packs.get(("temb_dg", which), tuple(lin.weight for lin in lins),
+                              lambda: torch.zeros(dim * Kt, dtype=torch.float32, device=lins[0].weight.device),
+                              jobs)
 
     def _temb_bias(self):
-        lins = [rb.time_mlp[1] for rb in self.res_blocks]
-        ver = tuple((lin.bias._version, lin.bias.data_ptr()) for lin in lins)
-        e = self.packs.entries.get("temb_b")
-        if e is None or e[0] != ver:
-            e = (ver, torch.cat([lin.bias.detach() for lin in lins], 0))
-            self.packs.entries["temb_b"] = e
-        return e[1]
+        """All 22 time_mlp biases side by side (a 1x1 FWD 'pack' with Kc = 1 is a copy)."""
+        lins = self._temb_lins(0)
+
+        def jobs(buf):
+            out, off = [], 0
+            for lin in lins:
+                co = lin.bias.shape[0]
+                out.append((lin.bias, buf, off, L.PACK_FWD, co, 1, 1, 1, 1, -1))
+                off += co
+            return out
+
+        return self.packs.get("temb_b", tuple(lin.bias for lin in lins),
+                              lambda: torch.empty(self.temb_total, dtype=torch.float32, device=lins[0].bias.device),
+                              jobs)
 
     # ---------------------------------------------------------------------------------------
     def _conv(self, srcs, conv, taps, OH, OW, Cout, mode=L.MODE_NORMAL, stride=1, pro=None, drop=None,
@@ -246,6 +306,7 @@ class UNetExecutor:
     def forward(self, x, t, y, keep):
         m = self.m
         self.device = x.device
+        self.packs.refresh()        # every weight the last step changed, repacked in one launch
         dt = self.dt
         N, Cin, H, W = x.shape
         x = x.contiguous().float()

@@ -70,6 +70,131 @@ class GradSync:
             self.done = 0
 
 
+class FlatAdamW:
+    """clip_grad_norm_ + torch.optim.AdamW.step + EMA as one streaming kernel over flat fp32 buffers.
+
+    The UNet's parameters are re-seated as views of one flat buffer laid out like the executor's flat
+    gradient buffer (reverse module order), and so are the optimizer's exp_avg / exp_avg_sq (kept in
+    `optimizer.state` in torch's own format, so optimizer.state_dict() and checkpoints are unchanged) and
+    the EMA model's parameters. The step is then dmc_grad_norm_flat (norm + clip coefficient, on device)
+    followed by dmc_adamw_flat (clip scaling, AdamW, EMA in one pass: ~36 B/parameter of HBM traffic
+    instead of the ~700 launches of the reference's clip + foreach AdamW + per-tensor EMA).
+    Used only when the optimizer is a plain torch.optim.AdamW over exactly the model's parameters;
+    anything else takes the reference path (clip, optimizer.step(), EMA).
+    """
+
+    def __init__(self, model, optimizer, ema_model=None):
+        self.model, self.opt, self.ema = model, optimizer, ema_model
+        self.ex = model.executor
+        self.params = list(model.parameters())
+        self._bound = False
+
+    @staticmethod
+    def supported(model, optimizer):
+        if type(optimizer) is not torch.optim.AdamW or len(optimizer.param_groups) != 1:
+            return False
+        g = optimizer.param_groups[0]
+        if g.get("amsgrad") or g.get("maximize") or g.get("capturable") or g.get("differentiable"):
+            return False
+        mp = list(model.parameters())
+        if {id(p) for p in g["params"]} != {id(p) for p in mp} or len(g["params"]) != len(mp):
+            return False
+        return all(p.dtype == torch.float32 and p.is_cuda and p.requires_grad for p in mp)
+
+    def _bind(self):
+        ex, dev = self.ex, self.params[0].device
+        n = ex.gtotal
+        self.flat_p = torch.empty(n, dtype=torch.float32, device=dev)
+        self.flat_m = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.flat_v = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.slots = []
+        st = self.opt.state
+        steps = set()
+        for i, p in enumerate(self.params):
+            o = ex.goff[i]
+            view = self.flat_p[o:o + p.numel()].view(p.shape)
+            view.copy_(p.detach())
+            p.data = view
+            s = st.get(p)
+            if s and "exp_avg" in s:
+                self.flat_m[o:o + p.numel()].copy_(s["exp_avg"].reshape(-1))
+                self.flat_v[o:o + p.numel()].copy_(s["exp_avg_sq"].reshape(-1))
+                steps.add(float(s["step"]))
+            self.slots.append((p, o))
+        if len(steps) > 1:
+            raise RuntimeError(f"FlatAdamW: parameters have different step counts {sorted(steps)}")
+        self.t = int(steps.pop()) if steps else 0
+        self.step_t = torch.tensor(float(self.t), dtype=torch.float32)
+        for p, o in self.slots:
+            st[p] = {"step": self.step_t, "exp_avg": self.flat_m[o:o + p.numel()].view(p.shape),
+                     "exp_avg_sq": self.flat_v[o:o + p.numel()].view(p.shape)}
+        self.state_obj = st
+        self.flat_e = None
+        if self.ema is not None:
+            ep = dict(self.ema.named_parameters())
+            names = [k for k, _ in self.model.named_parameters()]
+            if set(ep) != set(names) or any(b.is_floating_point() for b in self.ema.buffers()):
+                raise RuntimeError("FlatAdamW: EMA model layout differs from the model")
+            self.flat_e = torch.empty(n, dtype=torch.float32, device=dev)
+            for (p, o), k in zip(self.slots, names):
+                e = ep[k]
+                view = self.flat_e[o:o + p.numel()].view(p.shape)
+                view.copy_(e.detach())
+                e.data = view
+            self.ema_params = [ep[k] for k in names]
+        self.expect = [(p, self.flat_p.data_ptr() + 4 * o) for p, o in self.slots]
+        if self.flat_e is not None:
+            self.expect += [(e, self.flat_e.data_ptr() + 4 * o) for e, (_, o) in zip(self.ema_params, self.slots)]
+        self._bound = True
+
+    def _valid(self):
+        """The flat binding still holds: nobody re-seated a parameter (model.to(...)), replaced the optimizer
+        state (load_state_dict) or left gradients outside the executor's flat buffer (accumulation)."""
+        if self.opt.state is not self.state_obj or any(p.data_ptr() != a for p, a in self.expect):
+            return False
+        st = self.opt.state
+        return all(st.get(p, {}).get("exp_avg") is not None and
+                   st[p]["exp_avg"].data_ptr() == self.flat_m.data_ptr() + 4 * o for p, o in self.slots[:1])
+
+    def grads_flat(self):
+        flat = getattr(self.ex, "flat", None)
+        if flat is None:
+            return None
+        base = flat.data_ptr()
+        for p, o in self.slots:
+            if p.grad is None or p.grad.data_ptr() != base + 4 * o:
+                return None
+        return flat
+
+    def step(self, max_norm=1.0, ema_decay=None):
+        """Returns the gradient norm (device scalar), or None when the flat path does not apply."""
+        if not self._bound or not self._valid():
+            self._bind()
+        g = self.grads_flat()
+        if g is None:
+            # the caller falls back to torch's optimizer.step(): give every parameter its own step counter
+            # (torch increments each one) and re-bind from the optimizer state next time
+            for p, _ in self.slots:
+                self.opt.state[p]["step"] = torch.tensor(float(self.t), dtype=torch.float32)
+            self._bound = False
+            return None
+        total, coef = K.grad_norm_flat(g, max_norm if max_norm is not None else -1.0)
+        grp = self.opt.param_groups[0]
+        lr, (b1, b2), eps, wd = float(grp["lr"]), grp["betas"], grp["eps"], grp["weight_decay"]
+        self.t += 1
+        self.step_t.fill_(float(self.t))
+        bc1 = 1 - b1 ** self.t
+        bc2 = 1 - b2 ** self.t
+        use_ema = self.flat_e is not None and ema_decay is not None
+        K.adamw_flat(self.flat_p, g, self.flat_m, self.flat_v, self.flat_e if use_ema else None, coef,
+                     1 - lr * wd, 1 - b1, b2, 1 - b2, eps, (lr / bc1) * -1, bc2 ** 0.5,
+                     ema_decay if use_ema else 1.0, (1 - ema_decay) if use_ema else 0.0)
+        self.ex.wgen += 1
+        if use_ema:
+            self.ema.executor.wgen += 1
+        return total
+
+
 class DiffusionTrainer:
     """Trainer for diffusion models (utils/trainer.py:21-421)."""
 
@@ -132,6 +257,10 @@ class DiffusionTrainer:
             self.ema_model = None
         self._ema_refs = None
         self._clip_refs = None
+        self._flat = None
+        if _is_dmc_unet(self._module) and FlatAdamW.supported(self._module, optimizer) and (
+                self.ema_model is None or _is_dmc_unet(self.ema_model)):
+            self._flat = FlatAdamW(self._module, optimizer, self.ema_model)
 
         self.best_loss = float('inf')
         self.start_epoch = 1
@@ -150,7 +279,7 @@ class DiffusionTrainer:
 
     def load_checkpoint(self, checkpoint_path):
         print(f"Loading checkpoint from {checkpoint_path}...")
-        checkpoint = torch.load(checkpoint_path, map_location=self.device, weights_only=False)
+        checkpoint = torch.load(checkpoint_path, map_location=self.device, weights_only=True)
         self._module.load_state_dict(checkpoint['model_state_dict'])
         if 'optimizer_state_dict' in checkpoint and self.optimizer:
             self.optimizer.load_state_dict(checkpoint['optimizer_state_dict'])
@@ -225,11 +354,16 @@ class DiffusionTrainer:
         loss = loss / self.gradient_accumulation_steps
         loss.backward()
         if (i + 1) % self.gradient_accumulation_steps == 0:
-            self._clip(1.0)
-            self.optimizer.step()
-            self.optimizer.zero_grad()
-            if self.use_ema:
-                self._update_ema()
+            fused = self._flat is not None and self._flat.step(
+                1.0, self.ema_decay if (self.use_ema and self.ema_model is not None) else None) is not None
+            if fused:
+                self.optimizer.zero_grad()
+            else:
+                self._clip(1.0)
+                self.optimizer.step()
+                self.optimizer.zero_grad()
+                if self.use_ema:
+                    self._update_ema()
         return loss
 
     def train_epoch(self, epoch):

@@ -87,6 +87,19 @@ int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_dy, const vo
  * into a 4x4 stride-2 kernel). Padding is zero-filled. */
 int dmc_pack_weight(int pack_mode, int dtype, const float* w, int Cout, int Cin, int kh, int kw,
                     int Kc, void* dst, void* stream);
+/* Batched repack of every stale weight in one launch (the per-step refresh after optimizer.step;
+ * replaces one dmc_pack_weight per conv and mode). Each job is cut into tiles on the host
+ * (dmc_pack_tiles: {job index, a, b} int triples); `jobs` and `tiles` are DEVICE arrays.
+ * koff < 0: the job writes its whole rows including the zero padding of Kc; koff >= 0 (a DGRAD of a
+ * row-concatenation, e.g. the 22 time_mlp weights of models/unet.py:40-43 as one GEMM, or a Kc = 1
+ * FWD "pack" = copy into a concatenated bias): only its own column block [koff, koff + extent). */
+typedef struct dmc_pack_job {
+  const float* w;            /* fp32 master weight [Cout][Cin][kh][kw] */
+  void* dst;                 /* packed [rows][ntaps][Kc] of dtype */
+  int dtype, mode, Cout, Cin, kh, kw, Kc, koff;
+} dmc_pack_job;
+int dmc_pack_tiles(const dmc_pack_job* job, int job_index, int* tiles, int cap);   /* HOST pointers */
+int dmc_pack_weights(const dmc_pack_job* jobs, const int* tiles, int ntiles, void* stream);
 
 /* GroupNorm statistics (models/unet.py:35,51,80,238; eps 1e-5) over the virtual concat of x1/x2:
  * mean_rstd [N][G][2]; scale/shift [N][C] = folded affine for the consumer's prologue.
@@ -185,6 +198,21 @@ int dmc_ema_update(const dmc_tensor_ref* refs, int count, float decay, void* str
  */
 int dmc_clip_grad_norm(const dmc_tensor_ref* refs, int count, float max_norm, float* total_norm,
                        float* workspace, void* stream);   /* workspace >= 16*count + 16 floats */
+/* Flat-buffer optimizer step (parameters, gradients, moments and EMA share one fp32 layout).
+ * dmc_grad_norm_flat: total_norm = ||g||_2, coef = min(1, max_norm/(total_norm+1e-6)) (max_norm <= 0:
+ * coef = 1) -- torch.nn.utils.clip_grad_norm_ of utils/trainer.py:259, with the scaling deferred to
+ * the consumer. workspace >= 1024 floats.
+ * dmc_adamw_flat: g *= coef[0] (coef may be NULL), then torch.optim.AdamW.step (train.py:142-146;
+ * foreach path, amsgrad=False) in torch's operation order: p *= wd_mul; m = lerp(m, g, lerp_w);
+ * v = v*beta2 + one_minus_beta2*g*g; p += neg_step_size * m / (sqrt(v)/bc2_sqrt + eps). The host
+ * computes the scalars in double like torch (wd_mul = 1-lr*wd, lerp_w = 1-beta1, neg_step_size =
+ * -lr/(1-beta1^t), bc2_sqrt = sqrt(1-beta2^t)). Then, if ema != NULL, ema = ema*ema_decay +
+ * ema_one_minus*p (utils/trainer.py:187-202). */
+int dmc_grad_norm_flat(const float* g, long n, float max_norm, float* total_norm, float* coef,
+                       float* workspace, void* stream);
+int dmc_adamw_flat(float* p, const float* g, float* m, float* v, float* ema, long n, const float* coef,
+                   float wd_mul, float lerp_w, float beta2, float one_minus_beta2, float eps,
+                   float neg_step_size, float bc2_sqrt, float ema_decay, float ema_one_minus, void* stream);
 /* y = silu(x) (fp32); NHWC dtype -> NCHW fp32 (the inverse of dmc_pack_input); y += x (dtype). */
 int dmc_silu_fwd(const float* x, float* y, long n, void* stream);
 int dmc_unpack_output(int dtype, const void* src, int ld, int N, int C, int H, int W, float* dst,

@@ -21,6 +21,24 @@ if [[ $STAGES == *p* ]]; then
     || { tail -30 "$O/prof_bench.err"; exit 1; }
   f=$(find "$O/prof" -name '*kernel_stats.csv' | head -1); python3 scripts/prof_summary.py "$f" 10 20
 fi
+if [[ $STAGES == *s* ]]; then
+  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { tail -30 "$O/smoke.log"; exit 1; }
+  tail -1 "$O/smoke.log"
+fi
+if [[ $STAGES == *T* ]]; then   # training-only kernel trace: 3 warm-up + 10 steps
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/proft" -o proft --output-format csv -- \
+    python3 bench.py --steps 10 --warmup 3 --no-cpu --no-sample --no-roofline > "$O/proft.json" 2> "$O/proft.err" \
+    || { tail -30 "$O/proft.err"; exit 1; }
+  python3 scripts/trace_summary.py "$(find "$O/proft" -name '*kernel_trace.csv' | head -1)" --steps 9 --marker adamw_flat --top 45 > "$O/proft_summary.txt"
+  head -30 "$O/proft_summary.txt"
+fi
+if [[ $STAGES == *S* ]]; then   # sampling-only kernel trace: 2 DDIM-50 runs
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/profs" -o profs --output-format csv -- \
+    python3 bench.py --no-train --no-cpu --no-roofline > "$O/profs.json" 2> "$O/profs.err" \
+    || { tail -30 "$O/profs.err"; exit 1; }
+  python3 scripts/trace_summary.py "$(find "$O/profs" -name '*kernel_trace.csv' | head -1)" --steps 100 --top 40 > "$O/profs_summary.txt"
+  head -25 "$O/profs_summary.txt"
+fi
 if [[ $STAGES == *m* ]]; then
   P="python3 bench.py --roofline-only"
   timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d "$O/fetch" -o fetch --output-format csv -- $P > /dev/null

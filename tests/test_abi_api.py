@@ -21,7 +21,7 @@ def test_library_exports_header_symbols():
     _ensure_lib()
     import ctypes
     hdr = (ROOT / "include" / "dmc.h").read_text()
-    names = sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(dmc_\w+)\s*\(", hdr, re.M)))
+    names = sorted(set(re.findall(r"^\s*(?:int|long|size_t|const char\*)\s+(dmc_\w+)\s*\(", hdr, re.M)))
     assert len(names) >= 29, names
     lib = ctypes.CDLL(str(ROOT / "diffusion_models_collection_amd" / "libdmc.so"))
     missing = [n for n in names if not hasattr(lib, n)]

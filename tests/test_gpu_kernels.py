@@ -330,3 +330,70 @@ def test_quantile_threshold_matches_torch():
     x0r = torch.clamp(x0r, -s, s) / s
     torch.testing.assert_close(eps.cpu(), e_ref, rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(x0.cpu(), x0r, rtol=1e-5, atol=1e-5)
+
+
+def test_pack_weights_batch_matches_single_packs():
+    """One dmc_pack_weights launch over mixed jobs == the per-weight dmc_pack_weight packs (all modes,
+    bf16/fp32 destinations, column-block (koff) jobs of a row concatenation, a Kc=1 bias copy)."""
+    L, K = _lib()
+    torch.manual_seed(11)
+    w3 = torch.randn(24, 16, 3, 3, device=DEV)
+    w1 = torch.randn(40, 24, device=DEV)
+    lins = [torch.randn(co, 32, device=DEV) for co in (8, 16, 24)]
+    bias = [torch.randn(co, device=DEV) for co in (8, 16, 24)]
+    bf = torch.bfloat16
+    Kc3, Kc1 = L.kc_for(16, bf), L.kc_for(24, torch.float32)
+    refs = {
+        "fwd": K.pack_weight(L.PACK_FWD, bf, w3, Kc3),
+        "dg": K.pack_weight(L.PACK_DGRAD, bf, w3, L.kc_for(24, bf)),
+        "up": K.pack_weight(L.PACK_UPDGRAD, bf, w3, L.kc_for(24, bf)),
+        "lin": K.pack_weight(L.PACK_FWD, torch.float32, w1, Kc1),
+        "cat_dg": K.pack_weight(L.PACK_DGRAD, torch.float32, torch.cat(lins, 0), 64),
+    }
+    outs = {k: torch.full_like(v, 7.0) for k, v in refs.items()}
+    outs["cat_dg"].zero_()     # koff jobs never touch the padding columns: zero from allocation
+    bcat = torch.empty(48, device=DEV)
+    jobs = [(w3, outs["fwd"], 0, L.PACK_FWD, 24, 16, 3, 3, Kc3, -1),
+            (w3, outs["dg"], 0, L.PACK_DGRAD, 24, 16, 3, 3, L.kc_for(24, bf), -1),
+            (w3, outs["up"], 0, L.PACK_UPDGRAD, 24, 16, 3, 3, L.kc_for(24, bf), -1),
+            (w1, outs["lin"], 0, L.PACK_FWD, 40, 24, 1, 1, Kc1, -1)]
+    off = 0
+    for wl, b in zip(lins, bias):
+        jobs.append((wl, outs["cat_dg"], 0, L.PACK_DGRAD, wl.shape[0], 32, 1, 1, 64, off))
+        jobs.append((b, bcat, off, L.PACK_FWD, wl.shape[0], 1, 1, 1, 1, -1))
+        off += wl.shape[0]
+    K.PackBatch(jobs, DEV).launch()
+    for k in refs:
+        assert torch.equal(outs[k], refs[k]), k
+    assert torch.equal(bcat, torch.cat(bias))
+
+
+@pytest.mark.parametrize("n", [4099, 1 << 20])
+def test_flat_grad_norm_and_adamw_match_torch(n):
+    """dmc_grad_norm_flat + dmc_adamw_flat (clip, AdamW, EMA) vs clip_grad_norm_ + torch.optim.AdamW + the
+    reference EMA (utils/trainer.py:198-202), 3 steps, ragged n."""
+    L, K = _lib()
+    torch.manual_seed(5)
+    p = torch.randn(n, device=DEV)
+    ema = p.clone()
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    pr = torch.nn.Parameter(p.clone())
+    opt = torch.optim.AdamW([pr], lr=1e-3, weight_decay=1e-2, foreach=True)
+    er = ema.clone()
+    lr, (b1, b2), eps, wd, d = 1e-3, (0.9, 0.999), 1e-8, 1e-2, 0.99
+    for t in range(1, 4):
+        g = torch.randn(n, device=DEV) * (0.01 if t == 2 else 1.0)
+        total, coef = K.grad_norm_flat(g, 1.0)
+        bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
+        K.adamw_flat(p, g, m, v, ema, coef, 1 - lr * wd, 1 - b1, b2, 1 - b2, eps, (lr / bc1) * -1, bc2 ** 0.5,
+                     d, 1 - d)
+        pr.grad = g.clone()
+        tr = torch.nn.utils.clip_grad_norm_([pr], 1.0)
+        opt.step()
+        er.mul_(d).add_(pr.detach(), alpha=1 - d)
+        torch.testing.assert_close(total, tr, rtol=1e-5, atol=0)
+        torch.testing.assert_close(p, pr.detach(), rtol=1e-6, atol=1e-7)
+        torch.testing.assert_close(m, opt.state[pr]["exp_avg"], rtol=1e-5, atol=1e-8)
+        torch.testing.assert_close(v, opt.state[pr]["exp_avg_sq"], rtol=1e-5, atol=1e-10)
+        torch.testing.assert_close(ema, er, rtol=1e-6, atol=1e-7)
