@@ -204,12 +204,18 @@ __global__ __launch_bounds__(256) void gn_bwd_partial(GnBwd b, float* partial /*
   }
 }
 
-// per n: A[n][c] = sum over splits; coef[n][g] = (sum_c gamma*A1 / cnt, sum_c gamma*A2 / cnt)
-__global__ void gn_bwd_final(int C, int G, int HW, int splits, const float* partial, const float* gamma,
-                             float* A /*[n][C][2]*/, float* coef /*[n][G][2]*/) {
-  const int n = blockIdx.x;
+// One block per n: A[n][c] = sum over splits of the partials; coef (m1, m2) per group from the gamma-
+// weighted channel sums; and the per-(n, c) coefficients of the apply pass with the GN affine folded in:
+//   z = x*sc + sh (the SiLU input), dx = ka*dz + u*(x - mean) + w  (dz = dL/dz),
+//   ka = rstd*gm, u = -rstd^2*m2, w = -rstd*m1.
+// dgamma/dbeta = column sums of A over n (colsum_kernel).
+__global__ __launch_bounds__(256) void gn_bwd_final(int C, int G, int HW, int splits, const float* partial,
+                                                    const float* mr, const float* gamma, const float* beta,
+                                                    float* A /*[n][C][2]*/, float* cf /*[6][N][C]*/) {
+  const int n = blockIdx.x, N = gridDim.x;
   const int cpg = C / G;
   __shared__ float sA[1024][2];
+  __shared__ float sm[64][2];
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float v1 = 0.f, v2 = 0.f;
     for (int sp = 0; sp < splits; ++sp) {
@@ -226,8 +232,23 @@ __global__ void gn_bwd_final(int C, int G, int HW, int splits, const float* part
   for (int g = threadIdx.x; g < G; g += blockDim.x) {
     float m1 = 0.f, m2 = 0.f;
     for (int c = g * cpg; c < (g + 1) * cpg; ++c) { m1 += sA[c][0]; m2 += sA[c][1]; }
-    coef[((size_t)n * G + g) * 2] = m1 / cnt;
-    coef[((size_t)n * G + g) * 2 + 1] = m2 / cnt;
+    sm[g][0] = m1 / cnt;
+    sm[g][1] = m2 / cnt;
+  }
+  __syncthreads();
+  const size_t NC = (size_t)N * C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int g = c / cpg;
+    const float mean = mr[((size_t)n * G + g) * 2], rstd = mr[((size_t)n * G + g) * 2 + 1];
+    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    const size_t i = (size_t)n * C + c;
+    const float sc = rstd * gm;
+    cf[i] = sc;
+    cf[NC + i] = bt - mean * sc;
+    cf[2 * NC + i] = sc;
+    cf[3 * NC + i] = -rstd * rstd * sm[g][1];
+    cf[4 * NC + i] = mean;
+    cf[5 * NC + i] = -rstd * sm[g][0];
   }
 }
 
@@ -322,19 +343,30 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(Src2 s, int HW, const flo
   }
 }
 
-// dx = rstd * (dz * gamma - m1 - xhat * m2) per element. Grid (N, pixel splits) like gn_apply_kernel: a
-// thread owns one 16-byte channel chunk column of one sample, so every per-channel coefficient is computed
-// once into registers and the pixel walk is pure streaming (x, g in; dx out).
+// dx = ka*dz + u*(x - mean) + w per element with the per-(n, c) coefficients of gn_bwd_final (vector loads).
+// Grid (N, pixel splits) like gn_apply_kernel: a thread owns one 16-byte channel chunk column of one
+// sample and walks pixels, streaming x, g in and dx out. Optionally (sum_part != NULL) it also reduces its
+// output per (n, split, c) -- the bias / time-embedding gradient of the layer that produced x -- so dx is
+// never re-read for that.
+template <int EPC>
+DMC_DEV void load_coef(const float* p, float* v) {
+#pragma unroll
+  for (int i = 0; i < EPC; i += 4) {
+    const v4f q = *(const v4f*)(p + i);
+    v[i] = q[0]; v[i + 1] = q[1]; v[i + 2] = q[2]; v[i + 3] = q[3];
+  }
+}
+
 template <typename T>
-__global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* coef, char* dx1, char* dx2, int ld1,
-                                                    int ld2, int acc1, int acc2) {
+__global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* cf, char* dx1, char* dx2, int ld1,
+                                                    int ld2, int acc1, int acc2, float* sum_part) {
   constexpr int EPC = TT<T>::KPL;
-  const int C = b.s.C1 + b.s.C2, cpg = C / b.G, CPR = C / EPC, rpi = 256 / CPR;
-  const int col = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
-  if (r0 >= rpi) return;
-  const int n = blockIdx.x;
+  const int C = b.s.C1 + b.s.C2, CPR = C / EPC, rpi = 256 / CPR;
+  const int tid = threadIdx.x, col = tid % CPR, r0 = tid / CPR;
+  const bool active = r0 < rpi;
+  const int n = blockIdx.x, sp = blockIdx.y;
   const int per = (b.HW + gridDim.y - 1) / gridDim.y;
-  const int pb = blockIdx.y * per, pe = min(b.HW, pb + per);
+  const int pb = sp * per, pe = min(b.HW, pb + per);
   const int c0 = col * EPC;
   const bool first = c0 < b.s.C1;
   char* const dst = first ? dx1 : dx2;
@@ -351,46 +383,65 @@ __global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* coef, 
       }
     }
   };
-  // the first rows are in flight while the per-channel coefficients load
-  if (pb + r0 < pe) issue(pb + r0);
-  float mean[EPC], rstd[EPC], gm[EPC], bt[EPC], ka[EPC], kb[EPC], kc[EPC];
+  if (active && pb + r0 < pe) issue(pb + r0);   // the first rows are in flight while the coefficients load
+  const size_t NC = (size_t)gridDim.x * C, ci = (size_t)n * C + c0;
+  float sc[EPC], sh[EPC], ka[EPC], ku[EPC], km[EPC], kw[EPC], sum[EPC];
+  load_coef<EPC>(cf + ci, sc);
+  load_coef<EPC>(cf + NC + ci, sh);
+  load_coef<EPC>(cf + 2 * NC + ci, ka);
+  load_coef<EPC>(cf + 3 * NC + ci, ku);
+  load_coef<EPC>(cf + 4 * NC + ci, km);
+  load_coef<EPC>(cf + 5 * NC + ci, kw);
 #pragma unroll
-  for (int e = 0; e < EPC; ++e) {
-    const int c = c0 + e, g = c / cpg;
-    mean[e] = b.mr[((size_t)n * b.G + g) * 2];
-    rstd[e] = b.mr[((size_t)n * b.G + g) * 2 + 1];
-    gm[e] = b.gamma ? b.gamma[c] : 1.f;
-    bt[e] = b.beta ? b.beta[c] : 0.f;
-    ka[e] = rstd[e] * gm[e];
-    kb[e] = rstd[e] * coef[((size_t)n * b.G + g) * 2];
-    kc[e] = rstd[e] * coef[((size_t)n * b.G + g) * 2 + 1];
+  for (int e = 0; e < EPC; ++e) sum[e] = 0.f;
+  if (active) {
+    for (int p0 = pb + r0; p0 < pe; p0 += UNR * rpi) {
+      if (p0 != pb + r0) issue(p0);
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (p0 + u * rpi >= pe) break;
+        const int pix = n * b.HW + p0 + u * rpi;
+        float x[EPC], gv[EPC], o[EPC];
+        Chunk<T>::unpack(bx[u], x);
+        Chunk<T>::unpack(bg[u], gv);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+          float gg = gv[e];
+          if (b.dthresh) gg = drop_keep((uint64_t)pix * C + c0 + e, b.dseed, b.dthresh) ? gg * b.dscale : 0.f;
+          float dz = gg;
+          if (b.silu) {
+            const float z = fmaf(x[e], sc[e], sh[e]);
+            const float sg = sigmoid_f(z);
+            dz = gg * sg * (1.f + z * (1.f - sg));
+          }
+          o[e] = fmaf(ka[e], dz, fmaf(ku[e], x[e] - km[e], kw[e]));
+        }
+        if (acc) {
+          float prev[EPC];
+          Chunk<T>::unpack(bp[u], prev);
+#pragma unroll
+          for (int e = 0; e < EPC; ++e) o[e] += prev[e];
+        }
+        const v4i packed = Chunk<T>::pack(o);
+        *(v4i*)(dst + ((size_t)pix * ldd + cd) * sizeof(T)) = packed;
+        if (sum_part) {
+          // sum what was stored (bf16-rounded in bf16 mode), like a later channel-sum pass would
+          Chunk<T>::unpack(packed, o);
+#pragma unroll
+          for (int e = 0; e < EPC; ++e) sum[e] += o[e];
+        }
+      }
+    }
   }
-  for (int p0 = pb + r0; p0 < pe; p0 += UNR * rpi) {
-    if (p0 != pb + r0) issue(p0);
+  if (!sum_part) return;
+  __shared__ float red[256][8];
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-    if (p0 + u * rpi >= pe) break;
-    const int pix = n * b.HW + p0 + u * rpi;
-    float x[EPC], gv[EPC], o[EPC];
-    Chunk<T>::unpack(bx[u], x);
-    Chunk<T>::unpack(bg[u], gv);
-#pragma unroll
-    for (int e = 0; e < EPC; ++e) {
-      float gg = gv[e];
-      if (b.dthresh) gg = drop_keep((uint64_t)pix * C + c0 + e, b.dseed, b.dthresh) ? gg * b.dscale : 0.f;
-      float xh;
-      const float dz = gn_dz(x[e], gg, mean[e], rstd[e], gm[e], bt[e], xh, b.silu);
-      o[e] = ka[e] * dz - kb[e] - kc[e] * xh;
-    }
-    v4i* q = (v4i*)(dst + ((size_t)pix * ldd + cd) * sizeof(T));
-    if (acc) {
-      float prev[EPC];
-      Chunk<T>::unpack(bp[u], prev);
-#pragma unroll
-      for (int e = 0; e < EPC; ++e) o[e] += prev[e];
-    }
-    *q = Chunk<T>::pack(o);
-    }
+  for (int e = 0; e < EPC; ++e) red[tid][e] = active ? sum[e] : 0.f;
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    float v = 0.f;
+    for (int r = 0; r < rpi; ++r) v += red[r * CPR + c / EPC][c % EPC];
+    sum_part[((size_t)n * gridDim.y + sp) * C + c] = v;
   }
 }
 
@@ -444,6 +495,17 @@ __global__ void chsum_nc(int N, int C, int splits, const float* partial, float* 
   }
 }
 
+// out_nc (may be NULL) and out_c = column sums over all n and splits (may be NULL) of partial [N][splits][C]
+void chsum_finish(hipStream_t s, int N, int C, int splits, const float* partial, float* out_nc, int ld_out,
+                  float* out_c, float scale) {
+  if (out_nc) {
+    const long tot = (long)N * C;
+    chsum_nc<<<(int)((tot + 255) / 256 < 4096 ? (tot + 255) / 256 : 4096), 256, 0, s>>>(N, C, splits, partial, out_nc,
+                                                                                          ld_out, scale);
+  }
+  if (out_c) colsum_kernel<<<(C + 63) / 64, 1024, 0, s>>>(partial, N * splits, C, C, 1, out_c, nullptr, scale);
+}
+
 int host_splits(int N, int HW, int C, int epc) {
   const int cpr = (C + epc - 1) / epc;
   const int rpi = 256 / cpr > 0 ? 256 / cpr : 1;
@@ -458,7 +520,7 @@ int host_splits(int N, int HW, int C, int epc) {
 extern "C" size_t dmc_gn_workspace(int N, int C, int G, int HW) {
   const int splits = host_splits(N, HW, C, 4);  // fp32 chunking gives the largest split count
   size_t stats = (size_t)N * splits * G * 2;
-  size_t bwd = (size_t)N * splits * C * 2 + (size_t)N * C * 2 + (size_t)N * G * 2;
+  size_t bwd = (size_t)N * splits * C * 2 + (size_t)N * C * 2 + (size_t)N * C * 6 + (size_t)N * splits * C;
   return (stats > bwd ? stats : bwd) * sizeof(float) + 256;
 }
 
@@ -489,12 +551,14 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
                                int C2, int ld1, int ld2, int G, const float* mean_rstd, const float* gamma,
                                const float* beta, int silu, uint32_t drop_seed, uint32_t drop_thresh, float drop_scale, void* dx1,
                                void* dx2, int ld_dx1, int ld_dx2, int accumulate1, int accumulate2, float* dgamma,
-                               float* dbeta, void* workspace, void* stream) {
+                               float* dbeta, float* dx_sum_nc, int ld_sum_nc, float* dx_sum_c, void* workspace,
+                               void* stream) {
   const int epc = dtype == DMC_F32 ? 4 : 8;
   const int C = C1 + C2;
-  DMC_REQUIRE(C % G == 0 && C <= 1024, "gn_bwd: C %d / G %d", C, G);
+  DMC_REQUIRE(C % G == 0 && C <= 1024 && G <= 64, "gn_bwd: C %d / G %d", C, G);
   DMC_REQUIRE(C1 % epc == 0 && C2 % epc == 0 && C / epc <= 256, "gn_bwd: channel alignment");
   DMC_REQUIRE(ld_g % epc == 0 && ld_dx1 % epc == 0 && (C2 == 0 || ld_dx2 % epc == 0), "gn_bwd: pitch alignment");
+  DMC_REQUIRE(!(dx_sum_nc || dx_sum_c) || C2 == 0, "gn_bwd: dx channel sums need a single source");
   hipStream_t s = dmc::as_stream(stream);
   GnBwd b;
   b.s = Src2{(const char*)x1, (const char*)x2, C1, C2, ld1, ld2};
@@ -505,17 +569,22 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
   b.silu = silu;
   float* partial = (float*)workspace;
   float* A = partial + (size_t)N * b.splits * C * 2;
-  float* coef = A + (size_t)N * C * 2;
+  float* cf = A + (size_t)N * C * 2;
+  float* sums = cf + (size_t)N * C * 6;
+  const bool want_sums = dx_sum_nc || dx_sum_c;
   dim3 gr(N, b.splits);
   if (dtype == DMC_F32) gn_bwd_partial<float><<<gr, 256, 0, s>>>(b, partial);
   else gn_bwd_partial<bf16_t><<<gr, 256, 0, s>>>(b, partial);
-  gn_bwd_final<<<N, 256, 0, s>>>(C, G, HW, b.splits, partial, gamma, A, coef);
+  gn_bwd_final<<<N, 256, 0, s>>>(C, G, HW, b.splits, partial, mean_rstd, gamma, beta, A, cf);
   // dbeta[c] = sum_n A[n][c][0], dgamma[c] = sum_n A[n][c][1]
   colsum_kernel<<<(C + 63) / 64, 1024, 0, s>>>(A, N, C, (long)C * 2, 2, dbeta, dgamma, 1.0f);
   if (dtype == DMC_F32)
-    gn_bwd_apply<float><<<gr, 256, 0, s>>>(b, coef, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, accumulate1, accumulate2);
+    gn_bwd_apply<float><<<gr, 256, 0, s>>>(b, cf, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, accumulate1, accumulate2,
+                                           want_sums ? sums : nullptr);
   else
-    gn_bwd_apply<bf16_t><<<gr, 256, 0, s>>>(b, coef, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, accumulate1, accumulate2);
+    gn_bwd_apply<bf16_t><<<gr, 256, 0, s>>>(b, cf, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, accumulate1, accumulate2,
+                                            want_sums ? sums : nullptr);
+  if (want_sums) chsum_finish(s, N, C, b.splits, sums, dx_sum_nc, ld_sum_nc, dx_sum_c, 1.0f);
   return dmc::check_launch("dmc_gn_silu_bwd");
 }
 
@@ -533,12 +602,7 @@ extern "C" int dmc_channel_sum(int dtype, const void* dy, int N, int HW, int C, 
   dim3 g(N, splits);
   if (dtype == DMC_F32) chsum_partial<float><<<g, 256, 0, s>>>((const char*)dy, HW, C, ld, splits, partial);
   else chsum_partial<bf16_t><<<g, 256, 0, s>>>((const char*)dy, HW, C, ld, splits, partial);
-  if (out_nc) {
-    const long tot = (long)N * C;
-    chsum_nc<<<(int)((tot + 255) / 256 < 4096 ? (tot + 255) / 256 : 4096), 256, 0, s>>>(N, C, splits, partial, out_nc,
-                                                                                          ld_out, scale);
-  }
-  if (out_c) colsum_kernel<<<(C + 63) / 64, 1024, 0, s>>>(partial, N * splits, C, C, 1, out_c, nullptr, scale);
+  chsum_finish(s, N, C, splits, partial, out_nc, ld_out, out_c, scale);
   return dmc::check_launch("dmc_channel_sum");
 }
 

@@ -164,12 +164,15 @@ def gn_apply(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, scale, shift, silu=True, dr
 
 
 def gn_bwd(dtype, g, ld_g, x1, x2, N, HW, C1, C2, ld1, ld2, G, mr, gamma, beta, silu, drop, dx1, dx2, ld_dx1,
-           ld_dx2, acc1, acc2, dgamma, dbeta):
+           ld_dx2, acc1, acc2, dgamma, dbeta, dx_sum_nc=None, ld_sum_nc=0, dx_sum_c=None):
+    """GroupNorm(+SiLU+dropout) backward; optionally also the per-(n,c) / per-c pixel sums of dx (the bias and
+    time-embedding gradients of the layer that produced x), fused into the dx pass."""
     ws = SCRATCH.get(LIB.dmc_gn_workspace(N, C1 + C2, G, HW), g.device)
     seed, thresh, scale = drop if drop is not None else (0, 0, 1.0)
     check(LIB.dmc_gn_silu_bwd(L.dtype_code(dtype), ptr(g), ld_g, ptr(x1), ptr(x2), N, HW, C1, C2, ld1, ld2, G, ptr(mr),
                               ptr(gamma), ptr(beta), int(silu), seed, thresh, scale, ptr(dx1), ptr(dx2), ld_dx1, ld_dx2,
-                              int(acc1), int(acc2), ptr(dgamma), ptr(dbeta), ptr(ws), L.stream()), "dmc_gn_silu_bwd")
+                              int(acc1), int(acc2), ptr(dgamma), ptr(dbeta), ptr(dx_sum_nc), ld_sum_nc, ptr(dx_sum_c),
+                              ptr(ws), L.stream()), "dmc_gn_silu_bwd")
 
 
 def channel_sum(dtype, dy, N, HW, C, ld, out_nc=None, ld_out=0, out_c=None, scale=1.0):

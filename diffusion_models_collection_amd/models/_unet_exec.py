@@ -615,16 +615,15 @@ class UNetExecutor:
                 a.grad = dout          # identity shortcut: alias (dout is dead after this block)
             else:
                 K.add_(dt, a.grad, dout)
-        # GN2 + SiLU + dropout backward -> dh1
-        dh1 = torch.empty(N, H, W, Cout, dtype=dt, device=dout.device)
-        K.gn_bwd(dt, g2, Cout, h1.t, None, N, HW, Cout, 0, Cout, 0, gn2.num_groups, st2[2], gn2.weight, gn2.bias, True,
-                 drop, dh1, None, Cout, 0, 0, 0, gv(gn2.weight), gv(gn2.bias))
-        # time-embedding add: per-(n, c) pixel sums -> daddvec slice; conv1 bias
+        # GN2 + SiLU + dropout backward -> dh1, with its pixel sums fused in: per (n, c) -> the time-embedding
+        # add's gradient (daddvec slice), per c -> conv1's bias gradient
         off = self.temb_off[id(rb)]
         if self.daddvec is None:
             self.daddvec = torch.empty(N, self.temb_total, dtype=torch.float32, device=dout.device)
-        K.channel_sum(dt, dh1, N, HW, Cout, Cout, out_nc=self.daddvec[:, off:], ld_out=self.temb_total,
-                      out_c=gv(conv1.bias))
+        dh1 = torch.empty(N, H, W, Cout, dtype=dt, device=dout.device)
+        K.gn_bwd(dt, g2, Cout, h1.t, None, N, HW, Cout, 0, Cout, 0, gn2.num_groups, st2[2], gn2.weight, gn2.bias, True,
+                 drop, dh1, None, Cout, 0, 0, 0, gv(gn2.weight), gv(gn2.bias), dx_sum_nc=self.daddvec[:, off:],
+                 ld_sum_nc=self.temb_total, dx_sum_c=gv(conv1.bias))
         # conv1
         self._wgrad([a1], dh1, Cout, K.TAPS3, H, W, Cout, gv(conv1.weight))
         g1 = torch.empty(N, H, W, C1 + C2, dtype=dt, device=dout.device)

@@ -118,13 +118,15 @@ int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C
 /* Backward of a = dropout(SiLU(GroupNorm(x))) (silu=1) or a = GroupNorm(x) (silu=0, AttentionBlock
  * norm :80): g = dL/da (dtype, [pix][ld_g]); writes
  * dx (split into dx1/dx2 by channel like the sources; accumulate_k: add into existing),
- * dgamma/dbeta (fp32 [C], overwritten). */
+ * dgamma/dbeta (fp32 [C], overwritten) and, if dx_sum_nc / dx_sum_c are not NULL (single source
+ * only), the pixel sums of the stored dx per (n,c) ([N][ld_sum_nc]) / per c -- the bias and
+ * time-embedding gradients of the layer that produced x (models/unet.py:64), fused into the dx pass. */
 int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x1, const void* x2, int N,
                     int HW, int C1, int C2, int ld1, int ld2, int G, const float* mean_rstd,
                     const float* gamma, const float* beta, int silu, uint32_t drop_seed,
                     uint32_t drop_thresh, float drop_scale, void* dx1, void* dx2, int ld_dx1,
                     int ld_dx2, int accumulate1, int accumulate2, float* dgamma, float* dbeta,
-                    void* workspace, void* stream);
+                    float* dx_sum_nc, int ld_sum_nc, float* dx_sum_c, void* workspace, void* stream);
 
 /* Per-(n,c) pixel sums of dy [N][HW][ld] -> out_nc [N][ld_out] (may be NULL) and per-c
  * sums over n -> out_c [C] (may be NULL); both fp32, scaled by `scale`. Bias / embedding grads. */

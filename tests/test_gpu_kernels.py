@@ -248,6 +248,27 @@ def test_groupnorm_stats_and_backward(dt):
     dxk = nchw(torch.cat([dx1, dx2], -1).float().cpu())
     assert rel_err(dxk, x.grad) < (1e-4 if dt == torch.float32 else 2e-2)
     assert rel_err(dg.cpu(), gamma.grad) < 1e-4 and rel_err(db.cpu(), beta.grad) < 1e-4
+    # single source with dropout, accumulation and the fused pixel sums of the stored dx
+    xs = xd.contiguous()
+    scs, shs, mrs = K.gn_stats(dt, xs, None, N, H * W, C1 + C2, 0, C1 + C2, 0, G, 1e-5, gamma.detach().to(DEV),
+                               beta.detach().to(DEV))
+    prev = q(torch.randn(N, H, W, C1 + C2), dt).to(dt).to(DEV)
+    dxs = prev.clone()
+    snc = torch.full((N, 100), -7.0, device=DEV)
+    sc_ = torch.empty(C1 + C2, device=DEV)
+    drop = (1 << 30, 0, 4.0 / 3.0)   # keep prob 0.75
+    K.gn_bwd(dt, nhwc(gout).to(dt).to(DEV), C1 + C2, xs, None, N, H * W, C1 + C2, 0, C1 + C2, 0, G, mrs,
+             gamma.detach().to(DEV), beta.detach().to(DEV), True, drop, dxs, None, C1 + C2, 0, 1, 0, dg, db,
+             dx_sum_nc=snc, ld_sum_nc=100, dx_sum_c=sc_)
+    dx0 = torch.empty_like(xs)
+    K.gn_bwd(dt, nhwc(gout).to(dt).to(DEV), C1 + C2, xs, None, N, H * W, C1 + C2, 0, C1 + C2, 0, G, mrs,
+             gamma.detach().to(DEV), beta.detach().to(DEV), True, drop, dx0, None, C1 + C2, 0, 0, 0, dg, db)
+    torch.cuda.synchronize()
+    assert rel_err(dxs.float(), dx0.float() + prev.float()) < (1e-5 if dt == torch.float32 else 1e-2)
+    ref_nc = dxs.float().sum((1, 2))
+    torch.testing.assert_close(snc[:, :C1 + C2], ref_nc, rtol=1e-4, atol=1e-3)
+    assert (snc[:, C1 + C2:] == -7.0).all()
+    torch.testing.assert_close(sc_, ref_nc.sum(0), rtol=1e-4, atol=1e-3)
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
