@@ -30,6 +30,7 @@ struct ConvK {
   int sk_per; // K stages per split
   int x1_bytes, x2_bytes, w_bytes;  // operand extents for buffer resources (0: too large / absent)
   int dbg;    // probe-only ablation bits of the halo kernel (env DMC_HALO_DBG; 0 in production)
+  int dtype_bytes;  // 4 (fp32) or 2 (bf16) storage
 };
 
 // Source pixel of output pixel (n,oy,ox) under tap; returns -1 if it falls in the zero padding.
@@ -196,13 +197,16 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvK a) {
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  load_stage(0);
+  // split-K over grid.z: this block's stage range (whole K without a slab)
+  const int s_begin = a.sk ? blockIdx.z * a.sk_per : 0;
+  const int s_end = a.sk ? min(nstages, s_begin + a.sk_per) : nstages;
+  load_stage(s_begin);
   store_stage(0);
   __syncthreads();
   const int fr = lane & 15, fh = lane >> 4;
-  for (int s = 0; s < nstages; ++s) {
-    const int buf = s & 1;
-    if (s + 1 < nstages) load_stage(s + 1);
+  for (int s = s_begin; s < s_end; ++s) {
+    const int buf = (s - s_begin) & 1;
+    if (s + 1 < s_end) load_stage(s + 1);
     const char* A = lds[buf];
     const char* B = lds[buf] + BM * 128;
 #pragma unroll
@@ -224,8 +228,21 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvK a) {
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
     }
-    if (s + 1 < nstages) store_stage(buf ^ 1);
+    if (s + 1 < s_end) store_stage(buf ^ 1);
     __syncthreads();
+  }
+  if (a.sk) {
+    // raw partial sums -> slab [z][M][Cpad] (conv_splitk_epilogue_kernel reduces and applies the epilogue)
+    const int Cpad = gridDim.y * BN;
+    float* slab = a.sk + (size_t)blockIdx.z * a.M * Cpad;
+#pragma unroll
+    for (int j = 0; j < TM; ++j)
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int pix = m0 + wm * (BM / 2) + j * 16 + fr, co = n0 + wn * (BN / 2) + i * 16 + fh * 4;
+        if (pix < a.M) *(v4f*)(slab + (size_t)pix * Cpad + co) = acc[i][j];
+      }
+    return;
   }
   conv_epilogue<T, TN, TM>(a, acc, m0 + wm * (BM / 2), n0 + wn * (BN / 2));
 }
@@ -1206,6 +1223,7 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
   DMC_REQUIRE(d->Csplit >= 0 && d->Csplit <= d->Cout && (d->Csplit == d->Cout || d->Csplit % 4 == 0),
               "conv: Csplit %d", d->Csplit);
   k.x1 = (const char*)x1; k.x2 = (const char*)x2; k.w = (const char*)w; k.y1 = (char*)y1; k.y2 = (char*)y2;
+  k.dtype_bytes = d->dtype == DMC_F32 ? 4 : 2;
   k.N = d->N; k.H = d->H; k.W = d->W; k.C1 = d->C1; k.C2 = d->C2; k.ld1 = d->ld1; k.ld2 = d->ld2; k.Kc = d->Kc;
   k.OH = d->OH; k.OW = d->OW; k.Cout = d->Cout; k.ntaps = d->ntaps; k.mode = d->mode; k.stride = d->stride;
   // the kernels take the taps as a regular grid (no dynamically indexed kernel-argument arrays, which
@@ -1275,6 +1293,32 @@ FwdPlan plan_glds(const ConvK& k) {
   return p;
 }
 
+// Launch plan of the register-staged kernel: 128x128 tiles for big problems, else 64x64 tiles with split-K
+// when there are few tiles and many K stages.
+struct RegPlan {
+  bool big;
+  int splits, per;
+  size_t ws;
+};
+
+RegPlan plan_reg(const ConvK& k) {
+  RegPlan p{false, 1, 0, 0};
+  const long t128 = (long)dmc::cdiv(k.M, 128) * dmc::cdiv(k.Cout, 128);
+  if (t128 >= 384 && k.Cout >= 128) { p.big = true; return p; }
+  const int bk = k.dtype_bytes == 4 ? 32 : 64;
+  const int nst = k.ntaps * (k.Kc / bk);
+  const long t64 = (long)dmc::cdiv(k.M, 64) * dmc::cdiv(k.Cout, 64);
+  if (t64 >= 128 || nst < 16) return p;
+  int sp = (int)((256 + t64 - 1) / t64);
+  if (sp > nst / 8) sp = nst / 8;
+  if (sp > 16) sp = 16;
+  if (sp < 2) return p;
+  p.per = (nst + sp - 1) / sp;
+  p.splits = (nst + p.per - 1) / p.per;
+  p.ws = (size_t)p.splits * k.M * (size_t)dmc::cdiv(k.Cout, 64) * 64 * sizeof(float);
+  return p;
+}
+
 template <bool BUF>
 void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
   if (p.splits > 1) {
@@ -1316,10 +1360,20 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     return dmc::check_launch("dmc_conv2d");
   }
   // register-staged kernel (fp32 parity mode, or a fused prologue)
-  const long t128 = (long)dmc::cdiv(k.M, 128) * dmc::cdiv(k.Cout, 128);
-  if (t128 >= 384 && k.Cout >= 128) {
+  const RegPlan rp = plan_reg(k);
+  if (rp.big) {
     dim3 g(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128));
     conv_fwd_kernel<T, 128, 128><<<g, 256, 0, s>>>(k);
+  } else if (rp.splits > 1 && ws != nullptr && ws_bytes >= rp.ws && !getenv_flag("DMC_NO_SPLITK")) {
+    // few 64x64 tiles and a long K (the time-embedding GEMMs, K up to 4992): split K over grid.z
+    k.sk = (float*)ws;
+    k.sk_per = rp.per;
+    dim3 g(dmc::cdiv(k.M, 64), dmc::cdiv(k.Cout, 64), rp.splits);
+    conv_fwd_kernel<T, 64, 64><<<g, 256, 0, s>>>(k);
+    const int Cpad = dmc::cdiv(k.Cout, 64) * 64;
+    const long total = (long)k.M * Cpad / 4;
+    const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+    conv_splitk_epilogue_kernel<T><<<blocks, 256, 0, s>>>(k, rp.splits, Cpad);
   } else {
     dim3 g(dmc::cdiv(k.M, 64), dmc::cdiv(k.Cout, 64));
     conv_fwd_kernel<T, 64, 64><<<g, 256, 0, s>>>(k);
@@ -1348,7 +1402,8 @@ int wgrad_splits(const dmc_conv_desc* d, int* pps) {
 extern "C" size_t dmc_conv2d_workspace(const dmc_conv_desc* d) {
   ConvK k;
   if (fill_convk(d, nullptr, nullptr, nullptr, nullptr, nullptr, k)) return 0;
-  if (d->dtype != DMC_BF16 || d->prologue != DMC_PRO_NONE || k.M == 0) return 0;
+  if (k.M == 0) return 0;
+  if (d->dtype != DMC_BF16 || d->prologue != DMC_PRO_NONE || getenv_flag("DMC_NO_GLDS")) return plan_reg(k).ws;
   return plan_glds(k).ws;
 }
 

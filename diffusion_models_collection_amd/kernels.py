@@ -18,16 +18,22 @@ TAPS_UPDGRAD = [(u - 1, v - 1) for u in range(4) for v in range(4)]    # folded 
 
 
 class Scratch:
-    """Grow-only device scratch shared by the kernels of one stream (wgrad slabs, GN partials, ...)."""
+    """Grow-only device scratch (wgrad slabs, GN partials, ...), one buffer per HIP stream: kernels of one
+    stream run in order and may share it; kernels on another stream (the executor's weight-gradient side
+    stream) get their own. A buffer is allocated while its stream is current, so the caching allocator
+    never hands it to another stream while its kernels are pending."""
 
     def __init__(self):
-        self.buf = None
+        self.bufs = {}
 
     def get(self, nbytes: int, device) -> torch.Tensor:
         nbytes = max(int(nbytes), 256)
-        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
-            self.buf = torch.empty(int(nbytes * 1.25) + 4096, dtype=torch.uint8, device=device)
-        return self.buf
+        key = (torch.cuda.current_stream(device).cuda_stream, str(device))
+        buf = self.bufs.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(int(nbytes * 1.25) + 4096, dtype=torch.uint8, device=device)
+            self.bufs[key] = buf
+        return buf
 
 
 SCRATCH = Scratch()
@@ -77,18 +83,60 @@ def set_epilogue(d, bias=None, addvec=None, ld_add=0, resid=None, ld_res=0, silu
     d.out_nchw = int(out_nchw)
 
 
+class LayerProfile:
+    """Opt-in (DMC_LAYER_PROF=1) per-call timing of the conv launches, keyed by kind and shape: HIP events on
+    the launch stream around each call, read back by report(). Measurement tooling only."""
+
+    def __init__(self):
+        import os
+        self.on = os.environ.get("DMC_LAYER_PROF", "0") not in ("", "0")
+        self.pending = []
+
+    def wrap(self, kind, d, fn):
+        if not self.on:
+            return fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        M = d.N * d.OH * d.OW
+        key = (kind, d.dtype, d.N, d.H, d.W, d.C1 + d.C2, d.OH, d.OW, d.Cout, d.ntaps, d.mode)
+        self.pending.append((key, 2.0 * M * d.Cout * d.ntaps * (d.C1 + d.C2), e0, e1))
+
+    def report(self, steps=1):
+        torch.cuda.synchronize()
+        agg = {}
+        for key, fl, e0, e1 in self.pending:
+            a = agg.setdefault(key, [0, 0.0, 0.0])
+            a[0] += 1
+            a[1] += e0.elapsed_time(e1)
+            a[2] += fl
+        self.pending = []
+        rows = sorted(agg.items(), key=lambda kv: -kv[1][1])
+        tot = sum(v[1] for v in agg.values())
+        lines = [f"conv launches: {tot / steps:.3f} ms/step"]
+        for (kind, dt, N, H, W, Cin, OH, OW, Cout, nt, mode), (n, ms, fl) in rows:
+            lines.append(f"{ms / steps * 1e3:8.1f} us/step  n/step {n / steps:4.1f}  avg {ms / n * 1e3:7.1f} us  "
+                         f"{fl / (ms * 1e-3) / 1e12:7.1f} TF/s  {kind:5s} N{N} {H}x{W}x{Cin} -> {OH}x{OW}x{Cout} "
+                         f"taps {nt} mode {mode}")
+        return "\n".join(lines)
+
+
+PROF = LayerProfile()
+
+
 def conv(d, x1, x2, w, y1, y2=None):
     nbytes = LIB.dmc_conv2d_workspace(ctypes.byref(d))
     ws = SCRATCH.get(nbytes, y1.device) if nbytes else None
-    check(LIB.dmc_conv2d(ctypes.byref(d), ptr(x1), ptr(x2), ptr(w), ptr(y1), ptr(y2), ptr(ws), nbytes, L.stream()),
-          "dmc_conv2d")
+    PROF.wrap("conv", d, lambda: check(LIB.dmc_conv2d(ctypes.byref(d), ptr(x1), ptr(x2), ptr(w), ptr(y1), ptr(y2),
+                                                      ptr(ws), nbytes, L.stream()), "dmc_conv2d"))
 
 
 def wgrad(d, dy, ld_dy, x1, x2, dw, scale=1.0):
     nbytes = LIB.dmc_conv2d_wgrad_workspace(ctypes.byref(d))
     ws = SCRATCH.get(nbytes, dy.device)
-    check(LIB.dmc_conv2d_wgrad(ctypes.byref(d), ptr(dy), ld_dy, ptr(x1), ptr(x2), ptr(ws), ptr(dw), scale, L.stream()),
-          "dmc_conv2d_wgrad")
+    PROF.wrap("wgrad", d, lambda: check(LIB.dmc_conv2d_wgrad(ctypes.byref(d), ptr(dy), ld_dy, ptr(x1), ptr(x2), ptr(ws),
+                                                             ptr(dw), scale, L.stream()), "dmc_conv2d_wgrad"))
 
 
 def pack_weight(mode, dtype, w, Kc, out=None):

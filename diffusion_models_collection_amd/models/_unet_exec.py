@@ -17,7 +17,9 @@ fly (dropout masks come from a counter hash, never stored). Every parameter grad
 into one flat fp32 buffer (views are handed to autograd), which is also what the data-parallel
 all-reduce works on.
 """
+import contextlib
 import math
+import os
 from typing import List, Optional
 
 import torch
@@ -111,6 +113,10 @@ class UNetExecutor:
         self.daddvec = None
         self.training_grad_scale = 1.0
         self.grad_hook = None       # called as hook(flat_grad, lo, hi) when a range of grads is final
+        # measured slower on MI355X (the overlapped kernels contend for LDS and CUs): opt-in only
+        self.use_side = os.environ.get("DMC_SIDE_STREAM", "0") not in ("", "0")
+        self.side = None
+        self._side_reads = {}
 
     # ---------------------------------------------------------------------------------------
     def _layout_grads(self):
@@ -292,7 +298,44 @@ class UNetExecutor:
         if act.grad is None:
             act.grad = torch.empty_like(act.t)
             return act.grad, 0
+        self._guard(act.grad)
         return act.grad, 1
+
+    # ---- weight-gradient side stream --------------------------------------------------------
+    # The backward has two chains per layer: the input-gradient chain (dgrad conv -> GroupNorm backward ->
+    # next layer), which is the critical path, and the weight/bias gradients, which only the optimizer
+    # needs. The latter run on a second HIP stream so they fill the CUs the latency-bound GroupNorm and
+    # small-M kernels leave idle. Hazards: (1) a side kernel reads tensors the main stream may free
+    # (record_stream) or later accumulate into (an aliased gradient buffer: _guard makes the main stream
+    # wait for the side reads first); (2) the flat gradient buffer is complete only after a join.
+    @contextlib.contextmanager
+    def _side(self, *reads):
+        if not self.use_side:
+            yield
+            return
+        main = torch.cuda.current_stream()
+        if self.side is None or self.side.device != main.device:
+            self.side = torch.cuda.Stream(device=main.device)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            yield
+        ev = torch.cuda.Event()
+        ev.record(self.side)
+        for t in reads:
+            t.record_stream(self.side)
+            self._side_reads[t.untyped_storage().data_ptr()] = ev
+
+    def _guard(self, t):
+        """The main stream is about to write `t` in place: wait for pending side-stream reads of it."""
+        if self._side_reads:
+            ev = self._side_reads.pop(t.untyped_storage().data_ptr(), None)
+            if ev is not None:
+                torch.cuda.current_stream().wait_event(ev)
+
+    def _join_side(self):
+        if self.use_side and self.side is not None:
+            torch.cuda.current_stream().wait_stream(self.side)
+        self._side_reads = {}
 
     # =========================================================================================
     def run(self, x, t, y=None):
@@ -488,7 +531,10 @@ class UNetExecutor:
                 while cursor < len(order) and final[order[cursor]]:
                     cursor += 1
                 hi = self.goff[order[cursor]] if cursor < len(order) else self.gtotal
+                if getattr(hook, "wants", None) is None or hook.wants(hi, kind == "temb"):
+                    self._join_side()      # the side stream's weight gradients of that prefix are written
                 hook(flat, hi, kind == "temb")
+        self._join_side()
         self.daddvec = None
         grads = [self._gview(flat, p) for p in self.params]
         return dx, grads
@@ -523,8 +569,9 @@ class UNetExecutor:
                 Co = m.out_channels
                 ldo = (Co + self.chunk - 1) // self.chunk * self.chunk
                 dy = K.pack_input(dt, dout.contiguous(), ldo)
-                self._wgrad([ao], dy, ldo, K.TAPS3, H, W, Co, gv(convo.weight))
-                K.channel_sum(dt, dy, N, H * W, Co, ldo, out_c=gv(convo.bias))
+                with self._side(ao.t, dy):
+                    self._wgrad([ao], dy, ldo, K.TAPS3, H, W, Co, gv(convo.weight))
+                    K.channel_sum(dt, dy, N, H * W, Co, ldo, out_c=gv(convo.bias))
                 g = torch.empty(N, H, W, h.C, dtype=dt, device=dout.device)
                 dya = Act(dy, H, W, Co)
                 self._conv([dya], convo, K.TAPS3_DGRAD, H, W, h.C, out=g, packmode=L.PACK_DGRAD,
@@ -540,8 +587,9 @@ class UNetExecutor:
                 _, layer, a, out = rec
                 N = a.t.shape[0]
                 dy = out.grad
-                self._wgrad([a], dy, out.C, K.TAPS3, out.H, out.W, out.C, gv(layer.conv.weight), stride=2)
-                K.channel_sum(dt, dy, N, out.H * out.W, out.C, out.C, out_c=gv(layer.conv.bias))
+                with self._side(a.t, dy):
+                    self._wgrad([a], dy, out.C, K.TAPS3, out.H, out.W, out.C, gv(layer.conv.weight), stride=2)
+                    K.channel_sum(dt, dy, N, out.H * out.W, out.C, out.C, out_c=gv(layer.conv.bias))
                 buf, acc = self._grad_target(a)
                 dya = Act(dy, out.H, out.W, out.C)
                 self._conv([dya], layer.conv, K.TAPS3_DGRAD, a.H, a.W, a.C, mode=L.MODE_DILATE,
@@ -550,9 +598,19 @@ class UNetExecutor:
                 _, layer, a, out = rec
                 N = a.t.shape[0]
                 dy = out.grad
-                self._wgrad([a], dy, out.C, K.TAPS3, out.H, out.W, out.C, gv(layer.conv.weight),
-                            mode=L.MODE_UPSAMPLE)
-                K.channel_sum(dt, dy, N, out.H * out.W, out.C, out.C, out_c=gv(layer.conv.bias))
+                with self._side(a.t, dy):
+                    if dt == torch.bfloat16:
+                        # weight gradient over the materialised nearest-x2 input: the halo wgrad kernel (x halo
+                        # in LDS for all 9 taps) on it is ~4x faster than the strided upsample-mode kernel,
+                        # and the 2x2 replication costs one streaming pass
+                        C = a.t.shape[-1]
+                        up = a.t[:, :, None, :, None, :].expand(N, a.H, 2, a.W, 2, C).reshape(N, 2 * a.H, 2 * a.W, C)
+                        self._wgrad([Act(up, 2 * a.H, 2 * a.W, a.C)], dy, out.C, K.TAPS3, out.H, out.W, out.C,
+                                    gv(layer.conv.weight))
+                    else:
+                        self._wgrad([a], dy, out.C, K.TAPS3, out.H, out.W, out.C, gv(layer.conv.weight),
+                                    mode=L.MODE_UPSAMPLE)
+                    K.channel_sum(dt, dy, N, out.H * out.W, out.C, out.C, out_c=gv(layer.conv.bias))
                 buf, acc = self._grad_target(a)
                 dya = Act(dy, out.H, out.W, out.C)
                 self._conv([dya], layer.conv, K.TAPS_UPDGRAD, a.H, a.W, a.C, stride=2, out=buf,
@@ -562,8 +620,9 @@ class UNetExecutor:
                 N = h.t.shape[0]
                 dy = h.grad
                 conv = m.input_conv
-                self._wgrad([xin], dy, h.C, K.TAPS3, h.H, h.W, h.C, gv(conv.weight))
-                K.channel_sum(dt, dy, N, h.H * h.W, h.C, h.C, out_c=gv(conv.bias))
+                with self._side(xin.t, dy):
+                    self._wgrad([xin], dy, h.C, K.TAPS3, h.H, h.W, h.C, gv(conv.weight))
+                    K.channel_sum(dt, dy, N, h.H * h.W, h.C, h.C, out_c=gv(conv.bias))
                 if xg:
                     ldx = xin.t.shape[-1]
                     g = torch.empty(N, h.H, h.W, ldx, dtype=dt, device=dout.device)
@@ -585,15 +644,17 @@ class UNetExecutor:
         dout = out.grad
         HW = H * W
         # conv2 (weight, bias) and its input gradient; a2 = dropout(SiLU(GN2(h1))) was kept from forward
-        self._wgrad([a2], dout, Cout, K.TAPS3, H, W, Cout, gv(conv2.weight))
-        K.channel_sum(dt, dout, N, HW, Cout, Cout, out_c=gv(conv2.bias))
+        with self._side(a2.t, dout):
+            self._wgrad([a2], dout, Cout, K.TAPS3, H, W, Cout, gv(conv2.weight))
+            K.channel_sum(dt, dout, N, HW, Cout, Cout, out_c=gv(conv2.bias))
         g2 = torch.empty(N, H, W, Cout, dtype=dt, device=dout.device)
         self._conv([Act(dout, H, W, Cout)], conv2, K.TAPS3_DGRAD, H, W, Cout, out=g2, packmode=L.PACK_DGRAD)
         # shortcut
         if isinstance(rb.shortcut, torch.nn.Conv2d):
             sc = rb.shortcut
-            self._wgrad(srcs, dout, Cout, K.TAPS1, H, W, Cout, gv(sc.weight))
-            K.channel_sum(dt, dout, N, HW, Cout, Cout, out_c=gv(sc.bias))
+            with self._side(*[x.t for x in srcs], dout):
+                self._wgrad(srcs, dout, Cout, K.TAPS1, H, W, Cout, gv(sc.weight))
+                K.channel_sum(dt, dout, N, HW, Cout, Cout, out_c=gv(sc.bias))
             if len(srcs) == 1:
                 buf, acc = self._grad_target(a)
                 self._conv([Act(dout, H, W, Cout)], sc, K.TAPS1, H, W, C1, out=buf, resid=buf if acc else None,
@@ -614,6 +675,7 @@ class UNetExecutor:
             if a.grad is None:
                 a.grad = dout          # identity shortcut: alias (dout is dead after this block)
             else:
+                self._guard(a.grad)
                 K.add_(dt, a.grad, dout)
         # GN2 + SiLU + dropout backward -> dh1, with its pixel sums fused in: per (n, c) -> the time-embedding
         # add's gradient (daddvec slice), per c -> conv1's bias gradient
@@ -625,7 +687,8 @@ class UNetExecutor:
                  drop, dh1, None, Cout, 0, 0, 0, gv(gn2.weight), gv(gn2.bias), dx_sum_nc=self.daddvec[:, off:],
                  ld_sum_nc=self.temb_total, dx_sum_c=gv(conv1.bias))
         # conv1
-        self._wgrad([a1], dh1, Cout, K.TAPS3, H, W, Cout, gv(conv1.weight))
+        with self._side(a1.t, dh1):
+            self._wgrad([a1], dh1, Cout, K.TAPS3, H, W, Cout, gv(conv1.weight))
         g1 = torch.empty(N, H, W, C1 + C2, dtype=dt, device=dout.device)
         self._conv([Act(dh1, H, W, Cout)], conv1, K.TAPS3_DGRAD, H, W, C1 + C2, out=g1, packmode=L.PACK_DGRAD)
         b1, acc1 = self._grad_target(a)
@@ -659,19 +722,22 @@ class UNetExecutor:
         hd = C // heads
         dout = out.grad
         # proj
-        self._wgrad([o], dout, C, K.TAPS1, H, W, C, gv(ab.proj.weight))
-        K.channel_sum(dt, dout, N, HW, C, C, out_c=gv(ab.proj.bias))
+        with self._side(o.t, dout):
+            self._wgrad([o], dout, C, K.TAPS1, H, W, C, gv(ab.proj.weight))
+            K.channel_sum(dt, dout, N, HW, C, C, out_c=gv(ab.proj.bias))
         do = torch.empty(N, H, W, C, dtype=dt, device=dout.device)
         self._conv([Act(dout, H, W, C)], ab.proj, K.TAPS1, H, W, C, out=do, packmode=L.PACK_DGRAD)
         # residual: x gets dout
         if a.grad is None:
             a.grad = dout
         else:
+            self._guard(a.grad)
             K.add_(dt, a.grad, dout)
         dqkv = torch.empty(N, H, W, 3 * C, dtype=dt, device=dout.device)
         K.attn_bwd(dt, qkv.t, 3 * C, o.t, do, C, lse, N, HW, heads, hd, dqkv, 3 * C)
-        self._wgrad([an], dqkv, 3 * C, K.TAPS1, H, W, 3 * C, gv(ab.qkv.weight))
-        K.channel_sum(dt, dqkv, N, HW, 3 * C, 3 * C, out_c=gv(ab.qkv.bias))
+        with self._side(an.t, dqkv):
+            self._wgrad([an], dqkv, 3 * C, K.TAPS1, H, W, 3 * C, gv(ab.qkv.weight))
+            K.channel_sum(dt, dqkv, N, HW, 3 * C, 3 * C, out_c=gv(ab.qkv.bias))
         g = torch.empty(N, H, W, C, dtype=dt, device=dout.device)
         self._conv([Act(dqkv, H, W, 3 * C)], ab.qkv, K.TAPS1, H, W, C, out=g, packmode=L.PACK_DGRAD)
         K.gn_bwd(dt, g, C, a.t, None, N, HW, C, 0, C, 0, ab.norm.num_groups, st[2], ab.norm.weight, ab.norm.bias,

@@ -55,6 +55,10 @@ class GradSync:
         self.world = dist.get_world_size(process_group)
         executor.grad_hook = self.hook
 
+    def wants(self, hi, final):
+        """Whether hook(flat, hi, final) will issue an all-reduce (the executor then joins its side stream)."""
+        return hi - self.done >= self.bucket or (final and hi > self.done) or final
+
     def hook(self, flat, hi, final):
         if hi - self.done >= self.bucket or (final and hi > self.done):
             seg = flat[self.done:hi]

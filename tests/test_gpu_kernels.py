@@ -44,7 +44,8 @@ def q(x, dt):
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("case", ["s1_concat_gn", "s2", "up", "1x1", "ragged_in", "splitk_concat", "splitk_ragged"])
 def test_conv_forward(dt, case):
-    """splitk_*: small M with deep K, which the bf16 planner runs as split-K over grid.z + epilogue kernel."""
+    """splitk_*: small M with deep K, which both planners (bf16 LDS-DMA, fp32 register-staged) run as split-K
+    over grid.z + epilogue kernel."""
     L, K = _lib()
     torch.manual_seed(0)
     N, H, W = 2, 8, 8
@@ -93,7 +94,7 @@ def test_conv_forward(dt, case):
     y = torch.empty(N, OH, OW, Cout, dtype=dt, device=DEV)
     rd = nhwc(resid).to(dt).to(DEV)
     K.set_epilogue(d, bias=bias.to(DEV), addvec=addv.to(DEV), ld_add=Cout, resid=rd, ld_res=Cout, ldy1=Cout)
-    if case.startswith("splitk") and dt == torch.bfloat16:
+    if case.startswith("splitk"):
         import ctypes
         assert L.LIB.dmc_conv2d_workspace(ctypes.byref(d)) > 0   # the planner does choose split-K here
     K.conv(d, x1d, x2d, wp, y)
@@ -418,3 +419,31 @@ def test_flat_grad_norm_and_adamw_match_torch(n):
         torch.testing.assert_close(m, opt.state[pr]["exp_avg"], rtol=1e-5, atol=1e-8)
         torch.testing.assert_close(v, opt.state[pr]["exp_avg_sq"], rtol=1e-5, atol=1e-10)
         torch.testing.assert_close(ema, er, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("Cin,Cout", [(4992, 512), (512, 4992)])
+def test_conv_fp32_gemm_splitk_silu_pre(Cin, Cout):
+    """The time-embedding GEMMs (1x1 'conv' over N=128 rows, fp32): split-K register-staged kernel with the
+    SiLU-derivative (silu_pre) and bias epilogue, vs torch fp32."""
+    import ctypes
+    L, K = _lib()
+    torch.manual_seed(8)
+    N = 128
+    x = torch.randn(N, Cin)
+    w = torch.randn(Cout, Cin) / math.sqrt(Cin)
+    bias = torch.randn(Cout)
+    z = torch.randn(N, Cout)
+    sg = torch.sigmoid(z)
+    ref = (x @ w.t() + bias) * sg * (1 + z * (1 - sg))
+    Kc = L.kc_for(Cin, torch.float32)
+    wp = K.pack_weight(L.PACK_FWD, torch.float32, w.to(DEV), Kc)
+    xd = torch.zeros(N, 1, 1, Kc, device=DEV)
+    xd[..., :Cin] = x.view(N, 1, 1, Cin).to(DEV)
+    y = torch.empty(N, 1, 1, Cout, device=DEV)
+    d = K.make_desc(torch.float32, N, 1, 1, Cin, 0, Kc, 0, Kc, 1, 1, Cout, K.TAPS1)
+    K.set_epilogue(d, bias=bias.to(DEV), silu_pre=z.to(DEV), ld_silu=Cout, ldy1=Cout)
+    if Cin > 1024:
+        assert L.LIB.dmc_conv2d_workspace(ctypes.byref(d)) > 0
+    K.conv(d, xd, None, wp, y)
+    torch.cuda.synchronize()
+    assert rel_err(y.view(N, Cout).cpu(), ref) < 1e-5
