@@ -21,6 +21,10 @@ SHAPES = {
     "r512_8": (128, 8, 8, 256, 256, 256, "3"),       # small M: split-K
     "r512_4": (128, 4, 4, 256, 256, 256, "3"),
     "qkv_16": (128, 16, 16, 256, 0, 768, "1"),
+    "p1_8": (128, 8, 8, 256, 0, 256, "1"),
+    "p1_16": (128, 16, 16, 256, 0, 256, "1"),
+    "r256_8": (128, 8, 8, 256, 0, 256, "3"),
+    "r256_4": (128, 4, 4, 256, 0, 256, "3"),
 }
 
 
