@@ -181,6 +181,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps if not args.no_train else 0):
         trainer.train_step(pool[i % 4], 0)
+    host_el = time.perf_counter() - t0      # host enqueue time (the GPU may still be running)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if world > 1:
@@ -201,6 +202,7 @@ def main():
                       "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
                       "parallelism": f"dp{world}"},
            "per_gpu_imgs_per_sec": round(value / world, 2),
+           "host_enqueue_ms_per_step": round(host_el / max(args.steps, 1) * 1e3, 3),
            "train_tflops_per_gpu": round(value / world * TRAIN_GFLOP_PER_IMG / 1e3, 2)}
 
     if not args.no_sample:
