@@ -1,7 +1,7 @@
 // Fused self-attention (forward + backward) for AttentionBlock, models/unet.py:84-99, on gfx950 MFMA.
 //
 // The reference materialises S = QK^T/sqrt(hd) ([B,heads,L,L]), runs softmax and a second bmm. Here
-// scores never leave registers: online softmax (flash style), K/V tiles of 64 keys staged in LDS.
+// scores never leave registers: online softmax (flash style) over 64-key tiles read from LDS.
 //
 // Orientation: scores are computed TRANSPOSED, S^T = K * Q^T (keys on the accumulator rows, one query
 // per lane column), so that
@@ -12,12 +12,21 @@
 //   operand is read with ds_read_b64_tr_b16 from those same key rows.
 // Backward: dQ kernel (per query tile, same structure as forward) and dK/dV kernel (per key tile, the
 // query index on the accumulator rows). P is recomputed from the saved log-sum-exp.
+//
+// Two launch structures share the per-tile bodies below:
+//   * row-resident (L padded to 64 <= 256, the UNet's 16x16 and 8x8 attention): a 512-thread block owns
+//     HG whole heads (HG * Lp <= 256 rows), stages every row its tiles read -- K and V (forward, dQ) or
+//     Q, dO, lse and delta (dK/dV) -- into LDS ONCE with all loads in flight together, then each of its
+//     8 waves runs 16-row tiles against them without another barrier;
+//   * staged (longer sequences): a 256-thread block per 64 rows re-stages 64-row tiles behind two
+//     barriers per tile.
 #include "dmc_common.h"
 #include "dmc_internal.h"
 
 namespace {
 
 constexpr float kLog2e = 1.4426950408889634f;
+constexpr int kResRows = 256;   // LDS rows per operand image of the resident kernels
 
 struct AttnK {
   const char* qkv; int ld_qkv;
@@ -58,6 +67,40 @@ DMC_DEV void stage_tile(const AttnK& a, const char* base, int ld, int n, int r0,
   }
 }
 
+// Resident staging: rows r = g*Lp + tok (head h0+g, token tok) of two [token][d] slices (channel offsets
+// cA / cB) into LDS images A and B; rows past L, past the block's HG heads or past the last head are
+// zero. Every thread issues all its loads before its first LDS store (one global round trip); rows that
+// are not needed load row 0 of the image (always valid) and are zeroed, so no load sits behind a branch.
+template <typename T, int HDP>
+DMC_DEV void stage_rows2(const AttnK& a, const char* bA, int ldA, int cA, const char* bB, int ldB, int cB, int n,
+                         int h0, int HG, int Lp, char* A, char* B) {
+  constexpr int KPL = TT<T>::KPL;
+  constexpr int CPR = HDP / KPL;
+  constexpr int PITCH = HDP * sizeof(T) + 16;
+  constexpr int PER = kResRows * CPR / 512;
+  v4i va[PER], vb[PER];
+  bool ok[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = threadIdx.x + j * 512;
+    const int r = i / CPR, c = i - r * CPR;
+    const int g = r / Lp, tok = r - g * Lp, d0 = c * KPL;
+    ok[j] = g < HG && h0 + g < a.heads && tok < a.L && d0 < a.hd;
+    const size_t row = (size_t)n * a.L + (ok[j] ? tok : 0);
+    const int off = ok[j] ? (h0 + g) * a.hd + d0 : 0;
+    va[j] = *(const v4i*)(bA + (row * ldA + cA + off) * sizeof(T));
+    vb[j] = *(const v4i*)(bB + (row * ldB + cB + off) * sizeof(T));
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = threadIdx.x + j * 512;
+    const int r = i / CPR, c = i - r * CPR;
+    if (!ok[j]) { va[j] = v4i{0, 0, 0, 0}; vb[j] = v4i{0, 0, 0, 0}; }
+    *(v4i*)(A + r * PITCH + c * 16) = va[j];
+    *(v4i*)(B + r * PITCH + c * 16) = vb[j];
+  }
+}
+
 // A operand = transposed LDS tile (rows = tokens kc-chunk, cols = d tile dt), with the token order of
 // the accumulator-as-operand fragment.
 template <typename T, int PITCH>
@@ -94,113 +137,249 @@ DMC_DEV void store_d4(char* base, size_t idx, const float* v) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Per-tile bodies. Each works on the lane's own row (query, or key for dK/dV) against one 64-row LDS
+// tile; sK/sV/sQ/sD point at that tile's first row, which is row k0 / q0 of the sequence.
+
+// Forward: online-softmax update of (m, lsum, o) with keys [k0, k0+64).
 template <typename T, int HDP>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnK a) {
+DMC_DEV void fwd_keys(const AttnK& a, const char* sK, const char* sV, int k0, const v4i* qf, float sl2, float& m,
+                      float& lsum, v4f* o) {
   constexpr int KPL = TT<T>::KPL;
   constexpr int DC = HDP / (4 * KPL);
   constexpr int DT = HDP / 16;
   constexpr int KC = (sizeof(T) == 2) ? 2 : 4;   // key chunks per 64-key tile for the PV product
   constexpr int PITCH = HDP * sizeof(T) + 16;
-  __shared__ __attribute__((aligned(16))) char sK[64 * PITCH];
-  __shared__ __attribute__((aligned(16))) char sV[64 * PITCH];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int h = lane >> 4, r = lane & 15;
-  const int nh = blockIdx.y, n = nh / a.heads, hh = nh % a.heads;
-  const int C = a.heads * a.hd;
-  const int q = blockIdx.x * 64 + wave * 16 + r;
-  v4i qf[DC];
-  load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, q, hh * a.hd, qf);
-  const float sl2 = a.scale * kLog2e;
-  float m = -INFINITY, lsum = 0.f;
-  v4f o[DT];
+  const int h = (threadIdx.x & 63) >> 4;
+  float p[4][4];
+  float mt = -INFINITY;
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt) o[dt] = v4f{0.f, 0.f, 0.f, 0.f};
-
-  for (int k0 = 0; k0 < a.L; k0 += 64) {
-    __syncthreads();
-    stage_tile<T, HDP>(a, a.qkv, a.ld_qkv, n, k0, C + hh * a.hd, sK);
-    stage_tile<T, HDP>(a, a.qkv, a.ld_qkv, n, k0, 2 * C + hh * a.hd, sV);
-    __syncthreads();
-    float p[4][4];
-    float mt = -INFINITY;
+  for (int t = 0; t < 4; ++t) {
+    v4f s = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      v4f s = {0.f, 0.f, 0.f, 0.f};
+    for (int dc = 0; dc < DC; ++dc) s = mma16<T>(s, lds_frag_rows(sK, PITCH, 16 * t, dc * 64), qf[dc]);
 #pragma unroll
-      for (int dc = 0; dc < DC; ++dc) s = mma16<T>(s, lds_frag_rows(sK, PITCH, 16 * t, dc * 64), qf[dc]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = k0 + 16 * t + 4 * h + i;
-        p[t][i] = key < a.L ? s[i] * sl2 : -INFINITY;
-        mt = fmaxf(mt, p[t][i]);
-      }
-    }
-    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float mn = fmaxf(m, mt);
-    const float alpha = exp2f(m - mn);
-    float rs = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { p[t][i] = exp2f(p[t][i] - mn); rs += p[t][i]; }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
-    lsum = lsum * alpha + rs;
-    m = mn;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      o[dt] *= alpha;
-#pragma unroll
-      for (int kc = 0; kc < KC; ++kc) o[dt] = mma16<T>(o[dt], tr_tok_frag<T, PITCH>(sV, kc, dt), acc_frag<T>(p, kc));
+    for (int i = 0; i < 4; ++i) {
+      const int key = k0 + 16 * t + 4 * h + i;
+      p[t][i] = key < a.L ? s[i] * sl2 : -INFINITY;
+      mt = fmaxf(mt, p[t][i]);
     }
   }
-  if (q < a.L) {
-    const float inv = 1.f / lsum;
+  mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+  mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+  const float mn = fmaxf(m, mt);
+  const float alpha = exp2f(m - mn);
+  float rs = 0.f;
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      const int d = 16 * dt + 4 * h;
-      if (d < a.hd) {
-        float v[4] = {o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv};
-        store_d4<T>(a.out, (size_t)(n * a.L + q) * a.ld_out + hh * a.hd + d, v);
-      }
-    }
-    if (h == 0) a.lse_out[(size_t)nh * a.L + q] = (m + log2f(lsum)) / kLog2e;
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { p[t][i] = exp2f(p[t][i] - mn); rs += p[t][i]; }
+  rs += __shfl_xor(rs, 16, 64);
+  rs += __shfl_xor(rs, 32, 64);
+  lsum = lsum * alpha + rs;
+  m = mn;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    o[dt] *= alpha;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) o[dt] = mma16<T>(o[dt], tr_tok_frag<T, PITCH>(sV, kc, dt), acc_frag<T>(p, kc));
   }
 }
 
 template <typename T, int HDP>
-__global__ __launch_bounds__(256) void attn_dq_kernel(AttnK a) {
+DMC_DEV void fwd_store(const AttnK& a, int n, int hh, int q, float m, float lsum, const v4f* o) {
+  constexpr int DT = HDP / 16;
+  const int h = (threadIdx.x & 63) >> 4;
+  if (q >= a.L) return;
+  const float inv = 1.f / lsum;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const int d = 16 * dt + 4 * h;
+    if (d < a.hd) {
+      float v[4] = {o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv};
+      store_d4<T>(a.out, (size_t)(n * a.L + q) * a.ld_out + hh * a.hd + d, v);
+    }
+  }
+  if (h == 0) a.lse_out[(size_t)(n * a.heads + hh) * a.L + q] = (m + log2f(lsum)) / kLog2e;
+}
+
+// dQ: delta = rowsum(dO * O) of the lane's query (also published for dK/dV). All 2*HDP/KPL loads are
+// issued before the first use (clamped addresses, dropped values past hd), not one round trip per chunk.
+template <typename T, int HDP>
+DMC_DEV float dq_delta(const AttnK& a, int n, int hh, int q) {
+  constexpr int KPL = TT<T>::KPL;
+  constexpr int NCH = HDP / KPL;
+  const size_t row = (size_t)(n * a.L + (q < a.L ? q : 0)) * a.ld_o + hh * a.hd;
+  v4i vo[NCH], vd[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int d0 = i * KPL < a.hd ? i * KPL : 0;
+    vo[i] = *(const v4i*)(a.o + (row + d0) * sizeof(T));
+    vd[i] = *(const v4i*)(a.dout + (row + d0) * sizeof(T));
+  }
+  float dl = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    if (i * KPL < a.hd) {
+      float fo[KPL], fd[KPL];
+      Chunk<T>::unpack(vo[i], fo);
+      Chunk<T>::unpack(vd[i], fd);
+#pragma unroll
+      for (int e = 0; e < KPL; ++e) dl = fmaf(fo[e], fd[e], dl);
+    }
+  }
+  if (q >= a.L) return 0.f;
+  if ((threadIdx.x & 63) < 16) a.delta_out[(size_t)(n * a.heads + hh) * a.L + q] = dl;
+  return dl;
+}
+
+// dQ += dS K over keys [k0, k0+64), P recomputed from the log-sum-exp, dS = P (dP - delta)
+template <typename T, int HDP>
+DMC_DEV void dq_keys(const AttnK& a, const char* sK, const char* sV, int k0, const v4i* qf, const v4i* df, float sl2,
+                     float lse2, float dl, v4f* dq) {
   constexpr int KPL = TT<T>::KPL;
   constexpr int DC = HDP / (4 * KPL);
   constexpr int DT = HDP / 16;
   constexpr int KC = (sizeof(T) == 2) ? 2 : 4;
   constexpr int PITCH = HDP * sizeof(T) + 16;
+  const int h = (threadIdx.x & 63) >> 4;
+  float ds[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dc = 0; dc < DC; ++dc) {
+      s = mma16<T>(s, lds_frag_rows(sK, PITCH, 16 * t, dc * 64), qf[dc]);
+      dp = mma16<T>(dp, lds_frag_rows(sV, PITCH, 16 * t, dc * 64), df[dc]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int key = k0 + 16 * t + 4 * h + i;
+      const float pv = key < a.L ? exp2f(s[i] * sl2 - lse2) : 0.f;
+      ds[t][i] = pv * (dp[i] - dl);
+    }
+  }
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) dq[dt] = mma16<T>(dq[dt], tr_tok_frag<T, PITCH>(sK, kc, dt), acc_frag<T>(ds, kc));
+}
+
+template <typename T, int HDP>
+DMC_DEV void dq_store(const AttnK& a, int n, int hh, int q, const v4f* dq) {
+  constexpr int DT = HDP / 16;
+  const int h = (threadIdx.x & 63) >> 4;
+  if (q >= a.L) return;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const int d = 16 * dt + 4 * h;
+    if (d < a.hd) {
+      float v[4] = {dq[dt][0] * a.scale, dq[dt][1] * a.scale, dq[dt][2] * a.scale, dq[dt][3] * a.scale};
+      store_d4<T>(a.out, (size_t)(n * a.L + q) * a.ld_out + hh * a.hd + d, v);
+    }
+  }
+}
+
+// dK/dV of the lane's key over queries [q0, q0+64): sL = log2-scaled lse (+inf past L -> P = 0), sDl = delta
+template <typename T, int HDP>
+DMC_DEV void dkdv_queries(const char* sQ, const char* sD, const float* sL, const float* sDl, const v4i* kf,
+                          const v4i* vf, float sl2, v4f* dk, v4f* dv) {
+  constexpr int KPL = TT<T>::KPL;
+  constexpr int DC = HDP / (4 * KPL);
+  constexpr int DT = HDP / 16;
+  constexpr int KC = (sizeof(T) == 2) ? 2 : 4;
+  constexpr int PITCH = HDP * sizeof(T) + 16;
+  const int h = (threadIdx.x & 63) >> 4;
+  float p[4][4], ds[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dc = 0; dc < DC; ++dc) {
+      s = mma16<T>(s, lds_frag_rows(sQ, PITCH, 16 * t, dc * 64), kf[dc]);
+      dp = mma16<T>(dp, lds_frag_rows(sD, PITCH, 16 * t, dc * 64), vf[dc]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int qi = 16 * t + 4 * h + i;   // query (row) within the tile
+      const float pv = exp2f(s[i] * sl2 - sL[qi]);
+      p[t][i] = pv;
+      ds[t][i] = pv * (dp[i] - sDl[qi]);
+    }
+  }
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      dv[dt] = mma16<T>(dv[dt], tr_tok_frag<T, PITCH>(sD, kc, dt), acc_frag<T>(p, kc));
+      dk[dt] = mma16<T>(dk[dt], tr_tok_frag<T, PITCH>(sQ, kc, dt), acc_frag<T>(ds, kc));
+    }
+  }
+}
+
+template <typename T, int HDP>
+DMC_DEV void dkdv_store(const AttnK& a, int n, int hh, int key, const v4f* dk, const v4f* dv) {
+  constexpr int DT = HDP / 16;
+  const int h = (threadIdx.x & 63) >> 4;
+  if (key >= a.L) return;
+  const int C = a.heads * a.hd;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const int d = 16 * dt + 4 * h;
+    if (d < a.hd) {
+      float vk[4] = {dk[dt][0] * a.scale, dk[dt][1] * a.scale, dk[dt][2] * a.scale, dk[dt][3] * a.scale};
+      float vv[4] = {dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]};
+      const size_t row = (size_t)(n * a.L + key) * a.ld_out;
+      store_d4<T>(a.out, row + C + hh * a.hd + d, vk);
+      store_d4<T>(a.out, row + 2 * C + hh * a.hd + d, vv);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Staged kernels: grid (L/64 row tiles, N*heads), 4 waves x 16 rows.
+template <typename T, int HDP>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnK a) {
+  constexpr int DC = HDP / (4 * TT<T>::KPL);
+  constexpr int DT = HDP / 16;
+  constexpr int PITCH = HDP * sizeof(T) + 16;
   __shared__ __attribute__((aligned(16))) char sK[64 * PITCH];
   __shared__ __attribute__((aligned(16))) char sV[64 * PITCH];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int h = lane >> 4, r = lane & 15;
+  const int wave = threadIdx.x >> 6;
   const int nh = blockIdx.y, n = nh / a.heads, hh = nh % a.heads;
   const int C = a.heads * a.hd;
-  const int q = blockIdx.x * 64 + wave * 16 + r;
+  const int q = blockIdx.x * 64 + wave * 16 + (threadIdx.x & 15);
+  v4i qf[DC];
+  load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, q, hh * a.hd, qf);
+  float m = -INFINITY, lsum = 0.f;
+  v4f o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < a.L; k0 += 64) {
+    __syncthreads();
+    stage_tile<T, HDP>(a, a.qkv, a.ld_qkv, n, k0, C + hh * a.hd, sK);
+    stage_tile<T, HDP>(a, a.qkv, a.ld_qkv, n, k0, 2 * C + hh * a.hd, sV);
+    __syncthreads();
+    fwd_keys<T, HDP>(a, sK, sV, k0, qf, a.scale * kLog2e, m, lsum, o);
+  }
+  fwd_store<T, HDP>(a, n, hh, q, m, lsum, o);
+}
+
+template <typename T, int HDP>
+__global__ __launch_bounds__(256) void attn_dq_kernel(AttnK a) {
+  constexpr int DC = HDP / (4 * TT<T>::KPL);
+  constexpr int DT = HDP / 16;
+  constexpr int PITCH = HDP * sizeof(T) + 16;
+  __shared__ __attribute__((aligned(16))) char sK[64 * PITCH];
+  __shared__ __attribute__((aligned(16))) char sV[64 * PITCH];
+  const int wave = threadIdx.x >> 6;
+  const int nh = blockIdx.y, n = nh / a.heads, hh = nh % a.heads;
+  const int C = a.heads * a.hd;
+  const int q = blockIdx.x * 64 + wave * 16 + (threadIdx.x & 15);
   v4i qf[DC], df[DC];
   load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, q, hh * a.hd, qf);
   load_tok_frags<T, DC>(a, a.dout, a.ld_o, n, q, hh * a.hd, df);
   const float lse2 = q < a.L ? a.lse[(size_t)nh * a.L + q] * kLog2e : 0.f;
-  // delta_q = rowsum(dO * O), computed here (every lane for its own query) and published for dK/dV
-  float dl = 0.f;
-  if (q < a.L) {
-    const size_t row = (size_t)(n * a.L + q) * a.ld_o + hh * a.hd;
-    for (int d0 = 0; d0 < a.hd; d0 += KPL) {
-      float fo[KPL], fd[KPL];
-      Chunk<T>::unpack(*(const v4i*)(a.o + (row + d0) * sizeof(T)), fo);
-      Chunk<T>::unpack(*(const v4i*)(a.dout + (row + d0) * sizeof(T)), fd);
-#pragma unroll
-      for (int e = 0; e < KPL; ++e) dl = fmaf(fo[e], fd[e], dl);
-    }
-    if (h == 0) a.delta_out[(size_t)nh * a.L + q] = dl;
-  }
-  const float sl2 = a.scale * kLog2e;
+  const float dl = dq_delta<T, HDP>(a, n, hh, q);
   v4f dq[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) dq[dt] = v4f{0.f, 0.f, 0.f, 0.f};
@@ -209,58 +388,26 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnK a) {
     stage_tile<T, HDP>(a, a.qkv, a.ld_qkv, n, k0, C + hh * a.hd, sK);
     stage_tile<T, HDP>(a, a.qkv, a.ld_qkv, n, k0, 2 * C + hh * a.hd, sV);
     __syncthreads();
-    float ds[4][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int dc = 0; dc < DC; ++dc) {
-        s = mma16<T>(s, lds_frag_rows(sK, PITCH, 16 * t, dc * 64), qf[dc]);
-        dp = mma16<T>(dp, lds_frag_rows(sV, PITCH, 16 * t, dc * 64), df[dc]);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = k0 + 16 * t + 4 * h + i;
-        const float pv = key < a.L ? exp2f(s[i] * sl2 - lse2) : 0.f;
-        ds[t][i] = pv * (dp[i] - dl);
-      }
-    }
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int kc = 0; kc < KC; ++kc) dq[dt] = mma16<T>(dq[dt], tr_tok_frag<T, PITCH>(sK, kc, dt), acc_frag<T>(ds, kc));
+    dq_keys<T, HDP>(a, sK, sV, k0, qf, df, a.scale * kLog2e, lse2, dl, dq);
   }
-  if (q < a.L) {
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      const int d = 16 * dt + 4 * h;
-      if (d < a.hd) {
-        float v[4] = {dq[dt][0] * a.scale, dq[dt][1] * a.scale, dq[dt][2] * a.scale, dq[dt][3] * a.scale};
-        store_d4<T>(a.out, (size_t)(n * a.L + q) * a.ld_out + hh * a.hd + d, v);
-      }
-    }
-  }
+  dq_store<T, HDP>(a, n, hh, q, dq);
 }
 
 template <typename T, int HDP>
 __global__ __launch_bounds__(256) void attn_dkdv_kernel(AttnK a) {
-  constexpr int KPL = TT<T>::KPL;
-  constexpr int DC = HDP / (4 * KPL);
+  constexpr int DC = HDP / (4 * TT<T>::KPL);
   constexpr int DT = HDP / 16;
-  constexpr int KC = (sizeof(T) == 2) ? 2 : 4;
   constexpr int PITCH = HDP * sizeof(T) + 16;
   __shared__ __attribute__((aligned(16))) char sQ[64 * PITCH];
   __shared__ __attribute__((aligned(16))) char sD[64 * PITCH];
   __shared__ float sL[64], sDl[64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int h = lane >> 4, r = lane & 15;
+  const int wave = threadIdx.x >> 6;
   const int nh = blockIdx.y, n = nh / a.heads, hh = nh % a.heads;
   const int C = a.heads * a.hd;
-  const int key = blockIdx.x * 64 + wave * 16 + r;
+  const int key = blockIdx.x * 64 + wave * 16 + (threadIdx.x & 15);
   v4i kf[DC], vf[DC];
   load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, key, C + hh * a.hd, kf);
   load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, key, 2 * C + hh * a.hd, vf);
-  const float sl2 = a.scale * kLog2e;
   v4f dk[DT], dv[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) { dk[dt] = v4f{0.f, 0.f, 0.f, 0.f}; dv[dt] = v4f{0.f, 0.f, 0.f, 0.f}; }
@@ -274,56 +421,157 @@ __global__ __launch_bounds__(256) void attn_dkdv_kernel(AttnK a) {
       sDl[threadIdx.x] = qq < a.L ? a.delta[(size_t)nh * a.L + qq] : 0.f;
     }
     __syncthreads();
-    float p[4][4], ds[4][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int dc = 0; dc < DC; ++dc) {
-        s = mma16<T>(s, lds_frag_rows(sQ, PITCH, 16 * t, dc * 64), kf[dc]);
-        dp = mma16<T>(dp, lds_frag_rows(sD, PITCH, 16 * t, dc * 64), vf[dc]);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int qi = 16 * t + 4 * h + i;   // query (row) within the tile
-        const float pv = exp2f(s[i] * sl2 - sL[qi]);   // sL = +inf for padded queries -> 0
-        p[t][i] = pv;
-        ds[t][i] = pv * (dp[i] - sDl[qi]);
-      }
-    }
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-#pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        dv[dt] = mma16<T>(dv[dt], tr_tok_frag<T, PITCH>(sD, kc, dt), acc_frag<T>(p, kc));
-        dk[dt] = mma16<T>(dk[dt], tr_tok_frag<T, PITCH>(sQ, kc, dt), acc_frag<T>(ds, kc));
-      }
-    }
+    dkdv_queries<T, HDP>(sQ, sD, sL, sDl, kf, vf, a.scale * kLog2e, dk, dv);
   }
-  if (key < a.L) {
+  dkdv_store<T, HDP>(a, n, hh, key, dk, dv);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Resident kernels: grid N * heads/HG blocks of 8 waves; a block's 16-row tiles are head-major
+// (tile -> head g = tile / tiles_per_head) and dealt to the waves round-robin.
+template <typename T, int HDP>
+__global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnK a, int HG, int Lp) {
+  constexpr int DC = HDP / (4 * TT<T>::KPL);
+  constexpr int DT = HDP / 16;
+  constexpr int PITCH = HDP * sizeof(T) + 16;
+  __shared__ __attribute__((aligned(16))) char lds[2 * kResRows * PITCH];
+  char* const sK = lds;
+  char* const sV = lds + kResRows * PITCH;
+  const int wave = threadIdx.x >> 6, r = threadIdx.x & 15;
+  const int groups = (a.heads + HG - 1) / HG;
+  const int n = blockIdx.x / groups, h0 = (blockIdx.x - n * groups) * HG;
+  const int C = a.heads * a.hd;
+  stage_rows2<T, HDP>(a, a.qkv, a.ld_qkv, C, a.qkv, a.ld_qkv, 2 * C, n, h0, HG, Lp, sK, sV);
+  __syncthreads();
+  const int tph = (a.L + 15) / 16;
+  for (int tile = wave; tile < HG * tph; tile += 8) {
+    const int g = tile / tph, hh = h0 + g;
+    if (hh >= a.heads) break;   // wave-uniform; later tiles belong to later heads
+    const int q = (tile - g * tph) * 16 + r;
+    v4i qf[DC];
+    load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, q, hh * a.hd, qf);
+    float m = -INFINITY, lsum = 0.f;
+    v4f o[DT];
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      const int d = 16 * dt + 4 * h;
-      if (d < a.hd) {
-        float vk[4] = {dk[dt][0] * a.scale, dk[dt][1] * a.scale, dk[dt][2] * a.scale, dk[dt][3] * a.scale};
-        float vv[4] = {dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]};
-        const size_t row = (size_t)(n * a.L + key) * a.ld_out;
-        store_d4<T>(a.out, row + C + hh * a.hd + d, vk);
-        store_d4<T>(a.out, row + 2 * C + hh * a.hd + d, vv);
-      }
-    }
+    for (int dt = 0; dt < DT; ++dt) o[dt] = v4f{0.f, 0.f, 0.f, 0.f};
+    const size_t base = (size_t)g * Lp * PITCH;
+    for (int k0 = 0; k0 < a.L; k0 += 64)
+      fwd_keys<T, HDP>(a, sK + base + k0 * PITCH, sV + base + k0 * PITCH, k0, qf, a.scale * kLog2e, m, lsum, o);
+    fwd_store<T, HDP>(a, n, hh, q, m, lsum, o);
   }
 }
 
 template <typename T, int HDP>
+__global__ __launch_bounds__(512) void attn_dq_res_kernel(AttnK a, int HG, int Lp) {
+  constexpr int DC = HDP / (4 * TT<T>::KPL);
+  constexpr int DT = HDP / 16;
+  constexpr int PITCH = HDP * sizeof(T) + 16;
+  __shared__ __attribute__((aligned(16))) char lds[2 * kResRows * PITCH];
+  char* const sK = lds;
+  char* const sV = lds + kResRows * PITCH;
+  const int wave = threadIdx.x >> 6, r = threadIdx.x & 15;
+  const int groups = (a.heads + HG - 1) / HG;
+  const int n = blockIdx.x / groups, h0 = (blockIdx.x - n * groups) * HG;
+  const int C = a.heads * a.hd;
+  stage_rows2<T, HDP>(a, a.qkv, a.ld_qkv, C, a.qkv, a.ld_qkv, 2 * C, n, h0, HG, Lp, sK, sV);
+  __syncthreads();
+  const int tph = (a.L + 15) / 16;
+  for (int tile = wave; tile < HG * tph; tile += 8) {
+    const int g = tile / tph, hh = h0 + g;
+    if (hh >= a.heads) break;
+    const int q = (tile - g * tph) * 16 + r;
+    const size_t nh = (size_t)n * a.heads + hh;
+    v4i qf[DC], df[DC];
+    load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, q, hh * a.hd, qf);
+    load_tok_frags<T, DC>(a, a.dout, a.ld_o, n, q, hh * a.hd, df);
+    const float lse2 = q < a.L ? a.lse[nh * a.L + q] * kLog2e : 0.f;
+    const float dl = dq_delta<T, HDP>(a, n, hh, q);
+    v4f dq[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) dq[dt] = v4f{0.f, 0.f, 0.f, 0.f};
+    const size_t base = (size_t)g * Lp * PITCH;
+    for (int k0 = 0; k0 < a.L; k0 += 64)
+      dq_keys<T, HDP>(a, sK + base + k0 * PITCH, sV + base + k0 * PITCH, k0, qf, df, a.scale * kLog2e, lse2, dl, dq);
+    dq_store<T, HDP>(a, n, hh, q, dq);
+  }
+}
+
+template <typename T, int HDP>
+__global__ __launch_bounds__(512) void attn_dkdv_res_kernel(AttnK a, int HG, int Lp) {
+  constexpr int DC = HDP / (4 * TT<T>::KPL);
+  constexpr int DT = HDP / 16;
+  constexpr int PITCH = HDP * sizeof(T) + 16;
+  __shared__ __attribute__((aligned(16))) char lds[2 * kResRows * PITCH + 2 * kResRows * sizeof(float)];
+  char* const sQ = lds;
+  char* const sD = lds + kResRows * PITCH;
+  float* const sL = (float*)(lds + 2 * kResRows * PITCH);
+  float* const sDl = sL + kResRows;
+  const int wave = threadIdx.x >> 6, r = threadIdx.x & 15;
+  const int groups = (a.heads + HG - 1) / HG;
+  const int n = blockIdx.x / groups, h0 = (blockIdx.x - n * groups) * HG;
+  const int C = a.heads * a.hd;
+  stage_rows2<T, HDP>(a, a.qkv, a.ld_qkv, 0, a.dout, a.ld_o, 0, n, h0, HG, Lp, sQ, sD);
+  if (threadIdx.x < kResRows) {
+    const int g = threadIdx.x / Lp, tok = threadIdx.x - g * Lp;
+    const bool ok = g < HG && h0 + g < a.heads && tok < a.L;
+    const size_t idx = ((size_t)n * a.heads + h0 + g) * a.L + tok;
+    sL[threadIdx.x] = ok ? a.lse[idx] * kLog2e : INFINITY;
+    sDl[threadIdx.x] = ok ? a.delta[idx] : 0.f;
+  }
+  __syncthreads();
+  const int tph = (a.L + 15) / 16;
+  for (int tile = wave; tile < HG * tph; tile += 8) {
+    const int g = tile / tph, hh = h0 + g;
+    if (hh >= a.heads) break;
+    const int key = (tile - g * tph) * 16 + r;
+    v4i kf[DC], vf[DC];
+    load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, key, C + hh * a.hd, kf);
+    load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, key, 2 * C + hh * a.hd, vf);
+    v4f dk[DT], dv[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) { dk[dt] = v4f{0.f, 0.f, 0.f, 0.f}; dv[dt] = v4f{0.f, 0.f, 0.f, 0.f}; }
+    const int row0 = g * Lp;
+    for (int q0 = 0; q0 < a.L; q0 += 64)
+      dkdv_queries<T, HDP>(sQ + (size_t)(row0 + q0) * PITCH, sD + (size_t)(row0 + q0) * PITCH, sL + row0 + q0,
+                           sDl + row0 + q0, kf, vf, a.scale * kLog2e, dk, dv);
+    dkdv_store<T, HDP>(a, n, hh, key, dk, dv);
+  }
+}
+
+// Heads per block of the resident kernels, 0 when the padded sequence exceeds kResRows rows (or the
+// staged kernels are forced with DMC_ATTN_STAGED). The largest divisor of heads that fits and still
+// leaves >= 256 blocks where the batch allows; DMC_ATTN_HG overrides the choice (tests).
+int res_heads(const AttnK& a, int* Lp) {
+  *Lp = dmc::cdiv(a.L, 64) * 64;
+  if (*Lp > kResRows || getenv_flag("DMC_ATTN_STAGED")) return 0;
+  int hg = kResRows / *Lp;
+  if (hg > a.heads) hg = a.heads;
+  const char* force = getenv("DMC_ATTN_HG");
+  if (force && atoi(force) > 0) return atoi(force) < hg ? atoi(force) : hg;
+  while (hg > 1 && (a.heads % hg != 0 || (long)a.N * (a.heads / hg) < 256)) --hg;
+  return hg;
+}
+
+template <typename T, int HDP>
 int launch_all(bool fwd, AttnK a, float* delta, hipStream_t s) {
+  int Lp;
+  const int hg = res_heads(a, &Lp);
+  if (!fwd) { a.delta = delta; a.delta_out = delta; }
+  if (hg > 0) {
+    const int blocks = a.N * dmc::cdiv(a.heads, hg);
+    if (fwd) {
+      attn_fwd_res_kernel<T, HDP><<<blocks, 512, 0, s>>>(a, hg, Lp);
+      return dmc::check_launch("dmc_attn_fwd");
+    }
+    attn_dq_res_kernel<T, HDP><<<blocks, 512, 0, s>>>(a, hg, Lp);
+    attn_dkdv_res_kernel<T, HDP><<<blocks, 512, 0, s>>>(a, hg, Lp);
+    return dmc::check_launch("dmc_attn_bwd");
+  }
   dim3 g(dmc::cdiv(a.L, 64), a.N * a.heads);
   if (fwd) {
     attn_fwd_kernel<T, HDP><<<g, 256, 0, s>>>(a);
     return dmc::check_launch("dmc_attn_fwd");
   }
-  a.delta = delta;
-  a.delta_out = delta;
   attn_dq_kernel<T, HDP><<<g, 256, 0, s>>>(a);
   attn_dkdv_kernel<T, HDP><<<g, 256, 0, s>>>(a);
   return dmc::check_launch("dmc_attn_bwd");

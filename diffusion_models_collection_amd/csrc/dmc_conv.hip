@@ -540,7 +540,12 @@ DMC_DEV void wait_vm_dyn(int n) {
     case 2: __builtin_amdgcn_s_waitcnt(waitcnt_vm(2)); break;
     case 3: __builtin_amdgcn_s_waitcnt(waitcnt_vm(3)); break;
     case 4: __builtin_amdgcn_s_waitcnt(waitcnt_vm(4)); break;
-    default: __builtin_amdgcn_s_waitcnt(waitcnt_vm(5)); break;  // n >= 5: waiting for more is still correct
+    case 5: __builtin_amdgcn_s_waitcnt(waitcnt_vm(5)); break;
+    case 6: __builtin_amdgcn_s_waitcnt(waitcnt_vm(6)); break;
+    case 7: __builtin_amdgcn_s_waitcnt(waitcnt_vm(7)); break;
+    case 8: __builtin_amdgcn_s_waitcnt(waitcnt_vm(8)); break;
+    case 9: __builtin_amdgcn_s_waitcnt(waitcnt_vm(9)); break;
+    default: __builtin_amdgcn_s_waitcnt(waitcnt_vm(10)); break;  // n >= 10: waiting for more is still correct
   }
 }
 
@@ -572,14 +577,14 @@ DMC_DEV void halo_issue(const ConvK& a, char* buf, int c0, int wave, int pb, int
                                                (first ? h1[p] : h2[p]) + c2, 0, 0, 0);
 }
 
-template <int HP>
+template <int HP, int WS>
 __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int nimg) {
   using T = bf16_t;
   constexpr int NW = 8, WM = 4, BM = 256, BN = 128;
   constexpr int HB = HP * NW * 1024;             // bytes per halo buffer
-  constexpr int WB = BN * 128;                   // bytes per weight slot
+  constexpr int WB = BN * 128;                   // bytes per weight slot (WS slots)
   constexpr int EP = BN * 4 + 16;                // epilogue row pitch (fp32)
-  constexpr int LDS_BYTES = (2 * HB + 3 * WB) > BM * EP ? (2 * HB + 3 * WB) : BM * EP;
+  constexpr int LDS_BYTES = (2 * HB + WS * WB) > BM * EP ? (2 * HB + WS * WB) : BM * EP;
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   char* const wring = lds + 2 * HB;
 
@@ -639,30 +644,48 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
   auto issue_w = [&](int s) {
     const int c = s / 9, t = s - c * 9;
     const unsigned koff = (unsigned)(t * a.Kc + c * 64) * 2u;
-    dma_pieces<2>(a.w, a.w_bytes, wring + (s % 3) * WB + wave * 2 * 1024, ob, koff, 0, 2);
+    dma_pieces<2>(a.w, a.w_bytes, wring + (s % WS) * WB + wave * 2 * 1024, ob, koff, 0, 2);
   };
   auto part_b = [](int k) { return k * HP / 3; };
-  // vector-memory instructions a wave issues in slot t (after the barrier of stage t)
-  auto slot_count = [&](int t) {
+  // halo pieces a wave issues in slot t (after the barrier of stage t): chunk c+1's halo, in three parts
+  auto halo_count = [&](int t) {
     const int c = t / 9, k = t - c * 9;
-    return (t + 2 < nst ? 2 : 0) + ((k < 3 && c + 1 < nch) ? part_b(k + 1) - part_b(k) : 0);
+    return (k < 3 && c + 1 < nch) ? part_b(k + 1) - part_b(k) : 0;
   };
+  // vector-memory instructions a wave issues in slot t: weight slice t+WS-1, then the halo part
+  auto slot_count = [&](int t) { return (t + WS - 1 < nst ? 2 : 0) + halo_count(t); };
+  // what may stay in flight when stage s starts: everything the wave issued after weight slice s (slot
+  // s-WS+1, or the prologue); the halo part issued beside that slice belongs to the next chunk
+  auto after_w = [&](int s) {
+    const int ts = s - (WS - 1);
+    int n = 0;
+    if (ts < 0) {
+      for (int q = s + 1; q < WS - 1 && q < nst; ++q) n += 2;
+      for (int t = 0; t < s; ++t) n += slot_count(t);
+    } else {
+      n = halo_count(ts);
+      for (int t = ts + 1; t < s; ++t) n += slot_count(t);
+    }
+    return n;
+  };
+  if ((a.dbg & 32) && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);   // probe: static priority, younger half
 
   halo_issue<HP>(a, lds, 0, wave, 0, HP, h1, h2);
-  issue_w(0);
-  if (nst > 1) issue_w(1);
+  for (int q = 0; q < WS - 1 && q < nst; ++q) issue_w(q);
   for (int s = 0; s < nst; ++s) {
-    wait_vm_dyn(s == 0 ? (nst > 1 ? 2 : 0) : slot_count(s - 1));
+    wait_vm_dyn(after_w(s));
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
     const int c = s / 9, t = s - c * 9;
-    if (!(a.dbg & 2)) {
-      if (s + 2 < nst) issue_w(s + 2);
+    const bool dma = !(a.dbg & 2), late = a.dbg & 64;   // probe: issue the DMA after the first MFMA half
+    auto issue_stage = [&]() {
+      if (s + WS - 1 < nst) issue_w(s + WS - 1);
       if (t < 3 && c + 1 < nch) halo_issue<HP>(a, lds + ((c + 1) & 1) * HB, (c + 1) * 64, wave, part_b(t), part_b(t + 1), h1, h2);
-    }
+    };
+    if (dma && !late) issue_stage();
     if (a.dbg & 4) continue;
     const char* A = lds + (c & 1) * HB;
     const char* Bw = wring + (s % 3) * WB;
@@ -688,11 +711,14 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j][0] += __builtin_bit_cast(float, fa[i][0] ^ fb[j][0]);
       } else {
+        if (a.dbg & 16) __builtin_amdgcn_s_setprio(1);   // probe: priority around the MFMA cluster
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
+        if (a.dbg & 16) __builtin_amdgcn_s_setprio(0);
       }
+      if (ks == 0 && dma && late) issue_stage();
     }
   }
   __syncthreads();
@@ -703,6 +729,155 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
       *(v4f*)(lds + (wm * 64 + j * 16 + fr) * EP + (wn * 64 + i * 16 + fh * 4) * 4) = acc[i][j];
   __syncthreads();
   if (a.dbg & 8) return;
+  for (int idx = threadIdx.x; idx < BM * BN / 4; idx += NW * 64) {
+    const int pl = idx / (BN / 4), cg = idx - pl * (BN / 4);
+    const v4f v = *(const v4f*)(lds + pl * EP + cg * 16);
+    conv_store_tile<T>(a, v, m0 + pl, n0 + cg * 4);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Register-weight variant of conv3x3_halo_kernel (same tile, halo image and fragment reads). Each wave
+// loads its own 64x64 weight fragments of tap stage s+1 straight into VGPRs while stage s computes (the
+// four waves sharing a slice hit the same L1 lines), and the next chunk's halo is staged through VGPRs
+// too (loaded at the chunk's first tap, written to the other LDS buffer at its last). No weight LDS
+// traffic, no LDS-DMA issue per tap, and ONE barrier per 64-channel chunk instead of one per tap; all
+// loads are ordinary VGPR loads, so the compiler's counted waits cover them.
+
+// 16-byte loads at byte offsets off[p] + add from base; kOOB offsets read zero (the load goes to base
+// and its value is dropped: no branch around the load)
+template <int N>
+DMC_DEV void reg_load16(const char* base, const unsigned* off, unsigned add, v4i* out) {
+#pragma unroll
+  for (int p = 0; p < N; ++p) {
+    const bool ok = off[p] != kOOB;
+    v4i v = *(const v4i*)(base + (ok ? off[p] + add : 0u));
+    if (!ok) v = v4i{0, 0, 0, 0};
+    out[p] = v;
+  }
+}
+
+template <int HP>
+__global__ __launch_bounds__(512) void conv3x3_halo_rw_kernel(ConvK a, int R, int nimg) {
+  using T = bf16_t;
+  constexpr int NW = 8, WM = 4, BM = 256, BN = 128;
+  constexpr int HB = HP * NW * 1024;             // bytes per halo buffer
+  constexpr int EP = BN * 4 + 16;                // epilogue row pitch (fp32)
+  constexpr int LDS_BYTES = 2 * HB > BM * EP ? 2 * HB : BM * EP;
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int lrow = lane >> 3;
+  const int lc = (lane & 7) ^ lrow;
+  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
+  const int n_first = m0 / a.OHW;
+  const int r0 = (m0 - n_first * a.OHW) / OW;
+
+  // halo source offsets per piece, as in conv3x3_halo_kernel (kOOB = zero padding / past the halo)
+  unsigned h1[HP], h2[HP];
+#pragma unroll
+  for (int p = 0; p < HP; ++p) {
+    const int h = (wave * HP + p) * 8 + lrow;
+    h1[p] = kOOB; h2[p] = kOOB;
+    if (h < npix) {
+      const int img = h / segpix, rem = h - img * segpix;
+      const int hy = rem / HW, hx = rem - hy * HW;
+      const int iy = r0 + hy - 1, ix = hx - 1;
+      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
+        const unsigned sp = (unsigned)(((n_first + img) * a.H + iy) * a.W + ix);
+        h1[p] = (sp * a.ld1 + lc * 8) * 2u;
+        h2[p] = (sp * a.ld2 + lc * 8) * 2u;
+      }
+    }
+  }
+  // weight fragments of this lane: rows co = n0 + wn*64 + 16i + fr, 16-byte chunk fh (ks 0) / fh+4 (ks 1)
+  const int fr = lane & 15, fh = lane >> 4;
+  const unsigned wrow = (unsigned)(a.ntaps * a.Kc);
+  unsigned wo[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int co = n0 + wn * 64 + i * 16 + fr;
+    const unsigned o = ((unsigned)co * wrow + fh * 8) * 2u;
+    wo[i] = co < a.Cout ? o : kOOB;
+    wo[4 + i] = co < a.Cout ? o + 64u : kOOB;
+  }
+  int hb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = wm * 64 + j * 16 + fr;
+    const int img = m / (R * OW), rem = m - img * (R * OW);
+    const int r = rem / OW, col = rem - r * OW;
+    hb[j] = img * segpix + (r + 1) * HW + col + 1;
+  }
+
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int nch = a.Kc / 64, nst = nch * 9;
+  v4i hv[HP];
+  auto halo_load = [&](int c0) __attribute__((always_inline)) {
+    if (c0 < a.C1) reg_load16<HP>(a.x1, h1, (unsigned)c0 * 2u, hv);
+    else reg_load16<HP>(a.x2, h2, (unsigned)(c0 - a.C1) * 2u, hv);
+  };
+  auto halo_store = [&](int buf) __attribute__((always_inline)) {
+    char* dst = lds + buf * HB + wave * HP * 1024 + lane * 16;
+#pragma unroll
+    for (int p = 0; p < HP; ++p) *(v4i*)(dst + p * 1024) = hv[p];
+  };
+  auto load_w = [&](int s, v4i* f) __attribute__((always_inline)) {
+    const int c = s / 9, t = s - c * 9;
+    reg_load16<8>(a.w, wo, (unsigned)(t * a.Kc + c * 64) * 2u, f);
+  };
+  auto stage = [&](int s, const v4i* cur, v4i* nxt) __attribute__((always_inline)) {
+    const int c = s / 9, t = s - c * 9;
+    load_w(s + 1 < nst ? s + 1 : s, nxt);   // always issued: no branch around the loads
+    if (t == 0 && c + 1 < nch) halo_load((c + 1) * 64);
+    const char* A = lds + (c & 1) * HB;
+    const int ty = t / 3, tx = t - ty * 3;
+    const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = ks * 4 + fh;
+      v4i fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int h = hb[j] + delta;
+        fb[j] = *(const v4i*)(A + h * 128 + ((chunk ^ (h & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], cur[ks * 4 + i], fb[j]);
+    }
+    if (t == 8 && c + 1 < nch) {
+      // buffer (c+1)&1 was last read in chunk c-1, which every wave finished before the previous barrier
+      halo_store((c + 1) & 1);
+      __syncthreads();
+    }
+  };
+
+  halo_load(0);
+  v4i wa[8], wb[8];
+  load_w(0, wa);
+  halo_store(0);
+  __syncthreads();
+  for (int s = 0; s < nst; s += 2) {
+    stage(s, wa, wb);
+    if (s + 1 < nst) stage(s + 1, wb, wa);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *(v4f*)(lds + (wm * 64 + j * 16 + fr) * EP + (wn * 64 + i * 16 + fh * 4) * 4) = acc[i][j];
+  __syncthreads();
   for (int idx = threadIdx.x; idx < BM * BN / 4; idx += NW * 64) {
     const int pl = idx / (BN / 4), cg = idx - pl * (BN / 4);
     const v4f v = *(const v4f*)(lds + pl * EP + cg * 16);
@@ -723,6 +898,113 @@ int halo_plan(const ConvK& k, int* R, int* nimg) {
   else return 0;
   const int npix = *nimg * (*R + 2) * (k.OW + 2);
   return npix <= 6 * 64 ? 6 : npix <= 7 * 64 ? 7 : 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Narrow convs: GEMM K or N is a sliver of an MFMA tile. The UNet's input conv (3 channels in,
+// models/unet.py:188), the input gradient of its output conv (3 channels in) and the output conv itself
+// (3 channels out, :241), padded into the 128-wide tiles above, cost as much as a 128-channel layer. Here
+// both operands are read straight from global memory in fragment layout (lane = (row fr, 16-byte k chunk
+// fh)), one wave per 64 output pixels, no LDS and no barrier. Loads are never behind a branch: rows that
+// do not exist load a valid row and are zeroed.
+
+// zero the elements >= n of a 16-byte chunk (the padding channels of a narrow source may hold anything)
+template <typename T>
+DMC_DEV v4i mask_chunk(v4i v, int n) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    if (sizeof(T) == 4) {
+      if (d >= n) v[d] = 0;
+    } else {
+      if (2 * d >= n) v[d] = 0;
+      else if (2 * d + 1 >= n) v[d] &= 0xffff;
+    }
+  }
+  return v;
+}
+
+DMC_DEV void pixel_coords(const ConvK& a, int pix, int& n, int& oy, int& ox) {
+  n = pix < a.M ? pix / a.OHW : -1;
+  const int rem = pix - (n < 0 ? 0 : n) * a.OHW;
+  oy = rem / a.OW;
+  ox = rem - oy * a.OW;
+}
+
+// Narrow input (one source of <= one chunk of channels): a k step is 4 taps x that chunk, so 9 taps are
+// 3 MFMA k steps; a wave owns 64 pixels x 32 output channels (2 x 4 accumulator tiles; the 4 x 4
+// epilogue of a 64-channel tile spills in bf16).
+template <typename T>
+__global__ __launch_bounds__(256) void conv_narrow_in_kernel(ConvK a) {
+  const int lane = threadIdx.x & 63;
+  const int fr = lane & 15, fh = lane >> 4;
+  const int p0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+  const int n0 = blockIdx.y * 32;
+  if (p0 >= a.M) return;   // wave-uniform; the kernel has no barrier
+  int pn[4], poy[4], pox[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) pixel_coords(a, p0 + 16 * j + fr, pn[j], poy[j], pox[j]);
+  const size_t wrow = (size_t)a.ntaps * a.Kc;
+  v4f acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int t0 = 0; t0 < a.ntaps; t0 += 4) {
+    const int tap = t0 + fh;
+    const bool tok = tap < a.ntaps;
+    const int tp = tok ? tap : 0;
+    v4i fa[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int co = n0 + 16 * i + fr;
+      v4i w = *(const v4i*)(a.w + ((size_t)(co < a.Cout ? co : 0) * wrow + (size_t)tp * a.Kc) * sizeof(T));
+      if (!(tok && co < a.Cout)) w = v4i{0, 0, 0, 0};
+      fa[i] = w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int sp = (pn[j] >= 0 && tok) ? src_pixel(a, pn[j], poy[j], pox[j], tp) : -1;
+      const v4i fb = mask_chunk<T>(load_act_chunk<T>(a, pn[j], sp, 0), a.C1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb);
+    }
+  }
+  conv_epilogue<T, 2, 4>(a, acc, p0, n0);
+}
+
+// Narrow output (Cout <= 16): the output channels are ONE 16-wide MFMA tile; a wave owns 64 pixels and
+// walks K = taps x input chunks.
+template <typename T>
+__global__ __launch_bounds__(256) void conv_narrow_out_kernel(ConvK a) {
+  constexpr int EPC = TT<T>::KPL;
+  const int lane = threadIdx.x & 63;
+  const int fr = lane & 15, fh = lane >> 4;
+  const int p0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+  if (p0 >= a.M) return;   // wave-uniform; the kernel has no barrier
+  int pn[4], poy[4], pox[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) pixel_coords(a, p0 + 16 * j + fr, pn[j], poy[j], pox[j]);
+  const bool wok = fr < a.Cout;
+  const char* wbase = a.w + (size_t)(wok ? fr : 0) * a.ntaps * a.Kc * sizeof(T);
+  const int Cin = a.C1 + a.C2;
+  v4f acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < a.ntaps; ++t) {
+    int sp[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sp[j] = pn[j] >= 0 ? src_pixel(a, pn[j], poy[j], pox[j], t) : -1;
+    for (int k0 = 0; k0 < Cin; k0 += 4 * EPC) {
+      const int c = k0 + fh * EPC;   // < Kc: Kc is Cin rounded up past the 4-chunk k step
+      v4i fw = *(const v4i*)(wbase + ((size_t)t * a.Kc + c) * sizeof(T));
+      if (!wok) fw = v4i{0, 0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[j] = mma16<T>(acc[j], fw, mask_chunk<T>(load_act_chunk<T>(a, pn[j], sp[j], c), Cin - c));
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) conv_store_tile<T>(a, acc[j], p0 + 16 * j + fr, fh * 4);
 }
 
 // split-K reduction + the regular epilogue: out(pix, co..co+3) = epilogue(sum_z slab[z][pix][co..])
@@ -1338,6 +1620,17 @@ void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
 
 template <typename T>
 int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
+  constexpr int EPC = TT<T>::KPL;
+  if (!getenv_flag("DMC_NO_NARROW")) {
+    if (k.C2 == 0 && k.C1 <= EPC && k.Cout >= 16) {
+      conv_narrow_in_kernel<T><<<dim3(dmc::cdiv(k.M, 256), dmc::cdiv(k.Cout, 32)), 256, 0, s>>>(k);
+      return dmc::check_launch("dmc_conv2d");
+    }
+    if (k.Cout <= 8 && (k.C2 == 0 || k.C1 % EPC == 0)) {
+      conv_narrow_out_kernel<T><<<dmc::cdiv(k.M, 256), 256, 0, s>>>(k);
+      return dmc::check_launch("dmc_conv2d");
+    }
+  }
   if (sizeof(T) == 2 && k.prologue == DMC_PRO_NONE && !getenv_flag("DMC_NO_GLDS")) {
     // bf16, plain operands: LDS-DMA pipelined kernel
     FwdPlan p = plan_glds(k);
@@ -1351,10 +1644,16 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
       const char* dbg = getenv("DMC_HALO_DBG");
       k.dbg = dbg ? atoi(dbg) : 0;
     }
-    if (hp == 6)
-      conv3x3_halo_kernel<6><<<dim3(k.M / 256, dmc::cdiv(k.Cout, 128)), 512, 0, s>>>(k, R, nimg);
+    const dim3 hg(k.M / 256, dmc::cdiv(k.Cout, 128));
+    if (hp && getenv_flag("DMC_HALO_RW")) {
+      if (hp == 6) conv3x3_halo_rw_kernel<6><<<hg, 512, 0, s>>>(k, R, nimg);
+      else conv3x3_halo_rw_kernel<7><<<hg, 512, 0, s>>>(k, R, nimg);
+    } else if (hp == 6 && getenv_flag("DMC_HALO_WS4"))
+      conv3x3_halo_kernel<6, 4><<<hg, 512, 0, s>>>(k, R, nimg);
+    else if (hp == 6)
+      conv3x3_halo_kernel<6, 3><<<hg, 512, 0, s>>>(k, R, nimg);
     else if (hp == 7)
-      conv3x3_halo_kernel<7><<<dim3(k.M / 256, dmc::cdiv(k.Cout, 128)), 512, 0, s>>>(k, R, nimg);
+      conv3x3_halo_kernel<7, 3><<<hg, 512, 0, s>>>(k, R, nimg);
     else if (buf) launch_glds<true>(k, p, s);
     else launch_glds<false>(k, p, s);
     return dmc::check_launch("dmc_conv2d");

@@ -260,10 +260,22 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float* in, int R, in
   const int c = blockIdx.x * 64 + lane;
   float s0 = 0.f, s1 = 0.f;
   if (c < C) {
-    // 4 rows in flight per thread (the row count is small: the loop is latency-, not bandwidth-bound)
+    // 8 rows in flight per thread (the row count is small: the loop is latency-, not bandwidth-bound);
+    // rows are still added in ascending order
     const float* p = in + (size_t)c * stride;
     const bool two = out1 != nullptr;
     int r = slice;
+    for (; r + 16 * 7 < R; r += 128) {
+      float a[8], b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = p[(size_t)(r + 16 * u) * ld];
+      if (two) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) b[u] = p[(size_t)(r + 16 * u) * ld + 1];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { s0 += a[u]; s1 += b[u]; }
+    }
     for (; r + 48 < R; r += 64) {
       float a[4], b[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll

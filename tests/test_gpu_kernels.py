@@ -42,11 +42,14 @@ def q(x, dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("case", ["s1_concat_gn", "s2", "up", "1x1", "ragged_in", "splitk_concat", "splitk_ragged"])
-def test_conv_forward(dt, case):
+@pytest.mark.parametrize("case", ["s1_concat_gn", "s2", "up", "1x1", "ragged_in", "ragged_in_generic", "narrow_out",
+                                  "splitk_concat", "splitk_ragged"])
+def test_conv_forward(dt, case, monkeypatch):
     """splitk_*: small M with deep K, which both planners (bf16 LDS-DMA, fp32 register-staged) run as split-K
-    over grid.z + epilogue kernel."""
+    over grid.z + epilogue kernel. ragged_in (3 input channels) and narrow_out (3 output channels) run the
+    narrow-conv kernels; ragged_in_generic is the same conv on the tiled kernels (DMC_NO_NARROW)."""
     L, K = _lib()
+    monkeypatch.setenv("DMC_NO_NARROW", "1" if case == "ragged_in_generic" else "0")
     torch.manual_seed(0)
     N, H, W = 2, 8, 8
     C1, C2, Cout = 32, 16, 48
@@ -61,9 +64,11 @@ def test_conv_forward(dt, case):
         C2, mode, OH, OW = 0, L.MODE_UPSAMPLE, 16, 16
     elif case == "1x1":
         taps, k = K.TAPS1, 1
-    elif case == "ragged_in":
+    elif case.startswith("ragged_in"):
         C1, C2 = 3, 0
-    ld1 = C1 if case != "ragged_in" else L.chunk_for(dt)
+    elif case == "narrow_out":
+        Cout = 3
+    ld1 = C1 if not case.startswith("ragged_in") else L.chunk_for(dt)
     x1 = torch.randn(N, C1, H, W)
     x2 = torch.randn(N, C2, H, W) if C2 else None
     w = torch.randn(Cout, C1 + C2, k, k) / math.sqrt((C1 + C2) * k * k)
@@ -83,7 +88,8 @@ def test_conv_forward(dt, case):
     resid = torch.randn(N, Cout, OH, OW)
     yr = yr + q(resid, dt)
     # kernel
-    x1d = torch.zeros(N, H, W, ld1, dtype=dt, device=DEV)
+    # padding channels of a narrow source hold garbage: the kernels must not read them into the sum
+    x1d = torch.full((N, H, W, ld1), 1e4, dtype=dt, device=DEV)
     x1d[..., :C1] = nhwc(x1).to(dt).to(DEV)
     x2d = nhwc(x2).to(dt).to(DEV) if x2 is not None else None
     Kc = L.kc_for(C1 + C2, dt)
@@ -158,11 +164,15 @@ def test_conv_dgrad_wgrad(dt, case):
     assert e1 < lim and e2 < (1e-5 if dt == torch.float32 else 1e-2), (e1, e2)
 
 
+@pytest.mark.parametrize("variant", ["ring3", "ring4", "regw"])
 @pytest.mark.parametrize("case", ["fwd32_concat", "fwd16_ragged_cout", "dgrad32", "fwd8_multi_image", "fallback_4x4"])
-def test_conv3x3_halo_kernel(case, monkeypatch):
+def test_conv3x3_halo_kernel(case, variant, monkeypatch):
     """bf16 3x3 stride-1 convs on the LDS-halo kernel (whole-row 256-pixel tiles) vs an fp32 reference and
-    vs the per-tap kernel (DMC_NO_HALO) on the same inputs."""
+    vs the per-tap kernel (DMC_NO_HALO) on the same inputs. Variants: 3- or 4-slot LDS-DMA weight ring
+    (DMC_HALO_WS4), register-staged weights (DMC_HALO_RW)."""
     L, K = _lib()
+    monkeypatch.setenv("DMC_HALO_WS4", "1" if variant == "ring4" else "0")
+    monkeypatch.setenv("DMC_HALO_RW", "1" if variant == "regw" else "0")
     dt = torch.bfloat16
     torch.manual_seed(5)
     N, H, C1, C2, Cout, taps, pm = 2, 32, 64, 64, 128, K.TAPS3, L.PACK_FWD
@@ -273,9 +283,14 @@ def test_groupnorm_stats_and_backward(dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("path", ["auto", "staged", "hg4"])
 @pytest.mark.parametrize("Lq,hd", [(16, 64), (64, 64), (256, 64), (1024, 64), (64, 8), (100, 16)])
-def test_attention_fwd_bwd(dt, Lq, hd):
+def test_attention_fwd_bwd(dt, Lq, hd, path, monkeypatch):
+    """auto: row-resident kernels for L <= 256 (one head per block at this batch), staged above; staged: the
+    64-row-tile kernels everywhere (DMC_ATTN_STAGED); hg4: resident blocks owning 4 heads where they fit."""
     L, K = _lib()
+    monkeypatch.setenv("DMC_ATTN_STAGED", "1" if path == "staged" else "0")
+    monkeypatch.setenv("DMC_ATTN_HG", "4" if path == "hg4" else "0")
     torch.manual_seed(3)
     N, heads = 2, 4
     C = heads * hd

@@ -110,6 +110,39 @@ def test_cifar_unet_train_step_grads_match_oracle():
         assert rel(p.grad, sd[k].grad) < 5e-4, (k, rel(p.grad, sd[k].grad))
 
 
+def test_p_losses_every_timestep_matches_oracle():
+    """north_star: p_losses within 1e-4 over the 1k diffusion steps. Every t in [0, 1000) once, one p_losses
+    call per timestep (tiny conditional UNet with the reference fixture's weights, fp32, l2), against the
+    oracle's per-sample loss; l1 / huber as the batch mean over all 1000 timesteps. Tolerance 1e-4 relative
+    to max(1, |loss|)."""
+    from diffusion_models_collection_amd.diffusion import DDPM
+    from oracle.unet_oracle import make_oracle
+    from oracle import diffusion_oracle as DO
+    m, g = build("unet_tiny_cond")
+    m.eval()
+    orc, _ = make_oracle(split_params(g, "param/"), TINY["unet_tiny_cond"])
+    gen = torch.Generator().manual_seed(11)
+    T = 1000
+    x0 = torch.rand(T, 3, 16, 16, generator=gen) * 2 - 1
+    noise = torch.randn(T, 3, 16, 16, generator=gen)
+    t = torch.arange(T)
+    y = torch.randint(0, 10, (T,), generator=gen)
+    with torch.no_grad():
+        pred = orc.forward(DO.q_sample(DO.schedule(), x0, t, noise), t, y)
+    ddpm = DDPM(device=DEV)
+    xd, nd, td, yd = x0.to(DEV), noise.to(DEV), t.to(DEV), y.to(DEV)
+    with torch.no_grad():
+        got = torch.stack([ddpm.p_losses(m, xd[i:i + 1], td[i:i + 1], yd[i:i + 1], noise=nd[i:i + 1])
+                           for i in range(T)]).reshape(T).cpu()
+        ref = ((noise - pred) ** 2).mean(dim=(1, 2, 3))
+        err = (got - ref).abs() / ref.abs().clamp(min=1.0)
+        assert err.max().item() < 1e-4, (int(err.argmax()), err.max().item())
+        for lt in ("l1", "huber"):
+            gl = ddpm.p_losses(m, xd, td, yd, noise=nd, loss_type=lt).item()
+            rl = DO.loss(lt, noise, pred).item()
+            assert abs(gl - rl) < 1e-4 * max(1.0, abs(rl)), (lt, gl, rl)
+
+
 def test_diffusion_ops_match_reference():
     from diffusion_models_collection_amd.diffusion import DDPM, DDIM
     g = load_golden("diffusion_ops")
