@@ -308,6 +308,46 @@ DMC_DEV void conv_store_tile(const ConvK& a, const v4f accv, const int pix, cons
   }
 }
 
+// Epilogue of the LDS-staged kernels: the block's BM x BN fp32 tile (LDS rows of EP bytes) through the conv
+// epilogue. A thread keeps ONE 4-channel group (NT is a multiple of BN/4) and walks every (NT*4/BN)-th
+// pixel row, so the bias load, the output select and the channel addressing are hoisted out of the loop
+// and the image index is tracked incrementally instead of divided per element (conv_store_tile's general
+// form costs more VALU than the tile's MFMAs leave room for). NCHW output, fused silu' and ragged channel
+// groups take conv_store_tile.
+template <typename T, int BM, int BN, int NT>
+DMC_DEV void tile_epilogue(const ConvK& a, const char* lds, int EP, int m0, int n0) {
+  constexpr int CG = BN / 4, RS = NT / CG;
+  const int cg = threadIdx.x % CG, r0 = threadIdx.x / CG;
+  const int co = n0 + cg * 4;
+  if (a.out_nchw || a.silu_pre || (a.Cout & 3)) {
+    for (int pl = r0; pl < BM; pl += RS) conv_store_tile<T>(a, *(const v4f*)(lds + pl * EP + cg * 16), m0 + pl, co);
+    return;
+  }
+  if (co >= a.Cout) return;
+  const bool of32 = a.out_f32 != 0;
+  const v4f b = a.bias ? *(const v4f*)(a.bias + co) : v4f{0.f, 0.f, 0.f, 0.f};
+  const bool first = co < a.Csplit;
+  char* const y = first ? a.y1 : a.y2;
+  const int ldy = first ? a.ldy1 : a.ldy2, cy = first ? co : co - a.Csplit;
+  int n = (m0 + r0) / a.OHW, nend = (n + 1) * a.OHW;
+  for (int pl = r0; pl < BM; pl += RS) {
+    const int pix = m0 + pl;
+    if (pix >= a.M) break;
+    v4f v = *(const v4f*)(lds + pl * EP + cg * 16) + b;
+    if (a.addvec) {
+      while (pix >= nend) { ++n; nend += a.OHW; }
+      v += *(const v4f*)(a.addvec + (size_t)n * a.ld_add + co);
+    }
+    float f[4] = {v[0], v[1], v[2], v[3]};
+    if (a.resid) {
+      float r[4];
+      load4<T>(a.resid, (size_t)pix * a.ld_res + co, r, of32);
+      f[0] += r[0]; f[1] += r[1]; f[2] += r[2]; f[3] += r[3];
+    }
+    store4<T>(y, (size_t)pix * ldy + cy, f, of32);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // bf16 forward / dgrad kernel without prologue: global->LDS DMA (global_load_lds_dwordx4) into a
 // 3-stage LDS ring, counted vmcnt + one raw barrier per stage, 64x64 output per wave.
@@ -516,11 +556,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
     }
     return;
   }
-  for (int idx = threadIdx.x; idx < BM * BN / 4; idx += NW * 64) {
-    const int pl = idx / (BN / 4), cg = idx - pl * (BN / 4);
-    const v4f v = *(const v4f*)(lds + pl * EP + cg * 16);
-    conv_store_tile<T>(a, v, m0 + pl, n0 + cg * 4);
-  }
+  tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -729,11 +765,7 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
       *(v4f*)(lds + (wm * 64 + j * 16 + fr) * EP + (wn * 64 + i * 16 + fh * 4) * 4) = acc[i][j];
   __syncthreads();
   if (a.dbg & 8) return;
-  for (int idx = threadIdx.x; idx < BM * BN / 4; idx += NW * 64) {
-    const int pl = idx / (BN / 4), cg = idx - pl * (BN / 4);
-    const v4f v = *(const v4f*)(lds + pl * EP + cg * 16);
-    conv_store_tile<T>(a, v, m0 + pl, n0 + cg * 4);
-  }
+  tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -878,11 +910,7 @@ __global__ __launch_bounds__(512) void conv3x3_halo_rw_kernel(ConvK a, int R, in
     for (int i = 0; i < 4; ++i)
       *(v4f*)(lds + (wm * 64 + j * 16 + fr) * EP + (wn * 64 + i * 16 + fh * 4) * 4) = acc[i][j];
   __syncthreads();
-  for (int idx = threadIdx.x; idx < BM * BN / 4; idx += NW * 64) {
-    const int pl = idx / (BN / 4), cg = idx - pl * (BN / 4);
-    const v4f v = *(const v4f*)(lds + pl * EP + cg * 16);
-    conv_store_tile<T>(a, v, m0 + pl, n0 + cg * 4);
-  }
+  tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
 }
 
 // Geometry of the halo kernel for this conv, or false if it does not apply.
