@@ -31,6 +31,7 @@ class ConvDesc(ctypes.Structure):
         ("tap_dy", _c_int * 16), ("tap_dx", _c_int * 16),
         ("prologue", _c_int), ("pro_scale", _c_p), ("pro_shift", _c_p), ("ld_pro", _c_int),
         ("drop_seed", _c_u32), ("drop_thresh", _c_u32), ("drop_scale", _c_f), ("drop_ld", _c_int),
+        ("drop_seed_base", _c_p),
         ("bias", _c_p), ("addvec", _c_p), ("ld_add", _c_int), ("resid", _c_p), ("ld_res", _c_int),
         ("silu_pre", _c_p), ("ld_silu", _c_int), ("Csplit", _c_int), ("ldy1", _c_int), ("ldy2", _c_int),
         ("out_f32", _c_int), ("out_nchw", _c_int),
@@ -66,9 +67,9 @@ def _load():
         "dmc_gn_stats": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_f,
                                   _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
         "dmc_gn_apply": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p,
-                                  _c_int, _c_u32, _c_u32, _c_f, _c_p, _c_int, _c_p]),
+                                  _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_int, _c_p]),
         "dmc_gn_silu_bwd": (_c_int, [_c_int, _c_p, _c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int,
-                                     _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_u32, _c_u32, _c_f, _c_p, _c_p,
+                                     _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_p,
                                      _c_int, _c_int, _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_p, _c_p, _c_p]),
         "dmc_channel_sum_workspace": (_c_size, [_c_int, _c_int, _c_int]),
         "dmc_channel_sum": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_p, _c_int, _c_p, _c_f, _c_p,
@@ -95,6 +96,7 @@ def _load():
         "dmc_clip_grad_norm": (_c_int, [_c_p, _c_int, _c_f, _c_p, _c_p, _c_p]),
         "dmc_grad_norm_flat": (_c_int, [_c_p, _c_long, _c_f, _c_p, _c_p, _c_p, _c_p]),
         "dmc_adamw_flat": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_long, _c_p] + [_c_f] * 9 + [_c_p]),
+        "dmc_adamw_flat_dev": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_long, _c_p, _c_p, _c_p]),
         "dmc_silu_fwd": (_c_int, [_c_p, _c_p, _c_long, _c_p]),
         "dmc_unpack_output": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p]),
         "dmc_add": (_c_int, [_c_int, _c_p, _c_p, _c_long, _c_p]),
@@ -124,7 +126,9 @@ def ptr(t):
 
 
 def stream():
-    return torch.cuda.current_stream().cuda_stream
+    """Raw hipStream_t of torch's current stream on the current device (the direct C accessors: the
+    torch.cuda.current_stream() object path costs several microseconds per kernel launch)."""
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
 
 
 def dtype_code(dt: torch.dtype) -> int:

@@ -20,7 +20,7 @@ struct ConvK {
   int N, H, W, C1, C2, ld1, ld2, Kc, OH, OW, Cout, ntaps, mode, stride;
   int tkw, tdy0, tdx0, tsy, tsx;   // tap grid: tap t -> (tdy0 + tsy*(t / tkw), tdx0 + tsx*(t % tkw))
   int prologue; const float* psc; const float* psh; int ldp;
-  uint32_t dseed, dthresh; float dscale; int dld;
+  uint32_t dseed, dthresh; float dscale; int dld; const uint32_t* dseed_base;
   const float* bias; const float* addvec; int ld_add;
   const char* resid; int ld_res; const float* silu_pre; int ld_silu;
   int Csplit, ldy1, ldy2, out_f32, out_nchw;
@@ -82,8 +82,9 @@ DMC_DEV v4i load_act_chunk(const ConvK& a, int n, int sp, int c) {
     }
     if (a.dthresh) {
       const uint64_t base = (uint64_t)sp * a.dld + c;
+      const uint32_t seed = a.dseed + (a.dseed_base ? *a.dseed_base : 0u);
 #pragma unroll
-      for (int e = 0; e < EPC; ++e) f[e] = drop_keep(base + e, a.dseed, a.dthresh) ? f[e] * a.dscale : 0.f;
+      for (int e = 0; e < EPC; ++e) f[e] = drop_keep(base + e, seed, a.dthresh) ? f[e] * a.dscale : 0.f;
     }
     v = Chunk<T>::pack(f);
   }
@@ -1552,6 +1553,7 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
   }
   k.prologue = d->prologue; k.psc = d->pro_scale; k.psh = d->pro_shift; k.ldp = d->ld_pro;
   k.dseed = d->drop_seed; k.dthresh = d->drop_thresh; k.dscale = d->drop_scale; k.dld = d->drop_ld;
+  k.dseed_base = d->drop_seed_base;
   k.bias = d->bias; k.addvec = d->addvec; k.ld_add = d->ld_add; k.resid = (const char*)d->resid; k.ld_res = d->ld_res;
   k.silu_pre = d->silu_pre; k.ld_silu = d->ld_silu;
   k.Csplit = d->Csplit; k.ldy1 = d->ldy1; k.ldy2 = d->ldy2; k.out_f32 = d->out_f32; k.out_nchw = d->out_nchw;

@@ -392,7 +392,18 @@ struct AdamWArgs {
   const float* coef;
   long n;
   float wd_mul, w1, b2, omb2, neg_step, bc2_sqrt, eps, ema_d, ema_om;   // host-computed like torch (double -> float)
+  const float* hyper;   // if set, the nine scalars are read from device memory (dmc_adamw_flat_dev order)
 };
+
+// the scalars of a graph-replayed step live in device memory, refreshed by one H2D copy per step
+DMC_DEV AdamWArgs adamw_resolve(const AdamWArgs& a0) {
+  AdamWArgs a = a0;
+  if (const float* h = a0.hyper) {
+    a.wd_mul = h[0]; a.w1 = h[1]; a.b2 = h[2]; a.omb2 = h[3]; a.eps = h[4];
+    a.neg_step = h[5]; a.bc2_sqrt = h[6]; a.ema_d = h[7]; a.ema_om = h[8];
+  }
+  return a;
+}
 
 DMC_DEV void adamw_elem(const AdamWArgs& a, float c, float& p, float g, float& m, float& v, float* e) {
   g = g * c;
@@ -405,7 +416,8 @@ DMC_DEV void adamw_elem(const AdamWArgs& a, float c, float& p, float g, float& m
   if (e) *e = *e * a.ema_d + a.ema_om * p;
 }
 
-__global__ __launch_bounds__(256) void adamw_flat_kernel(AdamWArgs a) {
+__global__ __launch_bounds__(256) void adamw_flat_kernel(AdamWArgs a0) {
+  const AdamWArgs a = adamw_resolve(a0);
   const float c = a.coef ? a.coef[0] : 1.0f;
   const long n4 = a.n / 4;
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n4; q += (long)gridDim.x * blockDim.x) {
@@ -593,7 +605,17 @@ extern "C" int dmc_adamw_flat(float* p, const float* g, float* m, float* v, floa
   DMC_REQUIRE((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v | (uintptr_t)ema) & 15) == 0,
               "adamw_flat: buffers must be 16-byte aligned");
   AdamWArgs a{p, g, m, v, ema, coef, n, wd_mul, lerp_w, beta2, one_minus_beta2, neg_step_size, bc2_sqrt, eps,
-              ema_decay, ema_one_minus};
+              ema_decay, ema_one_minus, nullptr};
   adamw_flat_kernel<<<grid_for(n / 4 + 1, 256, 4096), 256, 0, dmc::as_stream(stream)>>>(a);
   return dmc::check_launch("dmc_adamw_flat");
+}
+
+extern "C" int dmc_adamw_flat_dev(float* p, const float* g, float* m, float* v, float* ema, long n, const float* coef,
+                                  const float* hyper, void* stream) {
+  DMC_REQUIRE((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v | (uintptr_t)ema) & 15) == 0,
+              "adamw_flat_dev: buffers must be 16-byte aligned");
+  DMC_REQUIRE(hyper != nullptr, "adamw_flat_dev: hyper must point to 9 device floats");
+  AdamWArgs a{p, g, m, v, ema, coef, n, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, hyper};
+  adamw_flat_kernel<<<grid_for(n / 4 + 1, 256, 4096), 256, 0, dmc::as_stream(stream)>>>(a);
+  return dmc::check_launch("dmc_adamw_flat_dev");
 }

@@ -126,8 +126,11 @@ struct GnBwd {
   int HW, G, splits;
   const float* mr; const float* gamma; const float* beta;
   uint32_t dseed, dthresh; float dscale;
+  const uint32_t* dseed_base;   // device word added to dseed when not NULL
   int silu;
 };
+
+DMC_DEV uint32_t drop_seed(uint32_t seed, const uint32_t* base) { return seed + (base ? *base : 0u); }
 
 // dz for one element (recomputes the forward)
 DMC_DEV float gn_dz(float x, float gv, float mean, float rstd, float gm, float bt, float& xhat, int silu) {
@@ -142,6 +145,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void gn_bwd_partial(GnBwd b, float* partial /*[n][split][C][2]*/) {
   constexpr int EPC = TT<T>::KPL;
   const int n = blockIdx.x, sp = blockIdx.y;
+  const uint32_t dseed = drop_seed(b.dseed, b.dseed_base);
   const int C = b.s.C1 + b.s.C2, cpg = C / b.G;
   const int CPR = C / EPC, rpi = 256 / CPR;
   const int tid = threadIdx.x, col = tid % CPR, r0 = tid / CPR;
@@ -184,7 +188,7 @@ __global__ __launch_bounds__(256) void gn_bwd_partial(GnBwd b, float* partial /*
 #pragma unroll
       for (int e = 0; e < EPC; ++e) {
         float g = gv[e];
-        if (b.dthresh) g = drop_keep((uint64_t)pix * C + c0 + e, b.dseed, b.dthresh) ? g * b.dscale : 0.f;
+        if (b.dthresh) g = drop_keep((uint64_t)pix * C + c0 + e, dseed, b.dthresh) ? g * b.dscale : 0.f;
         float xh;
         const float dz = gn_dz(x[e], g, mean[e], rstd[e], gm[e], bt[e], xh, b.silu);
         a1[e] += dz;
@@ -311,8 +315,9 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float* in, int R, in
 // registers) and walks pixels of one sample, so each wave streams whole contiguous rows.
 template <typename T>
 __global__ __launch_bounds__(256) void gn_apply_kernel(Src2 s, int HW, const float* scale, const float* shift,
-                                                       int silu, uint32_t seed, uint32_t thresh, float dscale, char* out,
-                                                       int ldo, int splits) {
+                                                       int silu, uint32_t seed0, const uint32_t* seed_base,
+                                                       uint32_t thresh, float dscale, char* out, int ldo, int splits) {
+  const uint32_t seed = drop_seed(seed0, seed_base);
   constexpr int EPC = TT<T>::KPL;
   const int C = s.C1 + s.C2, CPR = C / EPC;
   const int rpi = 256 / CPR;
@@ -377,6 +382,7 @@ __global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* cf, ch
   const int tid = threadIdx.x, col = tid % CPR, r0 = tid / CPR;
   const bool active = r0 < rpi;
   const int n = blockIdx.x, sp = blockIdx.y;
+  const uint32_t dseed = drop_seed(b.dseed, b.dseed_base);
   const int per = (b.HW + gridDim.y - 1) / gridDim.y;
   const int pb = sp * per, pe = min(b.HW, pb + per);
   const int c0 = col * EPC;
@@ -419,7 +425,7 @@ __global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* cf, ch
 #pragma unroll
         for (int e = 0; e < EPC; ++e) {
           float gg = gv[e];
-          if (b.dthresh) gg = drop_keep((uint64_t)pix * C + c0 + e, b.dseed, b.dthresh) ? gg * b.dscale : 0.f;
+          if (b.dthresh) gg = drop_keep((uint64_t)pix * C + c0 + e, dseed, b.dthresh) ? gg * b.dscale : 0.f;
           float dz = gg;
           if (b.silu) {
             const float z = fmaf(x[e], sc[e], sh[e]);
@@ -561,7 +567,8 @@ extern "C" int dmc_gn_stats(int dtype, const void* x1, const void* x2, int N, in
 
 extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x1, const void* x2, int N, int HW, int C1,
                                int C2, int ld1, int ld2, int G, const float* mean_rstd, const float* gamma,
-                               const float* beta, int silu, uint32_t drop_seed, uint32_t drop_thresh, float drop_scale, void* dx1,
+                               const float* beta, int silu, uint32_t drop_seed, const uint32_t* drop_seed_base,
+                               uint32_t drop_thresh, float drop_scale, void* dx1,
                                void* dx2, int ld_dx1, int ld_dx2, int accumulate1, int accumulate2, float* dgamma,
                                float* dbeta, float* dx_sum_nc, int ld_sum_nc, float* dx_sum_c, void* workspace,
                                void* stream) {
@@ -577,7 +584,7 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
   b.g = (const char*)g; b.ld_g = ld_g; b.HW = HW; b.G = G;
   b.splits = host_splits(N, HW, C, epc);
   b.mr = mean_rstd; b.gamma = gamma; b.beta = beta;
-  b.dseed = drop_seed; b.dthresh = drop_thresh; b.dscale = drop_scale;
+  b.dseed = drop_seed; b.dthresh = drop_thresh; b.dscale = drop_scale; b.dseed_base = drop_seed_base;
   b.silu = silu;
   float* partial = (float*)workspace;
   float* A = partial + (size_t)N * b.splits * C * 2;
@@ -619,8 +626,9 @@ extern "C" int dmc_channel_sum(int dtype, const void* dy, int N, int HW, int C, 
 }
 
 extern "C" int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1, int ld2,
-                            const float* scale, const float* shift, int silu, uint32_t drop_seed, uint32_t drop_thresh,
-                            float drop_scale, void* out, int ld_out, void* stream) {
+                            const float* scale, const float* shift, int silu, uint32_t drop_seed,
+                            const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* out,
+                            int ld_out, void* stream) {
   const int epc = dtype == DMC_F32 ? 4 : 8;
   DMC_REQUIRE(C1 % epc == 0 && C2 % epc == 0 && ld_out % epc == 0 && (C1 + C2) / epc <= 256,
               "gn_apply: channel alignment");
@@ -632,10 +640,10 @@ extern "C" int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, in
   Src2 src{(const char*)x1, (const char*)x2, C1, C2, ld1, ld2};
   dim3 g(N, splits);
   if (dtype == DMC_F32)
-    gn_apply_kernel<float><<<g, 256, 0, s>>>(src, HW, scale, shift, silu, drop_seed, drop_thresh, drop_scale,
+    gn_apply_kernel<float><<<g, 256, 0, s>>>(src, HW, scale, shift, silu, drop_seed, drop_seed_base, drop_thresh, drop_scale,
                                              (char*)out, ld_out, splits);
   else
-    gn_apply_kernel<bf16_t><<<g, 256, 0, s>>>(src, HW, scale, shift, silu, drop_seed, drop_thresh, drop_scale,
+    gn_apply_kernel<bf16_t><<<g, 256, 0, s>>>(src, HW, scale, shift, silu, drop_seed, drop_seed_base, drop_thresh, drop_scale,
                                               (char*)out, ld_out, splits);
   return dmc::check_launch("dmc_gn_apply");
 }

@@ -28,7 +28,7 @@ class Scratch:
 
     def get(self, nbytes: int, device) -> torch.Tensor:
         nbytes = max(int(nbytes), 256)
-        key = (torch.cuda.current_stream(device).cuda_stream, str(device))
+        key = L.stream()   # stream handles are unique across devices
         buf = self.bufs.get(key)
         if buf is None or buf.numel() < nbytes:
             buf = torch.empty(int(nbytes * 1.25) + 4096, dtype=torch.uint8, device=device)
@@ -54,17 +54,22 @@ def make_desc(dtype, N, H, W, C1, C2, ld1, ld2, Kc, OH, OW, Cout, taps, mode=L.M
     return d
 
 
+def drop_args(drop):
+    """(seed, seed_base, thresh, scale) of a dropout spec (seed, thresh, scale[, seed_base]): seed_base is the
+    device address of a uint32 added to seed in the kernels (a graph-captured step reads its seed there)."""
+    if drop is None:
+        return 0, None, 0, 1.0
+    return drop[0], (drop[3] if len(drop) > 3 else None), drop[1], drop[2]
+
+
 def set_prologue(d, kind=L.PRO_NONE, scale=None, shift=None, ld=0, drop=None, drop_ld=0):
     d.prologue = kind
     d._keep_pro = (scale, shift)   # the descriptor holds raw pointers: keep the tensors alive with it
     d.pro_scale = ptr(scale)
     d.pro_shift = ptr(shift)
     d.ld_pro = ld
-    if drop is not None:
-        d.drop_seed, d.drop_thresh, d.drop_scale = drop
-        d.drop_ld = drop_ld
-    else:
-        d.drop_seed, d.drop_thresh, d.drop_scale, d.drop_ld = 0, 0, 1.0, 0
+    d.drop_seed, d.drop_seed_base, d.drop_thresh, d.drop_scale = drop_args(drop)
+    d.drop_ld = drop_ld if drop is not None else 0
 
 
 def set_epilogue(d, bias=None, addvec=None, ld_add=0, resid=None, ld_res=0, silu_pre=None, ld_silu=0,
@@ -205,9 +210,9 @@ def gn_apply(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, scale, shift, silu=True, dr
     C = C1 + C2
     if out is None:
         out = torch.empty(N * HW * C, dtype=dtype, device=x1.device)
-    seed, thresh, dscale = drop if drop is not None else (0, 0, 1.0)
+    seed, base, thresh, dscale = drop_args(drop)
     check(LIB.dmc_gn_apply(L.dtype_code(dtype), ptr(x1), ptr(x2), N, HW, C1, C2, ld1, ld2, ptr(scale), ptr(shift),
-                           int(silu), seed, thresh, dscale, ptr(out), C, L.stream()), "dmc_gn_apply")
+                           int(silu), seed, base, thresh, dscale, ptr(out), C, L.stream()), "dmc_gn_apply")
     return out
 
 
@@ -216,10 +221,11 @@ def gn_bwd(dtype, g, ld_g, x1, x2, N, HW, C1, C2, ld1, ld2, G, mr, gamma, beta, 
     """GroupNorm(+SiLU+dropout) backward; optionally also the per-(n,c) / per-c pixel sums of dx (the bias and
     time-embedding gradients of the layer that produced x), fused into the dx pass."""
     ws = SCRATCH.get(LIB.dmc_gn_workspace(N, C1 + C2, G, HW), g.device)
-    seed, thresh, scale = drop if drop is not None else (0, 0, 1.0)
+    seed, base, thresh, scale = drop_args(drop)
     check(LIB.dmc_gn_silu_bwd(L.dtype_code(dtype), ptr(g), ld_g, ptr(x1), ptr(x2), N, HW, C1, C2, ld1, ld2, G, ptr(mr),
-                              ptr(gamma), ptr(beta), int(silu), seed, thresh, scale, ptr(dx1), ptr(dx2), ld_dx1, ld_dx2,
-                              int(acc1), int(acc2), ptr(dgamma), ptr(dbeta), ptr(dx_sum_nc), ld_sum_nc, ptr(dx_sum_c),
+                              ptr(gamma), ptr(beta), int(silu), seed, base, thresh, scale, ptr(dx1), ptr(dx2), ld_dx1,
+                              ld_dx2, int(acc1), int(acc2), ptr(dgamma), ptr(dbeta), ptr(dx_sum_nc), ld_sum_nc,
+                              ptr(dx_sum_c),
                               ptr(ws), L.stream()), "dmc_gn_silu_bwd")
 
 
@@ -376,3 +382,9 @@ def grad_norm_flat(g, max_norm):
 def adamw_flat(p, g, m, v, ema, coef, wd_mul, lerp_w, beta2, omb2, eps, neg_step, bc2_sqrt, ema_decay, ema_om):
     check(LIB.dmc_adamw_flat(ptr(p), ptr(g), ptr(m), ptr(v), ptr(ema), p.numel(), ptr(coef), wd_mul, lerp_w, beta2,
                              omb2, eps, neg_step, bc2_sqrt, ema_decay, ema_om, L.stream()), "dmc_adamw_flat")
+
+
+def adamw_flat_dev(p, g, m, v, ema, coef, hyper):
+    """adamw_flat with the nine scalars (same order as adamw_flat's) read from the fp32 device tensor hyper."""
+    check(LIB.dmc_adamw_flat_dev(ptr(p), ptr(g), ptr(m), ptr(v), ptr(ema), p.numel(), ptr(coef), ptr(hyper),
+                                 L.stream()), "dmc_adamw_flat_dev")

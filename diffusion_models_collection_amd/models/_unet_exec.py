@@ -113,6 +113,7 @@ class UNetExecutor:
         self.daddvec = None
         self.training_grad_scale = 1.0
         self.grad_hook = None       # called as hook(flat_grad, lo, hi) when a range of grads is final
+        self.seed_ptr = None        # device address of the dropout seed word (graph-captured training step)
         # measured slower on MI355X (the overlapped kernels contend for LDS and CUs): opt-in only
         self.use_side = os.environ.get("DMC_SIDE_STREAM", "0") not in ("", "0")
         self.side = None
@@ -359,7 +360,11 @@ class UNetExecutor:
         if drop_on:
             p = float(m.dropout)
             self._drop = (min(int(round(p * 4294967296.0)), 4294967295), 1.0 / (1.0 - p) if p < 1 else 0.0)
-            self._seed_base = _seed_from_torch()
+            if self.seed_ptr is not None:
+                # graph capture: the kernels add the step's seed from device memory (set per replay)
+                self._seed_base = 0
+            else:
+                self._seed_base = _seed_from_torch()
         else:
             self._drop = None
         self._blk_idx = 0
@@ -472,6 +477,8 @@ class UNetExecutor:
         drop = None
         if self._drop is not None:
             drop = ((self._seed_base + 7919 * self._blk_idx) & 0xFFFFFFFF, self._drop[0], self._drop[1])
+            if self.seed_ptr is not None:
+                drop = drop + (self.seed_ptr,)
         self._blk_idx += 1
         a2 = self._apply([h1], st2, silu=True, drop=drop)
         out = self._new(N, H, W, Cout)

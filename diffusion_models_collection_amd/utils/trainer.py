@@ -183,20 +183,148 @@ class FlatAdamW:
             self._bound = False
             return None
         total, coef = K.grad_norm_flat(g, max_norm if max_norm is not None else -1.0)
+        sc = self.scalars(ema_decay)
+        K.adamw_flat(self.flat_p, g, self.flat_m, self.flat_v, self.flat_e if self.uses_ema(ema_decay) else None,
+                     coef, *sc)
+        self.bump(ema_decay)
+        return total
+
+    def uses_ema(self, ema_decay):
+        return self.flat_e is not None and ema_decay is not None
+
+    def scalars(self, ema_decay):
+        """Advance the step count; the nine dmc_adamw_flat scalars of this step, in double like torch:
+        (1-lr*wd, 1-beta1, beta2, 1-beta2, eps, -lr/(1-beta1^t), sqrt(1-beta2^t), ema decay, 1-ema decay)."""
         grp = self.opt.param_groups[0]
         lr, (b1, b2), eps, wd = float(grp["lr"]), grp["betas"], grp["eps"], grp["weight_decay"]
         self.t += 1
         self.step_t.fill_(float(self.t))
         bc1 = 1 - b1 ** self.t
         bc2 = 1 - b2 ** self.t
-        use_ema = self.flat_e is not None and ema_decay is not None
-        K.adamw_flat(self.flat_p, g, self.flat_m, self.flat_v, self.flat_e if use_ema else None, coef,
-                     1 - lr * wd, 1 - b1, b2, 1 - b2, eps, (lr / bc1) * -1, bc2 ** 0.5,
-                     ema_decay if use_ema else 1.0, (1 - ema_decay) if use_ema else 0.0)
+        use_ema = self.uses_ema(ema_decay)
+        return (1 - lr * wd, 1 - b1, b2, 1 - b2, eps, (lr / bc1) * -1, bc2 ** 0.5,
+                ema_decay if use_ema else 1.0, (1 - ema_decay) if use_ema else 0.0)
+
+    def bump(self, ema_decay):
+        """The parameters (and EMA) changed: the executors repack their weights on the next forward."""
         self.ex.wgen += 1
-        if use_ema:
+        if self.uses_ema(ema_decay):
             self.ema.executor.wgen += 1
-        return total
+
+
+class GraphedTrainStep:
+    """The training step captured once as a HIP graph and replayed (single process, fused optimizer path).
+
+    An eager step is ~950 kernel launches whose Python/ctypes enqueue costs about as much host time as the
+    GPU needs to run them (bench.py host_enqueue_ms_per_step); a replay is one graph launch. Everything
+    that differs per step stays outside the graph, with the eager step's RNG calls in the eager order: the
+    batch and labels are copied into static buffers, t (torch.randint) and the noise (torch.randn_like) are
+    drawn eagerly into static buffers, and the dropout seed (torch's CPU generator, as the eager forward
+    draws it) and the nine AdamW/EMA scalars go to device memory with one pinned H2D copy per step; the
+    captured kernels read them there (drop_seed_base, dmc_adamw_flat_dev). Replays are therefore bitwise
+    identical to eager steps (tests/test_gpu_model.py). Captured after WARM eager steps, once per batch
+    shape; a step with another shape, or any capture failure, runs eagerly.
+    """
+    WARM = 2
+    RING = 4
+
+    def __init__(self, trainer):
+        self.tr = trainer
+        self.calls = 0
+        self.graph = None
+        self.failed = False
+        self.key = None
+
+    @staticmethod
+    def supported(trainer):
+        import os
+        return (os.environ.get("DMC_GRAPH", "1") != "0" and not trainer.is_distributed
+                and trainer._flat is not None and trainer.gradient_accumulation_steps == 1
+                and _is_dmc_unet(trainer._raw_model))
+
+    def _key(self, images, y):
+        return (tuple(images.shape), images.device, None if y is None else tuple(y.shape))
+
+    def _capture(self, images, y):
+        tr = self.tr
+        f = tr._flat
+        dev = images.device
+        ex = tr._raw_model.executor
+        self.x_s = torch.empty_like(images)
+        self.n_s = torch.empty_like(images)
+        self.t_s = torch.empty(images.shape[0], dtype=torch.long, device=dev)
+        self.y_s = None if y is None else torch.empty_like(y)
+        self.h_dev = torch.zeros(16, dtype=torch.float32, device=dev)   # [0..8] AdamW scalars, [9] seed
+        self.ring = [torch.zeros(16, dtype=torch.float32).pin_memory() for _ in range(self.RING)]
+        self.ring_ev = [None] * self.RING
+        self.slot = 0
+        self.use_ema = f.uses_ema(tr.ema_decay if tr.use_ema else None)
+        drop_on = tr._raw_model.training and tr._raw_model.dropout > 0
+        self.drop_on = drop_on
+        ex.wgen += 1                      # the captured forward must contain the weight-pack launch
+        g = torch.cuda.CUDAGraph()
+        ex.seed_ptr = self.h_dev.data_ptr() + 9 * 4
+        try:
+            with torch.cuda.graph(g):
+                loss = tr.diffusion.p_losses(tr.model, self.x_s, self.t_s, self.y_s, noise=self.n_s,
+                                             loss_type=tr.loss_type)
+                loss.backward()
+                grad = f.grads_flat()
+                if grad is None:
+                    raise RuntimeError("gradients are not in the executor's flat buffer")
+                _, coef = K.grad_norm_flat(grad, 1.0)
+                K.adamw_flat_dev(f.flat_p, grad, f.flat_m, f.flat_v, f.flat_e if self.use_ema else None, coef,
+                                 self.h_dev)
+        finally:
+            ex.seed_ptr = None
+        tr.optimizer.zero_grad()
+        self.graph, self.loss_s = g, loss.detach()
+
+    def step(self, images, t, y):
+        """One training step; returns the loss, or None when this step must run eagerly."""
+        self.calls += 1
+        if self.failed or self.calls <= self.WARM:
+            return None
+        tr = self.tr
+        f = tr._flat
+        if not f._bound or not f._valid():
+            return None
+        key = self._key(images, y)
+        if self.graph is None or key != self.key:
+            if self.graph is not None:
+                return None           # one captured shape (the last, ragged batch of an epoch runs eagerly)
+            try:
+                self._capture(images, y)
+                self.key = key
+            except Exception as e:    # noqa: BLE001 -- any capture problem: stay eager
+                self.failed = True
+                self.graph = None
+                if tr.is_main_process:
+                    print(f"[dmc] training-step graph capture failed, running eagerly: {e}")
+                return None
+        from ..models._unet_exec import _seed_from_torch
+        self.x_s.copy_(images)
+        self.t_s.copy_(t)
+        self.n_s.copy_(torch.randn_like(images))       # p_losses' draw, same generator and order
+        if y is not None:
+            self.y_s.copy_(y)
+        ema_decay = tr.ema_decay if tr.use_ema else None
+        h = torch.zeros(16, dtype=torch.float32)
+        h[:9] = torch.tensor(f.scalars(ema_decay), dtype=torch.float32)
+        if self.drop_on:
+            h.view(torch.int32)[9] = _seed_from_torch()
+        k = self.slot % self.RING
+        self.slot += 1
+        if self.ring_ev[k] is not None:
+            self.ring_ev[k].synchronize()      # the pinned slot's previous copy has been consumed
+        self.ring[k].copy_(h)
+        self.h_dev.copy_(self.ring[k], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.ring_ev[k] = ev
+        self.graph.replay()
+        f.bump(ema_decay)
+        return self.loss_s.clone()
 
 
 class DiffusionTrainer:
@@ -265,6 +393,7 @@ class DiffusionTrainer:
         if _is_dmc_unet(self._module) and FlatAdamW.supported(self._module, optimizer) and (
                 self.ema_model is None or _is_dmc_unet(self.ema_model)):
             self._flat = FlatAdamW(self._module, optimizer, self.ema_model)
+        self._graph = GraphedTrainStep(self) if GraphedTrainStep.supported(self) else None
 
         self.best_loss = float('inf')
         self.start_epoch = 1
@@ -354,6 +483,10 @@ class DiffusionTrainer:
         images = images.to(self.device, non_blocking=True)
         batch_size = images.shape[0]
         t = torch.randint(0, self.diffusion.num_timesteps, (batch_size,), device=self.device).long()
+        if self._graph is not None and self._module.training:
+            loss = self._graph.step(images, t, labels_for_loss)
+            if loss is not None:
+                return loss
         loss = self.diffusion.p_losses(self.model, images, t, labels_for_loss, loss_type=self.loss_type)
         loss = loss / self.gradient_accumulation_steps
         loss.backward()

@@ -55,6 +55,7 @@ typedef struct dmc_conv_desc {
   uint32_t drop_thresh;      /* 0 = no dropout */
   float drop_scale;          /* 1/(1-p) */
   int drop_ld;               /* channel count used in the dropout element index */
+  const uint32_t* drop_seed_base; /* device word added to drop_seed when not NULL (seed varies per graph replay) */
   const float* bias;         /* [Cout] or NULL */
   const float* addvec;       /* [N][ld_add] added per (n, co) (time/label embedding) or NULL */
   int ld_add;
@@ -113,7 +114,8 @@ int dmc_gn_stats(int dtype, const void* x1, const void* x2, int N, int HW, int C
  * (dtype, [pix][ld_out]); dropout keeps element (pix, c) iff hash(seed, pix*C + c) >= drop_thresh. */
 int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1,
                  int ld2, const float* scale, const float* shift, int silu, uint32_t drop_seed,
-                 uint32_t drop_thresh, float drop_scale, void* out, int ld_out, void* stream);
+                 const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* out, int ld_out,
+                 void* stream);
 
 /* Backward of a = dropout(SiLU(GroupNorm(x))) (silu=1) or a = GroupNorm(x) (silu=0, AttentionBlock
  * norm :80): g = dL/da (dtype, [pix][ld_g]); writes
@@ -124,7 +126,8 @@ int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C
 int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x1, const void* x2, int N,
                     int HW, int C1, int C2, int ld1, int ld2, int G, const float* mean_rstd,
                     const float* gamma, const float* beta, int silu, uint32_t drop_seed,
-                    uint32_t drop_thresh, float drop_scale, void* dx1, void* dx2, int ld_dx1,
+                    const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* dx1, void* dx2,
+                    int ld_dx1,
                     int ld_dx2, int accumulate1, int accumulate2, float* dgamma, float* dbeta,
                     float* dx_sum_nc, int ld_sum_nc, float* dx_sum_c, void* workspace, void* stream);
 
@@ -215,6 +218,12 @@ int dmc_grad_norm_flat(const float* g, long n, float max_norm, float* total_norm
 int dmc_adamw_flat(float* p, const float* g, float* m, float* v, float* ema, long n, const float* coef,
                    float wd_mul, float lerp_w, float beta2, float one_minus_beta2, float eps,
                    float neg_step_size, float bc2_sqrt, float ema_decay, float ema_one_minus, void* stream);
+
+/* dmc_adamw_flat with the nine step scalars read from device memory (hyper[0..8] = wd_mul, lerp_w, beta2,
+ * one_minus_beta2, eps, neg_step_size, bc2_sqrt, ema_decay, ema_one_minus), so a captured HIP graph of
+ * the training step replays with the current learning rate and bias corrections (one H2D copy per step). */
+int dmc_adamw_flat_dev(float* p, const float* g, float* m, float* v, float* ema, long n, const float* coef,
+                       const float* hyper, void* stream);
 /* y = silu(x) (fp32); NHWC dtype -> NCHW fp32 (the inverse of dmc_pack_input); y += x (dtype). */
 int dmc_silu_fwd(const float* x, float* y, long n, void* stream);
 int dmc_unpack_output(int dtype, const void* src, int ld, int N, int C, int H, int W, float* dst,

@@ -316,3 +316,48 @@ def test_flat_adamw_trainer_matches_torch_optimizer_path(tmp_path):
             if step == 0:
                 torch.testing.assert_close(sa["exp_avg"], sb["exp_avg"], rtol=1e-4, atol=1e-7)
                 torch.testing.assert_close(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=1e-4, atol=1e-10)
+
+
+@pytest.mark.parametrize("conditional", [False, True])
+def test_graphed_train_step_matches_eager(conditional, monkeypatch):
+    """The HIP-graph training step (utils/trainer.py GraphedTrainStep: 2 eager warmup steps, capture, replays)
+    computes bitwise what the eager step computes: same losses, parameters and EMA over 6 steps, bf16, dropout
+    and classifier-free label dropout on. Per-step inputs (t, noise, dropout seed, AdamW scalars) come from
+    the same generators in the same order in both modes."""
+    from diffusion_models_collection_amd.models import UNet
+    from diffusion_models_collection_amd.diffusion import DDPM
+    from diffusion_models_collection_amd.utils.trainer import DiffusionTrainer
+    mp = dict(image_size=(16, 16), in_channels=3, model_channels=32, out_channels=3, num_res_blocks=1,
+              attention_resolutions=(8,), dropout=0.1, channel_mult=(1, 2), use_attention=True)
+    ncls = 10 if conditional else None
+
+    def run(graph):
+        monkeypatch.setenv("DMC_GRAPH", "1" if graph else "0")
+        torch.manual_seed(0)
+        torch.cuda.manual_seed(0)
+        m = UNet(**mp, num_classes=ncls, compute_dtype="bf16").to(DEV)
+        opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4)
+        cfg = {"epochs": 1, "save_dir": "/tmp/dmc_graph_ckpt", "sample_dir": "/tmp/dmc_graph_smp", "loss_type": "l2",
+               "use_ema": True, "ema_decay": 0.99, "conditional": conditional, "num_classes": ncls,
+               "cfg_dropout_prob": 0.2, "model_type": "unet", "model_params": dict(mp)}
+        tr = DiffusionTrainer(m, DDPM(device=DEV), None, opt, None, device=DEV, config=cfg)
+        assert (tr._graph is not None) == graph
+        m.train()
+        gen = torch.Generator().manual_seed(5)
+        losses = []
+        for i in range(6):
+            x = (torch.rand(8, 3, 16, 16, generator=gen) * 2 - 1).to(DEV)
+            batch = (x, torch.randint(0, 10, (8,), generator=gen).to(DEV)) if conditional else x
+            losses.append(tr.train_step(batch, i).detach().float().cpu().reshape(()))
+        torch.cuda.synchronize()
+        sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+        ema = {k: v.detach().cpu().clone() for k, v in tr.ema_model.state_dict().items()}
+        return torch.stack(losses), sd, ema, tr
+
+    le, se, ee, _ = run(False)
+    lg, sg, eg, trg = run(True)
+    assert trg._graph.graph is not None and not trg._graph.failed
+    assert torch.equal(le, lg), (le, lg)
+    for k in se:
+        assert torch.equal(se[k], sg[k]), k
+        assert torch.equal(ee[k], eg[k]), k
