@@ -296,11 +296,12 @@ class GraphedTrainStep:
             try:
                 self._capture(images, y)
                 self.key = key
-            except Exception as e:    # noqa: BLE001 -- any capture problem: stay eager
+            except Exception:    # noqa: BLE001 -- any capture problem: stay eager
+                import traceback
                 self.failed = True
                 self.graph = None
                 if tr.is_main_process:
-                    print(f"[dmc] training-step graph capture failed, running eagerly: {e}")
+                    print("[dmc] training-step graph capture failed, running eagerly:\n" + traceback.format_exc())
                 return None
         from ..models._unet_exec import _seed_from_torch
         self.x_s.copy_(images)

@@ -198,8 +198,11 @@ def test_diffusion_ops_match_reference():
         assert rel(got, g["ddim_eta_sample"]) < TRAJ
 
 
-def test_trainer_trajectory_matches_reference(tmp_path):
-    """5 DiffusionTrainer steps (clip, AdamW, EMA) with injected t/noise vs the reference's own run."""
+def test_trainer_trajectory_matches_reference(tmp_path, monkeypatch):
+    """5 DiffusionTrainer steps (clip, AdamW, EMA) with injected t/noise vs the reference's own run. The
+    injection patches p_losses / torch.randint per call, so the step runs eagerly (DMC_GRAPH=0); the graphed
+    step is held to the eager one by test_graphed_train_step_matches_eager."""
+    monkeypatch.setenv("DMC_GRAPH", "0")
     from diffusion_models_collection_amd.models import UNet
     from diffusion_models_collection_amd.diffusion import DDPM
     from diffusion_models_collection_amd.utils.trainer import DiffusionTrainer
@@ -264,7 +267,7 @@ def test_bf16_training_step_finite_and_dropout_deterministic():
     assert res[0][0] == res[1][0] and torch.equal(res[0][1], res[1][1])
 
 
-def test_flat_adamw_trainer_matches_torch_optimizer_path(tmp_path):
+def test_flat_adamw_trainer_matches_torch_optimizer_path(tmp_path, monkeypatch):
     """The trainer's fused flat step (clip + AdamW + EMA in one kernel, packs refreshed in one launch) gives
     the same parameters, optimizer state and EMA as the reference path (clip_grad_norm_, AdamW.step,
     per-tensor EMA), and survives an optimizer/model state_dict round trip (re-bind).
@@ -273,6 +276,7 @@ def test_flat_adamw_trainer_matches_torch_optimizer_path(tmp_path):
     rounding (1e-3 lr); later steps see gradients of slightly different weights, and Adam turns rounding-
     level differences of near-zero gradients into up to lr-sized moves, so those are bounded by 0.25 lr
     (as in test_trainer_trajectory_matches_reference)."""
+    monkeypatch.setenv("DMC_GRAPH", "0")   # the eager fused optimizer step is the subject here
     from diffusion_models_collection_amd.models import UNet
     from diffusion_models_collection_amd.diffusion import DDPM
     from diffusion_models_collection_amd.utils.trainer import DiffusionTrainer
