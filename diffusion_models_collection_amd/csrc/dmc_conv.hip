@@ -309,6 +309,41 @@ DMC_DEV void conv_store_tile(const ConvK& a, const v4f accv, const int pix, cons
   }
 }
 
+// bf16 form of tile_epilogue with 8 channels (one 16-byte store) per thread and row
+template <int BM, int BN, int NT>
+DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int n0) {
+  constexpr int CG = BN / 8, RS = NT / CG;
+  const int cg = threadIdx.x % CG, r0 = threadIdx.x / CG;
+  const int co = n0 + cg * 8;
+  if (co >= a.Cout) return;
+  v4f b0 = {0.f, 0.f, 0.f, 0.f}, b1 = {0.f, 0.f, 0.f, 0.f};
+  if (a.bias) { b0 = *(const v4f*)(a.bias + co); b1 = *(const v4f*)(a.bias + co + 4); }
+  const bool first = co < a.Csplit;
+  char* const y = first ? a.y1 : a.y2;
+  const int ldy = first ? a.ldy1 : a.ldy2, cy = first ? co : co - a.Csplit;
+  int n = (m0 + r0) / a.OHW, nend = (n + 1) * a.OHW;
+  for (int pl = r0; pl < BM; pl += RS) {
+    const int pix = m0 + pl;
+    if (pix >= a.M) break;
+    v4f v0 = *(const v4f*)(lds + pl * EP + cg * 32) + b0;
+    v4f v1 = *(const v4f*)(lds + pl * EP + cg * 32 + 16) + b1;
+    if (a.addvec) {
+      while (pix >= nend) { ++n; nend += a.OHW; }
+      const float* av = a.addvec + (size_t)n * a.ld_add + co;
+      v0 += *(const v4f*)av;
+      v1 += *(const v4f*)(av + 4);
+    }
+    float f[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    if (a.resid) {
+      float r[8];
+      Chunk<bf16_t>::unpack(*(const v4i*)(a.resid + ((size_t)pix * a.ld_res + co) * 2), r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] += r[e];
+    }
+    *(v4i*)(y + ((size_t)pix * ldy + cy) * 2) = Chunk<bf16_t>::pack(f);
+  }
+}
+
 // Epilogue of the LDS-staged kernels: the block's BM x BN fp32 tile (LDS rows of EP bytes) through the conv
 // epilogue. A thread keeps ONE 4-channel group (NT is a multiple of BN/4) and walks every (NT*4/BN)-th
 // pixel row, so the bias load, the output select and the channel addressing are hoisted out of the loop
@@ -322,6 +357,10 @@ DMC_DEV void tile_epilogue(const ConvK& a, const char* lds, int EP, int m0, int 
   const int co = n0 + cg * 4;
   if (a.out_nchw || a.silu_pre || (a.Cout & 3)) {
     for (int pl = r0; pl < BM; pl += RS) conv_store_tile<T>(a, *(const v4f*)(lds + pl * EP + cg * 16), m0 + pl, co);
+    return;
+  }
+  if (sizeof(T) == 2 && !a.out_f32 && !((a.Cout | a.Csplit | a.ldy1 | a.ldy2 | a.ld_res) & 7)) {
+    tile_epilogue8<BM, BN, NT>(a, lds, EP, m0, n0);   // 16-byte stores: half the store instructions
     return;
   }
   if (co >= a.Cout) return;

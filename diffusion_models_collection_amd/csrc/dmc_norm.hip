@@ -374,16 +374,61 @@ DMC_DEV void load_coef(const float* p, float* v) {
   }
 }
 
+// Column sums of a row-major fp32 matrix by one 256-thread block, 64 columns from c0 (4 row slices, 8 rows
+// in flight each, slices added in fixed order): out0[c] = scale * sum_r in[r*ld + c*stride], out1 likewise at +1
+// (out1 may be NULL). The block form of colsum_kernel, for kernels that take the reduction into spare blocks.
+DMC_DEV void colsum_block(const float* in, int R, int C, long ld, int stride, int c0, float* out0, float* out1,
+                          float scale) {
+  __shared__ float red[2][4][64];
+  const int lane = threadIdx.x & 63, slice = threadIdx.x >> 6;
+  const int c = c0 + lane;
+  const bool two = out1 != nullptr;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < C) {
+    const float* p = in + (size_t)c * stride;
+    int r = slice;
+    for (; r + 4 * 7 < R; r += 32) {
+      float a0[8], a1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a0[u] = p[(size_t)(r + 4 * u) * ld];
+      if (two) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a1[u] = p[(size_t)(r + 4 * u) * ld + 1];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { s0 += a0[u]; s1 += a1[u]; }
+    }
+    for (; r < R; r += 4) {
+      s0 += p[(size_t)r * ld];
+      if (two) s1 += p[(size_t)r * ld + 1];
+    }
+  }
+  red[0][slice][lane] = s0;
+  red[1][slice][lane] = s1;
+  __syncthreads();
+  if (slice == 0 && c < C) {
+    out0[c] = scale * (((red[0][0][lane] + red[0][1][lane]) + red[0][2][lane]) + red[0][3][lane]);
+    if (two) out1[c] = scale * (((red[1][0][lane] + red[1][1][lane]) + red[1][2][lane]) + red[1][3][lane]);
+  }
+}
+
+// grid (N, splits + 1): rows 0..splits-1 write dx; in the last row, block x < ceil(C/64) reduces 64 columns of A
+// into dbeta/dgamma (A is complete: gn_bwd_final ran before this launch).
 template <typename T>
 __global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* cf, char* dx1, char* dx2, int ld1,
-                                                    int ld2, int acc1, int acc2, float* sum_part) {
+                                                    int ld2, int acc1, int acc2, float* sum_part, const float* A,
+                                                    float* dbeta, float* dgamma) {
   constexpr int EPC = TT<T>::KPL;
   const int C = b.s.C1 + b.s.C2, CPR = C / EPC, rpi = 256 / CPR;
+  if ((int)blockIdx.y == b.splits) {
+    if ((int)blockIdx.x * 64 < C) colsum_block(A, gridDim.x, C, (long)C * 2, 2, blockIdx.x * 64, dbeta, dgamma, 1.f);
+    return;
+  }
   const int tid = threadIdx.x, col = tid % CPR, r0 = tid / CPR;
   const bool active = r0 < rpi;
   const int n = blockIdx.x, sp = blockIdx.y;
   const uint32_t dseed = drop_seed(b.dseed, b.dseed_base);
-  const int per = (b.HW + gridDim.y - 1) / gridDim.y;
+  const int per = (b.HW + b.splits - 1) / b.splits;
   const int pb = sp * per, pe = min(b.HW, pb + per);
   const int c0 = col * EPC;
   const bool first = c0 < b.s.C1;
@@ -459,7 +504,7 @@ __global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* cf, ch
   for (int c = tid; c < C; c += 256) {
     float v = 0.f;
     for (int r = 0; r < rpi; ++r) v += red[r * CPR + c / EPC][c % EPC];
-    sum_part[((size_t)n * gridDim.y + sp) * C + c] = v;
+    sum_part[((size_t)n * b.splits + sp) * C + c] = v;
   }
 }
 
@@ -501,12 +546,17 @@ __global__ __launch_bounds__(256) void chsum_partial(const char* dy, int HW, int
   }
 }
 
-// out_nc[n][c] = scale * sum_split partial[n][split][c]   (one thread per (n, c))
-__global__ void chsum_nc(int N, int C, int splits, const float* partial, float* out_nc, int ld_out, float scale) {
+// both reductions of chsum_finish in one launch: blocks [0, nb_nc) sum the splits per (n, c), the next
+// ceil(C/64) blocks the column sums
+__global__ __launch_bounds__(256) void chsum_finish_kernel(int N, int C, int splits, const float* partial, float* out_nc,
+                                                          int ld_out, float* out_c, float scale, int nb_nc) {
+  if ((int)blockIdx.x >= nb_nc) {
+    colsum_block(partial, N * splits, C, C, 1, (blockIdx.x - nb_nc) * 64, out_c, nullptr, scale);
+    return;
+  }
   const long total = (long)N * C;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = i % C;
-    const int n = i / C;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)nb_nc * 256) {
+    const int c = i % C, n = i / C;
     float v = 0.f;
     for (int sp = 0; sp < splits; ++sp) v += partial[((size_t)n * splits + sp) * C + c];
     out_nc[(size_t)n * ld_out + c] = v * scale;
@@ -516,12 +566,11 @@ __global__ void chsum_nc(int N, int C, int splits, const float* partial, float* 
 // out_nc (may be NULL) and out_c = column sums over all n and splits (may be NULL) of partial [N][splits][C]
 void chsum_finish(hipStream_t s, int N, int C, int splits, const float* partial, float* out_nc, int ld_out,
                   float* out_c, float scale) {
-  if (out_nc) {
-    const long tot = (long)N * C;
-    chsum_nc<<<(int)((tot + 255) / 256 < 4096 ? (tot + 255) / 256 : 4096), 256, 0, s>>>(N, C, splits, partial, out_nc,
-                                                                                          ld_out, scale);
-  }
-  if (out_c) colsum_kernel<<<(C + 63) / 64, 1024, 0, s>>>(partial, N * splits, C, C, 1, out_c, nullptr, scale);
+  const long tot = (long)N * C;
+  const int nb_nc = out_nc ? (int)((tot + 255) / 256 < 4096 ? (tot + 255) / 256 : 4096) : 0;
+  const int nb_c = out_c ? (C + 63) / 64 : 0;
+  if (nb_nc + nb_c == 0) return;
+  chsum_finish_kernel<<<nb_nc + nb_c, 256, 0, s>>>(N, C, splits, partial, out_nc, ld_out, out_c, scale, nb_nc);
 }
 
 int host_splits(int N, int HW, int C, int epc) {
@@ -595,14 +644,16 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
   if (dtype == DMC_F32) gn_bwd_partial<float><<<gr, 256, 0, s>>>(b, partial);
   else gn_bwd_partial<bf16_t><<<gr, 256, 0, s>>>(b, partial);
   gn_bwd_final<<<N, 256, 0, s>>>(C, G, HW, b.splits, partial, mean_rstd, gamma, beta, A, cf);
-  // dbeta[c] = sum_n A[n][c][0], dgamma[c] = sum_n A[n][c][1]
-  colsum_kernel<<<(C + 63) / 64, 1024, 0, s>>>(A, N, C, (long)C * 2, 2, dbeta, dgamma, 1.0f);
+  // dx, plus dbeta[c] = sum_n A[n][c][0], dgamma[c] = sum_n A[n][c][1] in the grid's extra row (needs N >= C/64)
+  const bool fused_cs = N * 64 >= C;
+  const dim3 ga(N, b.splits + (fused_cs ? 1 : 0));
+  if (!fused_cs) colsum_kernel<<<(C + 63) / 64, 1024, 0, s>>>(A, N, C, (long)C * 2, 2, dbeta, dgamma, 1.0f);
   if (dtype == DMC_F32)
-    gn_bwd_apply<float><<<gr, 256, 0, s>>>(b, cf, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, accumulate1, accumulate2,
-                                           want_sums ? sums : nullptr);
+    gn_bwd_apply<float><<<ga, 256, 0, s>>>(b, cf, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, accumulate1, accumulate2,
+                                           want_sums ? sums : nullptr, A, dbeta, dgamma);
   else
-    gn_bwd_apply<bf16_t><<<gr, 256, 0, s>>>(b, cf, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, accumulate1, accumulate2,
-                                            want_sums ? sums : nullptr);
+    gn_bwd_apply<bf16_t><<<ga, 256, 0, s>>>(b, cf, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, accumulate1, accumulate2,
+                                            want_sums ? sums : nullptr, A, dbeta, dgamma);
   if (want_sums) chsum_finish(s, N, C, b.splits, sums, dx_sum_nc, ld_sum_nc, dx_sum_c, 1.0f);
   return dmc::check_launch("dmc_gn_silu_bwd");
 }
