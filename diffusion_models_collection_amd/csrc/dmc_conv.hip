@@ -309,10 +309,13 @@ DMC_DEV void conv_store_tile(const ConvK& a, const v4f accv, const int pix, cons
   }
 }
 
-// bf16 form of tile_epilogue with 8 channels (one 16-byte store) per thread and row
+// bf16 form of tile_epilogue with 8 channels (one 16-byte store) per thread and row. The rows are unrolled with
+// every residual load issued up front, and the embedding row is reloaded only when the image changes, so the
+// store phase pays one global round trip instead of one per row (it runs with no other block on the CU to
+// hide it).
 template <int BM, int BN, int NT>
 DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int n0) {
-  constexpr int CG = BN / 8, RS = NT / CG;
+  constexpr int CG = BN / 8, RS = NT / CG, IT = BM / RS;
   const int cg = threadIdx.x % CG, r0 = threadIdx.x / CG;
   const int co = n0 + cg * 8;
   if (co >= a.Cout) return;
@@ -321,26 +324,42 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
   const bool first = co < a.Csplit;
   char* const y = first ? a.y1 : a.y2;
   const int ldy = first ? a.ldy1 : a.ldy2, cy = first ? co : co - a.Csplit;
-  int n = (m0 + r0) / a.OHW, nend = (n + 1) * a.OHW;
-  for (int pl = r0; pl < BM; pl += RS) {
-    const int pix = m0 + pl;
-    if (pix >= a.M) break;
-    v4f v0 = *(const v4f*)(lds + pl * EP + cg * 32) + b0;
-    v4f v1 = *(const v4f*)(lds + pl * EP + cg * 32 + 16) + b1;
-    if (a.addvec) {
-      while (pix >= nend) { ++n; nend += a.OHW; }
-      const float* av = a.addvec + (size_t)n * a.ld_add + co;
-      v0 += *(const v4f*)av;
-      v1 += *(const v4f*)(av + 4);
-    }
-    float f[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-    if (a.resid) {
-      float r[8];
-      Chunk<bf16_t>::unpack(*(const v4i*)(a.resid + ((size_t)pix * a.ld_res + co) * 2), r);
+  v4i rr[IT];
+  if (a.resid) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] += r[e];
+    for (int k = 0; k < IT; ++k) {
+      const int pix = min(m0 + r0 + k * RS, a.M - 1);
+      rr[k] = *(const v4i*)(a.resid + ((size_t)pix * a.ld_res + co) * 2);
     }
-    *(v4i*)(y + ((size_t)pix * ldy + cy) * 2) = Chunk<bf16_t>::pack(f);
+  }
+  int n = (m0 + r0) / a.OHW, nend = (n + 1) * a.OHW;
+  v4f e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
+  if (a.addvec) {
+    e0 = *(const v4f*)(a.addvec + (size_t)n * a.ld_add + co);
+    e1 = *(const v4f*)(a.addvec + (size_t)n * a.ld_add + co + 4);
+  }
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const int pl = r0 + k * RS;
+    const int pix = m0 + pl;
+    if (pix < a.M) {
+      if (a.addvec && pix >= nend) {
+        n = pix / a.OHW;
+        nend = (n + 1) * a.OHW;
+        e0 = *(const v4f*)(a.addvec + (size_t)n * a.ld_add + co);
+        e1 = *(const v4f*)(a.addvec + (size_t)n * a.ld_add + co + 4);
+      }
+      const v4f v0 = *(const v4f*)(lds + pl * EP + cg * 32) + b0 + e0;
+      const v4f v1 = *(const v4f*)(lds + pl * EP + cg * 32 + 16) + b1 + e1;
+      float f[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      if (a.resid) {
+        float r[8];
+        Chunk<bf16_t>::unpack(rr[k], r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += r[e];
+      }
+      *(v4i*)(y + ((size_t)pix * ldy + cy) * 2) = Chunk<bf16_t>::pack(f);
+    }
   }
 }
 

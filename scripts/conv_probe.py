@@ -28,7 +28,7 @@ SHAPES = {
 }
 
 
-def run(name, iters):
+def run(name, iters, epi="bias"):
     B, H, W, C1, C2, Cout, kind = SHAPES[name]
     dt = torch.bfloat16
     dev = "cuda"
@@ -41,7 +41,12 @@ def run(name, iters):
     wp = K.pack_weight(L.PACK_FWD, dt, w, Kc)
     y = torch.empty(B, H, W, Cout, device=dev, dtype=dt)
     d = K.make_desc(dt, B, H, W, C1, C2, C1, C2, Kc, H, W, Cout, taps)
-    K.set_epilogue(d, bias=torch.randn(Cout, device=dev), ldy1=Cout)
+    if epi == "full":   # ResBlock conv2 epilogue: bias + time embedding + residual
+        resid = torch.randn(B, H, W, Cout, device=dev).to(dt)
+        K.set_epilogue(d, bias=torch.randn(Cout, device=dev), addvec=torch.randn(B, Cout, device=dev), ld_add=Cout,
+                       resid=resid, ld_res=Cout, ldy1=Cout)
+    else:
+        K.set_epilogue(d, bias=torch.randn(Cout, device=dev), ldy1=Cout)
     ws = L.LIB.dmc_conv2d_workspace(ctypes.byref(d))
     for _ in range(3):
         K.conv(d, x1, x2, wp, y)
@@ -62,9 +67,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="all")
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--epi", default="bias", choices=["bias", "full"])
     a = ap.parse_args()
     for name in (SHAPES if a.shape == "all" else [a.shape]):
-        run(name, a.iters)
+        run(name, a.iters, a.epi)
 
 
 if __name__ == "__main__":
