@@ -783,7 +783,7 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
     if (dma && !late) issue_stage();
     if (a.dbg & 4) continue;
     const char* A = lds + (c & 1) * HB;
-    const char* Bw = wring + (s % 3) * WB;
+    const char* Bw = wring + (s % WS) * WB;
     const int ty = t / 3, tx = t - ty * 3;
     const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
 #pragma unroll
