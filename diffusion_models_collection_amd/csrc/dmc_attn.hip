@@ -130,8 +130,8 @@ DMC_DEV void store_d4(char* base, size_t idx, const float* v) {
     *(v4f*)(base + idx * 4) = v4f{v[0], v[1], v[2], v[3]};
   } else {
     v2i x;
-    x[0] = (int)(f2bf(v[0]) | (f2bf(v[1]) << 16));
-    x[1] = (int)(f2bf(v[2]) | (f2bf(v[3]) << 16));
+    x[0] = (int)f2bf2(v[0], v[1]);
+    x[1] = (int)f2bf2(v[2], v[3]);
     *(v2i*)(base + idx * 2) = x;
   }
 }

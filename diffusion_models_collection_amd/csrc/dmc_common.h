@@ -27,12 +27,14 @@ typedef int v2i __attribute__((ext_vector_type(2)));
 #define LDS_AS __attribute__((address_space(3)))
 
 DMC_DEV float bf2f(uint32_t b) { return __uint_as_float(b << 16); }
-DMC_DEV uint32_t f2bf(float f) {
-  // round-to-nearest-even; NaN stays NaN
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return u >> 16;
+typedef float v2f __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// fp32 -> bf16, round to nearest even (NaN stays NaN): the gfx950 conversion instruction v_cvt_pk_bf16_f32,
+// branch-free (a software rounding with a NaN test compiles to an exec-mask branch per element)
+DMC_DEV uint32_t f2bf(float f) { return __builtin_bit_cast(unsigned short, (__bf16)f); }
+// two values -> one dword (lo in bits 0..15), one v_cvt_pk_bf16_f32
+DMC_DEV uint32_t f2bf2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((v2f){lo, hi}, bf16x2));
 }
 
 template <typename T> struct TT;
@@ -69,7 +71,7 @@ template <> struct Chunk<bf16_t> {
   static DMC_DEV v4i pack(const float* f) {
     v4i c;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) c[i] = (int)(f2bf(f[2 * i]) | (f2bf(f[2 * i + 1]) << 16));
+    for (int i = 0; i < 4; ++i) c[i] = (int)f2bf2(f[2 * i], f[2 * i + 1]);
     return c;
   }
 };

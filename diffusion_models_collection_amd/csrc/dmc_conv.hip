@@ -110,8 +110,8 @@ DMC_DEV void store4(char* p, size_t idx, const float* v, bool f32) {
     *(v4f*)(p + idx * 4) = x;
   } else {
     v2i x;
-    x[0] = (int)(f2bf(v[0]) | (f2bf(v[1]) << 16));
-    x[1] = (int)(f2bf(v[2]) | (f2bf(v[3]) << 16));
+    x[0] = (int)f2bf2(v[0], v[1]);
+    x[1] = (int)f2bf2(v[2], v[3]);
     *(v2i*)(p + idx * 2) = x;
   }
 }
