@@ -377,9 +377,10 @@ DMC_DEV void load_coef(const float* p, float* v) {
 // Column sums of a row-major fp32 matrix by one 256-thread block, 64 columns from c0 (4 row slices, 8 rows
 // in flight each, slices added in fixed order): out0[c] = scale * sum_r in[r*ld + c*stride], out1 likewise at +1
 // (out1 may be NULL). The block form of colsum_kernel, for kernels that take the reduction into spare blocks.
+template <int SL>   // row slices = blockDim.x / 64
 DMC_DEV void colsum_block(const float* in, int R, int C, long ld, int stride, int c0, float* out0, float* out1,
                           float scale) {
-  __shared__ float red[2][4][64];
+  __shared__ float red[2][SL][64];
   const int lane = threadIdx.x & 63, slice = threadIdx.x >> 6;
   const int c = c0 + lane;
   const bool two = out1 != nullptr;
@@ -387,18 +388,18 @@ DMC_DEV void colsum_block(const float* in, int R, int C, long ld, int stride, in
   if (c < C) {
     const float* p = in + (size_t)c * stride;
     int r = slice;
-    for (; r + 4 * 7 < R; r += 32) {
+    for (; r + SL * 7 < R; r += SL * 8) {
       float a0[8], a1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int u = 0; u < 8; ++u) a0[u] = p[(size_t)(r + 4 * u) * ld];
+      for (int u = 0; u < 8; ++u) a0[u] = p[(size_t)(r + SL * u) * ld];
       if (two) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) a1[u] = p[(size_t)(r + 4 * u) * ld + 1];
+        for (int u = 0; u < 8; ++u) a1[u] = p[(size_t)(r + SL * u) * ld + 1];
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) { s0 += a0[u]; s1 += a1[u]; }
     }
-    for (; r < R; r += 4) {
+    for (; r < R; r += SL) {
       s0 += p[(size_t)r * ld];
       if (two) s1 += p[(size_t)r * ld + 1];
     }
@@ -407,8 +408,11 @@ DMC_DEV void colsum_block(const float* in, int R, int C, long ld, int stride, in
   red[1][slice][lane] = s1;
   __syncthreads();
   if (slice == 0 && c < C) {
-    out0[c] = scale * (((red[0][0][lane] + red[0][1][lane]) + red[0][2][lane]) + red[0][3][lane]);
-    if (two) out1[c] = scale * (((red[1][0][lane] + red[1][1][lane]) + red[1][2][lane]) + red[1][3][lane]);
+    float t0 = 0.f, t1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < SL; ++k) { t0 += red[0][k][lane]; t1 += red[1][k][lane]; }
+    out0[c] = scale * t0;
+    if (two) out1[c] = scale * t1;
   }
 }
 
@@ -421,7 +425,7 @@ __global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* cf, ch
   constexpr int EPC = TT<T>::KPL;
   const int C = b.s.C1 + b.s.C2, CPR = C / EPC, rpi = 256 / CPR;
   if ((int)blockIdx.y == b.splits) {
-    if ((int)blockIdx.x * 64 < C) colsum_block(A, gridDim.x, C, (long)C * 2, 2, blockIdx.x * 64, dbeta, dgamma, 1.f);
+    if ((int)blockIdx.x * 64 < C) colsum_block<4>(A, gridDim.x, C, (long)C * 2, 2, blockIdx.x * 64, dbeta, dgamma, 1.f);
     return;
   }
   const int tid = threadIdx.x, col = tid % CPR, r0 = tid / CPR;
@@ -548,14 +552,15 @@ __global__ __launch_bounds__(256) void chsum_partial(const char* dy, int HW, int
 
 // both reductions of chsum_finish in one launch: blocks [0, nb_nc) sum the splits per (n, c), the next
 // ceil(C/64) blocks the column sums
-__global__ __launch_bounds__(256) void chsum_finish_kernel(int N, int C, int splits, const float* partial, float* out_nc,
-                                                          int ld_out, float* out_c, float scale, int nb_nc) {
+__global__ __launch_bounds__(1024) void chsum_finish_kernel(int N, int C, int splits, const float* partial,
+                                                           float* out_nc, int ld_out, float* out_c, float scale,
+                                                           int nb_nc) {
   if ((int)blockIdx.x >= nb_nc) {
-    colsum_block(partial, N * splits, C, C, 1, (blockIdx.x - nb_nc) * 64, out_c, nullptr, scale);
+    colsum_block<16>(partial, N * splits, C, C, 1, (blockIdx.x - nb_nc) * 64, out_c, nullptr, scale);
     return;
   }
   const long total = (long)N * C;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)nb_nc * 256) {
+  for (long i = blockIdx.x * 1024L + threadIdx.x; i < total; i += (long)nb_nc * 1024) {
     const int c = i % C, n = i / C;
     float v = 0.f;
     for (int sp = 0; sp < splits; ++sp) v += partial[((size_t)n * splits + sp) * C + c];
@@ -567,10 +572,10 @@ __global__ __launch_bounds__(256) void chsum_finish_kernel(int N, int C, int spl
 void chsum_finish(hipStream_t s, int N, int C, int splits, const float* partial, float* out_nc, int ld_out,
                   float* out_c, float scale) {
   const long tot = (long)N * C;
-  const int nb_nc = out_nc ? (int)((tot + 255) / 256 < 4096 ? (tot + 255) / 256 : 4096) : 0;
+  const int nb_nc = out_nc ? (int)((tot + 1023) / 1024 < 1024 ? (tot + 1023) / 1024 : 1024) : 0;
   const int nb_c = out_c ? (C + 63) / 64 : 0;
   if (nb_nc + nb_c == 0) return;
-  chsum_finish_kernel<<<nb_nc + nb_c, 256, 0, s>>>(N, C, splits, partial, out_nc, ld_out, out_c, scale, nb_nc);
+  chsum_finish_kernel<<<nb_nc + nb_c, 1024, 0, s>>>(N, C, splits, partial, out_nc, ld_out, out_c, scale, nb_nc);
 }
 
 int host_splits(int N, int HW, int C, int epc) {
