@@ -39,6 +39,11 @@ if [[ $STAGES == *S* ]]; then   # sampling-only kernel trace: 2 DDIM-50 runs
   python3 scripts/trace_summary.py "$(find "$O/profs" -name '*kernel_trace.csv' | head -1)" --steps 100 --top 40 > "$O/profs_summary.txt"
   head -25 "$O/profs_summary.txt"
 fi
+if [[ $STAGES == *r* ]]; then   # kernel stats of the roofline conv alone (bench.py --roofline-only), for profiles/
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$O/profr" -o profr --output-format csv -- \
+    python3 bench.py --roofline-only > "$O/profr.json" 2> "$O/profr.err" || { tail -30 "$O/profr.err"; exit 1; }
+  cat "$O/profr.json"; cat "$(find "$O/profr" -name '*kernel_stats.csv' | head -1)"
+fi
 if [[ $STAGES == *m* ]]; then
   P="python3 bench.py --roofline-only"
   timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d "$O/fetch" -o fetch --output-format csv -- $P > /dev/null
