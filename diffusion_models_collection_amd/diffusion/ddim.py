@@ -10,11 +10,39 @@ is done on device: if any t_next < 0, alpha_next = 1 for the whole batch, exactl
 CFG batches the cond/uncond forwards into one 2B forward and fuses combine + x0 + dynamic threshold
 (per-row torch.quantile restatement) into dmc_cfg_x0.
 """
+import os
+
 import torch
 from tqdm import tqdm
 
 from .. import kernels as K
 from .ddpm import DDPM, _require_cuda, diffusion_loss, make_betas
+
+
+class _StepGraph:
+    """One DDIM step (UNet forward + the fused update) captured as a HIP graph and replayed for the remaining
+    steps of a sampling loop: a step is ~300 kernel launches whose Python/ctypes enqueue is about as long as the
+    GPU work at B=128. Inputs x / t / t_next live in static buffers refreshed by device copies before each
+    replay; the output buffer is returned (the next step copies it in). Deterministic steps only (eta = 0), so
+    a replay computes bitwise what p_sample computes (tests/test_gpu_model.py)."""
+
+    def __init__(self, ddim, model, x, t, t_next, y):
+        self.x_s, self.t_s, self.tn_s = x.clone(), t.clone(), t_next.clone()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = ddim.p_sample(model, self.x_s, self.t_s, self.tn_s, y)
+
+    def step(self, x, t, t_next):
+        self.x_s.copy_(x)
+        self.t_s.copy_(t)
+        self.tn_s.copy_(t_next)
+        self.graph.replay()
+        return self.out
+
+    @staticmethod
+    def eligible(ddim, model, x, return_all):
+        return (os.environ.get("DMC_GRAPH", "1") != "0" and ddim.eta == 0 and not return_all and x.is_cuda
+                and getattr(model, "executor", None) is not None and not model.training)
 
 
 class DDIM:
@@ -101,13 +129,23 @@ class DDIM:
         imgs = []
         tab = self._ts_table(batch_size, img.device)
         S = len(self.inference_timesteps)
+        graph = None
+        use_graph = _StepGraph.eligible(self, model, img, return_all_timesteps)
         for i in tqdm(range(S), desc='DDIM Sampling'):
-            img = self.p_sample(model, img, tab[i], tab[i + 1], y)
+            if graph is None and use_graph and i >= 1:     # step 0 ran eagerly: caches and packs are in place
+                try:
+                    graph = _StepGraph(self, model, img, tab[i], tab[i + 1], y)
+                except Exception:   # noqa: BLE001 -- capture problem: stay eager
+                    use_graph = False
+            if graph is not None:
+                img = graph.step(img, tab[i], tab[i + 1])
+            else:
+                img = self.p_sample(model, img, tab[i], tab[i + 1], y)
             if return_all_timesteps:
                 imgs.append(img.cpu())
         if return_all_timesteps:
             return torch.stack(imgs, dim=0)
-        return img
+        return img.clone() if graph is not None else img
 
     @torch.no_grad()
     def sample_with_cfg(self, model, shape, y, cfg_scale=3.0, p_threshold=0.995, return_all_timesteps=False,

@@ -365,3 +365,25 @@ def test_graphed_train_step_matches_eager(conditional, monkeypatch):
     for k in se:
         assert torch.equal(se[k], sg[k]), k
         assert torch.equal(ee[k], eg[k]), k
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_ddim_sample_graph_matches_eager(dtype, monkeypatch):
+    """DDIM.sample replays its step as a HIP graph after the first eager step (diffusion/ddim.py _StepGraph);
+    the samples are bitwise those of the eager loop, conditional and unconditional."""
+    from diffusion_models_collection_amd.models import UNet
+    from diffusion_models_collection_amd.diffusion import DDIM
+    torch.manual_seed(3)
+    m = UNet(image_size=(16, 16), in_channels=3, model_channels=32, out_channels=3, num_res_blocks=1,
+             attention_resolutions=(8,), dropout=0.1, channel_mult=(1, 2), num_classes=10,
+             compute_dtype=dtype).to(DEV).eval()
+    ddim = DDIM(1000, 10, device=DEV)
+    xT = torch.randn(4, 3, 16, 16, device=DEV)
+    y = torch.tensor([1, 2, 3, 4], device=DEV)
+    outs = []
+    for g in ("0", "1"):
+        monkeypatch.setenv("DMC_GRAPH", g)
+        with torch.no_grad():
+            outs.append((ddim.sample(m, tuple(xT.shape), y, x_T=xT), ddim.sample(m, tuple(xT.shape), None, x_T=xT)))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
