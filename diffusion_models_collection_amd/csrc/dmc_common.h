@@ -129,8 +129,10 @@ template <> DMC_DEV v4i lds_frag_tr<bf16_t>(const char* base, int pitch, int k0,
 }
 
 // ---- misc ----
-DMC_DEV float silu_f(float z) { return z / (1.0f + __expf(-z)); }
-DMC_DEV float sigmoid_f(float z) { return 1.0f / (1.0f + __expf(-z)); }
+// v_rcp_f32 (1 ulp) instead of the IEEE division sequence (v_div_scale/fmas/fixup, ~10 VALU ops): the GN
+// backward passes recompute SiLU' per element and were VALU-bound on the division. exp(-z) = inf gives 0.
+DMC_DEV float sigmoid_f(float z) { return __builtin_amdgcn_rcpf(1.0f + __expf(-z)); }
+DMC_DEV float silu_f(float z) { return z * sigmoid_f(z); }
 
 // Counter-based hash for dropout masks: recomputable in backward from (seed, element index).
 DMC_DEV uint32_t hash_u32(uint32_t x, uint32_t seed) {
@@ -140,9 +142,12 @@ DMC_DEV uint32_t hash_u32(uint32_t x, uint32_t seed) {
   x *= 0xC2B2AE35u; x ^= x >> 16;
   return x;
 }
+// Element indices stay below 2^32 (N*H*W*C; 64x64 images at B=128 and C=512 are 2^28), so the inner hash
+// of the high word only mixes the seed: it is loop-invariant (scalar, hoisted), one hash per element remains.
+// Above 2^32 elements the mask pattern repeats.
+DMC_DEV uint32_t drop_seed_mix(uint32_t seed) { return hash_u32(0u, seed * 0x27d4eb2fu + 1u); }
 DMC_DEV bool drop_keep(uint64_t idx, uint32_t seed, uint32_t thresh) {
-  uint32_t h = hash_u32((uint32_t)idx ^ hash_u32((uint32_t)(idx >> 32), seed * 0x27d4eb2fu + 1u), seed);
-  return h >= thresh;
+  return hash_u32((uint32_t)idx ^ drop_seed_mix(seed), seed) >= thresh;
 }
 
 DMC_DEV float wave_sum(float v) {
