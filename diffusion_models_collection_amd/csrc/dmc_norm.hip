@@ -119,6 +119,85 @@ __global__ void gn_stats_final(Src2 s, int HW, int G, int splits, const float* p
   }
 }
 
+// Statistics of one sample per 1024-thread block, finalised in the same launch (no partial buffer, no second
+// kernel): used at training/sampling batch sizes, where N blocks fill the chip. Same shifted sums and fixed
+// reduction order as gn_stats_partial + gn_stats_final with splits = 1. Replaces a ~5 us dependent launch per
+// GroupNorm; the per-element work (unpack, sub, add, fma) keeps one CU's walk memory-bound.
+template <typename T>
+__global__ __launch_bounds__(1024) void gn_stats_one(Src2 s, int HW, int G, float eps, const float* gamma,
+                                                     const float* beta, float* mean_rstd, float* scale, float* shift) {
+  constexpr int EPC = TT<T>::KPL;
+  const int n = blockIdx.x;
+  const int C = s.C1 + s.C2, cpg = C / G;
+  const int CPR = C / EPC, rpi = 1024 / CPR;
+  const int tid = threadIdx.x, col = tid % CPR, r0 = tid / CPR;
+  const bool active = r0 < rpi;
+  __shared__ float red[1024][2 * EPC];
+  __shared__ float csum[1024][2];
+  __shared__ float gstat[64][2];
+  float s1[EPC], s2[EPC], K[EPC];
+  const int c0 = col * EPC;
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) {
+    s1[e] = 0.f; s2[e] = 0.f;
+    const int cg = ((c0 + e) / cpg) * cpg;
+    K[e] = (cg < s.C1) ? ld_as_f<T>(s.x1, (size_t)n * HW * s.ld1 + cg)
+                       : ld_as_f<T>(s.x2, (size_t)n * HW * s.ld2 + (cg - s.C1));
+  }
+  if (active) {
+    for (int p0 = r0; p0 < HW; p0 += UNR * rpi) {
+      v4i buf[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+        if (p0 + u * rpi < HW) buf[u] = load_chunk2<T>(s, n * HW + p0 + u * rpi, c0);
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (p0 + u * rpi >= HW) break;
+        float f[EPC];
+        Chunk<T>::unpack(buf[u], f);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+          const float d = f[e] - K[e];
+          s1[e] += d;
+          s2[e] = fmaf(d, d, s2[e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) { red[tid][2 * e] = active ? s1[e] : 0.f; red[tid][2 * e + 1] = active ? s2[e] : 0.f; }
+  __syncthreads();
+  for (int c = tid; c < C; c += 1024) {
+    const int cc = c / EPC, e = c % EPC;
+    float b1 = 0.f, b2 = 0.f;
+    for (int r = 0; r < rpi; ++r) { b1 += red[r * CPR + cc][2 * e]; b2 += red[r * CPR + cc][2 * e + 1]; }
+    csum[c][0] = b1; csum[c][1] = b2;
+  }
+  __syncthreads();
+  const float cnt = (float)cpg * (float)HW;
+  for (int g = tid; g < G; g += 1024) {
+    float a1 = 0.f, a2 = 0.f;
+    for (int c = g * cpg; c < (g + 1) * cpg; ++c) { a1 += csum[c][0]; a2 += csum[c][1]; }
+    const int cg = g * cpg;
+    const float Kg = (cg < s.C1) ? ld_as_f<T>(s.x1, (size_t)n * HW * s.ld1 + cg)
+                                 : ld_as_f<T>(s.x2, (size_t)n * HW * s.ld2 + (cg - s.C1));
+    const float m1 = a1 / cnt;
+    const float var = fmaxf(a2 / cnt - m1 * m1, 0.f);
+    const float mean = Kg + m1, rstd = 1.0f / sqrtf(var + eps);
+    gstat[g][0] = mean; gstat[g][1] = rstd;
+    if (mean_rstd) { mean_rstd[((size_t)n * G + g) * 2] = mean; mean_rstd[((size_t)n * G + g) * 2 + 1] = rstd; }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += 1024) {
+    const int g = c / cpg;
+    const float mean = gstat[g][0], rstd = gstat[g][1];
+    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    const float sc = rstd * gm;
+    scale[(size_t)n * C + c] = sc;
+    shift[(size_t)n * C + c] = bt - mean * sc;
+  }
+}
+
 // ---------------- backward of dropout(SiLU(GN(x))) ----------------
 struct GnBwd {
   Src2 s;
@@ -606,6 +685,11 @@ extern "C" int dmc_gn_stats(int dtype, const void* x1, const void* x2, int N, in
   DMC_REQUIRE(ld1 % epc == 0 && (C2 == 0 || ld2 % epc == 0), "gn_stats: pitch alignment");
   hipStream_t s = dmc::as_stream(stream);
   Src2 src{(const char*)x1, (const char*)x2, C1, C2, ld1, ld2};
+  // one block per sample when N blocks fill the chip and a sample is <= 1 MB (bf16, G <= 64)
+  if (dtype != DMC_F32 && !getenv_flag("DMC_GN_STATS_SPLIT") && N >= 64 && G <= 64 && (size_t)HW * C * 2 <= (1u << 20)) {
+    gn_stats_one<bf16_t><<<N, 1024, 0, s>>>(src, HW, G, eps, gamma, beta, mean_rstd, scale, shift);
+    return dmc::check_launch("dmc_gn_stats");
+  }
   const int splits = host_splits(N, HW, C, epc);
   float* partial = (float*)workspace;
   dim3 g(N, splits);

@@ -4,6 +4,7 @@ effective bandwidth of each pass (algorithmic bytes / time).
     python scripts/gn_probe.py [--iters N] [--shape NAME]
 """
 import argparse
+import os
 import sys
 from pathlib import Path
 
@@ -49,6 +50,9 @@ def run(name, iters):
     T = N * HW * C * 2
     r = {}
     r["stats"] = (timeit(lambda: K.gn_stats(dt, x, None, N, HW, C, 0, C, 0, 8, 1e-5, gamma, beta), iters), T)
+    os.environ["DMC_GN_STATS_SPLIT"] = "1"
+    r["stats_split"] = (timeit(lambda: K.gn_stats(dt, x, None, N, HW, C, 0, C, 0, 8, 1e-5, gamma, beta), iters), T)
+    os.environ["DMC_GN_STATS_SPLIT"] = "0"
     r["apply"] = (timeit(lambda: K.gn_apply(dt, x, None, N, HW, C, 0, C, 0, sc, sh, out=out), iters), 2 * T)
     r["apply_drop"] = (timeit(lambda: K.gn_apply(dt, x, None, N, HW, C, 0, C, 0, sc, sh, drop=drop, out=out),
                               iters), 2 * T)

@@ -230,6 +230,41 @@ def test_conv3x3_halo_kernel(case, variant, monkeypatch):
         assert rel_err(dws[0], dws[1]) < 1e-3, rel_err(dws[0], dws[1])
 
 
+@pytest.mark.parametrize("shape", [(64, 8, 8, 256, 256), (128, 32, 32, 128, 0), (96, 16, 16, 136, 120),
+                                   (64, 4, 4, 512, 0)])
+def test_groupnorm_stats_one_block_per_sample(shape, monkeypatch):
+    """bf16 at N >= 64: statistics of a sample in one 1024-thread block, finalised in the same launch
+    (gn_stats_one), vs torch fp32 group_norm statistics of the same bf16 values and vs the split path."""
+    L, K = _lib()
+    torch.manual_seed(5)
+    N, H, W, C1, C2 = shape
+    G, C = 8, C1 + C2
+    x = q(torch.randn(N, C, H, W) * 1.5 + 0.7, torch.bfloat16)
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C)
+    xd = nhwc(x).to(torch.bfloat16).to(DEV)
+    x1, x2 = xd[..., :C1].contiguous(), (xd[..., C1:].contiguous() if C2 else None)
+    outs = []
+    for split in ("0", "1"):
+        monkeypatch.setenv("DMC_GN_STATS_SPLIT", split)
+        sc, sh, mr = K.gn_stats(torch.bfloat16, x1, x2, N, H * W, C1, C2, C1, C2, G, 1e-5, gamma.to(DEV),
+                                beta.to(DEV))
+        torch.cuda.synchronize()
+        outs.append((sc.cpu(), sh.cpu(), mr.cpu()))
+    xv = x.view(N, G, -1).double()
+    mean, var = xv.mean(-1), xv.var(-1, unbiased=False)
+    rstd = (var + 1e-5).rsqrt()
+    for sc, sh, mr in outs:
+        m = mr.view(N, G, 2)
+        torch.testing.assert_close(m[..., 0].double(), mean, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(m[..., 1].double(), rstd, rtol=1e-4, atol=1e-5)
+        sc_ref = (rstd.repeat_interleave(C // G, 1) * gamma.double())
+        torch.testing.assert_close(sc.view(N, C).double(), sc_ref, rtol=1e-4, atol=1e-5)
+        sh_ref = beta.double() - mean.repeat_interleave(C // G, 1) * sc_ref
+        torch.testing.assert_close(sh.view(N, C).double(), sh_ref, rtol=1e-4, atol=1e-4)
+    for a, b in zip(outs[0], outs[1]):
+        torch.testing.assert_close(a, b, rtol=2e-5, atol=2e-5)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_groupnorm_stats_and_backward(dt):
     L, K = _lib()
