@@ -335,6 +335,100 @@ __global__ __launch_bounds__(256) void gn_bwd_final(int C, int G, int HW, int sp
   }
 }
 
+// gn_bwd_partial + gn_bwd_final in one launch for small samples: one 1024-thread block walks all pixels of
+// sample n, reduces the per-channel sums in LDS (fixed order) and writes A and the apply coefficients exactly
+// as gn_bwd_final does. Used at N >= 64 where HW*C <= 64K (the 16x16 and smaller levels): there the two-kernel
+// form is launch-latency bound (~6 us for the final kernel alone).
+template <typename T>
+__global__ __launch_bounds__(1024) void gn_bwd_one(GnBwd b, float* A /*[n][C][2]*/, float* cf /*[6][N][C]*/) {
+  constexpr int EPC = TT<T>::KPL;
+  const int n = blockIdx.x, N = gridDim.x;
+  const uint32_t dseed = drop_seed(b.dseed, b.dseed_base);
+  const int C = b.s.C1 + b.s.C2, cpg = C / b.G, G = b.G;
+  const int CPR = C / EPC, rpi = 1024 / CPR;
+  const int tid = threadIdx.x, col = tid % CPR, r0 = tid / CPR;
+  const bool active = r0 < rpi;
+  __shared__ float red[1024][2 * EPC];
+  __shared__ float sA[1024][2];
+  __shared__ float sm[64][2];
+  const int c0 = col * EPC;
+  float mean[EPC], rstd[EPC], gm[EPC], bt[EPC], a1[EPC], a2[EPC];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) {
+    const int c = c0 + e, g = c / cpg;
+    mean[e] = b.mr[((size_t)n * G + g) * 2];
+    rstd[e] = b.mr[((size_t)n * G + g) * 2 + 1];
+    gm[e] = b.gamma ? b.gamma[c] : 1.f;
+    bt[e] = b.beta ? b.beta[c] : 0.f;
+    a1[e] = 0.f; a2[e] = 0.f;
+  }
+  if (active) {
+    for (int p0 = r0; p0 < b.HW; p0 += UNR * rpi) {
+      v4i bx[UNR], bg[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int pix = n * b.HW + p0 + u * rpi;
+        if (p0 + u * rpi < b.HW) {
+          bx[u] = load_chunk2<T>(b.s, pix, c0);
+          bg[u] = *(const v4i*)(b.g + ((size_t)pix * b.ld_g + c0) * sizeof(T));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (p0 + u * rpi >= b.HW) break;
+        const int pix = n * b.HW + p0 + u * rpi;
+        float x[EPC], gv[EPC];
+        Chunk<T>::unpack(bx[u], x);
+        Chunk<T>::unpack(bg[u], gv);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+          float g = gv[e];
+          if (b.dthresh) g = drop_keep((uint64_t)pix * C + c0 + e, dseed, b.dthresh) ? g * b.dscale : 0.f;
+          float xh;
+          const float dz = gn_dz(x[e], g, mean[e], rstd[e], gm[e], bt[e], xh, b.silu);
+          a1[e] += dz;
+          a2[e] = fmaf(dz, xh, a2[e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) { red[tid][2 * e] = active ? a1[e] : 0.f; red[tid][2 * e + 1] = active ? a2[e] : 0.f; }
+  __syncthreads();
+  for (int c = tid; c < C; c += 1024) {
+    const int cc = c / EPC, e = c % EPC;
+    float v1 = 0.f, v2 = 0.f;
+    for (int r = 0; r < rpi; ++r) { v1 += red[r * CPR + cc][2 * e]; v2 += red[r * CPR + cc][2 * e + 1]; }
+    A[((size_t)n * C + c) * 2] = v1;
+    A[((size_t)n * C + c) * 2 + 1] = v2;
+    const float g_ = b.gamma ? b.gamma[c] : 1.f;
+    sA[c][0] = v1 * g_; sA[c][1] = v2 * g_;
+  }
+  __syncthreads();
+  const float cnt = (float)cpg * (float)b.HW;
+  for (int g = tid; g < G; g += 1024) {
+    float m1 = 0.f, m2 = 0.f;
+    for (int c = g * cpg; c < (g + 1) * cpg; ++c) { m1 += sA[c][0]; m2 += sA[c][1]; }
+    sm[g][0] = m1 / cnt;
+    sm[g][1] = m2 / cnt;
+  }
+  __syncthreads();
+  const size_t NC = (size_t)N * C;
+  for (int c = tid; c < C; c += 1024) {
+    const int g = c / cpg;
+    const float mu = b.mr[((size_t)n * G + g) * 2], rs = b.mr[((size_t)n * G + g) * 2 + 1];
+    const float g_ = b.gamma ? b.gamma[c] : 1.f, bb = b.beta ? b.beta[c] : 0.f;
+    const size_t i = (size_t)n * C + c;
+    const float sc = rs * g_;
+    cf[i] = sc;
+    cf[NC + i] = bb - mu * sc;
+    cf[2 * NC + i] = sc;
+    cf[3 * NC + i] = -rs * rs * sm[g][1];
+    cf[4 * NC + i] = mu;
+    cf[5 * NC + i] = -rs * sm[g][0];
+  }
+}
+
 // Column sums of a row-major fp32 matrix: out0[c] = scale * sum_r in[r*ld + c*stride], out1 likewise at +1.
 // 1024 threads = 64 columns x 16 row slices; slices combined in fixed order (deterministic).
 __global__ __launch_bounds__(1024) void colsum_kernel(const float* in, int R, int C, long ld, int stride, float* out0,
@@ -730,9 +824,13 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
   float* sums = cf + (size_t)N * C * 6;
   const bool want_sums = dx_sum_nc || dx_sum_c;
   dim3 gr(N, b.splits);
-  if (dtype == DMC_F32) gn_bwd_partial<float><<<gr, 256, 0, s>>>(b, partial);
-  else gn_bwd_partial<bf16_t><<<gr, 256, 0, s>>>(b, partial);
-  gn_bwd_final<<<N, 256, 0, s>>>(C, G, HW, b.splits, partial, mean_rstd, gamma, beta, A, cf);
+  if (dtype != DMC_F32 && N >= 64 && HW * C <= 65536 && !getenv_flag("DMC_GN_BWD_SPLIT")) {
+    gn_bwd_one<bf16_t><<<N, 1024, 0, s>>>(b, A, cf);
+  } else {
+    if (dtype == DMC_F32) gn_bwd_partial<float><<<gr, 256, 0, s>>>(b, partial);
+    else gn_bwd_partial<bf16_t><<<gr, 256, 0, s>>>(b, partial);
+    gn_bwd_final<<<N, 256, 0, s>>>(C, G, HW, b.splits, partial, mean_rstd, gamma, beta, A, cf);
+  }
   // dx, plus dbeta[c] = sum_n A[n][c][0], dgamma[c] = sum_n A[n][c][1] in the grid's extra row (needs N >= C/64)
   const bool fused_cs = N * 64 >= C;
   const dim3 ga(N, b.splits + (fused_cs ? 1 : 0));

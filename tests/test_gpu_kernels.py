@@ -265,6 +265,46 @@ def test_groupnorm_stats_one_block_per_sample(shape, monkeypatch):
         torch.testing.assert_close(a, b, rtol=2e-5, atol=2e-5)
 
 
+@pytest.mark.parametrize("shape", [(64, 8, 8, 256, 256), (128, 16, 16, 256, 0), (64, 4, 4, 384, 128)])
+def test_groupnorm_backward_one_block_per_sample(shape, monkeypatch):
+    """bf16 at N >= 64 and HW*C <= 64K: the per-channel sums and apply coefficients of a sample in one
+    1024-thread block (gn_bwd_one) vs torch fp32 autograd of SiLU(GN(x)), and vs the partial+final path, with
+    dropout and the fused dx pixel sums."""
+    L, K = _lib()
+    torch.manual_seed(6)
+    N, H, W, C1, C2 = shape
+    G, C, dt = 8, C1 + C2, torch.bfloat16
+    x = q(torch.randn(N, C, H, W) * 1.3 + 0.4, dt).requires_grad_(True)
+    gamma = (torch.rand(C) + 0.5).requires_grad_(True)
+    beta = torch.randn(C).requires_grad_(True)
+    a = F.silu(F.group_norm(x, G, gamma, beta, 1e-5))
+    gout = q(torch.randn_like(a), dt)
+    a.backward(gout)
+    xd = nhwc(x.detach()).to(dt).to(DEV)
+    x1, x2 = xd[..., :C1].contiguous(), (xd[..., C1:].contiguous() if C2 else None)
+    gd, gm_d, bt_d = nhwc(gout).to(dt).to(DEV), gamma.detach().to(DEV), beta.detach().to(DEV)
+    _, _, mr = K.gn_stats(dt, x1, x2, N, H * W, C1, C2, C1, C2, G, 1e-5, gm_d, bt_d)
+    res = {}
+    for split in ("0", "1"):
+        monkeypatch.setenv("DMC_GN_BWD_SPLIT", split)
+        for drop in (None, (7, 1 << 30, 4.0 / 3.0)):   # (seed, thresh, scale): keep prob 0.75
+            dx1, dx2 = torch.empty_like(x1), (torch.empty_like(x2) if C2 else None)
+            dg, db = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+            K.gn_bwd(dt, gd, C, x1, x2, N, H * W, C1, C2, C1, C2, G, mr, gm_d, bt_d, True, drop, dx1, dx2, C1, C2,
+                     0, 0, dg, db)
+            torch.cuda.synchronize()
+            dx = torch.cat([dx1, dx2], -1) if C2 else dx1
+            res[(split, drop is None)] = (dx.float().cpu(), dg.cpu(), db.cpu())
+    dxk, dgk, dbk = res[("0", True)]
+    assert rel_err(nchw(dxk), x.grad) < 2e-2
+    assert rel_err(dgk, gamma.grad) < 1e-4 and rel_err(dbk, beta.grad) < 1e-4
+    for nodrop in (True, False):
+        for u, v in zip(res[("0", nodrop)], res[("1", nodrop)]):
+            assert rel_err(u, v) < 1e-2, (nodrop, rel_err(u, v))
+    # dropout changes the result (keep prob 0.75), identically on both paths
+    assert rel_err(res[("0", False)][0], dxk) > 1e-2
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_groupnorm_stats_and_backward(dt):
     L, K = _lib()
@@ -305,7 +345,7 @@ def test_groupnorm_stats_and_backward(dt):
     dxs = prev.clone()
     snc = torch.full((N, 100), -7.0, device=DEV)
     sc_ = torch.empty(C1 + C2, device=DEV)
-    drop = (1 << 30, 0, 4.0 / 3.0)   # keep prob 0.75
+    drop = (7, 1 << 30, 4.0 / 3.0)   # (seed, thresh, scale): keep prob 0.75
     K.gn_bwd(dt, nhwc(gout).to(dt).to(DEV), C1 + C2, xs, None, N, H * W, C1 + C2, 0, C1 + C2, 0, G, mrs,
              gamma.detach().to(DEV), beta.detach().to(DEV), True, drop, dxs, None, C1 + C2, 0, 1, 0, dg, db,
              dx_sum_nc=snc, ld_sum_nc=100, dx_sum_c=sc_)
