@@ -17,6 +17,8 @@ The JSON line also carries:
   cpu_baseline  the CPU oracle (oracle/unet_oracle.py, fp32, a port of the reference path) running the
                 same train step on the host cores, rank 0 only, bounded sample (B=32, 3 timed steps)
   ddim50        DDIM-50 sampling img/s (eta 0, B=128 per GPU, replicas)
+  ddim50_cfg    DDIM-50 + classifier-free guidance (scale 3.0, dynamic threshold 0.995) img/s, conditional
+                UNet (10 classes), B=128 per GPU as one 256-row forward per step
 """
 import argparse
 import json
@@ -136,6 +138,7 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-sample", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-cfg", action="store_true", help="skip the conditional CFG sampling line")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--sample-steps", type=int, default=50)
     ap.add_argument("--no-train", action="store_true", help="sampling only (profiling)")
@@ -223,6 +226,28 @@ def main():
             sel = tt.item()
         out["ddim50"] = {"value": round(world * B / sel, 2), "unit": "img/s", "batch_per_gpu": B,
                          "steps": args.sample_steps, "seconds": round(sel, 3), "scaling": "replicas"}
+        if not args.no_cfg:
+            # conditional UNet (10 classes), DDIM-50 + classifier-free guidance 3.0 + dynamic thresholding
+            # (diffusion/ddim.py:251-346): cond and null-label rows as ONE 2B forward per step
+            torch.manual_seed(43 + rank)
+            cmodel = UNet(**CIFAR, num_classes=10, compute_dtype=args.dtype).to(dev).eval()
+            yl = torch.arange(B, device=dev) % 10
+            with torch.no_grad():
+                ddim.sample_with_cfg(cmodel, (B, 3, 32, 32), yl, cfg_scale=3.0)
+                if world > 1:
+                    dist.barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                ddim.sample_with_cfg(cmodel, (B, 3, 32, 32), yl, cfg_scale=3.0)
+                torch.cuda.synchronize()
+                cel = time.perf_counter() - t0
+            if world > 1:
+                tt = torch.tensor([cel], device=dev)
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                cel = tt.item()
+            out["ddim50_cfg"] = {"value": round(world * B / cel, 2), "unit": "img/s", "batch_per_gpu": B,
+                                 "steps": args.sample_steps, "cfg_scale": 3.0, "p_threshold": 0.995,
+                                 "forward_batch": 2 * B, "seconds": round(cel, 3), "scaling": "replicas"}
     if rank == 0 and not args.no_roofline:
         out["roofline"] = conv_roofline(dtype)
     if rank == 0 and world == 1 and not args.no_cpu:
