@@ -119,6 +119,23 @@ __global__ void gn_stats_final(Src2 s, int HW, int G, int splits, const float* p
   }
 }
 
+// Channel totals of the 1024-thread one-block kernels: red[t][2e], [2e+1] hold thread t's two partial sums
+// of channel (t % CPR)*EPC + e over its pixel rows (row t / CPR). tpc adjacent lanes per channel split the
+// rpi rows and combine by xor-shuffles (fixed order), instead of one thread walking all rows.
+template <int EPC>
+DMC_DEV void onecta_chan_totals(const float (*red)[2 * EPC], int C, int CPR, int rpi, float (*out)[2]) {
+  int tpc = 1;
+  while (tpc * 2 * C <= 1024 && tpc < 16) tpc *= 2;
+  const int c = threadIdx.x / tpc, q = threadIdx.x % tpc;
+  float b1 = 0.f, b2 = 0.f;
+  if (c < C) {
+    const int cc = c / EPC, e = c % EPC;
+    for (int r = q; r < rpi; r += tpc) { b1 += red[r * CPR + cc][2 * e]; b2 += red[r * CPR + cc][2 * e + 1]; }
+  }
+  for (int o = tpc / 2; o > 0; o >>= 1) { b1 += __shfl_xor(b1, o, 64); b2 += __shfl_xor(b2, o, 64); }
+  if (c < C && q == 0) { out[c][0] = b1; out[c][1] = b2; }
+}
+
 // Statistics of one sample per 1024-thread block, finalised in the same launch (no partial buffer, no second
 // kernel): used at training/sampling batch sizes, where N blocks fill the chip. Same shifted sums and fixed
 // reduction order as gn_stats_partial + gn_stats_final with splits = 1. Replaces a ~5 us dependent launch per
@@ -167,17 +184,15 @@ __global__ __launch_bounds__(1024) void gn_stats_one(Src2 s, int HW, int G, floa
 #pragma unroll
   for (int e = 0; e < EPC; ++e) { red[tid][2 * e] = active ? s1[e] : 0.f; red[tid][2 * e + 1] = active ? s2[e] : 0.f; }
   __syncthreads();
-  for (int c = tid; c < C; c += 1024) {
-    const int cc = c / EPC, e = c % EPC;
-    float b1 = 0.f, b2 = 0.f;
-    for (int r = 0; r < rpi; ++r) { b1 += red[r * CPR + cc][2 * e]; b2 += red[r * CPR + cc][2 * e + 1]; }
-    csum[c][0] = b1; csum[c][1] = b2;
-  }
+  onecta_chan_totals<EPC>(red, C, CPR, rpi, csum);
   __syncthreads();
   const float cnt = (float)cpg * (float)HW;
-  for (int g = tid; g < G; g += 1024) {
+  const int wv = tid >> 6, ln = tid & 63;
+  for (int g = wv; g < G; g += 16) {   // one wave per group
     float a1 = 0.f, a2 = 0.f;
-    for (int c = g * cpg; c < (g + 1) * cpg; ++c) { a1 += csum[c][0]; a2 += csum[c][1]; }
+    for (int c = g * cpg + ln; c < (g + 1) * cpg; c += 64) { a1 += csum[c][0]; a2 += csum[c][1]; }
+    a1 = wave_sum(a1); a2 = wave_sum(a2);
+    if (ln != 0) continue;
     const int cg = g * cpg;
     const float Kg = (cg < s.C1) ? ld_as_f<T>(s.x1, (size_t)n * HW * s.ld1 + cg)
                                  : ld_as_f<T>(s.x2, (size_t)n * HW * s.ld2 + (cg - s.C1));
@@ -395,22 +410,23 @@ __global__ __launch_bounds__(1024) void gn_bwd_one(GnBwd b, float* A /*[n][C][2]
 #pragma unroll
   for (int e = 0; e < EPC; ++e) { red[tid][2 * e] = active ? a1[e] : 0.f; red[tid][2 * e + 1] = active ? a2[e] : 0.f; }
   __syncthreads();
+  onecta_chan_totals<EPC>(red, C, CPR, rpi, sA);
+  __syncthreads();
   for (int c = tid; c < C; c += 1024) {
-    const int cc = c / EPC, e = c % EPC;
-    float v1 = 0.f, v2 = 0.f;
-    for (int r = 0; r < rpi; ++r) { v1 += red[r * CPR + cc][2 * e]; v2 += red[r * CPR + cc][2 * e + 1]; }
+    const float v1 = sA[c][0], v2 = sA[c][1];
     A[((size_t)n * C + c) * 2] = v1;
     A[((size_t)n * C + c) * 2 + 1] = v2;
-    const float g_ = b.gamma ? b.gamma[c] : 1.f;
-    sA[c][0] = v1 * g_; sA[c][1] = v2 * g_;
   }
-  __syncthreads();
   const float cnt = (float)cpg * (float)b.HW;
-  for (int g = tid; g < G; g += 1024) {
+  const int wv = tid >> 6, ln = tid & 63;
+  for (int g = wv; g < G; g += 16) {   // one wave per group: gamma-weighted channel totals
     float m1 = 0.f, m2 = 0.f;
-    for (int c = g * cpg; c < (g + 1) * cpg; ++c) { m1 += sA[c][0]; m2 += sA[c][1]; }
-    sm[g][0] = m1 / cnt;
-    sm[g][1] = m2 / cnt;
+    for (int c = g * cpg + ln; c < (g + 1) * cpg; c += 64) {
+      const float g_ = b.gamma ? b.gamma[c] : 1.f;
+      m1 = fmaf(sA[c][0], g_, m1); m2 = fmaf(sA[c][1], g_, m2);
+    }
+    m1 = wave_sum(m1); m2 = wave_sum(m2);
+    if (ln == 0) { sm[g][0] = m1 / cnt; sm[g][1] = m2 / cnt; }
   }
   __syncthreads();
   const size_t NC = (size_t)N * C;
