@@ -1509,55 +1509,93 @@ __global__ void pack_weight_kernel(int mode, const float* w, int Cout, int Cin, 
 // Every stale weight pack of a step in ONE launch (was one launch per conv and mode). The host cuts each
 // job into tiles (dmc_pack_tiles); a block packs one tile through LDS so that both the read of the fp32
 // master weight and the write of the packed rows are contiguous:
-//   FWD     tile = (row co, 256 columns k0..): reads w[co][k0..k0+255][taps] (one contiguous run),
-//           writes dst[co][t][k0..] per tap;
-//   DGRAD / UPDGRAD  tile = (8 input channels c0.., 64 output channels co0..): reads w[co][c0..c0+7][taps]
-//           (64 runs of 8*taps floats), writes dst[c][t][co0..co0+63] (64 consecutive columns).
-constexpr int kPackFwdK = 256, kPackDgC = 8, kPackDgCo = 64;
+//   FWD     tile = (4 rows co0.., 256 columns k0..): reads w[co][k0..k0+255][taps] (one contiguous run per
+//           row), writes dst[co][t][k0..] per tap;
+//   DGRAD / UPDGRAD  tile = (16 input channels c0.., 64 output channels co0..): reads w[co][c0..c0+15][taps]
+//           (64 runs of 16*taps floats), writes dst[c][t][co0..co0+63] (64 consecutive columns).
+constexpr int kPackFwdK = 256, kPackFwdCo = 4, kPackDgC = 16, kPackDgCo = 64;
+constexpr int kPackDgP = kPackDgC * 9 + 1;   // odd LDS row pitch: lanes (one output channel each) hit distinct banks
+constexpr int kPackLds = kPackDgCo * kPackDgP > kPackFwdCo * kPackFwdK * 9 ? kPackDgCo * kPackDgP
+                                                                          : kPackFwdCo * kPackFwdK * 9;
+
+// The tile loops are division-free (lane -> column, wave / loop -> row): with per-element index divisions
+// the pack was VALU-bound.
 __global__ __launch_bounds__(256) void pack_tiles_kernel(const dmc_pack_job* jobs, const int* tiles) {
-  __shared__ float sw[kPackDgCo * kPackDgC * 9 > kPackFwdK * 9 ? kPackDgCo * kPackDgC * 9 : kPackFwdK * 9];
+  __shared__ float sw[kPackLds];
   const int* tl = tiles + 3 * blockIdx.x;
   const dmc_pack_job J = jobs[tl[0]];
   const int khkw = J.kh * J.kw;
   const int koff = J.koff >= 0 ? J.koff : 0;
   const bool f32 = J.dtype == DMC_F32;
+  const int tid = threadIdx.x, wv = tid >> 6, ln = tid & 63;
   auto store = [&](long di, float v) {
     if (f32) ((float*)J.dst)[di] = v;
     else ((bf16_t*)J.dst)[di] = (bf16_t)f2bf(v);
   };
   if (J.mode == DMC_PACK_FWD) {
-    const int co = tl[1], k0 = tl[2];
+    // tile = (rows co0..co0+3, 256 columns k0..): row r's run w[co0+r][k0..k0+kv)[taps] lands at sw[r*256*9..]
+    const int co0 = tl[1], k0 = tl[2];
+    const int nco = min(kPackFwdCo, J.Cout - co0);
     const int KW = J.koff >= 0 ? J.Cin : J.Kc;
     const int kn = min(kPackFwdK, KW - k0);
     const int kv = max(0, min(kn, J.Cin - k0));          // columns backed by the weight (rest: zero padding)
-    const float* src = J.w + ((size_t)co * J.Cin + k0) * khkw;
-    for (int i = threadIdx.x; i < kv * khkw; i += 256) sw[i] = src[i];
-    __syncthreads();
-    for (int i = threadIdx.x; i < khkw * kn; i += 256) {
-      const int t = i / kn, k = i - t * kn;
-      store(((long)co * khkw + t) * J.Kc + koff + k0 + k, k < kv ? sw[k * khkw + t] : 0.f);
+    const int run = kv * khkw;
+    for (int j0 = tid; j0 < run; j0 += 3 * 256) {       // up to 12 loads in flight per thread
+      float v[kPackFwdCo][3];
+#pragma unroll
+      for (int r = 0; r < kPackFwdCo; ++r)
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const int j = j0 + u * 256;
+          v[r][u] = (r < nco && j < run) ? J.w[((size_t)(co0 + r) * J.Cin + k0) * khkw + j] : 0.f;
+        }
+#pragma unroll
+      for (int r = 0; r < kPackFwdCo; ++r)
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+          if (r < nco && j0 + u * 256 < run) sw[r * kPackFwdK * 9 + j0 + u * 256] = v[r][u];
     }
+    __syncthreads();
+    for (int r = 0; r < nco; ++r)
+      for (int t = 0; t < khkw; ++t)
+        for (int k = tid; k < kn; k += 256)
+          store(((long)(co0 + r) * khkw + t) * J.Kc + koff + k0 + k, k < kv ? sw[r * kPackFwdK * 9 + k * khkw + t] : 0.f);
     return;
   }
+  // DGRAD / UPDGRAD: tile = (cn input channels c0.., con output channels co0..)
   const int c0 = tl[1], co0 = tl[2];
   const int KW = J.koff >= 0 ? J.Cout : J.Kc;              // columns this job writes
   const int cn = min(kPackDgC, J.Cin - c0), con = min(kPackDgCo, KW - co0);
   const int cov = max(0, min(con, J.Cout - co0));           // columns backed by the weight
-  const int run = cn * khkw;
-  for (int i = threadIdx.x; i < cov * run; i += 256) {
-    const int r = i / run, j = i - r * run;
-    sw[r * kPackDgC * 9 + j] = J.w[((size_t)(co0 + r) * J.Cin + c0) * khkw + j];
+  const int run = cn * khkw;                                // <= 16 * 9 = 144 = 64 * 3 - 48
+  for (int r0 = wv; r0 < cov; r0 += 16) {                  // wave -> rows r0, r0+4, r0+8, r0+12; lane -> column
+    float v[4][3];
+#pragma unroll
+    for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int r = r0 + 4 * a2, j = ln + 64 * u;
+        v[a2][u] = (r < cov && j < run) ? J.w[((size_t)(co0 + r) * J.Cin + c0) * khkw + j] : 0.f;
+      }
+#pragma unroll
+    for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int r = r0 + 4 * a2, j = ln + 64 * u;
+        if (r < cov && j < run) sw[r * kPackDgP + j] = v[a2][u];
+      }
   }
   __syncthreads();
   const int ntaps = J.mode == DMC_PACK_UPDGRAD ? 16 : khkw;
-  for (int i = threadIdx.x; i < cn * ntaps * con; i += 256) {
-    const int q = i / con, co = i - q * con;
-    const int c = q / ntaps, t = q - c * ntaps;
+  const int co = ln;                                        // con <= 64 columns, one per lane
+  for (int q = wv; q < cn * ntaps; q += 4) {
+    const int c = q / ntaps, t = q - c * ntaps;             // wave-uniform
+    if (co >= con) continue;
     float v = 0.f;
     if (co < cov) {
-      const float* wv = sw + co * kPackDgC * 9 + c * khkw;
+      const float* wp = sw + co * kPackDgP + c * khkw;
       if (J.mode == DMC_PACK_DGRAD) {
-        v = wv[t];
+        v = wp[t];
       } else {
         // folded nearest-x2 taps (see pack_value)
         const int u = t >> 2, vv = t & 3;
@@ -1567,7 +1605,7 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(const dmc_pack_job* job
           if (y < 0) continue;
           for (int b1 = 0; b1 < 2; ++b1) {
             const int x = khs[vv][b1];
-            if (x >= 0) v += wv[y * 3 + x];
+            if (x >= 0) v += wp[y * 3 + x];
           }
         }
       }
@@ -1899,7 +1937,7 @@ extern "C" int dmc_pack_tiles(const dmc_pack_job* j, int job_index, int* tiles, 
   };
   if (j->mode == DMC_PACK_FWD) {
     const int KW = j->koff >= 0 ? j->Cin : j->Kc;
-    for (int co = 0; co < j->Cout; ++co)
+    for (int co = 0; co < j->Cout; co += kPackFwdCo)
       for (int k0 = 0; k0 < KW; k0 += kPackFwdK) put(co, k0);
   } else {
     const int KW = j->koff >= 0 ? j->Cout : j->Kc;
