@@ -661,7 +661,9 @@ class UNetExecutor:
             sc = rb.shortcut
             with self._side(*[x.t for x in srcs], dout):
                 self._wgrad(srcs, dout, Cout, K.TAPS1, H, W, Cout, gv(sc.weight))
-                K.channel_sum(dt, dout, N, HW, Cout, Cout, out_c=gv(sc.bias))
+                # the shortcut's bias gradient is the same pixel sum of dout as conv2's (computed just above,
+                # in order on this stream): a copy instead of a second two-kernel channel sum
+                gv(sc.bias).copy_(gv(conv2.bias))
             if len(srcs) == 1:
                 buf, acc = self._grad_target(a)
                 self._conv([Act(dout, H, W, Cout)], sc, K.TAPS1, H, W, C1, out=buf, resid=buf if acc else None,
