@@ -139,6 +139,8 @@ def main():
     ap.add_argument("--no-sample", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-cfg", action="store_true", help="skip the conditional CFG sampling line")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (RCCL over xGMI) for real runs; gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--sample-steps", type=int, default=50)
     ap.add_argument("--no-train", action="store_true", help="sampling only (profiling)")
@@ -151,11 +153,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one rank per GPU; --dist-backend gloo with more ranks than GPUs is a rehearsal of the multi-rank code
+    # path on a 1-GPU box (ranks share the card, gloo stages the all-reduces through the host)
+    ndev = torch.cuda.device_count()
+    gpu = local_rank % ndev if args.dist_backend == "gloo" else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     from diffusion_models_collection_amd.models import UNet
     from diffusion_models_collection_amd.diffusion import DDPM, DDIM

@@ -1716,7 +1716,7 @@ RegPlan plan_reg(const ConvK& k) {
   const int bk = k.dtype_bytes == 4 ? 32 : 64;
   const int nst = k.ntaps * (k.Kc / bk);
   const long t64 = (long)dmc::cdiv(k.M, 64) * dmc::cdiv(k.Cout, 64);
-  if (t64 >= 128 || nst < 16) return p;
+  if (t64 >= 256 || nst < 16) return p;   // e.g. the 128 x 512 x 4992 time-embedding GEMM: 156 tiles -> split 2
   int sp = (int)((256 + t64 - 1) / t64);
   if (sp > nst / 8) sp = nst / 8;
   if (sp > 16) sp = 16;
