@@ -57,6 +57,7 @@ def _load():
         "dmc_version": (_c_int, []),
         "dmc_last_error": (ctypes.c_char_p, []),
         "dmc_conv2d_workspace": (_c_size, [ctypes.POINTER(ConvDesc)]),
+        "dmc_conv_halo_prologue": (_c_int, [ctypes.POINTER(ConvDesc)]),
         "dmc_conv2d": (_c_int, [ctypes.POINTER(ConvDesc), _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_size, _c_p]),
         "dmc_conv2d_wgrad_workspace": (_c_size, [ctypes.POINTER(ConvDesc)]),
         "dmc_conv2d_wgrad": (_c_int, [ctypes.POINTER(ConvDesc), _c_p, _c_int, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p]),

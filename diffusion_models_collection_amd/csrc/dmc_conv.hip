@@ -672,7 +672,48 @@ DMC_DEV void halo_issue(const ConvK& a, char* buf, int c0, int wave, int pb, int
                                                (first ? h1[p] : h2[p]) + c2, 0, 0, 0);
 }
 
-template <int HP, int WS>
+// Inference prologue on the resident halo (prologue DMC_PRO_AFFINE_SILU, no dropout, one image per tile): each
+// wave rewrites the pieces it DMA'd as SiLU(x * scale[n][c] + shift[n][c]) -- the exact op sequence and bf16
+// rounding of gn_apply_kernel, so the conv sees bitwise the operand a materialised GN-apply pass would have
+// written. Zero-padding rows (kOOB) stay zero: the reference pads the normalised activation. A lane's 8
+// channels are the same in every piece, so its scale/shift (ss/tt) are loaded once per chunk, a chunk ahead.
+DMC_DEV void halo_pro_load(const ConvK& a, int n, int c0, v4f* st) {
+  const int lane = threadIdx.x & 63, lrow = lane >> 3, lc = (lane & 7) ^ lrow;
+  const float* sc = a.psc + (size_t)n * a.ldp + c0 + lc * 8;
+  const float* sh = a.psh + (size_t)n * a.ldp + c0 + lc * 8;
+  st[0] = *(const v4f*)sc; st[1] = *(const v4f*)(sc + 4);
+  st[2] = *(const v4f*)sh; st[3] = *(const v4f*)(sh + 4);
+}
+// The rewrite's LDS accesses are inline asm: for plain C++ LDS stores hipcc inserts vmcnt(0) (they may alias
+// the in-flight LDS-DMA), draining the weight ring; a wave only touches the pieces its own, already-landed
+// DMA wrote, and nobody reads them before the next block barrier.
+DMC_DEV v4i lds_read_b128_sync(const char* p) {
+  v4i v;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((unsigned)(uintptr_t)p) : "memory");
+  return v;
+}
+DMC_DEV void lds_write_b128(char* p, v4i v) {
+  asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
+}
+template <int HP>
+DMC_DEV void halo_affine_silu(char* buf, int wave, const unsigned* h1, const v4f* st) {
+  const int lane = threadIdx.x & 63;
+  const float ss[8] = {st[0][0], st[0][1], st[0][2], st[0][3], st[1][0], st[1][1], st[1][2], st[1][3]};
+  const float tt[8] = {st[2][0], st[2][1], st[2][2], st[2][3], st[3][0], st[3][1], st[3][2], st[3][3]};
+#pragma unroll
+  for (int p = 0; p < HP; ++p) {
+    if (h1[p] == kOOB) continue;
+    char* q = buf + (wave * HP + p) * 1024 + lane * 16;
+    float f[8];
+    Chunk<bf16_t>::unpack(lds_read_b128_sync(q), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = silu_f(fmaf(f[e], ss[e], tt[e]));
+    lds_write_b128(q, Chunk<bf16_t>::pack(f));
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <int HP, int WS, bool PRO = false>
 __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int nimg) {
   using T = bf16_t;
   constexpr int NW = 8, WM = 4, BM = 256, BN = 128;
@@ -765,8 +806,17 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
   };
   if ((a.dbg & 32) && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);   // probe: static priority, younger half
 
+  // GN+SiLU prologue on the halo (one image per tile): this lane's scale/shift of chunk 0
+  constexpr bool pro = PRO;   // separate instantiation: the plain kernel's code is unchanged
+  v4f pst[4];
+  if (pro) halo_pro_load(a, n_first, 0, pst);
   halo_issue<HP>(a, lds, 0, wave, 0, HP, h1, h2);
   for (int q = 0; q < WS - 1 && q < nst; ++q) issue_w(q);
+  if (pro) {   // this wave's own chunk-0 pieces (the stage-0 barrier publishes them)
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    halo_affine_silu<HP>(lds, wave, h1, pst);
+    if (nch > 1) halo_pro_load(a, n_first, 64, pst);
+  }
   for (int s = 0; s < nst; ++s) {
     wait_vm_dyn(after_w(s));
     asm volatile("" ::: "memory");
@@ -814,6 +864,12 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
         if (a.dbg & 16) __builtin_amdgcn_s_setprio(0);
       }
       if (ks == 0 && dma && late) issue_stage();
+    }
+    if (pro && t == 8 && c + 1 < nch) {
+      // this wave's own pieces of chunk c+1 (issued in slots 9c..9c+2, landed: the stage's wait covered later
+      // weight slices); nobody reads that buffer before stage 9(c+1)'s barrier, which publishes the rewrite
+      halo_affine_silu<HP>(lds + ((c + 1) & 1) * HB, wave, h1, pst);
+      if (c + 2 < nch) halo_pro_load(a, n_first, (c + 2) * 64, pst);
     }
   }
   __syncthreads();
@@ -1727,6 +1783,22 @@ RegPlan plan_reg(const ConvK& k) {
   return p;
 }
 
+// Halo kernel with the GN-affine+SiLU prologue applied to the resident halo (inference: no dropout, the
+// normalised activation is not needed for a weight gradient). Returns the DMA pieces (6/7) or 0.
+int halo_pro_plan(const ConvK& k, int* R, int* nimg) {
+  if (k.dtype_bytes != 2 || k.prologue != DMC_PRO_AFFINE_SILU || k.dthresh != 0 || k.ldp < k.C1 + k.C2) return 0;
+  // opt-in (DMC_HALO_PRO=1): measured neutral for DDIM-50 at B=128 on MI355X (the saved GN-apply pass is
+  // paid back by a ~17 % slower conv: the halo rewrite's VALU work and its vmcnt(0) drains)
+  if (!getenv_flag("DMC_HALO_PRO") || getenv_flag("DMC_NO_HALO") || getenv_flag("DMC_NO_GLDS") ||
+      getenv_flag("DMC_NO_BUFLDS"))
+    return 0;
+  const bool buf = k.C1 % 64 == 0 && k.C2 % 64 == 0 && k.Kc == k.C1 + k.C2 && k.x1_bytes > 0 &&
+                   (k.C2 == 0 || k.x2_bytes > 0) && k.w_bytes > 0;
+  if (!buf || (plan_glds(k).splits != 1 && !getenv_flag("DMC_NO_SPLITK"))) return 0;
+  const int hp = halo_plan(k, R, nimg);
+  return *nimg == 1 ? hp : 0;   // one image per tile: a lane's scale/shift row is the same in every piece
+}
+
 template <bool BUF>
 void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
   if (p.splits > 1) {
@@ -1756,6 +1828,14 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
       conv_narrow_out_kernel<T><<<dmc::cdiv(k.M, 256), 256, 0, s>>>(k);
       return dmc::check_launch("dmc_conv2d");
     }
+  }
+  if (sizeof(T) == 2 && k.prologue == DMC_PRO_AFFINE_SILU) {
+    int R, nimg;
+    const int hp = halo_pro_plan(k, &R, &nimg);
+    const dim3 hg(k.M / 256, dmc::cdiv(k.Cout, 128));
+    k.dbg = 0;
+    if (hp == 6) { conv3x3_halo_kernel<6, 3, true><<<hg, 512, 0, s>>>(k, R, nimg); return dmc::check_launch("dmc_conv2d"); }
+    if (hp == 7) { conv3x3_halo_kernel<7, 3, true><<<hg, 512, 0, s>>>(k, R, nimg); return dmc::check_launch("dmc_conv2d"); }
   }
   if (sizeof(T) == 2 && k.prologue == DMC_PRO_NONE && !getenv_flag("DMC_NO_GLDS")) {
     // bf16, plain operands: LDS-DMA pipelined kernel
@@ -1925,6 +2005,16 @@ extern "C" int dmc_pack_weight(int pack_mode, int dtype, const float* w, int Cou
   else
     pack_weight_kernel<bf16_t><<<blocks, 256, 0, s>>>(pack_mode, w, Cout, Cin, kh, kw, Kc, (bf16_t*)dst);
   return dmc::check_launch("dmc_pack_weight");
+}
+
+// 1 when dmc_conv2d runs this descriptor on the halo kernel with its GN-affine+SiLU prologue applied to the
+// resident halo (bf16 3x3 stride-1, no dropout): the caller can skip materialising the GroupNorm output.
+extern "C" int dmc_conv_halo_prologue(const dmc_conv_desc* d) {
+  if (d == nullptr || d->dtype != DMC_BF16) return 0;
+  ConvK k;
+  if (fill_convk(d, nullptr, nullptr, nullptr, nullptr, nullptr, k) != 0) return 0;
+  int R, nimg;
+  return halo_pro_plan(k, &R, &nimg) ? 1 : 0;
 }
 
 extern "C" int dmc_pack_tiles(const dmc_pack_job* j, int job_index, int* tiles, int cap) {

@@ -137,6 +137,11 @@ def conv(d, x1, x2, w, y1, y2=None):
                                                       ptr(ws), nbytes, L.stream()), "dmc_conv2d"))
 
 
+def conv_halo_prologue(d):
+    """True when dmc_conv2d applies d's GN-affine+SiLU prologue on the halo kernel's resident halo."""
+    return bool(LIB.dmc_conv_halo_prologue(ctypes.byref(d)))
+
+
 def wgrad(d, dy, ld_dy, x1, x2, dw, scale=1.0):
     nbytes = LIB.dmc_conv2d_wgrad_workspace(ctypes.byref(d))
     ws = SCRATCH.get(nbytes, dy.device)

@@ -97,6 +97,7 @@ class UNetExecutor:
         self.dt = model.compute_dtype
         self.cdt = L.dtype_code(self.dt)
         self.chunk = L.chunk_for(self.dt)
+        self._halo_pro_cache = {}   # shape -> dmc_conv_halo_prologue verdict
         self.wgen = 0               # weight generation: bumped when a fused step rewrote the parameters
         self.packs = _PackCache(self)
         self.params = list(model.parameters())
@@ -291,6 +292,25 @@ class UNetExecutor:
                          b.t.shape[-1] if b else 0, st[0], st[1], silu=silu, drop=drop)
         return Act(out.view(N, a.H, a.W, C), a.H, a.W, C)
 
+    def _halo_pro_ok(self, srcs, Cout, st):
+        """Whether dmc_conv2d runs the 3x3 conv of SiLU(GN(srcs)) on the halo kernel with the GN+SiLU applied
+        to its resident halo (bf16 inference; dmc_conv_halo_prologue). Cached per shape and A/B switch."""
+        if self.dt != torch.bfloat16:
+            return False
+        a = srcs[0]
+        b = srcs[1] if len(srcs) > 1 else None
+        N = a.t.shape[0]
+        key = (N, a.H, a.W, a.C, b.C if b else 0, a.t.shape[-1], b.t.shape[-1] if b else 0, Cout,
+               os.environ.get("DMC_HALO_PRO", ""))
+        ok = self._halo_pro_cache.get(key)
+        if ok is None:
+            C1, C2 = a.C, (b.C if b else 0)
+            d = K.make_desc(self.dt, N, a.H, a.W, C1, C2, key[5], key[6], L.kc_for(C1 + C2, self.dt), a.H, a.W, Cout,
+                            K.TAPS3)
+            K.set_prologue(d, L.PRO_AFFINE_SILU, st[0], st[1], C1 + C2)
+            ok = self._halo_pro_cache[key] = K.conv_halo_prologue(d)
+        return ok
+
     def _new(self, N, H, W, C, dtype=None):
         return Act(torch.empty(N, H, W, C, dtype=dtype or self.dt, device=self.device), H, W, C)
 
@@ -460,13 +480,19 @@ class UNetExecutor:
         Cout = rb.out_channels
         gn1, conv1, gn2, conv2 = rb.conv1[0], rb.conv1[2], rb.conv2[0], rb.conv2[3]
         # a1 = SiLU(GN1(x)) materialised once (the 3x3 implicit GEMM reads every pixel 9x; the weight
-        # gradient re-reads it in backward)
+        # gradient re-reads it in backward). Inference (no tape): where the halo kernel takes the conv, it
+        # applies GN+SiLU to its LDS-resident halo instead and nothing is materialised.
         st1 = self._gn(srcs, gn1)
-        a1 = self._apply(srcs, st1, silu=True)
         h1 = self._new(N, H, W, Cout)
         off = self.temb_off[id(rb)]
-        self._conv([a1], conv1, K.TAPS3, H, W, Cout, bias=conv1.bias,
-                   addvec=self.addvec.view(N, -1)[:, off:], ld_add=self.temb_total, out=h1.t)
+        if tape is None and self._halo_pro_ok(srcs, Cout, st1):
+            a1 = None
+            self._conv(srcs, conv1, K.TAPS3, H, W, Cout, pro=(L.PRO_AFFINE_SILU, st1[0], st1[1]), bias=conv1.bias,
+                       addvec=self.addvec.view(N, -1)[:, off:], ld_add=self.temb_total, out=h1.t)
+        else:
+            a1 = self._apply(srcs, st1, silu=True)
+            self._conv([a1], conv1, K.TAPS3, H, W, Cout, bias=conv1.bias,
+                       addvec=self.addvec.view(N, -1)[:, off:], ld_add=self.temb_total, out=h1.t)
         st2 = self._gn([h1], gn2)
         if isinstance(rb.shortcut, torch.nn.Conv2d):
             s = torch.empty(N, H, W, Cout, dtype=self.dt, device=self.device)
@@ -480,9 +506,14 @@ class UNetExecutor:
             if self.seed_ptr is not None:
                 drop = drop + (self.seed_ptr,)
         self._blk_idx += 1
-        a2 = self._apply([h1], st2, silu=True, drop=drop)
         out = self._new(N, H, W, Cout)
-        self._conv([a2], conv2, K.TAPS3, H, W, Cout, bias=conv2.bias, resid=resid, out=out.t)
+        if tape is None and drop is None and self._halo_pro_ok([h1], Cout, st2):
+            a2 = None
+            self._conv([h1], conv2, K.TAPS3, H, W, Cout, pro=(L.PRO_AFFINE_SILU, st2[0], st2[1]), bias=conv2.bias,
+                       resid=resid, out=out.t)
+        else:
+            a2 = self._apply([h1], st2, silu=True, drop=drop)
+            self._conv([a2], conv2, K.TAPS3, H, W, Cout, bias=conv2.bias, resid=resid, out=out.t)
         st1 = (st1, a1)
         st2 = (st2, a2)
         if tape is not None:

@@ -73,6 +73,12 @@ typedef struct dmc_conv_desc {
  * workspace (dmc_conv2d_workspace() bytes, may be 0) enables split-K for small-M shapes; with a NULL
  * or too small workspace the call still succeeds without split-K. */
 size_t dmc_conv2d_workspace(const dmc_conv_desc* d);
+/* 1 when dmc_conv2d runs `d` (bf16 3x3 stride-1, prologue DMC_PRO_AFFINE_SILU, no dropout) on the halo kernel
+ * with SiLU(x*scale+shift) applied to the LDS-resident activation halo, so the caller need not materialise the
+ * GroupNorm output first (inference; replaces the GroupNorm -> SiLU -> Conv2d chain of models/unet.py:34-37,
+ * :55-60 without the intermediate tensor). 0 otherwise (dmc_conv2d then uses the register-staged kernel).
+ * Opt-in: only with DMC_HALO_PRO=1 in the environment (measured neutral for DDIM-50 at B=128). */
+int dmc_conv_halo_prologue(const dmc_conv_desc* d);
 int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2, const void* w,
                void* y1, void* y2, void* workspace, size_t ws_bytes, void* stream);
 

@@ -109,6 +109,53 @@ def test_conv_forward(dt, case, monkeypatch):
     assert rel_err(got, yr) < (1e-5 if dt == torch.float32 else 2e-2), rel_err(got, yr)
 
 
+@pytest.mark.parametrize("case", ["c32_two_sources", "c16_wide", "c32_384", "c8_multi_image"])
+def test_conv3x3_halo_gn_silu_prologue(case, monkeypatch):
+    """Inference prologue on the halo kernel: conv(SiLU(x*scale+shift)) with the GroupNorm affine + SiLU
+    applied to the LDS-resident halo equals, BITWISE, dmc_gn_apply materialisation followed by the plain halo
+    conv (same op sequence and bf16 rounding), and the fp32 torch reference within bf16 tolerance."""
+    L, K = _lib()
+    monkeypatch.setenv("DMC_NO_SPLITK", "1")   # small N: keep the planner on the halo kernel
+    monkeypatch.setenv("DMC_HALO_PRO", "1")    # opt-in path
+    dt = torch.bfloat16
+    torch.manual_seed(11)
+    N, H, C1, C2, Cout = {"c32_two_sources": (2, 32, 128, 64, 128), "c16_wide": (3, 16, 256, 0, 256),
+                          "c32_384": (2, 32, 256, 128, 128), "c8_multi_image": (8, 8, 128, 64, 128)}[case]
+    # tiles of several 8x8 images are not taken (a lane's scale/shift row would differ per piece): the conv
+    # then runs the register-staged prologue kernel, equal to the materialised path within bf16 rounding
+    halo = case != "c8_multi_image"
+    W, Cin, G = H, C1 + C2, 8
+    x = q(torch.randn(N, Cin, H, W) * 1.4 + 0.3, dt)
+    gamma, beta = torch.rand(Cin) + 0.5, torch.randn(Cin)
+    w = q(torch.randn(Cout, Cin, 3, 3) / math.sqrt(Cin * 9), dt)
+    bias = torch.randn(Cout)
+    xd = nhwc(x).to(dt).to(DEV)
+    x1d, x2d = (xd[..., :C1].contiguous(), xd[..., C1:].contiguous()) if C2 else (xd, None)
+    Kc = L.kc_for(Cin, dt)
+    wp = K.pack_weight(L.PACK_FWD, dt, w.to(DEV), Kc)
+    sc, sh, _ = K.gn_stats(dt, x1d, x2d, N, H * W, C1, C2, C1, C2, G, 1e-5, gamma.to(DEV), beta.to(DEV))
+    d = K.make_desc(dt, N, H, W, C1, C2, C1, C2, Kc, H, W, Cout, K.TAPS3)
+    K.set_prologue(d, L.PRO_AFFINE_SILU, sc, sh, Cin)
+    K.set_epilogue(d, bias=bias.to(DEV), ldy1=Cout)
+    assert K.conv_halo_prologue(d) == halo
+    y = torch.full((N, H, W, Cout), float("nan"), dtype=dt, device=DEV)
+    K.conv(d, x1d, x2d, wp, y)
+    a = K.gn_apply(dt, x1d, x2d, N, H * W, C1, C2, C1, C2, sc, sh, silu=True).view(N, H, W, Cin)
+    d0 = K.make_desc(dt, N, H, W, Cin, 0, Cin, 0, Kc, H, W, Cout, K.TAPS3)
+    K.set_epilogue(d0, bias=bias.to(DEV), ldy1=Cout)
+    y0 = torch.full((N, H, W, Cout), float("nan"), dtype=dt, device=DEV)
+    K.conv(d0, a, None, wp, y0)
+    torch.cuda.synchronize()
+    if halo:
+        assert torch.equal(y, y0), (y.float() - y0.float()).abs().max().item()
+    else:
+        assert rel_err(y.float(), y0.float()) < 1e-2
+    yr = F.conv2d(F.silu(F.group_norm(x, G, gamma, beta, 1e-5)), w, bias, padding=1)
+    assert rel_err(nchw(y.float().cpu()), yr) < 2e-2
+    monkeypatch.setenv("DMC_HALO_PRO", "0")
+    assert not K.conv_halo_prologue(d)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("case", ["s1", "s2", "up", "1x1_concat_split"])
 def test_conv_dgrad_wgrad(dt, case):

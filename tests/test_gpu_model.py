@@ -83,6 +83,28 @@ def test_cifar_unet_matches_oracle(dtype):
     assert rel(out2, out[:2]) < (1e-5 if dtype == "fp32" else 1e-2)
 
 
+def test_cifar_unet_inference_halo_prologue_bitwise(monkeypatch):
+    """bf16 inference at B=128 with the opt-in DMC_HALO_PRO=1: the ResBlock convs that take the GN+SiLU
+    prologue on the halo kernel (dmc_conv_halo_prologue) give bitwise the output of the materialised path."""
+    from diffusion_models_collection_amd.models import UNet
+    torch.manual_seed(42)
+    cfg = dict(image_size=(32, 32), in_channels=3, model_channels=128, out_channels=3, num_res_blocks=2,
+               attention_resolutions=(16, 8), dropout=0.1, channel_mult=(1, 2, 2, 2), num_classes=None,
+               use_attention=True)
+    m = UNet(**cfg, compute_dtype="bf16").to(DEV).eval()
+    x = torch.randn(128, 3, 32, 32, device=DEV)
+    t = torch.randint(0, 1000, (128,), device=DEV)
+    outs = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("DMC_HALO_PRO", on)
+        with torch.no_grad():
+            outs.append(m(x, t).clone())
+    ex = m._executor if hasattr(m, "_executor") else None
+    if ex is not None:
+        assert any(v for k, v in ex._halo_pro_cache.items() if k[-1] == "1"), "halo prologue never taken"
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_cifar_unet_train_step_grads_match_oracle():
     """One training step's loss and parameter gradients (dropout 0) vs the oracle, fp32, B=2."""
     from diffusion_models_collection_amd.models import UNet
