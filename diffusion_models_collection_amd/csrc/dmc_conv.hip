@@ -1891,7 +1891,8 @@ int wgrad_splits(const dmc_conv_desc* d, int* pps) {
   const long M = (long)d->N * d->OH * d->OW;
   const long KK = (long)d->ntaps * d->Kc;
   const long tiles = (long)dmc::cdiv(KK, 128) * dmc::cdiv(d->Cout, 128);
-  long splits = (512 + tiles - 1) / tiles;
+  static const long target = getenv("DMC_WG_BLOCKS") ? atol(getenv("DMC_WG_BLOCKS")) : 512;   // A/B knob
+  long splits = (target + tiles - 1) / tiles;
   const long max_splits = (M + 4 * sp - 1) / (4 * sp);  // at least 4 stages per split
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
