@@ -349,18 +349,31 @@ __global__ void scale_kernel(const dmc_tensor_ref* refs, const float* coef) {
 // ---------------- flat optimizer step ----------------
 // Parameters, gradients, AdamW moments and the EMA copy live in flat fp32 buffers with one common layout
 // (the executor's gradient order), so clip + AdamW + EMA are one streaming pass over 37 M elements.
-constexpr int kNormBlocks = 1024;
+constexpr int kNormBlocks = 1024;   // 4096 measured no faster (34 us: the walk reads ~4.4 TB/s either way)
 __global__ __launch_bounds__(256) void flat_sumsq_kernel(const float* g, long n, float* partial) {
   // block b sums the contiguous range [b*per, (b+1)*per): fixed order, deterministic
   const long per = ((n + kNormBlocks - 1) / kNormBlocks + 3) & ~3L;
   const long b0 = blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
-  float s = 0.f;
+  // four 16-byte loads in flight per thread (one at a time left the walk latency-bound: 35 us for 148 MB),
+  // four accumulators combined in a fixed order
+  float s = 0.f, sa[4] = {0.f, 0.f, 0.f, 0.f};
   long i = b0 + threadIdx.x * 4;
+  for (; i + 3 * 1024 + 3 < b1; i += 4 * 1024) {
+    v4f v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *(const v4f*)(g + i + u * 1024);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sa[u] = fmaf(v[u][0], v[u][0], sa[u]); sa[u] = fmaf(v[u][1], v[u][1], sa[u]);
+      sa[u] = fmaf(v[u][2], v[u][2], sa[u]); sa[u] = fmaf(v[u][3], v[u][3], sa[u]);
+    }
+  }
   for (; i + 3 < b1; i += 1024) {
     const v4f v = *(const v4f*)(g + i);
     s = fmaf(v[0], v[0], s); s = fmaf(v[1], v[1], s); s = fmaf(v[2], v[2], s); s = fmaf(v[3], v[3], s);
   }
   for (; i < b1; ++i) s = fmaf(g[i], g[i], s);
+  s += (sa[0] + sa[1]) + (sa[2] + sa[3]);
   __shared__ float red[4];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;

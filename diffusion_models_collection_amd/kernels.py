@@ -378,7 +378,7 @@ def clip_grad_norm(refs: TensorRefs, max_norm):
 def grad_norm_flat(g, max_norm):
     """(total_norm, clip coef) of a flat fp32 gradient buffer, both device scalars; no host sync."""
     out = torch.empty(2, dtype=torch.float32, device=g.device)
-    ws = SCRATCH.get(1024 * 4, g.device)
+    ws = SCRATCH.get(1024 * 4, g.device)   # one partial per dmc_grad_norm_flat block
     check(LIB.dmc_grad_norm_flat(ptr(g), g.numel(), float(max_norm), ptr(out), out.data_ptr() + 4, ptr(ws),
                                  L.stream()), "dmc_grad_norm_flat")
     return out[0], out[1:]
