@@ -99,6 +99,7 @@ def _load():
         "dmc_adamw_flat": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_long, _c_p] + [_c_f] * 9 + [_c_p]),
         "dmc_adamw_flat_dev": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_long, _c_p, _c_p, _c_p]),
         "dmc_silu_fwd": (_c_int, [_c_p, _c_p, _c_long, _c_p]),
+        "dmc_upsample2x_nhwc": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_int, _c_p]),
         "dmc_unpack_output": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p]),
         "dmc_add": (_c_int, [_c_int, _c_p, _c_p, _c_long, _c_p]),
     }

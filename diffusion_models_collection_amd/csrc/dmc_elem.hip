@@ -476,6 +476,27 @@ __global__ void add_kernel(T* y, const T* x, long n) {
   }
 }
 
+// Nearest x2 upsample of an NHWC activation (models/unet.py:118 F.interpolate(scale_factor=2, mode='nearest')),
+// materialised for the halo weight-gradient kernel: one 16-byte chunk read, four written per thread.
+__global__ __launch_bounds__(256) void upsample2x_nhwc_kernel(const char* x, int N, int H, int W, int cb, int ldb,
+                                                              char* y, int ldyb) {
+  const int chunks = cb / 16;
+  const long total = (long)N * H * W * chunks;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % chunks);
+    const long pix = i / chunks;
+    const int w = (int)(pix % W);
+    const long nh = pix / W;
+    const int h = (int)(nh % H), n = (int)(nh / H);
+    const v4i v = *(const v4i*)(x + pix * ldb + ch * 16);
+    const long o = (((long)n * 2 * H + 2 * h) * 2 * W + 2 * w) * ldyb + ch * 16;
+    *(v4i*)(y + o) = v;
+    *(v4i*)(y + o + ldyb) = v;
+    *(v4i*)(y + o + (long)2 * W * ldyb) = v;
+    *(v4i*)(y + o + (long)2 * W * ldyb + ldyb) = v;
+  }
+}
+
 __global__ void silu_kernel(const float* x, float* y, long n) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float v = x[i];
@@ -596,6 +617,18 @@ extern "C" int dmc_add(int dtype, void* y, const void* x, long n, void* stream) 
   if (dtype == DMC_F32) add_kernel<float><<<grid_for(n), 256, 0, s>>>((float*)y, (const float*)x, n);
   else add_kernel<bf16_t><<<grid_for(n), 256, 0, s>>>((bf16_t*)y, (const bf16_t*)x, n);
   return dmc::check_launch("dmc_add");
+}
+
+extern "C" int dmc_upsample2x_nhwc(int dtype, const void* x, int N, int H, int W, int C, int ld, void* y, int ldy,
+                                   void* stream) {
+  const int esz = dtype == DMC_F32 ? 4 : 2;
+  DMC_REQUIRE((C * esz) % 16 == 0 && (ld * esz) % 16 == 0 && (ldy * esz) % 16 == 0 && ld >= C && ldy >= C,
+              "upsample2x: channels/pitches must be 16-byte multiples (C=%d ld=%d ldy=%d)", C, ld, ldy);
+  const long total = (long)N * H * W * (C * esz / 16);
+  if (total == 0) return 0;
+  upsample2x_nhwc_kernel<<<grid_for(total, 256, 16384), 256, 0, dmc::as_stream(stream)>>>(
+      (const char*)x, N, H, W, C * esz, ld * esz, (char*)y, ldy * esz);
+  return dmc::check_launch("dmc_upsample2x_nhwc");
 }
 
 extern "C" int dmc_silu_fwd(const float* x, float* y, long n, void* stream) {

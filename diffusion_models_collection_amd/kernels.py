@@ -137,6 +137,15 @@ def conv(d, x1, x2, w, y1, y2=None):
                                                       ptr(ws), nbytes, L.stream()), "dmc_conv2d"))
 
 
+def upsample2x(dtype, x, C):
+    """Nearest x2 upsample of an NHWC [N, H, W, ld] activation's first C channels -> [N, 2H, 2W, C]."""
+    N, H, W, ld = x.shape
+    y = torch.empty(N, 2 * H, 2 * W, C, dtype=x.dtype, device=x.device)
+    check(LIB.dmc_upsample2x_nhwc(L.dtype_code(dtype), ptr(x), N, H, W, C, ld, ptr(y), C, L.stream()),
+          "dmc_upsample2x_nhwc")
+    return y
+
+
 def conv_halo_prologue(d):
     """True when dmc_conv2d applies d's GN-affine+SiLU prologue on the halo kernel's resident halo."""
     return bool(LIB.dmc_conv_halo_prologue(ctypes.byref(d)))

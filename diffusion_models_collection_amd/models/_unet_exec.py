@@ -641,8 +641,7 @@ class UNetExecutor:
                         # weight gradient over the materialised nearest-x2 input: the halo wgrad kernel (x halo
                         # in LDS for all 9 taps) on it is ~4x faster than the strided upsample-mode kernel,
                         # and the 2x2 replication costs one streaming pass
-                        C = a.t.shape[-1]
-                        up = a.t[:, :, None, :, None, :].expand(N, a.H, 2, a.W, 2, C).reshape(N, 2 * a.H, 2 * a.W, C)
+                        up = K.upsample2x(dt, a.t, a.t.shape[-1])
                         self._wgrad([Act(up, 2 * a.H, 2 * a.W, a.C)], dy, out.C, K.TAPS3, out.H, out.W, out.C,
                                     gv(layer.conv.weight))
                     else:

@@ -230,6 +230,11 @@ int dmc_adamw_flat(float* p, const float* g, float* m, float* v, float* ema, lon
  * the training step replays with the current learning rate and bias corrections (one H2D copy per step). */
 int dmc_adamw_flat_dev(float* p, const float* g, float* m, float* v, float* ema, long n, const float* coef,
                        const float* hyper, void* stream);
+/* y[n][2h+i][2w+j][c] = x[n][h][w][c] (i, j in {0,1}): nearest x2 upsample of an NHWC activation
+ * (models/unet.py:118 F.interpolate(scale_factor=2, mode='nearest')), materialised as the operand of the
+ * Upsample conv's weight gradient. C*esize, ld*esize and ldy*esize must be multiples of 16 bytes. */
+int dmc_upsample2x_nhwc(int dtype, const void* x, int N, int H, int W, int C, int ld, void* y, int ldy,
+                        void* stream);
 /* y = silu(x) (fp32); NHWC dtype -> NCHW fp32 (the inverse of dmc_pack_input); y += x (dtype). */
 int dmc_silu_fwd(const float* x, float* y, long n, void* stream);
 int dmc_unpack_output(int dtype, const void* src, int ld, int N, int C, int H, int W, float* dst,

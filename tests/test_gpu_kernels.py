@@ -109,6 +109,20 @@ def test_conv_forward(dt, case, monkeypatch):
     assert rel_err(got, yr) < (1e-5 if dt == torch.float32 else 2e-2), rel_err(got, yr)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_upsample2x_nhwc_bitwise(dt):
+    """Nearest x2 upsample (models/unet.py:118) of an NHWC activation with a padded channel pitch: bitwise equal
+    to torch's nearest interpolate of the same values."""
+    L, K = _lib()
+    torch.manual_seed(4)
+    N, H, W, C, ld = 3, 5, 7, 40, 48
+    x = torch.randn(N, H, W, ld).to(dt).to(DEV)
+    y = K.upsample2x(dt, x, C)
+    torch.cuda.synchronize()
+    ref = F.interpolate(x[..., :C].permute(0, 3, 1, 2).float(), scale_factor=2, mode="nearest")
+    assert torch.equal(y.permute(0, 3, 1, 2).float(), ref)
+
+
 @pytest.mark.parametrize("case", ["c32_two_sources", "c16_wide", "c32_384", "c8_multi_image"])
 def test_conv3x3_halo_gn_silu_prologue(case, monkeypatch):
     """Inference prologue on the halo kernel: conv(SiLU(x*scale+shift)) with the GroupNorm affine + SiLU
