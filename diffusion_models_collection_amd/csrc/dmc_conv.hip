@@ -1774,7 +1774,7 @@ RegPlan plan_reg(const ConvK& k) {
   const long t64 = (long)dmc::cdiv(k.M, 64) * dmc::cdiv(k.Cout, 64);
   if (t64 >= 256 || nst < 16) return p;   // e.g. the 128 x 512 x 4992 time-embedding GEMM: 156 tiles -> split 2
   int sp = (int)((256 + t64 - 1) / t64);
-  if (sp > nst / 8) sp = nst / 8;
+  if (sp > nst / 4) sp = nst / 4;   // >= 4 stages per split (the K=512 time-embedding GEMMs: 4 splits)
   if (sp > 16) sp = 16;
   if (sp < 2) return p;
   p.per = (nst + sp - 1) / sp;
