@@ -1438,9 +1438,12 @@ __global__ __launch_bounds__(512) void wgrad3x3_halo_kernel(ConvK a, const char*
     for (int u = 0; u < 9; ++u) acc[i][u] = v4f{0.f, 0.f, 0.f, 0.f};
 
   const int nt_blk = t_end - t_begin, nst = nt_blk * 4;
+  // the next tile's halo goes out in three parts (slots k = 0, 1, 2 of a tile): pieces [part_b(k), part_b(k+1))
+  // -- all HP of them (HP = 7 included: 2 + 2 + 3)
+  auto part_b = [](int k) { return k * HP / 3; };
   auto slot_count = [&](int st) {   // vector-memory instructions issued in slot st
     const int k = st & 3;
-    return (st + 2 < nst ? 2 : 0) + ((k < 3 && (st >> 2) + 1 < nt_blk) ? 2 : 0);
+    return (st + 2 < nst ? 2 : 0) + ((k < 3 && (st >> 2) + 1 < nt_blk) ? part_b(k + 1) - part_b(k) : 0);
   };
   if (nst > 0) {
     halo_offsets(t_begin);
@@ -1459,7 +1462,7 @@ __global__ __launch_bounds__(512) void wgrad3x3_halo_kernel(ConvK a, const char*
     const int tl = st >> 2, k = st & 3;
     if (st + 2 < nst) dy_issue(st + 2);
     if (k < 3 && tl + 1 < nt_blk) {
-      halo_issue_w((tl + 1) & 1, 2 * k, 2 * k + 2);
+      halo_issue_w((tl + 1) & 1, part_b(k), part_b(k + 1));
       if (k == 2 && tl + 2 < nt_blk) halo_offsets(t_begin + tl + 2);
     }
     const char* X = lds + (tl & 1) * HB;

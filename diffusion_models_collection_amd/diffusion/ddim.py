@@ -4,53 +4,20 @@ Same constructor (:27-36), attributes, inference timesteps (linspace(T-1, 0, S).
 built on the host so they are bit-identical) and methods (q_sample :87, p_losses :109, _extract :145,
 p_sample :154, sample :210, sample_with_cfg :251, set_inference_steps :348).
 
+Sampling loops replay one captured HIP graph per step after the first (diffusion/_graph.py).
 The per-step update is ONE fused kernel (dmc_ddim_step): alpha gathers on device, x0 prediction,
 clamp, sigma, direction term and the eta>0 noise. The reference's `t_next.min() >= 0` host sync (:176)
 is done on device: if any t_next < 0, alpha_next = 1 for the whole batch, exactly as the reference.
 CFG batches the cond/uncond forwards into one 2B forward and fuses combine + x0 + dynamic threshold
 (per-row torch.quantile restatement) into dmc_cfg_x0.
 """
-import os
-
 import torch
 from tqdm import tqdm
 
 from .. import kernels as K
+from . import _schedule
+from ._graph import StepGraph, run_loop
 from .ddpm import DDPM, _require_cuda, diffusion_loss, make_betas
-
-
-class _StepGraph:
-    """One DDIM step (UNet forward + the fused update) captured as a HIP graph and replayed for the remaining
-    steps of a sampling loop: a step is ~300 kernel launches whose Python/ctypes enqueue is about as long as the
-    GPU work at B=128. Inputs x / t / t_next live in static buffers refreshed by device copies before each
-    replay; the output buffer is returned (the next step copies it in). Deterministic steps only (eta = 0), so
-    a replay computes bitwise what p_sample computes (tests/test_gpu_model.py). The graph lives for one
-    sample() call (the weights may change between calls)."""
-
-    def __init__(self, ddim, model, x, t, t_next, y):
-        self.x_s, self.t_s, self.tn_s = x.clone(), t.clone(), t_next.clone()
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.out = ddim.p_sample(model, self.x_s, self.t_s, self.tn_s, y)
-
-    def step(self, x, t, t_next):
-        self.x_s.copy_(x)
-        self.t_s.copy_(t)
-        self.tn_s.copy_(t_next)
-        self.graph.replay()
-        return self.out
-
-    @staticmethod
-    def eligible(ddim, model, x, return_all):
-        """DMC_GRAPH=0 / 1 turns the replay off / on; by default it is used for batches of <= 32, where the
-        step's host enqueue exceeds its GPU time (at B=128 the step is GPU-bound and a per-call capture only
-        adds its own cost: 569 vs 602 img/s measured)."""
-        mode = os.environ.get("DMC_GRAPH")
-        if mode == "0" or ddim.eta != 0 or return_all or not x.is_cuda:
-            return False
-        if getattr(model, "executor", None) is None or model.training:
-            return False
-        return mode == "1" or x.shape[0] <= 32
 
 
 class DDIM:
@@ -62,22 +29,17 @@ class DDIM:
         self.num_inference_steps = num_inference_steps
         self.eta = eta
         self.device = device
-        betas = make_betas(num_timesteps, beta_start, beta_end, beta_schedule)
-        alphas = 1.0 - betas
-        ac = torch.cumprod(alphas, dim=0)
-        self.betas = betas.to(device)
-        self.alphas = alphas.to(device)
-        self.alphas_cumprod = ac.to(device)
-        self.sqrt_alphas_cumprod = torch.sqrt(ac).to(device)
-        self.sqrt_one_minus_alphas_cumprod = torch.sqrt(1.0 - ac).to(device)
+        tabs = _schedule.build_tables(num_timesteps, beta_start, beta_end, beta_schedule)
+        for k in ("betas", "alphas", "alphas_cumprod", "sqrt_alphas_cumprod", "sqrt_one_minus_alphas_cumprod"):
+            setattr(self, k, torch.from_numpy(tabs[k]).to(device))
         self._setup_inference_timesteps()
 
     def _cosine_beta_schedule(self, timesteps, s=0.008, device='cuda'):
         return make_betas(timesteps, 0, 0, "cosine").to(device)
 
     def _setup_inference_timesteps(self):
-        ts = torch.linspace(self.num_timesteps - 1, 0, self.num_inference_steps)
-        self.inference_timesteps = ts.round().long().to(self.device)
+        ts = _schedule.ddim_timesteps(self.num_timesteps, self.num_inference_steps)
+        self.inference_timesteps = torch.from_numpy(ts).to(self.device)
 
     def _tab(self, name, dev):
         v = getattr(self, name)
@@ -128,36 +90,47 @@ class DDIM:
         tab = torch.cat([ts, torch.full((1,), -1, dtype=torch.long, device=dev)])
         return tab.view(-1, 1).expand(-1, batch_size).contiguous()
 
+    def _noise(self, noise, i, x):
+        if self.eta <= 0:
+            return None
+        if noise is None:
+            return torch.randn_like(x)
+        return noise(i) if callable(noise) else noise[i].to(x.device)
+
     @torch.no_grad()
-    def sample(self, model, shape, y=None, return_all_timesteps=False, x_T=None):
-        """DDIM sampling loop (diffusion/ddim.py:210-249)."""
+    def sample(self, model, shape, y=None, return_all_timesteps=False, x_T=None, noise=None):
+        """DDIM sampling loop (diffusion/ddim.py:210-249). Optional (not in the reference): x_T, and for eta > 0
+        noise = [S, B, C, H, W] tensor or callable i -> tensor. Steps after the first replay one captured HIP
+        graph (diffusion/_graph.py)."""
         batch_size = shape[0]
         device = self.device
         img = torch.randn(shape, device=device) if x_T is None else x_T.to(device).float()
         imgs = []
         tab = self._ts_table(batch_size, img.device)
         S = len(self.inference_timesteps)
-        graph = None
-        use_graph = _StepGraph.eligible(self, model, img, return_all_timesteps)
-        for i in tqdm(range(S), desc='DDIM Sampling'):
-            if graph is None and use_graph and i >= 1:     # step 0 ran eagerly: caches and packs are in place
-                try:
-                    graph = _StepGraph(self, model, img, tab[i], tab[i + 1], y)
-                except Exception:   # noqa: BLE001 -- capture problem: stay eager
-                    use_graph = False
-            if graph is not None:
-                img = graph.step(img, tab[i], tab[i + 1])
-            else:
-                img = self.p_sample(model, img, tab[i], tab[i + 1], y)
+        bar = tqdm(total=S, desc='DDIM Sampling')
+
+        def inputs(i, x):
+            z = self._noise(noise, i, x)
+            return (x, tab[i], tab[i + 1]) + ((z,) if z is not None else ())
+
+        def fn(x, t, tn, z=None):
+            return self.p_sample(model, x, t, tn, y, noise=z)
+
+        def record(i, x):
+            bar.update(1)
             if return_all_timesteps:
-                imgs.append(img.cpu())
+                imgs.append(x.cpu())
+
+        img = run_loop(img, S, inputs, fn, StepGraph.eligible(model, img, True, False), record)
+        bar.close()
         if return_all_timesteps:
             return torch.stack(imgs, dim=0)
-        return img.clone() if graph is not None else img
+        return img
 
     @torch.no_grad()
     def sample_with_cfg(self, model, shape, y, cfg_scale=3.0, p_threshold=0.995, return_all_timesteps=False,
-                        x_T=None):
+                        x_T=None, noise=None):
         """DDIM + classifier-free guidance + dynamic thresholding (diffusion/ddim.py:251-346)."""
         if y is None:
             raise ValueError("CFG sampling requires class labels y.")
@@ -172,14 +145,25 @@ class DDIM:
         tab = self._ts_table(batch_size, dev)
         ac = self._tab("alphas_cumprod", dev)
         S = len(self.inference_timesteps)
-        for i in tqdm(range(S), desc=f"DDIM sampling with CFG scale {cfg_scale}"):
-            t = tab[i]
-            eps_c, eps_u = DDPM._cfg_eps(model, img, t, y)
-            eps_g, x0 = K.cfg_x0(img.contiguous(), eps_c.contiguous(), eps_u.contiguous(), cfg_scale, t, ac, None, 0,
+        bar = tqdm(total=S, desc=f"DDIM sampling with CFG scale {cfg_scale}")
+
+        def inputs(i, x):
+            z = self._noise(noise, i, x)
+            return (x, tab[i], tab[i + 1]) + ((z,) if z is not None else ())
+
+        def fn(x, t, tn, z=None):
+            eps_c, eps_u = DDPM._cfg_eps(model, x, t, y)
+            eps_g, x0 = K.cfg_x0(x.contiguous(), eps_c.contiguous(), eps_u.contiguous(), cfg_scale, t, ac, None, 0,
                                  p_threshold)
-            img = self.p_sample(model, img, t, tab[i + 1], y=None, clip_denoised=False, eps=eps_g, x0_pred=x0)
+            return self.p_sample(model, x, t, tn, y=None, clip_denoised=False, eps=eps_g, x0_pred=x0, noise=z)
+
+        def record(i, x):
+            bar.update(1)
             if return_all_timesteps:
-                imgs.append(img.cpu())
+                imgs.append(x.cpu())
+
+        img = run_loop(img, S, inputs, fn, StepGraph.eligible(model, img, True, False), record)
+        bar.close()
         if return_all_timesteps:
             return torch.stack(imgs, dim=0)
         return img

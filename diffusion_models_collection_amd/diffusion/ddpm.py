@@ -9,8 +9,8 @@ Arithmetic runs in fused HIP kernels (libdmc.so):
   CFG + threshold     -> dmc_cfg_x0 (combine, x0, per-row quantile, clamp, one launch)
 The cond/uncond forwards of CFG are batched into ONE 2B forward.
 
-Schedule tables are built on the host with the reference's exact fp32 op sequence (so they are
-bit-identical to the reference's), then uploaded once.
+Schedule tables are built on the host by _schedule.py: the reference's op sequence as explicit IEEE fp32
+numpy arithmetic (identical bits on every host), then uploaded once.
 
 Extra optional keyword arguments (not in the reference, all default to the reference behaviour):
 p_sample(noise=...), sample(x_T=...), sample_with_cfg(x_T=...) inject the Gaussian draws for parity tests.
@@ -20,26 +20,13 @@ import torch.nn.functional as F
 from tqdm import tqdm
 
 from .. import kernels as K
-
-
-def _cosine_betas(timesteps, s=0.008):
-    # diffusion/ddpm.py:73-82, on the host in fp32
-    steps = timesteps + 1
-    x = torch.linspace(0, timesteps, steps)
-    ac = torch.cos(((x / timesteps) + s) / (1 + s) * torch.pi * 0.5) ** 2
-    ac = ac / ac[0]
-    betas = 1 - (ac[1:] / ac[:-1])
-    return torch.clip(betas, 0.0001, 0.9999)
+from . import _schedule
+from ._graph import StepGraph, run_loop
 
 
 def make_betas(num_timesteps, beta_start, beta_end, beta_schedule):
-    if beta_schedule == "linear":
-        return torch.linspace(beta_start, beta_end, num_timesteps)
-    if beta_schedule == "cosine":
-        return _cosine_betas(num_timesteps)
-    if beta_schedule == "quadratic":
-        return torch.linspace(beta_start ** 0.5, beta_end ** 0.5, num_timesteps) ** 2
-    raise ValueError(f"Unknown beta schedule: {beta_schedule}")
+    """Beta schedule (diffusion/ddpm.py:39-46, cosine :73-82) as an fp32 CPU tensor (see _schedule.py)."""
+    return torch.from_numpy(_schedule.make_betas(num_timesteps, beta_start, beta_end, beta_schedule))
 
 
 def _require_cuda(*ts):
@@ -80,31 +67,12 @@ class DDPM:
     def __init__(self, num_timesteps=1000, beta_start=0.0001, beta_end=0.02, beta_schedule='linear', device='cuda'):
         self.num_timesteps = num_timesteps
         self.device = device
-        betas = make_betas(num_timesteps, beta_start, beta_end, beta_schedule)
-        alphas = 1.0 - betas
-        ac = torch.cumprod(alphas, dim=0)
-        ac_prev = F.pad(ac[:-1], (1, 0), value=1.0)
-        tabs = {
-            "betas": betas,
-            "alphas": alphas,
-            "alphas_cumprod": ac,
-            "alphas_cumprod_prev": ac_prev,
-            "sqrt_alphas_cumprod": torch.sqrt(ac),
-            "sqrt_one_minus_alphas_cumprod": torch.sqrt(1.0 - ac),
-            "sqrt_recip_alphas": torch.sqrt(1.0 / alphas),
-            "sqrt_recipm1_alphas_cumprod": torch.sqrt(1.0 / ac - 1),
-            "posterior_variance": betas * (1.0 - ac_prev) / (1.0 - ac),
-        }
-        tabs["posterior_log_variance_clipped"] = torch.log(torch.clamp(tabs["posterior_variance"], min=1e-20))
-        tabs["posterior_mean_coef1"] = betas * torch.sqrt(ac_prev) / (1.0 - ac)
-        tabs["posterior_mean_coef2"] = (1.0 - ac_prev) * torch.sqrt(alphas) / (1.0 - ac)
-        # recomputed by the reference on every p_mean_variance call (:170-171); identical values
-        tabs["sqrt_recip_alphas_cumprod"] = torch.sqrt(1.0 / ac)
+        tabs = _schedule.build_tables(num_timesteps, beta_start, beta_end, beta_schedule)
         for k, v in tabs.items():
-            setattr(self, k, v.to(device))
+            setattr(self, k, torch.from_numpy(v).to(device))
 
     def _cosine_beta_schedule(self, timesteps, s=0.008, device='cuda'):
-        return _cosine_betas(timesteps, s).to(device)
+        return make_betas(timesteps, 0, 0, "cosine").to(device)
 
     def _tab(self, name, dev):
         v = getattr(self, name)
@@ -165,18 +133,38 @@ class DDPM:
         _require_cuda(x, eps, noise)
         return self._step(x, eps, t, clip_denoised, x0_pred, noise)
 
+    def _noise(self, noise, i, x):
+        """Loop step i's Gaussian draw: the injected noise[i] (parity tests) or torch.randn_like(x)."""
+        if noise is None:
+            return torch.randn_like(x)
+        return noise(i) if callable(noise) else noise[i].to(x.device)
+
     @torch.no_grad()
-    def sample(self, model, shape, y=None, return_all_timesteps=False, x_T=None):
-        """Ancestral sampling over all timesteps (diffusion/ddpm.py:222-252)."""
+    def sample(self, model, shape, y=None, return_all_timesteps=False, x_T=None, noise=None):
+        """Ancestral sampling over all timesteps (diffusion/ddpm.py:222-252). Optional (not in the reference):
+        x_T, and noise = [T, B, C, H, W] tensor or callable i -> tensor, the z of loop step i (t = T-1-i).
+        Steps after the first replay one captured HIP graph (diffusion/_graph.py)."""
         batch_size = shape[0]
         device = self.device
         img = torch.randn(shape, device=device) if x_T is None else x_T.to(device).float()
+        T = self.num_timesteps
+        ts = torch.arange(T, device=img.device).view(-1, 1).expand(-1, batch_size).contiguous()
         imgs = []
-        ts = torch.arange(self.num_timesteps, device=img.device).view(-1, 1).expand(-1, batch_size).contiguous()
-        for i in tqdm(reversed(range(0, self.num_timesteps)), desc='Sampling', total=self.num_timesteps):
-            img = self.p_sample(model, img, ts[i], y)
+        bar = tqdm(total=T, desc='Sampling')
+
+        def inputs(i, x):
+            return x, ts[T - 1 - i], self._noise(noise, i, x)
+
+        def fn(x, t, z):
+            return self.p_sample(model, x, t, y, noise=z)
+
+        def record(i, x):
+            bar.update(1)
             if return_all_timesteps:
-                imgs.append(img.cpu())
+                imgs.append(x.cpu())
+
+        img = run_loop(img, T, inputs, fn, StepGraph.eligible(model, img, True, False), record)
+        bar.close()
         if return_all_timesteps:
             return torch.stack(imgs, dim=0)
         return img
@@ -190,8 +178,8 @@ class DDPM:
 
     @torch.no_grad()
     def sample_with_cfg(self, model, shape, y, cfg_scale=3.0, p_threshold=0.995, return_all_timesteps=False,
-                        x_T=None):
-        """Classifier-free guidance + dynamic thresholding (diffusion/ddpm.py:254-332)."""
+                        x_T=None, noise=None):
+        """Classifier-free guidance + dynamic thresholding (diffusion/ddpm.py:254-332); x_T / noise as sample()."""
         if y is None:
             raise ValueError("CFG sampling requires class labels y.")
         if p_threshold is not None and not (0.0 < float(p_threshold) < 1.0):
@@ -202,17 +190,27 @@ class DDPM:
         imgs = []
         y = y.to(img.device)
         dev = img.device
-        ts = torch.arange(self.num_timesteps, device=dev).view(-1, 1).expand(-1, batch_size).contiguous()
-        for i in tqdm(reversed(range(0, self.num_timesteps)), desc=f'DDPM Sampling with CFG scale {cfg_scale}',
-                      total=self.num_timesteps):
-            t = ts[i]
-            eps_c, eps_u = self._cfg_eps(model, img, t, y)
-            eps_g, x0 = K.cfg_x0(img.contiguous(), eps_c.contiguous(), eps_u.contiguous(), cfg_scale, t,
+        T = self.num_timesteps
+        ts = torch.arange(T, device=dev).view(-1, 1).expand(-1, batch_size).contiguous()
+        bar = tqdm(total=T, desc=f'DDPM Sampling with CFG scale {cfg_scale}')
+
+        def inputs(i, x):
+            return x, ts[T - 1 - i], self._noise(noise, i, x)
+
+        def fn(x, t, z):
+            eps_c, eps_u = self._cfg_eps(model, x, t, y)
+            eps_g, x0 = K.cfg_x0(x.contiguous(), eps_c.contiguous(), eps_u.contiguous(), cfg_scale, t,
                                  self._tab("sqrt_recip_alphas_cumprod", dev),
                                  self._tab("sqrt_recipm1_alphas_cumprod", dev), 1, p_threshold)
-            img = self.p_sample(model, img, t, y=None, clip_denoised=False, eps=eps_g, x0_pred=x0)
+            return self.p_sample(model, x, t, y=None, clip_denoised=False, eps=eps_g, x0_pred=x0, noise=z)
+
+        def record(i, x):
+            bar.update(1)
             if return_all_timesteps:
-                imgs.append(img.cpu())
+                imgs.append(x.cpu())
+
+        img = run_loop(img, T, inputs, fn, StepGraph.eligible(model, img, True, False), record)
+        bar.close()
         if return_all_timesteps:
             return torch.stack(imgs, dim=0)
         return img

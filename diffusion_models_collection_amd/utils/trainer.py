@@ -128,9 +128,13 @@ class FlatAdamW:
         if len(steps) > 1:
             raise RuntimeError(f"FlatAdamW: parameters have different step counts {sorted(steps)}")
         self.t = int(steps.pop()) if steps else 0
-        self.step_t = torch.tensor(float(self.t), dtype=torch.float32)
-        for p, o in self.slots:
-            st[p] = {"step": self.step_t, "exp_avg": self.flat_m[o:o + p.numel()].view(p.shape),
+        # one step tensor per parameter, as torch keeps them (a single shared tensor would be incremented once
+        # per parameter by a plain torch AdamW that loads the checkpoint): 0-dim views of distinct elements of
+        # one buffer, so a step updates all of them with one fill
+        self.steps_base = torch.full((len(self.slots),), float(self.t), dtype=torch.float32)
+        for i, (p, o) in enumerate(self.slots):
+            st[p] = {"step": self.steps_base[i],
+                     "exp_avg": self.flat_m[o:o + p.numel()].view(p.shape),
                      "exp_avg_sq": self.flat_v[o:o + p.numel()].view(p.shape)}
         self.state_obj = st
         self.flat_e = None
@@ -160,6 +164,9 @@ class FlatAdamW:
         return all(st.get(p, {}).get("exp_avg") is not None and
                    st[p]["exp_avg"].data_ptr() == self.flat_m.data_ptr() + 4 * o for p, o in self.slots[:1])
 
+    def _sync_steps(self):
+        self.steps_base.fill_(float(self.t))
+
     def grads_flat(self):
         flat = getattr(self.ex, "flat", None)
         if flat is None:
@@ -178,8 +185,7 @@ class FlatAdamW:
         if g is None:
             # the caller falls back to torch's optimizer.step(): give every parameter its own step counter
             # (torch increments each one) and re-bind from the optimizer state next time
-            for p, _ in self.slots:
-                self.opt.state[p]["step"] = torch.tensor(float(self.t), dtype=torch.float32)
+            self._sync_steps()
             self._bound = False
             return None
         total, coef = K.grad_norm_flat(g, max_norm if max_norm is not None else -1.0)
@@ -198,7 +204,7 @@ class FlatAdamW:
         grp = self.opt.param_groups[0]
         lr, (b1, b2), eps, wd = float(grp["lr"]), grp["betas"], grp["eps"], grp["weight_decay"]
         self.t += 1
-        self.step_t.fill_(float(self.t))
+        self.steps_base.fill_(float(self.t))
         bc1 = 1 - b1 ** self.t
         bc2 = 1 - b2 ** self.t
         use_ema = self.uses_ema(ema_decay)
@@ -457,6 +463,8 @@ class DiffusionTrainer:
         if self._ema_refs is None or self._ema_refs[0] != key:
             self._ema_refs = (key, K.TensorRefs(pairs, pairs[0][0].device))
         K.ema_update(self._ema_refs[1], self.ema_decay)
+        if getattr(self.ema_model, "executor", None) is not None:
+            self.ema_model.executor.wgen += 1      # raw-pointer update: the EMA executor must repack its weights
 
     def _clip(self, max_norm=1.0):
         """torch.nn.utils.clip_grad_norm_(params, max_norm) as one fused multi-tensor launch."""

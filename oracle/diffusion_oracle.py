@@ -9,6 +9,7 @@ utils/trainer.py of sunyzhi55/Diffusion_Models_Collection), written from the equ
   DDPM posterior    ddpm.py:151-220
   DDIM update       ddim.py:154-208
   CFG + threshold   ddim.py:300-325, ddpm.py:284-303
+  DDPM sample loops ddpm.py:222-332
   train step        utils/trainer.py:221-265 (clip 1.0 -> AdamW -> zero_grad -> EMA)
 Pinned by tests/test_oracle.py against tests/golden/ (fixtures produced by the reference itself).
 """
@@ -119,6 +120,31 @@ def ddim_sample(model_fn, ac_tab, ts, xT, y=None, eta=0.0, zs=None, cfg_scale=No
             x0 = dynamic_threshold(x0, p_threshold) if p_threshold is not None else x0.clamp(-1, 1)
             img = ddim_step(ac_tab, img, eps, tb, tn, eta, None if zs is None else zs[i], clip=False, x0=x0)
     return img
+
+
+def ddpm_sample(model_fn, tab, xT, zs, y=None, cfg_scale=None, p_threshold=0.995, snap=()):
+    """DDPM ancestral loop (ddpm.py:222-252) and its CFG variant (:254-332); zs[i] is the noise of loop step i
+    (t = T-1-i). Returns (final, [x after loop step s for s in snap])."""
+    img = xT
+    B = xT.shape[0]
+    T = tab["betas"].numel()
+    snaps = []
+    for i, ti in enumerate(reversed(range(T))):
+        t = torch.full((B,), ti, dtype=torch.long)
+        if cfg_scale is None:
+            img = ddpm_step(tab, img, model_fn(img, t, y), t, zs[i])
+        else:
+            ec = model_fn(img, t, y)
+            eu = model_fn(img, t, torch.zeros_like(y))
+            eps = eu + cfg_scale * (ec - eu)
+            nd = img.dim()
+            x0 = bcast((1.0 / tab["alphas_cumprod"]).sqrt(), t, nd) * img - bcast(
+                tab["sqrt_recipm1_alphas_cumprod"], t, nd) * eps
+            x0 = dynamic_threshold(x0, p_threshold) if p_threshold is not None else x0.clamp(-1, 1)
+            img = ddpm_step(tab, img, eps, t, zs[i], clip=False, x0=x0)
+        if i in snap:
+            snaps.append(img)
+    return img, snaps
 
 
 def ema_update(ema_sd, sd, decay):

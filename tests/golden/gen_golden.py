@@ -17,6 +17,19 @@ Fixture list (every array is float32 / int64 data, loaded with numpy.load(allow_
                      DDIM p_sample / sample trajectory (injected x_T), CFG+dynamic-threshold step
   trainer_traj.npz   5 DiffusionTrainer steps (dropout 0, injected t/noise), per-step loss,
                      final parameters and EMA
+  ddpm_sample.npz    DDPM.sample and DDPM.sample_with_cfg (diffusion/ddpm.py:222-332) on the tiny
+                     conditional UNet, T=1000, injected x_T and per-step z (numpy PCG64 standard normals,
+                     regenerated from their seeds by the tests); snapshots every 100 steps + final
+  unet_mnist.npz     full-width UNet at the MNIST shape (1x28x28, channel_mult=(1,2,2), 128 channels,
+                     BASELINE config #1) and
+  unet_64.npz        the CIFAR UNet params at 64x64 (BASELINE config #5): weights are NOT stored (the
+                     build's UNet reproduces the reference's initialisation from torch.manual_seed(1234);
+                     per-parameter checksums pin that), input, output, grad_x in full, and per parameter
+                     gradient sum / sum of squares / absmax plus 32 sampled entries
+  trainer_ckpt.pth   the reference's own save_checkpoint() dict after 2 trainer steps (tensors, numbers,
+                     strings and the config dict only: loads with torch.load(weights_only=True))
+  ckpt_resume.npz    the inputs of a 3rd step and the reference's loss / parameters / EMA after resuming
+                     from trainer_ckpt.pth and running it
 """
 import os
 import sys
@@ -230,9 +243,153 @@ def gen_trainer_traj():
     npz(OUT / "trainer_traj.npz", **arrs)
 
 
+def np_normal(seed, shape):
+    """Host-independent Gaussian draws (numpy PCG64 ziggurat, fp32): the tests regenerate them from the seed."""
+    return torch.from_numpy(np.random.default_rng(seed).standard_normal(shape, dtype=np.float32))
+
+
+def gen_ddpm_sample():
+    cfg = TINY_CFGS["unet_tiny_cond"]
+    torch.manual_seed(1234)
+    m = UNet(**cfg).float().eval()
+    B, shape = 2, (2, 3, 16, 16)
+    y = torch.tensor([3, 7])
+    ddpm = DDPM(1000, 1e-4, 0.02, "linear", device="cpu")
+    arrs = {"y": y, "xT_seed": np.array([100]), "z_seed": np.array([101]), "xT_seed_cfg": np.array([102]),
+            "z_seed_cfg": np.array([103])}
+    snap = list(range(99, 1000, 100))
+    arrs["snap_steps"] = np.array(snap)
+    orig_randn, orig_randn_like = torch.randn, torch.randn_like
+    for tag, xs, zsd, call in (
+            ("sample", 100, 101, lambda: ddpm.sample(m, shape, y, return_all_timesteps=True)),
+            ("cfg", 102, 103, lambda: ddpm.sample_with_cfg(m, shape, y, cfg_scale=3.0, return_all_timesteps=True))):
+        xT = np_normal(xs, shape)
+        zs = np_normal(zsd, (1000,) + shape)
+        it = iter(list(zs))
+        torch.randn = lambda *a, **kw: xT.clone()
+        torch.randn_like = lambda a, *k, **kw: next(it).clone()
+        try:
+            with torch.no_grad():
+                allt = call()
+        finally:
+            torch.randn, torch.randn_like = orig_randn, orig_randn_like
+        arrs[f"{tag}/snap"] = allt[snap]
+        arrs[f"{tag}/final"] = allt[-1]
+    npz(OUT / "ddpm_sample.npz", **arrs)
+
+
+BIG_CFGS = {
+    # BASELINE config #1 shape class: 28 -> 14 -> 7 maps, 1 channel, attention only in the 7x7 middle (L=49)
+    "unet_mnist": dict(image_size=(28, 28), in_channels=1, model_channels=128, out_channels=1, num_res_blocks=2,
+                       attention_resolutions=(16, 8), dropout=0.0, channel_mult=(1, 2, 2), num_classes=None,
+                       use_attention=True),
+    # BASELINE config #5: the CIFAR network at 64x64 (attention at 16 and 8, i.e. levels 2 and 3)
+    "unet_64": dict(image_size=(64, 64), in_channels=3, model_channels=128, out_channels=3, num_res_blocks=2,
+                    attention_resolutions=(16, 8), dropout=0.0, channel_mult=(1, 2, 2, 2), num_classes=None,
+                    use_attention=True),
+}
+NSAMP = 32
+
+
+def grad_summary(name, v, arrs, prefix):
+    v = v.detach().double().reshape(-1)
+    arrs[f"{prefix}sum/{name}"] = v.sum().reshape(1)
+    arrs[f"{prefix}sumsq/{name}"] = (v * v).sum().reshape(1)
+    arrs[f"{prefix}absmax/{name}"] = v.abs().max().reshape(1)
+    idx = np.random.default_rng(5).integers(0, v.numel(), NSAMP)
+    arrs[f"{prefix}idx/{name}"] = idx
+    arrs[f"{prefix}val/{name}"] = v[torch.from_numpy(idx)].float()
+
+
+def gen_big_unet(name, cfg, B=2):
+    torch.manual_seed(1234)
+    m = UNet(**cfg).float()
+    m.train()
+    g = torch.Generator().manual_seed(7)
+    C, (H, W) = cfg["in_channels"], cfg["image_size"]
+    x = torch.randn(B, C, H, W, generator=g).requires_grad_(True)
+    t = torch.tensor([17, 903][:B], dtype=torch.long)
+    out = m(x, t, None)
+    cot = torch.randn(out.shape, generator=g)
+    (out * cot).sum().backward()
+    arrs = {"x": x.detach(), "t": t, "out": out.detach(), "cot": cot, "grad_x": x.grad}
+    for k, v in m.state_dict().items():
+        arrs[f"psum/{k}"] = v.double().sum().reshape(1)
+        arrs[f"pabs/{k}"] = v.double().abs().sum().reshape(1)
+    for k, p in m.named_parameters():
+        grad_summary(k, p.grad, arrs, "g")
+    npz(OUT / f"{name}.npz", **arrs)
+
+
+def gen_checkpoint():
+    """reference save_checkpoint (utils/trainer.py:328-365) after 2 steps, then resume (:120-154) + 1 step."""
+    from utils import trainer as trainer_mod
+    cfg = dict(TINY_CFGS["unet_tiny_uncond"])
+    g = torch.Generator().manual_seed(31)
+    B = 4
+    images = [torch.rand(B, 3, 16, 16, generator=g) * 2 - 1 for _ in range(3)]
+    ts = [torch.randint(0, 1000, (B,), generator=g) for _ in range(3)]
+    noises = [torch.randn(B, 3, 16, 16, generator=g) for _ in range(3)]
+    ddpm = DDPM(1000, 1e-4, 0.02, "linear", device="cpu")
+    save_dir = Path("/tmp/gg_ckpt2")
+    config = {"epochs": 1, "save_dir": str(save_dir), "sample_dir": "/tmp/gg_smp2", "loss_type": "l2",
+              "use_ema": True, "ema_decay": 0.9, "model_type": "unet", "save_interval": 1000,
+              "model_params": {k: v for k, v in cfg.items() if k != "num_classes"}}
+    losses = []
+
+    def run(tr, imgs, tt, nn_):
+        t_it, n_it = iter(tt), iter(nn_)
+        orig_randint, orig_randn_like = torch.randint, torch.randn_like
+        orig_pl = ddpm.p_losses
+
+        def p_losses(model, x, t, y=None, noise=None, loss_type="l2"):
+            loss = orig_pl(model, x, t, y, noise=noise, loss_type=loss_type)
+            losses.append(loss.item())
+            return loss
+
+        ddpm.p_losses = p_losses
+        torch.randint = lambda *a, **kw: next(t_it)
+        torch.randn_like = lambda a, *k, **kw: next(n_it).clone()
+        try:
+            tr.train_loader = imgs
+            tr.train_epoch(1)
+        finally:
+            torch.randint, torch.randn_like = orig_randint, orig_randn_like
+            ddpm.p_losses = orig_pl
+
+    torch.manual_seed(1234)
+    m = UNet(**cfg).float()
+    opt = torch.optim.AdamW(m.parameters(), lr=2e-4, weight_decay=1e-4)
+    tr = trainer_mod.DiffusionTrainer(m, ddpm, images[:2], opt, None, device="cpu", config=config)
+    run(tr, images[:2], ts[:2], noises[:2])
+    tr.best_loss = 0.5
+    tr.save_checkpoint(1)
+    import shutil
+    shutil.copy(save_dir / "current_model.pth", OUT / "trainer_ckpt.pth")
+    # resume in a fresh trainer exactly as train.py would (new model + optimizer, resume_path)
+    torch.manual_seed(999)
+    m2 = UNet(**cfg).float()
+    opt2 = torch.optim.AdamW(m2.parameters(), lr=2e-4, weight_decay=1e-4)
+    tr2 = trainer_mod.DiffusionTrainer(m2, ddpm, images[2:], opt2, None, device="cpu", config=config,
+                                       resume_path=str(OUT / "trainer_ckpt.pth"))
+    run(tr2, images[2:], ts[2:], noises[2:])
+    arrs = {"images": torch.stack(images), "ts": torch.stack(ts), "noises": torch.stack(noises),
+            "losses": torch.tensor(losses), "start_epoch": np.array([tr2.start_epoch])}
+    for k, v in m2.state_dict().items():
+        arrs["final/" + k] = v
+    for k, v in tr2.ema_model.state_dict().items():
+        arrs["ema/" + k] = v
+    arrs["step_after"] = np.array([float(opt2.state[p]["step"]) for p in m2.parameters()])
+    npz(OUT / "ckpt_resume.npz", **arrs)
+
+
+GENERATORS = {"schedules": gen_schedules, "tiny": lambda: [gen_unet(n, c) for n, c in TINY_CFGS.items()],
+              "diffusion_ops": gen_diffusion_ops, "trainer_traj": gen_trainer_traj,
+              "ddpm_sample": gen_ddpm_sample, "big": lambda: [gen_big_unet(n, c) for n, c in BIG_CFGS.items()],
+              "checkpoint": gen_checkpoint}
+
+
 if __name__ == "__main__":
-    gen_schedules()
-    for n, c in TINY_CFGS.items():
-        gen_unet(n, c)
-    gen_diffusion_ops()
-    gen_trainer_traj()
+    # python tests/golden/gen_golden.py [name ...]   (default: every fixture)
+    for name in (sys.argv[1:] or list(GENERATORS)):
+        GENERATORS[name]()

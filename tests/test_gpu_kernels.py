@@ -226,7 +226,8 @@ def test_conv_dgrad_wgrad(dt, case):
 
 
 @pytest.mark.parametrize("variant", ["ring3", "ring4", "regw"])
-@pytest.mark.parametrize("case", ["fwd32_concat", "fwd16_ragged_cout", "dgrad32", "fwd8_multi_image", "fallback_4x4"])
+@pytest.mark.parametrize("case", ["fwd32_concat", "fwd16_ragged_cout", "dgrad32", "fwd8_multi_image", "fallback_4x4",
+                                  "fwd8_concat_b128", "fwd64_rows"])
 def test_conv3x3_halo_kernel(case, variant, monkeypatch):
     """bf16 3x3 stride-1 convs on the LDS-halo kernel (whole-row 256-pixel tiles) vs an fp32 reference and
     vs the per-tap kernel (DMC_NO_HALO) on the same inputs. Variants: 3- or 4-slot LDS-DMA weight ring
@@ -246,6 +247,12 @@ def test_conv3x3_halo_kernel(case, variant, monkeypatch):
         N, H, C1, C2, Cout, taps, pm = 1, 32, 192, 0, 64, K.TAPS3_DGRAD, L.PACK_DGRAD
     elif case == "fwd8_multi_image":
         N, H, C1, C2, Cout = 8, 8, 128, 64, 128   # 4 whole 8x8 images per 256-pixel tile (7 halo pieces/wave)
+    elif case == "fwd8_concat_b128":
+        # the UNet's 8x8 up blocks at B=128: 7 halo pieces per wave AND several 256-pixel tiles per wgrad block
+        # (round 2 fix: the 7th piece of the next tile's halo was never issued -> NaN weight gradients)
+        N, H, C1, C2, Cout = 128, 8, 256, 256, 256
+    elif case == "fwd64_rows":
+        N, H, C1, C2, Cout = 16, 64, 128, 0, 128  # 64-wide rows: 4-row tiles, 396 halo pixels (HP = 7)
     elif case == "fallback_4x4":
         N, H, C1, C2, Cout = 8, 4, 64, 0, 128     # halo of 16 images exceeds the LDS budget: per-tap kernel
     W = H

@@ -120,3 +120,103 @@ def test_oracle_trainer_trajectory():
         torch.testing.assert_close(sd[k].detach(), v, rtol=1e-4, atol=1e-6, msg=k)
     for k, v in split_params(g, "ema/").items():
         torch.testing.assert_close(ema[k], v, rtol=1e-4, atol=1e-6, msg=k)
+
+
+def np_normal(seed, shape):
+    """The fixture generator's host-independent Gaussian draws (tests/golden/gen_golden.py::np_normal)."""
+    import numpy as np
+    return torch.from_numpy(np.random.default_rng(seed).standard_normal(shape, dtype=np.float32))
+
+
+def test_oracle_ddpm_sample_loops():
+    """DDPM.sample / sample_with_cfg, 1000 steps, injected x_T and z (diffusion/ddpm.py:222-332)."""
+    g = load_golden("ddpm_sample")
+    orc, _ = make_oracle(split_params(load_golden("unet_tiny_cond"), "param/"), TINY["unet_tiny_cond"])
+    tab = DO.schedule()
+    f = lambda x, t, y: orc.forward(x, t, y)  # noqa: E731
+    shape = (2, 3, 16, 16)
+    snap = [int(s) for s in g["snap_steps"]]
+    with torch.no_grad():
+        for tag, cfg in (("sample", None), ("cfg", 3.0)):
+            xs, zs = (int(g["xT_seed"]), int(g["z_seed"])) if tag == "sample" else (int(g["xT_seed_cfg"]),
+                                                                                     int(g["z_seed_cfg"]))
+            fin, snaps = DO.ddpm_sample(f, tab, np_normal(xs, shape), np_normal(zs, (1000,) + shape), g["y"],
+                                        cfg_scale=cfg, snap=snap)
+            torch.testing.assert_close(fin, g[f"{tag}/final"], rtol=1e-4, atol=1e-4)
+            torch.testing.assert_close(torch.stack(snaps), g[f"{tag}/snap"], rtol=1e-4, atol=1e-4)
+
+
+BIG = {
+    "unet_mnist": dict(image_size=(28, 28), in_channels=1, model_channels=128, out_channels=1, num_res_blocks=2,
+                       attention_resolutions=(16, 8), dropout=0.0, channel_mult=(1, 2, 2), num_classes=None,
+                       use_attention=True),
+    "unet_64": dict(image_size=(64, 64), in_channels=3, model_channels=128, out_channels=3, num_res_blocks=2,
+                    attention_resolutions=(16, 8), dropout=0.0, channel_mult=(1, 2, 2, 2), num_classes=None,
+                    use_attention=True),
+}
+
+
+def big_init_state_dict(name):
+    """The build's UNet initialised from torch.manual_seed(1234), as the fixture generator initialised the
+    reference's; pinned against the fixture's per-tensor checksums."""
+    from diffusion_models_collection_amd.models import UNet
+    g = load_golden(name)
+    torch.manual_seed(1234)
+    sd = UNet(**BIG[name]).state_dict()
+    for k, v in sd.items():
+        assert float(v.double().sum()) == float(g[f"psum/{k}"]), k
+        assert float(v.double().abs().sum()) == float(g[f"pabs/{k}"]), k
+    return sd, g
+
+
+def check_grad_summary(name, grad, g, tol):
+    v = grad.detach().double().reshape(-1).cpu()
+    amax = float(g[f"gabsmax/{name}"])
+    scale = max(amax, 1e-12)
+    assert abs(float(v.abs().max()) - amax) <= tol * scale, (name, float(v.abs().max()), amax)
+    ref_n = float(g[f"gsumsq/{name}"]) ** 0.5
+    assert abs(float((v * v).sum()) ** 0.5 - ref_n) <= tol * max(ref_n, 1e-12) * 4, name
+    got = v[g[f"gidx/{name}"]].float()
+    assert (got - g[f"gval/{name}"]).abs().max().item() <= tol * scale, name
+
+
+@pytest.mark.parametrize("name", list(BIG))
+def test_oracle_big_unet_fwd_bwd(name):
+    """BASELINE configs #1 (MNIST 28x28, channel_mult (1,2,2)) and #5 (64x64) shapes, full width, B=2."""
+    sd0, g = big_init_state_dict(name)
+    orc, sd = make_oracle(sd0, BIG[name], requires_grad=True)
+    x = g["x"].clone().requires_grad_(True)
+    out = orc.forward(x, g["t"], None)
+    torch.testing.assert_close(out, g["out"], rtol=1e-4, atol=1e-4)
+    (out * g["cot"]).sum().backward()
+    torch.testing.assert_close(x.grad, g["grad_x"], rtol=1e-3, atol=1e-4)
+    for k, p in sd.items():
+        if p.grad is not None:
+            check_grad_summary(k, p.grad, g, 1e-3)
+
+
+def test_oracle_checkpoint_resume():
+    """utils/trainer.py:120-154 resume + one step (:221-265) from the reference's own checkpoint dict."""
+    from pathlib import Path
+    ck = torch.load(Path(__file__).parent / "golden" / "trainer_ckpt.pth", weights_only=True)
+    g = load_golden("ckpt_resume")
+    assert ck["epoch"] == 1 and int(g["start_epoch"]) == 2
+    cfg = dict(TINY["unet_tiny_uncond"])
+    orc, sd = make_oracle(ck["model_state_dict"], cfg, requires_grad=True)
+    params = list(sd.values())
+    opt = torch.optim.AdamW(params, lr=2e-4, weight_decay=1e-4)
+    opt.load_state_dict(ck["optimizer_state_dict"])
+    ema = {k: v.clone() for k, v in ck["ema_model_state_dict"].items()}
+    tab = DO.schedule()
+    x0, t, noise = g["images"][2], g["ts"][2], g["noises"][2]
+    loss = DO.loss("l2", noise, orc.forward(DO.q_sample(tab, x0, t, noise), t, None, training=True))
+    loss.backward()
+    torch.nn.utils.clip_grad_norm_(params, 1.0)
+    opt.step()
+    DO.ema_update(ema, {k: v.detach() for k, v in sd.items()}, 0.9)
+    torch.testing.assert_close(loss.reshape(1), g["losses"][2:3].float(), rtol=1e-5, atol=1e-6)
+    for k, v in split_params(g, "final/").items():
+        torch.testing.assert_close(sd[k].detach(), v, rtol=1e-4, atol=1e-6, msg=k)
+    for k, v in split_params(g, "ema/").items():
+        torch.testing.assert_close(ema[k], v, rtol=1e-4, atol=1e-6, msg=k)
+    assert all(float(s) == 3.0 for s in g["step_after"])
