@@ -16,9 +16,14 @@ The JSON line also carries:
                 2.5 PFLOP/s dense bf16 MFMA peak (MI355X_MICROARCH.md)
   cpu_baseline  the CPU oracle (oracle/unet_oracle.py, fp32, a port of the reference path) running the
                 same train step on the host cores, rank 0 only, bounded sample (B=32, 3 timed steps)
-  ddim50        DDIM-50 sampling img/s (eta 0, B=128 per GPU, replicas)
+  ddim50        DDIM-50 sampling img/s (eta 0, B=128 per GPU, replicas), with its own cpu_baseline (the
+                oracle's DDIM at B=16)
   ddim50_cfg    DDIM-50 + classifier-free guidance (scale 3.0, dynamic threshold 0.995) img/s, conditional
                 UNet (10 classes), B=128 per GPU as one 256-row forward per step
+  celeba64      BASELINE config #5 on one GPU: the same network at 64x64, train img/s and DDIM-100 img/s
+  fp32          the headline train step in the reference's own arithmetic (fp32 parity mode)
+(celeba64 / fp32 only at N=1; --no-extra skips them.) `--image-size 64 --sample-steps 100` makes config #5 the
+headline line instead.
 """
 import argparse
 import json
@@ -44,8 +49,11 @@ def log(*a):
 
 
 def conv_roofline(dtype, B=128):
-    """Time the dominant kernel (3x3 ResBlock conv 128->128 @32x32, B=128, GN+SiLU prologue, bias+temb
-    epilogue) with HIP events on the stream it is launched on."""
+    """Time the dominant kernel (the ResBlock 3x3 conv 128->128 @32x32, B=128, bias + time-embedding epilogue;
+    its GN+SiLU input is materialised by the GN-apply pass, as in training) with HIP events on the stream it is
+    launched on. `achieved` uses per-launch events (an event before and after every launch, so launches do not
+    overlap: the same isolation rocprofv3's kernel trace gives, whose average the committed profile holds);
+    `back_to_back_ms` is the average of 50 launches issued back to back (tails overlap)."""
     from diffusion_models_collection_amd import _lib as L, kernels as K
     H = W = 32
     C = 128
@@ -54,8 +62,6 @@ def conv_roofline(dtype, B=128):
     w = torch.randn(C, C, 3, 3, device=dev) * 0.03
     Kc = L.kc_for(C, dtype)
     wp = K.pack_weight(L.PACK_FWD, dtype, w, Kc)
-    sc = torch.rand(B, C, device=dev)
-    sh = torch.randn(B, C, device=dev)
     bias = torch.randn(C, device=dev)
     addv = torch.randn(B, C, device=dev)
     y = torch.empty(B, H, W, C, device=dev, dtype=dtype)
@@ -64,21 +70,27 @@ def conv_roofline(dtype, B=128):
     for _ in range(5):
         K.conv(d, x, None, wp, y)
     s = torch.cuda.current_stream()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     n = 50
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * n)]
+    for i in range(n):
+        ev[2 * i].record(s)
+        K.conv(d, x, None, wp, y)
+        ev[2 * i + 1].record(s)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(n):
         K.conv(d, x, None, wp, y)
     e1.record(s)
     e1.synchronize()
-    avg_ms = e0.elapsed_time(e1) / n
+    avg_ms = sum(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(n)) / n
+    b2b_ms = e0.elapsed_time(e1) / n
     flops = 2.0 * B * H * W * C * C * 9
     achieved = flops / (avg_ms * 1e-3) / 1e12
     return {"kernel": "conv3x3_halo_kernel bf16 implicit GEMM (ResBlock 3x3 128->128 @32x32, B=128, "
                       "bias+temb epilogue)" if dtype == torch.bfloat16 else "conv_fwd_kernel<f32,128,128>",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic(),
-            "flops_per_launch": flops, "avg_launch_ms": round(avg_ms, 4),
+            "flops_per_launch": flops, "avg_launch_ms": round(avg_ms, 4), "back_to_back_ms": round(b2b_ms, 4),
             "algorithmic_bytes_per_launch": 2 * (2 * B * H * W * C) + 2 * C * 9 * C}
 
 
@@ -93,11 +105,25 @@ def pmc_traffic():
         return json.load(fh).get("hbm_bytes_per_launch")
 
 
-def cpu_baseline(B=32, warm=1, steps=3, threads=16):
-    """The CPU oracle (a port of the reference path) doing the same train step on the host cores."""
+def cpu_cores():
+    """Cores this process may actually use: its CPU affinity, capped by a cgroup v2 CPU quota if one is set
+    (a GPU box shows the whole machine in os.cpu_count() but gives a job a share of it)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_baseline(B=32, warm=1, steps=3):
+    """The CPU oracle (a port of the reference path, fp32) doing the same train step on the host cores."""
     from oracle.unet_oracle import make_oracle
     from oracle import diffusion_oracle as DO
     from diffusion_models_collection_amd.models import UNet
+    threads = cpu_cores()
     torch.set_num_threads(threads)
     torch.manual_seed(42)
     m = UNet(**CIFAR)
@@ -124,9 +150,89 @@ def cpu_baseline(B=32, warm=1, steps=3, threads=16):
     for _ in range(steps):
         step()
     dt = time.perf_counter() - t0
-    return {"value": round(B * steps / dt, 3), "unit": "img/s", "cores": threads, "kind": "port",
+    return {"value": round(B * steps / dt, 3), "unit": "img/s", "cores": threads, "os_cpu_count": os.cpu_count(),
+            "kind": "port",
             "sample": f"oracle fp32 train step (q_sample, UNet fwd+bwd, clip, AdamW, EMA), B={B}, {steps} timed "
-                      f"steps after {warm} warm-up, torch CPU with {threads} threads"}
+                      f"steps after {warm} warm-up, torch CPU with {threads} threads (the cores available to the "
+                      f"process: affinity and cgroup quota)"}
+
+
+def cpu_ddim_baseline(B=16, steps=5, S=50):
+    """DDIM-50 sampling on the CPU oracle (B=16): `steps` of the 50 DDIM steps timed (a DDIM step is
+    one UNet forward + the update, identical work at every step), img/s extrapolated to the full 50-step loop."""
+    from oracle.unet_oracle import make_oracle
+    from oracle import diffusion_oracle as DO
+    from diffusion_models_collection_amd.models import UNet
+    threads = cpu_cores()
+    torch.set_num_threads(threads)
+    torch.manual_seed(42)
+    orc, _ = make_oracle(UNet(**CIFAR).state_dict(), dict(CIFAR, num_classes=None))
+    ac = DO.schedule()["alphas_cumprod"]
+    ts = DO.ddim_timesteps(1000, S)
+    img = torch.randn(B, 3, 32, 32)
+    with torch.no_grad():
+        t = torch.full((B,), int(ts[0]))
+        orc.forward(img, t, None)          # warm-up
+        t0 = time.perf_counter()
+        for i in range(steps):
+            t = torch.full((B,), int(ts[i]))
+            tn = torch.full((B,), int(ts[i + 1]))
+            img = DO.ddim_step(ac, img, orc.forward(img, t, None), t, tn)
+        dt = time.perf_counter() - t0
+    return {"value": round(B / (dt / steps * S), 4), "unit": "img/s", "cores": threads, "kind": "port",
+            "sample": f"oracle fp32 DDIM, B={B}, {steps} of {S} steps timed, img/s for the {S}-step loop"}
+
+
+def train_rate(trainer, pool, steps, warmup, world):
+    """Time `steps` train steps after `warmup`, barrier + synchronize on both sides, max over ranks."""
+    for i in range(warmup):
+        trainer.train_step(pool[i % len(pool)], 0)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        trainer.train_step(pool[i % len(pool)], 0)
+    host_el = time.perf_counter() - t0      # host enqueue time (the GPU may still be running)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return max_over_ranks(el, world), host_el
+
+
+def max_over_ranks(v, world):
+    if world > 1:
+        dist.barrier()
+        tt = torch.tensor([v], device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        v = tt.item()
+    return v
+
+
+def make_trainer(mp, dtype, dev, rank, world, num_classes=None):
+    from diffusion_models_collection_amd.models import UNet
+    from diffusion_models_collection_amd.diffusion import DDPM
+    from diffusion_models_collection_amd.utils.trainer import DiffusionTrainer
+    torch.manual_seed(42 + rank)
+    model = UNet(**mp, num_classes=num_classes, compute_dtype=dtype).to(dev)
+    ddpm = DDPM(1000, 1e-4, 0.02, "linear", device=dev)
+    opt = torch.optim.AdamW(model.parameters(), lr=2e-4, weight_decay=1e-4)
+    cfg = {"epochs": 1, "save_dir": "/tmp/dmc_bench_ckpt", "sample_dir": "/tmp/dmc_bench_smp", "loss_type": "l2",
+           "use_ema": True, "ema_decay": 0.9999, "model_type": "unet", "model_params": dict(mp)}
+    return model, DiffusionTrainer(model, ddpm, None, opt, None, device=dev, config=cfg, rank=rank, world_size=world)
+
+
+def sample_rate(fn, world):
+    """Seconds of one sampling call after a warm-up call (replicas: each rank samples its own batch)."""
+    with torch.no_grad():
+        fn()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    return max_over_ranks(el, world)
 
 
 def main():
@@ -145,6 +251,9 @@ def main():
     ap.add_argument("--sample-steps", type=int, default=50)
     ap.add_argument("--no-train", action="store_true", help="sampling only (profiling)")
     ap.add_argument("--roofline-only", action="store_true", help="time only the roofline conv (PMC passes)")
+    ap.add_argument("--image-size", type=int, default=32, help="32 (CIFAR-10, headline) or 64 (CelebA, config #5)")
+    ap.add_argument("--no-extra", dest="extra", action="store_false",
+                    help="skip the 64x64 (config #5) and fp32 side lines")
     args = ap.parse_args()
     if args.roofline_only:
         print(json.dumps(conv_roofline(torch.bfloat16 if args.dtype == "bf16" else torch.float32)), flush=True)
@@ -167,101 +276,92 @@ def main():
             dist.init_process_group("gloo", rank=rank, world_size=world)
 
     from diffusion_models_collection_amd.models import UNet
-    from diffusion_models_collection_amd.diffusion import DDPM, DDIM
-    from diffusion_models_collection_amd.utils.trainer import DiffusionTrainer
+    from diffusion_models_collection_amd.diffusion import DDIM
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    torch.manual_seed(42 + rank)
-    model = UNet(**CIFAR, compute_dtype=args.dtype).to(dev)
-    ddpm = DDPM(1000, 1e-4, 0.02, "linear", device=dev)
-    opt = torch.optim.AdamW(model.parameters(), lr=2e-4, weight_decay=1e-4)
-    cfg = {"epochs": 1, "save_dir": "/tmp/dmc_bench_ckpt", "sample_dir": "/tmp/dmc_bench_smp", "loss_type": "l2",
-           "use_ema": True, "ema_decay": 0.9999, "model_type": "unet", "model_params": dict(CIFAR)}
-    trainer = DiffusionTrainer(model, ddpm, None, opt, None, device=dev, config=cfg, rank=rank, world_size=world)
+    S = args.image_size
+    mp = dict(CIFAR, image_size=(S, S))
+    model, trainer = make_trainer(mp, args.dtype, dev, rank, world)
     B = args.batch
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    pool = [torch.rand(B, 3, 32, 32, device=dev, generator=gen) * 2 - 1 for _ in range(4)]
+    pool = [torch.rand(B, 3, S, S, device=dev, generator=gen) * 2 - 1 for _ in range(4)]
 
     model.train()
     if args.no_train:
         args.warmup, args.steps = 0, 1
-    for i in range(args.warmup):
-        trainer.train_step(pool[i % 4], 0)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps if not args.no_train else 0):
-        trainer.train_step(pool[i % 4], 0)
-    host_el = time.perf_counter() - t0      # host enqueue time (the GPU may still be running)
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        tt = torch.tensor([el], device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = tt.item()
+        el, host_el = 1.0, 0.0
+    else:
+        el, host_el = train_rate(trainer, pool, args.steps, args.warmup, world)
     ms = el / args.steps * 1e3
     value = world * B * args.steps / el
     log(f"[bench] rank {rank}: {ms:.2f} ms/step, {value:.1f} img/s aggregate")
+    gflop = TRAIN_GFLOP_PER_IMG * (S / 32) ** 2
 
-    out = {"metric": "CIFAR-10 UNet DDPM train imgs/sec (aggregate over GPUs)", "value": round(value, 2),
+    name = "CIFAR-10" if S == 32 else f"CelebA {S}x{S}"
+    out = {"metric": f"{name} UNet DDPM train imgs/sec (aggregate over GPUs)", "value": round(value, 2),
            "unit": "img/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
-           "data": "synthetic (U(-1,1) 32x32x3 batches resident in HBM, random-init weights)",
-           "config": {"workload": "configs/cifar10_unet.py UNet DDPM train step (q_sample, fwd, MSE, bwd, clip, "
-                                  "AdamW, EMA), dropout 0.1", "model": "UNet 37.06M (128ch, mult 1,2,2,2, attn 16/8)",
-                      "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
+           "data": f"synthetic (U(-1,1) {S}x{S}x3 batches resident in HBM, random-init weights)",
+           "config": {"workload": f"configs/cifar10_unet.py UNet DDPM train step at {S}x{S} (q_sample, fwd, MSE, "
+                                  "bwd, clip, AdamW, EMA), dropout 0.1", "model": "UNet 37.06M (128ch, mult 1,2,2,2, "
+                                  "attn 16/8)", "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
                       "parallelism": f"dp{world}"},
            "per_gpu_imgs_per_sec": round(value / world, 2),
            "host_enqueue_ms_per_step": round(host_el / max(args.steps, 1) * 1e3, 3),
-           "train_tflops_per_gpu": round(value / world * TRAIN_GFLOP_PER_IMG / 1e3, 2)}
+           "train_tflops_per_gpu": round(value / world * gflop / 1e3, 2)}
+    if args.no_train:
+        out["value"] = None
 
     if not args.no_sample:
         model.eval()
         ddim = DDIM(1000, args.sample_steps, device=dev)
-        with torch.no_grad():
-            ddim.sample(model, (B, 3, 32, 32))   # warm-up (also populates the weight pack cache)
-            if world > 1:
-                dist.barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            ddim.sample(model, (B, 3, 32, 32))
-            torch.cuda.synchronize()
-            sel = time.perf_counter() - t0
-        if world > 1:
-            tt = torch.tensor([sel], device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            sel = tt.item()
-        out["ddim50"] = {"value": round(world * B / sel, 2), "unit": "img/s", "batch_per_gpu": B,
-                         "steps": args.sample_steps, "seconds": round(sel, 3), "scaling": "replicas"}
+        sel = sample_rate(lambda: ddim.sample(model, (B, 3, S, S)), world)
+        out[f"ddim{args.sample_steps}"] = {"value": round(world * B / sel, 2), "unit": "img/s", "batch_per_gpu": B,
+                                           "steps": args.sample_steps, "seconds": round(sel, 3),
+                                           "scaling": "replicas"}
         if not args.no_cfg:
-            # conditional UNet (10 classes), DDIM-50 + classifier-free guidance 3.0 + dynamic thresholding
+            # conditional UNet (10 classes), DDIM + classifier-free guidance 3.0 + dynamic thresholding
             # (diffusion/ddim.py:251-346): cond and null-label rows as ONE 2B forward per step
             torch.manual_seed(43 + rank)
-            cmodel = UNet(**CIFAR, num_classes=10, compute_dtype=args.dtype).to(dev).eval()
+            cmodel = UNet(**mp, num_classes=10, compute_dtype=args.dtype).to(dev).eval()
             yl = torch.arange(B, device=dev) % 10
-            with torch.no_grad():
-                ddim.sample_with_cfg(cmodel, (B, 3, 32, 32), yl, cfg_scale=3.0)
-                if world > 1:
-                    dist.barrier()
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                ddim.sample_with_cfg(cmodel, (B, 3, 32, 32), yl, cfg_scale=3.0)
-                torch.cuda.synchronize()
-                cel = time.perf_counter() - t0
-            if world > 1:
-                tt = torch.tensor([cel], device=dev)
-                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-                cel = tt.item()
-            out["ddim50_cfg"] = {"value": round(world * B / cel, 2), "unit": "img/s", "batch_per_gpu": B,
-                                 "steps": args.sample_steps, "cfg_scale": 3.0, "p_threshold": 0.995,
-                                 "forward_batch": 2 * B, "seconds": round(cel, 3), "scaling": "replicas"}
+            cel = sample_rate(lambda: ddim.sample_with_cfg(cmodel, (B, 3, S, S), yl, cfg_scale=3.0), world)
+            out[f"ddim{args.sample_steps}_cfg"] = {"value": round(world * B / cel, 2), "unit": "img/s",
+                                                   "batch_per_gpu": B, "steps": args.sample_steps, "cfg_scale": 3.0,
+                                                   "p_threshold": 0.995, "forward_batch": 2 * B,
+                                                   "seconds": round(cel, 3), "scaling": "replicas"}
+            del cmodel
+    if args.extra and S == 32 and not args.no_train and world == 1:
+        # BASELINE config #5 beside the headline: the same network at 64x64 (CelebA), train + DDIM-100
+        del model, trainer
+        mp64 = dict(CIFAR, image_size=(64, 64))
+        m64, tr64 = make_trainer(mp64, args.dtype, dev, rank, world)
+        pool64 = [torch.rand(B, 3, 64, 64, device=dev, generator=gen) * 2 - 1 for _ in range(2)]
+        m64.train()
+        e64, _ = train_rate(tr64, pool64, 5, 3, world)
+        m64.eval()
+        d100 = DDIM(1000, 100, device=dev)
+        s64 = sample_rate(lambda: d100.sample(m64, (B, 3, 64, 64)), world)
+        out["celeba64"] = {"train_img_s": round(world * B * 5 / e64, 2), "train_ms_per_step": round(e64 / 5 * 1e3, 3),
+                           "ddim100_img_s": round(world * B / s64, 2), "ddim100_seconds": round(s64, 3),
+                           "batch_per_gpu": B, "dtype": args.dtype, "steps_timed": 5,
+                           "train_tflops_per_gpu": round(B * 5 / e64 * TRAIN_GFLOP_PER_IMG * 4 / 1e3, 2)}
+        del m64, tr64
+        if args.dtype == "bf16":
+            # the reference's own arithmetic (fp32) on the same step, for comparison with the bf16 headline
+            mf, trf = make_trainer(CIFAR, "fp32", dev, rank, world)
+            mf.train()
+            ef, _ = train_rate(trf, pool, 5, 2, world)
+            out["fp32"] = {"train_img_s": round(world * B * 5 / ef, 2), "train_ms_per_step": round(ef / 5 * 1e3, 3),
+                           "steps_timed": 5, "note": "exact-fp32 MFMA (v_mfma_f32_16x16x4f32) parity mode"}
+            del mf, trf
     if rank == 0 and not args.no_roofline:
         out["roofline"] = conv_roofline(dtype)
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
             out["cpu_baseline"] = cpu_baseline()
+            if f"ddim{args.sample_steps}" in out and S == 32:
+                out[f"ddim{args.sample_steps}"]["cpu_baseline"] = cpu_ddim_baseline(S=args.sample_steps)
         except Exception as e:  # the CPU leg must never hide the GPU result
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

@@ -55,6 +55,9 @@ def _load():
     lib = ctypes.CDLL(str(LIB_PATH))
     sig = {
         "dmc_version": (_c_int, []),
+        "dmc_set_option": (_c_int, [ctypes.c_char_p, _c_long]),
+        "dmc_get_option": (_c_long, [ctypes.c_char_p]),
+        "dmc_reset_options": (None, [_c_int]),
         "dmc_last_error": (ctypes.c_char_p, []),
         "dmc_conv2d_workspace": (_c_size, [ctypes.POINTER(ConvDesc)]),
         "dmc_conv_halo_prologue": (_c_int, [ctypes.POINTER(ConvDesc)]),
@@ -120,6 +123,19 @@ class DMCError(RuntimeError):
 def check(rc: int, what: str):
     if rc != 0:
         raise DMCError(f"{what} failed ({rc}): {LIB.dmc_last_error().decode()}")
+
+
+def set_option(name: str, value) -> None:
+    """Launch-plan A/B switch (include/dmc.h dmc_set_option), e.g. set_option("DMC_NO_HALO", 1)."""
+    check(LIB.dmc_set_option(name.encode(), int(value)), "set_option")
+
+
+def get_option(name: str) -> int:
+    return LIB.dmc_get_option(name.encode())
+
+
+def reset_options(from_env: bool = False) -> None:
+    LIB.dmc_reset_options(1 if from_env else 0)
 
 
 def ptr(t):

@@ -543,11 +543,11 @@ __global__ __launch_bounds__(512) void attn_dkdv_res_kernel(AttnK a, int HG, int
 // leaves >= 256 blocks where the batch allows; DMC_ATTN_HG overrides the choice (tests).
 int res_heads(const AttnK& a, int* Lp) {
   *Lp = dmc::cdiv(a.L, 64) * 64;
-  if (*Lp > kResRows || getenv_flag("DMC_ATTN_STAGED")) return 0;
+  if (*Lp > kResRows || dmc::opt(dmc::OPT_ATTN_STAGED)) return 0;
   int hg = kResRows / *Lp;
   if (hg > a.heads) hg = a.heads;
-  const char* force = getenv("DMC_ATTN_HG");
-  if (force && atoi(force) > 0) return atoi(force) < hg ? atoi(force) : hg;
+  const long force = dmc::opt(dmc::OPT_ATTN_HG);
+  if (force > 0) return force < hg ? (int)force : hg;
   while (hg > 1 && (a.heads % hg != 0 || (long)a.N * (a.heads / hg) < 256)) --hg;
   return hg;
 }

@@ -29,7 +29,6 @@ struct ConvK {
   float* sk;  // split-K partial slab (nullptr: no split)
   int sk_per; // K stages per split
   int x1_bytes, x2_bytes, w_bytes;  // operand extents for buffer resources (0: too large / absent)
-  int dbg;    // probe-only ablation bits of the halo kernel (env DMC_HALO_DBG; 0 in production)
   int dtype_bytes;  // 4 (fp32) or 2 (bf16) storage
 };
 
@@ -804,7 +803,6 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
     }
     return n;
   };
-  if ((a.dbg & 32) && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);   // probe: static priority, younger half
 
   // GN+SiLU prologue on the halo (one image per tile): this lane's scale/shift of chunk 0
   constexpr bool pro = PRO;   // separate instantiation: the plain kernel's code is unchanged
@@ -825,13 +823,8 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
     const int c = s / 9, t = s - c * 9;
-    const bool dma = !(a.dbg & 2), late = a.dbg & 64;   // probe: issue the DMA after the first MFMA half
-    auto issue_stage = [&]() {
-      if (s + WS - 1 < nst) issue_w(s + WS - 1);
-      if (t < 3 && c + 1 < nch) halo_issue<HP>(a, lds + ((c + 1) & 1) * HB, (c + 1) * 64, wave, part_b(t), part_b(t + 1), h1, h2);
-    };
-    if (dma && !late) issue_stage();
-    if (a.dbg & 4) continue;
+    if (s + WS - 1 < nst) issue_w(s + WS - 1);
+    if (t < 3 && c + 1 < nch) halo_issue<HP>(a, lds + ((c + 1) & 1) * HB, (c + 1) * 64, wave, part_b(t), part_b(t + 1), h1, h2);
     const char* A = lds + (c & 1) * HB;
     const char* Bw = wring + (s % WS) * WB;
     const int ty = t / 3, tx = t - ty * 3;
@@ -850,20 +843,10 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
         const int h = hb[j] + delta;
         fb[j] = *(const v4i*)(A + h * 128 + ((chunk ^ (h & 7)) << 4));
       }
-      if (a.dbg & 1) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j][0] += __builtin_bit_cast(float, fa[i][0] ^ fb[j][0]);
-      } else {
-        if (a.dbg & 16) __builtin_amdgcn_s_setprio(1);   // probe: priority around the MFMA cluster
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
-        if (a.dbg & 16) __builtin_amdgcn_s_setprio(0);
-      }
-      if (ks == 0 && dma && late) issue_stage();
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
     }
     if (pro && t == 8 && c + 1 < nch) {
       // this wave's own pieces of chunk c+1 (issued in slots 9c..9c+2, landed: the stage's wait covered later
@@ -879,7 +862,6 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
     for (int i = 0; i < 4; ++i)
       *(v4f*)(lds + (wm * 64 + j * 16 + fr) * EP + (wn * 64 + i * 16 + fh * 4) * 4) = acc[i][j];
   __syncthreads();
-  if (a.dbg & 8) return;
   tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
 }
 
@@ -1714,7 +1696,6 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
   k.Csplit = d->Csplit; k.ldy1 = d->ldy1; k.ldy2 = d->ldy2; k.out_f32 = d->out_f32; k.out_nchw = d->out_nchw;
   k.M = d->N * d->OH * d->OW; k.OHW = d->OH * d->OW;
   k.sk = nullptr; k.sk_per = 0;
-  k.dbg = 0;
   {
     const size_t esz = d->dtype == DMC_F32 ? 4 : 2;
     const size_t b1 = (size_t)d->N * d->H * d->W * d->ld1 * esz;
@@ -1792,12 +1773,12 @@ int halo_pro_plan(const ConvK& k, int* R, int* nimg) {
   if (k.dtype_bytes != 2 || k.prologue != DMC_PRO_AFFINE_SILU || k.dthresh != 0 || k.ldp < k.C1 + k.C2) return 0;
   // opt-in (DMC_HALO_PRO=1): measured neutral for DDIM-50 at B=128 on MI355X (the saved GN-apply pass is
   // paid back by a ~17 % slower conv: the halo rewrite's VALU work and its vmcnt(0) drains)
-  if (!getenv_flag("DMC_HALO_PRO") || getenv_flag("DMC_NO_HALO") || getenv_flag("DMC_NO_GLDS") ||
-      getenv_flag("DMC_NO_BUFLDS"))
+  if (!dmc::opt(dmc::OPT_HALO_PRO) || dmc::opt(dmc::OPT_NO_HALO) || dmc::opt(dmc::OPT_NO_GLDS) ||
+      dmc::opt(dmc::OPT_NO_BUFLDS))
     return 0;
   const bool buf = k.C1 % 64 == 0 && k.C2 % 64 == 0 && k.Kc == k.C1 + k.C2 && k.x1_bytes > 0 &&
                    (k.C2 == 0 || k.x2_bytes > 0) && k.w_bytes > 0;
-  if (!buf || (plan_glds(k).splits != 1 && !getenv_flag("DMC_NO_SPLITK"))) return 0;
+  if (!buf || (plan_glds(k).splits != 1 && !dmc::opt(dmc::OPT_NO_SPLITK))) return 0;
   const int hp = halo_plan(k, R, nimg);
   return *nimg == 1 ? hp : 0;   // one image per tile: a lane's scale/shift row is the same in every piece
 }
@@ -1822,7 +1803,7 @@ void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
 template <typename T>
 int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
   constexpr int EPC = TT<T>::KPL;
-  if (!getenv_flag("DMC_NO_NARROW")) {
+  if (!dmc::opt(dmc::OPT_NO_NARROW)) {
     if (k.C2 == 0 && k.C1 <= EPC && k.Cout >= 16) {
       conv_narrow_in_kernel<T><<<dim3(dmc::cdiv(k.M, 256), dmc::cdiv(k.Cout, 32)), 256, 0, s>>>(k);
       return dmc::check_launch("dmc_conv2d");
@@ -1836,28 +1817,23 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     int R, nimg;
     const int hp = halo_pro_plan(k, &R, &nimg);
     const dim3 hg(k.M / 256, dmc::cdiv(k.Cout, 128));
-    k.dbg = 0;
     if (hp == 6) { conv3x3_halo_kernel<6, 3, true><<<hg, 512, 0, s>>>(k, R, nimg); return dmc::check_launch("dmc_conv2d"); }
     if (hp == 7) { conv3x3_halo_kernel<7, 3, true><<<hg, 512, 0, s>>>(k, R, nimg); return dmc::check_launch("dmc_conv2d"); }
   }
-  if (sizeof(T) == 2 && k.prologue == DMC_PRO_NONE && !getenv_flag("DMC_NO_GLDS")) {
+  if (sizeof(T) == 2 && k.prologue == DMC_PRO_NONE && !dmc::opt(dmc::OPT_NO_GLDS)) {
     // bf16, plain operands: LDS-DMA pipelined kernel
     FwdPlan p = plan_glds(k);
-    if (p.splits > 1 && (ws == nullptr || ws_bytes < p.ws || getenv_flag("DMC_NO_SPLITK"))) { p.splits = 1; p.cfg = 2; }
+    if (p.splits > 1 && (ws == nullptr || ws_bytes < p.ws || dmc::opt(dmc::OPT_NO_SPLITK))) { p.splits = 1; p.cfg = 2; }
     if (p.splits > 1) { k.sk = (float*)ws; k.sk_per = p.per; }
     const bool buf = k.C1 % 64 == 0 && k.C2 % 64 == 0 && k.Kc == k.C1 + k.C2 && k.x1_bytes > 0 &&
-                     (k.C2 == 0 || k.x2_bytes > 0) && k.w_bytes > 0 && !getenv_flag("DMC_NO_BUFLDS");
+                     (k.C2 == 0 || k.x2_bytes > 0) && k.w_bytes > 0 && !dmc::opt(dmc::OPT_NO_BUFLDS);
     int R, nimg;
-    const int hp = (buf && p.splits == 1 && !getenv_flag("DMC_NO_HALO")) ? halo_plan(k, &R, &nimg) : 0;
-    if (hp) {
-      const char* dbg = getenv("DMC_HALO_DBG");
-      k.dbg = dbg ? atoi(dbg) : 0;
-    }
+    const int hp = (buf && p.splits == 1 && !dmc::opt(dmc::OPT_NO_HALO)) ? halo_plan(k, &R, &nimg) : 0;
     const dim3 hg(k.M / 256, dmc::cdiv(k.Cout, 128));
-    if (hp && getenv_flag("DMC_HALO_RW")) {
+    if (hp && dmc::opt(dmc::OPT_HALO_RW)) {
       if (hp == 6) conv3x3_halo_rw_kernel<6><<<hg, 512, 0, s>>>(k, R, nimg);
       else conv3x3_halo_rw_kernel<7><<<hg, 512, 0, s>>>(k, R, nimg);
-    } else if (hp == 6 && getenv_flag("DMC_HALO_WS4"))
+    } else if (hp == 6 && dmc::opt(dmc::OPT_HALO_WS4))
       conv3x3_halo_kernel<6, 4><<<hg, 512, 0, s>>>(k, R, nimg);
     else if (hp == 6)
       conv3x3_halo_kernel<6, 3><<<hg, 512, 0, s>>>(k, R, nimg);
@@ -1872,7 +1848,7 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
   if (rp.big) {
     dim3 g(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128));
     conv_fwd_kernel<T, 128, 128><<<g, 256, 0, s>>>(k);
-  } else if (rp.splits > 1 && ws != nullptr && ws_bytes >= rp.ws && !getenv_flag("DMC_NO_SPLITK")) {
+  } else if (rp.splits > 1 && ws != nullptr && ws_bytes >= rp.ws && !dmc::opt(dmc::OPT_NO_SPLITK)) {
     // few 64x64 tiles and a long K (the time-embedding GEMMs, K up to 4992): split K over grid.z
     k.sk = (float*)ws;
     k.sk_per = rp.per;
@@ -1894,7 +1870,7 @@ int wgrad_splits(const dmc_conv_desc* d, int* pps) {
   const long M = (long)d->N * d->OH * d->OW;
   const long KK = (long)d->ntaps * d->Kc;
   const long tiles = (long)dmc::cdiv(KK, 128) * dmc::cdiv(d->Cout, 128);
-  static const long target = getenv("DMC_WG_BLOCKS") ? atol(getenv("DMC_WG_BLOCKS")) : 512;   // A/B knob
+  const long target = dmc::opt(dmc::OPT_WG_BLOCKS);   // A/B knob
   long splits = (target + tiles - 1) / tiles;
   const long max_splits = (M + 4 * sp - 1) / (4 * sp);  // at least 4 stages per split
   if (splits > max_splits) splits = max_splits;
@@ -1912,7 +1888,7 @@ extern "C" size_t dmc_conv2d_workspace(const dmc_conv_desc* d) {
   ConvK k;
   if (fill_convk(d, nullptr, nullptr, nullptr, nullptr, nullptr, k)) return 0;
   if (k.M == 0) return 0;
-  if (d->dtype != DMC_BF16 || d->prologue != DMC_PRO_NONE || getenv_flag("DMC_NO_GLDS")) return plan_reg(k).ws;
+  if (d->dtype != DMC_BF16 || d->prologue != DMC_PRO_NONE || dmc::opt(dmc::OPT_NO_GLDS)) return plan_reg(k).ws;
   return plan_glds(k).ws;
 }
 
@@ -1935,7 +1911,7 @@ struct WgHaloPlan {
 
 WgHaloPlan wgrad_halo_plan(const dmc_conv_desc* d) {
   WgHaloPlan p{false, 0, 0, 1, 0, 0};
-  if (d->dtype != DMC_BF16 || getenv_flag("DMC_NO_HALO")) return p;
+  if (d->dtype != DMC_BF16 || dmc::opt(dmc::OPT_NO_HALO)) return p;
   ConvK k;
   if (fill_convk(d, nullptr, nullptr, nullptr, nullptr, nullptr, k)) return p;
   if (k.C1 % 64 || k.C2 % 64 || k.Kc != k.C1 + k.C2 || k.x1_bytes == 0 || (k.C2 && k.x2_bytes == 0)) return p;

@@ -11,6 +11,7 @@
 //   label embedding     models/unet.py:183, 256-258
 //   EMA                 utils/trainer.py:187-202
 //   clip_grad_norm_     utils/trainer.py:259
+#include <stdlib.h>
 #include <string.h>
 #include "dmc_common.h"
 #include "dmc_internal.h"
@@ -24,6 +25,54 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 }  // namespace dmc
+
+namespace dmc {
+namespace {
+struct OptDef {
+  const char* name;
+  long def;
+};
+// name (= environment variable), default
+constexpr OptDef kOpts[OPT_COUNT] = {
+    {"DMC_NO_NARROW", 0},  {"DMC_NO_GLDS", 0},        {"DMC_NO_SPLITK", 0},          {"DMC_NO_BUFLDS", 0},
+    {"DMC_NO_HALO", 0},    {"DMC_HALO_PRO", 0},       {"DMC_HALO_RW", 0},            {"DMC_HALO_WS4", 0},
+    {"DMC_GN_STATS_SPLIT", 0}, {"DMC_GN_BWD_SPLIT", 0}, {"DMC_ATTN_STAGED", 0},    {"DMC_ATTN_HG", 0},
+    {"DMC_WG_BLOCKS", 512}, {"DMC_GN_STATS_ONE_MAX", 1l << 20}, {"DMC_GN_BWD_ONE_MAX", 65536},
+};
+struct OptTable {
+  long v[OPT_COUNT];
+  OptTable() { reset(true); }
+  void reset(bool env) {
+    for (int i = 0; i < OPT_COUNT; ++i) {
+      v[i] = kOpts[i].def;
+      const char* e = env ? getenv(kOpts[i].name) : nullptr;
+      if (e && e[0]) v[i] = atol(e);
+    }
+  }
+};
+OptTable& table() {
+  static OptTable t;   // thread-safe one-time initialisation from the environment
+  return t;
+}
+}  // namespace
+long opt(Opt o) { return table().v[o]; }
+}  // namespace dmc
+
+extern "C" int dmc_set_option(const char* name, long value) {
+  for (int i = 0; i < dmc::OPT_COUNT; ++i)
+    if (strcmp(name, dmc::kOpts[i].name) == 0) {
+      dmc::table().v[i] = value;
+      return 0;
+    }
+  dmc::set_error("set_option: unknown option %s", name);
+  return 1;
+}
+extern "C" long dmc_get_option(const char* name) {
+  for (int i = 0; i < dmc::OPT_COUNT; ++i)
+    if (strcmp(name, dmc::kOpts[i].name) == 0) return dmc::table().v[i];
+  return -1;
+}
+extern "C" void dmc_reset_options(int from_env) { dmc::table().reset(from_env != 0); }
 
 extern "C" int dmc_version(void) { return 1; }
 extern "C" const char* dmc_last_error(void) { return dmc::g_err; }

@@ -19,12 +19,17 @@ inline int check_launch(const char* what) {
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 }  // namespace dmc
 
-// A/B switches for measurement (read once per process, never on the device).
-#include <stdlib.h>
-inline bool getenv_flag(const char* name) {
-  const char* v = getenv(name);
-  return v && v[0] && v[0] != '0';
-}
+// Launch-plan options (A/B switches for measurement and tests). Read ONCE per process from the environment
+// (DMC_* variables, at the first planner call) into one table; afterwards only dmc_set_option() /
+// dmc_reset_options() change it. The planners read plain fields, never the environment.
+namespace dmc {
+enum Opt {
+  OPT_NO_NARROW, OPT_NO_GLDS, OPT_NO_SPLITK, OPT_NO_BUFLDS, OPT_NO_HALO, OPT_HALO_PRO, OPT_HALO_RW, OPT_HALO_WS4,
+  OPT_GN_STATS_SPLIT, OPT_GN_BWD_SPLIT, OPT_ATTN_STAGED, OPT_ATTN_HG, OPT_WG_BLOCKS, OPT_GN_STATS_ONE_MAX,
+  OPT_GN_BWD_ONE_MAX, OPT_COUNT
+};
+long opt(Opt o);
+}  // namespace dmc
 
 #define DMC_REQUIRE(cond, ...)       \
   do {                               \

@@ -796,8 +796,8 @@ extern "C" int dmc_gn_stats(int dtype, const void* x1, const void* x2, int N, in
   hipStream_t s = dmc::as_stream(stream);
   Src2 src{(const char*)x1, (const char*)x2, C1, C2, ld1, ld2};
   // one block per sample when N blocks fill the chip and a sample is <= 1 MB (bf16, G <= 64)
-  static const long stats_max = getenv("DMC_GN_STATS_ONE_MAX") ? atol(getenv("DMC_GN_STATS_ONE_MAX")) : (1l << 20);
-  if (dtype != DMC_F32 && !getenv_flag("DMC_GN_STATS_SPLIT") && N >= 64 && G <= 64 && (long)HW * C * 2 <= stats_max) {
+  const long stats_max = dmc::opt(dmc::OPT_GN_STATS_ONE_MAX);
+  if (dtype != DMC_F32 && !dmc::opt(dmc::OPT_GN_STATS_SPLIT) && N >= 64 && G <= 64 && (long)HW * C * 2 <= stats_max) {
     gn_stats_one<bf16_t><<<N, 1024, 0, s>>>(src, HW, G, eps, gamma, beta, mean_rstd, scale, shift);
     return dmc::check_launch("dmc_gn_stats");
   }
@@ -841,8 +841,8 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
   float* sums = cf + (size_t)N * C * 6;
   const bool want_sums = dx_sum_nc || dx_sum_c;
   dim3 gr(N, b.splits);
-  static const long one_max = getenv("DMC_GN_BWD_ONE_MAX") ? atol(getenv("DMC_GN_BWD_ONE_MAX")) : 65536;   // A/B knob
-  if (dtype != DMC_F32 && N >= 64 && (long)HW * C <= one_max && !getenv_flag("DMC_GN_BWD_SPLIT")) {
+  const long one_max = dmc::opt(dmc::OPT_GN_BWD_ONE_MAX);   // A/B knob
+  if (dtype != DMC_F32 && N >= 64 && (long)HW * C <= one_max && !dmc::opt(dmc::OPT_GN_BWD_SPLIT)) {
     gn_bwd_one<bf16_t><<<N, 1024, 0, s>>>(b, A, cf);
   } else {
     if (dtype == DMC_F32) gn_bwd_partial<float><<<gr, 256, 0, s>>>(b, partial);

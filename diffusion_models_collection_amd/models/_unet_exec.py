@@ -301,7 +301,7 @@ class UNetExecutor:
         b = srcs[1] if len(srcs) > 1 else None
         N = a.t.shape[0]
         key = (N, a.H, a.W, a.C, b.C if b else 0, a.t.shape[-1], b.t.shape[-1] if b else 0, Cout,
-               os.environ.get("DMC_HALO_PRO", ""))
+               L.get_option("DMC_HALO_PRO"))
         ok = self._halo_pro_cache.get(key)
         if ok is None:
             C1, C2 = a.C, (b.C if b else 0)

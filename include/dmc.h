@@ -8,8 +8,9 @@
  *
  * Conventions
  *   - All pointers are device pointers unless stated; `stream` is a hipStream_t (NULL = default).
- *   - The library never allocates, never synchronises and keeps no mutable global state: callers
- *     pass every output and workspace buffer. Calls are graph-capturable.
+ *   - The library never allocates and never synchronises: callers pass every output and workspace
+ *     buffer. Its only mutable global state is the launch-option table below (read from the
+ *     environment once, then changed only by dmc_set_option). Calls are graph-capturable.
  *   - Return 0 on success, nonzero on a bad descriptor or launch error; dmc_last_error() explains.
  *   - Activations are NHWC (pixel rows, channel pitch `ld`); dtype is DMC_F32 (parity mode) or
  *     DMC_BF16 (perf mode). Statistics, biases, gradients of weights and reductions are fp32.
@@ -30,6 +31,13 @@ enum { DMC_PACK_FWD = 0, DMC_PACK_DGRAD = 1, DMC_PACK_UPDGRAD = 2 };
 
 int dmc_version(void);
 const char* dmc_last_error(void);
+
+/* Launch-plan options (A/B switches for measurement and tests, e.g. "DMC_NO_HALO"). The table is read once
+ * per process from the environment variables of the same names; afterwards only these calls change it.
+ * dmc_set_option returns nonzero for an unknown name; dmc_get_option returns -1 for one. */
+int dmc_set_option(const char* name, long value);
+long dmc_get_option(const char* name);
+void dmc_reset_options(int from_env);
 
 /* Implicit-GEMM convolution descriptor. Replaces nn.Conv2d / nn.Linear forward and input-gradient
  * of models/unet.py:34-60 (ResidualBlock), :81-82 (qkv/proj), :106 (Downsample), :116 (Upsample +

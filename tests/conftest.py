@@ -34,6 +34,18 @@ def golden():
     return load_golden
 
 
+@pytest.fixture
+def dmc_opt():
+    """Set libdmc launch-plan options (include/dmc.h dmc_set_option) for one test; defaults restored after."""
+    from diffusion_models_collection_amd import _lib as L
+
+    def set_(name, value):
+        L.set_option(name, int(value))
+
+    yield set_
+    L.reset_options(from_env=False)
+
+
 def pytest_collection_modifyitems(config, items):
     if gpu_available():
         return

@@ -21,7 +21,7 @@ def test_library_exports_header_symbols():
     _ensure_lib()
     import ctypes
     hdr = (ROOT / "include" / "dmc.h").read_text()
-    names = sorted(set(re.findall(r"^\s*(?:int|long|size_t|const char\*)\s+(dmc_\w+)\s*\(", hdr, re.M)))
+    names = sorted(set(re.findall(r"^\s*(?:int|long|void|size_t|const char\*)\s+(dmc_\w+)\s*\(", hdr, re.M)))
     assert len(names) >= 29, names
     lib = ctypes.CDLL(str(ROOT / "diffusion_models_collection_amd" / "libdmc.so"))
     missing = [n for n in names if not hasattr(lib, n)]
@@ -162,3 +162,21 @@ def test_dropin_registry_imports():
         sys.path.remove(str(ROOT / "dropin"))
         for mod in ("models", "diffusion", "utils", "utils.trainer", "utils.helpers"):
             sys.modules.pop(mod, None)
+
+
+def test_launch_option_table():
+    """include/dmc.h dmc_set_option / dmc_get_option / dmc_reset_options: the planners' A/B table (read from the
+    environment once) is changed only through these calls; unknown names are errors."""
+    _ensure_lib()
+    from diffusion_models_collection_amd import _lib as L
+    try:
+        assert L.get_option("DMC_WG_BLOCKS") == 512
+        L.set_option("DMC_NO_HALO", 1)
+        assert L.get_option("DMC_NO_HALO") == 1
+        L.reset_options(from_env=False)
+        assert L.get_option("DMC_NO_HALO") == 0
+        assert L.get_option("DMC_NOT_AN_OPTION") == -1
+        with pytest.raises(L.DMCError, match="unknown option"):
+            L.set_option("DMC_NOT_AN_OPTION", 1)
+    finally:
+        L.reset_options(from_env=False)

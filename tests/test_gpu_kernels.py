@@ -44,12 +44,12 @@ def q(x, dt):
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("case", ["s1_concat_gn", "s2", "up", "1x1", "ragged_in", "ragged_in_generic", "narrow_out",
                                   "splitk_concat", "splitk_ragged"])
-def test_conv_forward(dt, case, monkeypatch):
+def test_conv_forward(dt, case, monkeypatch, dmc_opt):
     """splitk_*: small M with deep K, which both planners (bf16 LDS-DMA, fp32 register-staged) run as split-K
     over grid.z + epilogue kernel. ragged_in (3 input channels) and narrow_out (3 output channels) run the
     narrow-conv kernels; ragged_in_generic is the same conv on the tiled kernels (DMC_NO_NARROW)."""
     L, K = _lib()
-    monkeypatch.setenv("DMC_NO_NARROW", "1" if case == "ragged_in_generic" else "0")
+    dmc_opt("DMC_NO_NARROW", 1 if case == "ragged_in_generic" else 0)
     torch.manual_seed(0)
     N, H, W = 2, 8, 8
     C1, C2, Cout = 32, 16, 48
@@ -124,13 +124,13 @@ def test_upsample2x_nhwc_bitwise(dt):
 
 
 @pytest.mark.parametrize("case", ["c32_two_sources", "c16_wide", "c32_384", "c8_multi_image"])
-def test_conv3x3_halo_gn_silu_prologue(case, monkeypatch):
+def test_conv3x3_halo_gn_silu_prologue(case, monkeypatch, dmc_opt):
     """Inference prologue on the halo kernel: conv(SiLU(x*scale+shift)) with the GroupNorm affine + SiLU
     applied to the LDS-resident halo equals, BITWISE, dmc_gn_apply materialisation followed by the plain halo
     conv (same op sequence and bf16 rounding), and the fp32 torch reference within bf16 tolerance."""
     L, K = _lib()
-    monkeypatch.setenv("DMC_NO_SPLITK", "1")   # small N: keep the planner on the halo kernel
-    monkeypatch.setenv("DMC_HALO_PRO", "1")    # opt-in path
+    dmc_opt("DMC_NO_SPLITK", 1)   # small N: keep the planner on the halo kernel
+    dmc_opt("DMC_HALO_PRO", 1)    # opt-in path
     dt = torch.bfloat16
     torch.manual_seed(11)
     N, H, C1, C2, Cout = {"c32_two_sources": (2, 32, 128, 64, 128), "c16_wide": (3, 16, 256, 0, 256),
@@ -166,7 +166,7 @@ def test_conv3x3_halo_gn_silu_prologue(case, monkeypatch):
         assert rel_err(y.float(), y0.float()) < 1e-2
     yr = F.conv2d(F.silu(F.group_norm(x, G, gamma, beta, 1e-5)), w, bias, padding=1)
     assert rel_err(nchw(y.float().cpu()), yr) < 2e-2
-    monkeypatch.setenv("DMC_HALO_PRO", "0")
+    dmc_opt("DMC_HALO_PRO", 0)
     assert not K.conv_halo_prologue(d)
 
 
@@ -228,16 +228,16 @@ def test_conv_dgrad_wgrad(dt, case):
 @pytest.mark.parametrize("variant", ["ring3", "ring4", "regw"])
 @pytest.mark.parametrize("case", ["fwd32_concat", "fwd16_ragged_cout", "dgrad32", "fwd8_multi_image", "fallback_4x4",
                                   "fwd8_concat_b128", "fwd64_rows"])
-def test_conv3x3_halo_kernel(case, variant, monkeypatch):
+def test_conv3x3_halo_kernel(case, variant, monkeypatch, dmc_opt):
     """bf16 3x3 stride-1 convs on the LDS-halo kernel (whole-row 256-pixel tiles) vs an fp32 reference and
     vs the per-tap kernel (DMC_NO_HALO) on the same inputs. Variants: 3- or 4-slot LDS-DMA weight ring
     (DMC_HALO_WS4), register-staged weights (DMC_HALO_RW)."""
     L, K = _lib()
-    monkeypatch.setenv("DMC_HALO_WS4", "1" if variant == "ring4" else "0")
-    monkeypatch.setenv("DMC_HALO_RW", "1" if variant == "regw" else "0")
+    dmc_opt("DMC_HALO_WS4", 1 if variant == "ring4" else 0)
+    dmc_opt("DMC_HALO_RW", 1 if variant == "regw" else 0)
     # at these small M the planner would split K over the LDS-DMA kernel instead; the halo kernel is what the
     # B=128 model runs, so keep split-K off here to exercise it
-    monkeypatch.setenv("DMC_NO_SPLITK", "1")
+    dmc_opt("DMC_NO_SPLITK", 1)
     dt = torch.bfloat16
     torch.manual_seed(5)
     N, H, C1, C2, Cout, taps, pm = 2, 32, 64, 64, 128, K.TAPS3, L.PACK_FWD
@@ -275,7 +275,7 @@ def test_conv3x3_halo_kernel(case, variant, monkeypatch):
     K.set_epilogue(d, bias=bias.to(DEV), ldy1=Cout)
     outs = []
     for no_halo in ("0", "1"):
-        monkeypatch.setenv("DMC_NO_HALO", no_halo)
+        dmc_opt("DMC_NO_HALO", int(no_halo))
         y = torch.full((N, H, W, Cout), float("nan"), dtype=dt, device=DEV)
         K.conv(d, x1d, x2d, wp, y)
         torch.cuda.synchronize()
@@ -289,7 +289,7 @@ def test_conv3x3_halo_kernel(case, variant, monkeypatch):
         gd = nhwc(g).to(dt).to(DEV)
         dws = []
         for no_halo in ("0", "1"):
-            monkeypatch.setenv("DMC_NO_HALO", no_halo)
+            dmc_opt("DMC_NO_HALO", int(no_halo))
             dw = torch.full(tuple(w.shape), float("nan"), device=DEV)
             K.wgrad(d, gd, Cout, x1d, x2d, dw)
             torch.cuda.synchronize()
@@ -300,7 +300,7 @@ def test_conv3x3_halo_kernel(case, variant, monkeypatch):
 
 @pytest.mark.parametrize("shape", [(64, 8, 8, 256, 256), (128, 32, 32, 128, 0), (96, 16, 16, 136, 120),
                                    (64, 4, 4, 512, 0)])
-def test_groupnorm_stats_one_block_per_sample(shape, monkeypatch):
+def test_groupnorm_stats_one_block_per_sample(shape, monkeypatch, dmc_opt):
     """bf16 at N >= 64: statistics of a sample in one 1024-thread block, finalised in the same launch
     (gn_stats_one), vs torch fp32 group_norm statistics of the same bf16 values and vs the split path."""
     L, K = _lib()
@@ -313,7 +313,7 @@ def test_groupnorm_stats_one_block_per_sample(shape, monkeypatch):
     x1, x2 = xd[..., :C1].contiguous(), (xd[..., C1:].contiguous() if C2 else None)
     outs = []
     for split in ("0", "1"):
-        monkeypatch.setenv("DMC_GN_STATS_SPLIT", split)
+        dmc_opt("DMC_GN_STATS_SPLIT", int(split))
         sc, sh, mr = K.gn_stats(torch.bfloat16, x1, x2, N, H * W, C1, C2, C1, C2, G, 1e-5, gamma.to(DEV),
                                 beta.to(DEV))
         torch.cuda.synchronize()
@@ -334,7 +334,7 @@ def test_groupnorm_stats_one_block_per_sample(shape, monkeypatch):
 
 
 @pytest.mark.parametrize("shape", [(64, 8, 8, 256, 256), (128, 16, 16, 256, 0), (64, 4, 4, 384, 128)])
-def test_groupnorm_backward_one_block_per_sample(shape, monkeypatch):
+def test_groupnorm_backward_one_block_per_sample(shape, monkeypatch, dmc_opt):
     """bf16 at N >= 64 and HW*C <= 64K: the per-channel sums and apply coefficients of a sample in one
     1024-thread block (gn_bwd_one) vs torch fp32 autograd of SiLU(GN(x)), and vs the partial+final path, with
     dropout and the fused dx pixel sums."""
@@ -354,7 +354,7 @@ def test_groupnorm_backward_one_block_per_sample(shape, monkeypatch):
     _, _, mr = K.gn_stats(dt, x1, x2, N, H * W, C1, C2, C1, C2, G, 1e-5, gm_d, bt_d)
     res = {}
     for split in ("0", "1"):
-        monkeypatch.setenv("DMC_GN_BWD_SPLIT", split)
+        dmc_opt("DMC_GN_BWD_SPLIT", int(split))
         for drop in (None, (7, 1 << 30, 4.0 / 3.0)):   # (seed, thresh, scale): keep prob 0.75
             dx1, dx2 = torch.empty_like(x1), (torch.empty_like(x2) if C2 else None)
             dg, db = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
@@ -431,12 +431,12 @@ def test_groupnorm_stats_and_backward(dt):
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("path", ["auto", "staged", "hg4"])
 @pytest.mark.parametrize("Lq,hd", [(16, 64), (64, 64), (256, 64), (1024, 64), (64, 8), (100, 16)])
-def test_attention_fwd_bwd(dt, Lq, hd, path, monkeypatch):
+def test_attention_fwd_bwd(dt, Lq, hd, path, monkeypatch, dmc_opt):
     """auto: row-resident kernels for L <= 256 (one head per block at this batch), staged above; staged: the
     64-row-tile kernels everywhere (DMC_ATTN_STAGED); hg4: resident blocks owning 4 heads where they fit."""
     L, K = _lib()
-    monkeypatch.setenv("DMC_ATTN_STAGED", "1" if path == "staged" else "0")
-    monkeypatch.setenv("DMC_ATTN_HG", "4" if path == "hg4" else "0")
+    dmc_opt("DMC_ATTN_STAGED", 1 if path == "staged" else 0)
+    dmc_opt("DMC_ATTN_HG", 4 if path == "hg4" else 0)
     torch.manual_seed(3)
     N, heads = 2, 4
     C = heads * hd

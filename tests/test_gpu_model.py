@@ -83,7 +83,7 @@ def test_cifar_unet_matches_oracle(dtype):
     assert rel(out2, out[:2]) < (1e-5 if dtype == "fp32" else 1e-2)
 
 
-def test_cifar_unet_inference_halo_prologue_bitwise(monkeypatch):
+def test_cifar_unet_inference_halo_prologue_bitwise(monkeypatch, dmc_opt):
     """bf16 inference at B=128 with the opt-in DMC_HALO_PRO=1: the ResBlock convs that take the GN+SiLU
     prologue on the halo kernel (dmc_conv_halo_prologue) give bitwise the output of the materialised path."""
     from diffusion_models_collection_amd.models import UNet
@@ -96,7 +96,7 @@ def test_cifar_unet_inference_halo_prologue_bitwise(monkeypatch):
     t = torch.randint(0, 1000, (128,), device=DEV)
     outs = []
     for on in ("1", "0"):
-        monkeypatch.setenv("DMC_HALO_PRO", on)
+        dmc_opt("DMC_HALO_PRO", int(on))
         with torch.no_grad():
             outs.append(m(x, t).clone())
     ex = m._executor if hasattr(m, "_executor") else None
