@@ -101,7 +101,7 @@ def test_cifar_unet_inference_halo_prologue_bitwise(monkeypatch, dmc_opt):
             outs.append(m(x, t).clone())
     ex = m._executor if hasattr(m, "_executor") else None
     if ex is not None:
-        assert any(v for k, v in ex._halo_pro_cache.items() if k[-1] == "1"), "halo prologue never taken"
+        assert any(v for k, v in ex._halo_pro_cache.items() if k[-1] == 1), "halo prologue never taken"
     assert torch.equal(outs[0], outs[1])
 
 
