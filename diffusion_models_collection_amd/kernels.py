@@ -281,8 +281,26 @@ def embed_bwd(y, rows, dout, dtable):
           "dmc_embed_bwd")
 
 
+def _same(ref, *ts, what):
+    """Host-side operand validation before a launch: a shape the kernel does not expect is a Python error, never
+    an out-of-bounds device access."""
+    for t in ts:
+        if t is not None and (t.shape != ref.shape or t.device != ref.device):
+            raise L.DMCError(f"{what}: operand shape {tuple(t.shape)} on {t.device}, expected {tuple(ref.shape)} on "
+                             f"{ref.device}")
+
+
+def _steps(N, dev, *ts, what):
+    for t in ts:
+        if t is not None and (t.numel() != N or t.dtype != torch.long or t.device != dev or not t.is_contiguous()):
+            raise L.DMCError(f"{what}: timesteps must be a contiguous int64 [{N}] tensor on {dev}, got "
+                             f"{t.dtype} {tuple(t.shape)} on {t.device}")
+
+
 def pack_input(dtype, x, ld, noise=None, t=None, a=None, b=None, out=None):
     N, C, H, W = x.shape
+    _same(x, noise, what="dmc_pack_input")
+    _steps(N, x.device, t, what="dmc_pack_input")
     if out is None:
         out = torch.empty(N, H, W, ld, dtype=dtype, device=x.device)
     check(LIB.dmc_pack_input(L.dtype_code(dtype), ptr(x), ptr(noise), ptr(t), ptr(a), ptr(b), N, C, H, W, ptr(out), ld,
@@ -308,12 +326,15 @@ def q_sample(x0, noise, t, a, b, out=None):
     if out is None:
         out = torch.empty_like(x0, dtype=torch.float32)
     N = x0.shape[0]
+    _same(x0, noise, out, what="dmc_q_sample")
+    _steps(N, x0.device, t, what="dmc_q_sample")
     check(LIB.dmc_q_sample(ptr(x0), ptr(noise), ptr(t), ptr(a), ptr(b), N, x0.numel() // max(N, 1), ptr(out),
                            L.stream()), "dmc_q_sample")
     return out
 
 
 def loss_fwd(loss_type, pred, target):
+    _same(pred, target, what="dmc_loss_fwd")
     n = pred.numel()
     loss = torch.empty((), dtype=torch.float32, device=pred.device)
     ws = SCRATCH.get(4096 * 4, pred.device)
@@ -333,6 +354,8 @@ def ddim_step(x, eps, t, t_next, alphas_cumprod, eta=0.0, clip=True, x0=None, z=
     if out is None:
         out = torch.empty_like(x)
     N = x.shape[0]
+    _same(x, eps, x0, z, out, what="dmc_ddim_step")
+    _steps(N, x.device, t, t_next, what="dmc_ddim_step")
     check(LIB.dmc_ddim_step(ptr(x), ptr(eps), ptr(x0), ptr(t), ptr(t_next), ptr(alphas_cumprod), N, x.numel() // N,
                             float(eta), int(clip), ptr(z), ptr(out), L.stream()), "dmc_ddim_step")
     return out
@@ -342,6 +365,8 @@ def ddpm_step(x, eps, t, sra, srm1, c1, c2, logvar, clip=True, x0=None, z=None, 
     if out is None:
         out = torch.empty_like(x)
     N = x.shape[0]
+    _same(x, eps, x0, z, out, what="dmc_ddpm_step")
+    _steps(N, x.device, t, what="dmc_ddpm_step")
     check(LIB.dmc_ddpm_step(ptr(x), ptr(eps), ptr(x0), ptr(t), ptr(sra), ptr(srm1), ptr(c1), ptr(c2), ptr(logvar), N,
                             x.numel() // N, int(clip), ptr(z), ptr(out), L.stream()), "dmc_ddpm_step")
     return out
@@ -349,6 +374,8 @@ def ddpm_step(x, eps, t, sra, srm1, c1, c2, logvar, clip=True, x0=None, z=None, 
 
 def cfg_x0(x, ec, eu, scale, t, ta, tb, mode, p_threshold):
     N = x.shape[0]
+    _same(x, ec, eu, what="dmc_cfg_x0")
+    _steps(N, x.device, t, what="dmc_cfg_x0")
     eps = torch.empty_like(x)
     x0 = torch.empty_like(x)
     p = float(p_threshold) if p_threshold is not None else -1.0

@@ -124,19 +124,22 @@ class UNetExecutor:
     def _layout_grads(self):
         """Flat fp32 gradient buffer layout.
 
-        Slots follow the order in which the backward finishes them (reverse module order), so a prefix
-        of the buffer is final early (data-parallel all-reduce buckets). The 22 time_mlp weights, their
-        biases and the label_proj weights are placed side by side at the end: the stacked projection
-        GEMM's weight gradient then lands in place with no copy.
+        Slots follow the order in which the backward finishes them, so a prefix of the buffer is final early
+        (data-parallel all-reduce buckets): reverse module order for the blocks, then the time embedding
+        (its backward runs right after the last ResidualBlock's, before the input conv's, see backward()),
+        with the 22 time_mlp weights, their biases and the label_proj weights side by side (the stacked
+        projection GEMM's weight gradient lands in place with no copy), and the input conv LAST: the bucket
+        still in flight when the backward ends is then only the input conv's 3.5K gradients.
         """
         m = self.m
         rbs = [mod for mod in m.modules() if type(mod).__name__ == "ResidualBlock"]
         tail = [rb.time_mlp[1].weight for rb in rbs] + [rb.time_mlp[1].bias for rb in rbs]
         if m.num_classes is not None:
             tail += [rb.label_proj[1].weight for rb in rbs]
-        tail_ids = {id(p) for p in tail}
+        last = list(m.input_conv.parameters())
+        tail_ids = {id(p) for p in tail + last}
         head = [p for p in reversed(self.params) if id(p) not in tail_ids]
-        order = head + tail
+        order = head + tail + last
         self.goff = [0] * len(self.params)
         off = 0
         for p in order:
@@ -557,8 +560,16 @@ class UNetExecutor:
             order = sorted(range(len(self.params)), key=lambda i: self.goff[i])
             final = [False] * len(self.params)
             cursor = 0
-        for rec in reversed(tape):
+        recs = list(reversed(tape))
+        # the time-embedding backward needs only the accumulated daddvec (complete after the last ResidualBlock):
+        # run it before the input conv's, so its gradients (and all but the input conv's) are final earlier
+        ti = next(i for i, r in enumerate(recs) if r[0] == "temb")
+        ci = next(i for i, r in enumerate(recs) if r[0] == "conv_in")
+        if ci < ti:
+            recs.insert(ci, recs.pop(ti))
+        for ri, rec in enumerate(recs):
             kind = rec[0]
+            last = ri == len(recs) - 1
             self._backward_record(rec, dout, gv)
             if kind == "conv_in" and rec[3]:
                 dx = self._dx
@@ -569,9 +580,9 @@ class UNetExecutor:
                 while cursor < len(order) and final[order[cursor]]:
                     cursor += 1
                 hi = self.goff[order[cursor]] if cursor < len(order) else self.gtotal
-                if getattr(hook, "wants", None) is None or hook.wants(hi, kind == "temb"):
+                if getattr(hook, "wants", None) is None or hook.wants(hi, last):
                     self._join_side()      # the side stream's weight gradients of that prefix are written
-                hook(flat, hi, kind == "temb")
+                hook(flat, hi, last)
         self._join_side()
         self.daddvec = None
         grads = [self._gview(flat, p) for p in self.params]
@@ -592,7 +603,15 @@ class UNetExecutor:
             return list(rec[1].parameters())
         if kind == "conv_in":
             return list(m.input_conv.parameters())
-        return list(self.params)   # temb: everything else is final now
+        # temb: the time embedding MLP, the label embedding and every block's time_mlp / label_proj
+        ps = list(m.time_embed.parameters())
+        if m.label_embed is not None:
+            ps += list(m.label_embed.parameters())
+        for rb in self.res_blocks:
+            ps += list(rb.time_mlp.parameters())
+            if rb.label_proj is not None:
+                ps += list(rb.label_proj.parameters())
+        return ps
 
     def _backward_record(self, rec, dout, gv):
         m = self.m
