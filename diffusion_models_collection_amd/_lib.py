@@ -105,6 +105,20 @@ def _load():
         "dmc_upsample2x_nhwc": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_int, _c_p]),
         "dmc_unpack_output": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p]),
         "dmc_add": (_c_int, [_c_int, _c_p, _c_p, _c_long, _c_p]),
+        "dmc_ln_mod_fwd": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_p, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_f,
+                                    _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_p, _c_int, _c_p, _c_p, _c_p]),
+        "dmc_ln_mod_bwd": (_c_int, [_c_int, _c_p, _c_int, _c_p, _c_p, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_p,
+                                    _c_p, _c_p, _c_p]),
+        "dmc_gate_bwd": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_u32, _c_p, _c_u32,
+                                  _c_f, _c_p, _c_int, _c_p, _c_p]),
+        "dmc_gelu_fwd": (_c_int, [_c_int, _c_p, _c_long, _c_int, _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_p]),
+        "dmc_gelu_bwd": (_c_int, [_c_int, _c_p, _c_p, _c_long, _c_int, _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_p]),
+        "dmc_timestep_embedding": (_c_int, [_c_p, _c_int, _c_int, _c_f, _c_p, _c_p]),
+        "dmc_unpatchify": (_c_int, [_c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p]),
+        "dmc_patchify_grad": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_int, _c_p]),
+        "dmc_add_bcast": (_c_int, [_c_p, _c_p, _c_long, _c_long, _c_p]),
+        "dmc_batch_sum": (_c_int, [_c_p, _c_long, _c_long, _c_p, _c_p]),
+        "dmc_patch_dgrad": (_c_int, [_c_p, _c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -429,3 +429,70 @@ def adamw_flat_dev(p, g, m, v, ema, coef, hyper):
     """adamw_flat with the nine scalars (same order as adamw_flat's) read from the fp32 device tensor hyper."""
     check(LIB.dmc_adamw_flat_dev(ptr(p), ptr(g), ptr(m), ptr(v), ptr(ema), p.numel(), ptr(coef), ptr(hyper),
                                  L.stream()), "dmc_adamw_flat_dev")
+
+
+# ---- DiT token-wise kernels (csrc/dmc_dit.hip) ----------------------------------------------------------------
+def _mod_ptr(mod, off):
+    """Device address of column `off` of the stacked modulation rows [B][ld_mod] (fp32)."""
+    return None if mod is None else mod.data_ptr() + 4 * off
+
+
+def ln_mod_fwd(dtype, x, T, C, L_, mod, ld_mod, off_shift, off_scale, eps, h, ld_h, mean, rstd, br=None, ld_br=0,
+               off_gate=0, drop=None, x_out=None):
+    seed, seed_base, thresh, scale = drop_args(drop)
+    check(LIB.dmc_ln_mod_fwd(L.dtype_code(dtype), ptr(x), ptr(br), ld_br, _mod_ptr(mod, off_gate) if br is not None
+                             else None, _mod_ptr(mod, off_shift), _mod_ptr(mod, off_scale), ld_mod, T, C, L_,
+                             float(eps), seed, seed_base, thresh, scale, ptr(x_out), ptr(h), ld_h, ptr(mean),
+                             ptr(rstd), L.stream()), "dmc_ln_mod_fwd")
+
+
+def ln_mod_bwd(dtype, dh, ld_dh, x, mean, rstd, mod, ld_mod, off_scale, T, C, L_, dx, dmod, off_dscale, off_dshift):
+    check(LIB.dmc_ln_mod_bwd(L.dtype_code(dtype), ptr(dh), ld_dh, ptr(x), ptr(mean), ptr(rstd),
+                             _mod_ptr(mod, off_scale), ld_mod, T, C, L_, ptr(dx), _mod_ptr(dmod, off_dscale),
+                             _mod_ptr(dmod, off_dshift), L.stream()), "dmc_ln_mod_bwd")
+
+
+def gate_bwd(dtype, dy, br, ld_br, mod, ld_mod, off_gate, T, C, L_, dbr, ld_dbr, dmod, off_dgate, drop=None):
+    seed, seed_base, thresh, scale = drop_args(drop)
+    check(LIB.dmc_gate_bwd(L.dtype_code(dtype), ptr(dy), ptr(br), ld_br, _mod_ptr(mod, off_gate), ld_mod, T, C, L_,
+                           seed, seed_base, thresh, scale, ptr(dbr), ld_dbr, _mod_ptr(dmod, off_dgate), L.stream()),
+          "dmc_gate_bwd")
+
+
+def gelu_fwd(dtype, u, rows, C, ld, a, drop=None):
+    seed, seed_base, thresh, scale = drop_args(drop)
+    check(LIB.dmc_gelu_fwd(L.dtype_code(dtype), ptr(u), rows, C, ld, seed, seed_base, thresh, scale, ptr(a),
+                           L.stream()), "dmc_gelu_fwd")
+
+
+def gelu_bwd(dtype, da, u, rows, C, ld, du, drop=None):
+    seed, seed_base, thresh, scale = drop_args(drop)
+    check(LIB.dmc_gelu_bwd(L.dtype_code(dtype), ptr(da), ptr(u), rows, C, ld, seed, seed_base, thresh, scale, ptr(du),
+                           L.stream()), "dmc_gelu_bwd")
+
+
+def timestep_embedding(t, dim, out, max_period=10000.0):
+    _steps(t.shape[0], out.device, t, what="dmc_timestep_embedding")
+    check(LIB.dmc_timestep_embedding(ptr(t), t.shape[0], dim, float(max_period), ptr(out), L.stream()),
+          "dmc_timestep_embedding")
+
+
+def unpatchify(src, ld_src, B, ht, wt, p, C, out):
+    check(LIB.dmc_unpatchify(ptr(src), ld_src, B, ht, wt, p, C, ptr(out), L.stream()), "dmc_unpatchify")
+
+
+def patchify_grad(dtype, dout, B, ht, wt, p, C, out, ld_out):
+    check(LIB.dmc_patchify_grad(L.dtype_code(dtype), ptr(dout), B, ht, wt, p, C, ptr(out), ld_out, L.stream()),
+          "dmc_patchify_grad")
+
+
+def add_bcast(x, v, rows, n):
+    check(LIB.dmc_add_bcast(ptr(x), ptr(v), rows, n, L.stream()), "dmc_add_bcast")
+
+
+def batch_sum(x, rows, n, out):
+    check(LIB.dmc_batch_sum(ptr(x), rows, n, ptr(out), L.stream()), "dmc_batch_sum")
+
+
+def patch_dgrad(dtok, ld, w, B, ht, wt, p, C, H, dx):
+    check(LIB.dmc_patch_dgrad(ptr(dtok), ld, ptr(w), B, ht, wt, p, C, H, ptr(dx), L.stream()), "dmc_patch_dgrad")

@@ -91,7 +91,87 @@ class _PackCache:
             self.entries[k] = (v,) + e[1:]
 
 
-class UNetExecutor:
+class ExecCore:
+    """What every backbone executor shares: weight packing through the pack cache, the generic implicit-GEMM conv
+    / weight-gradient launchers over 1-2 NHWC sources, activation allocation and views of the flat gradient
+    buffer. Subclasses set self.dt, self.packs, self.device, self.training_grad_scale, self.pindex, self.goff."""
+
+    def _gview(self, flat, p):
+        i = self.pindex[id(p)]
+        o = self.goff[i]
+        return flat[o:o + p.numel()].view(p.shape)
+
+    # ---------------------------------------------------------------------------------------
+    def _wpack(self, conv, mode, Kc, dtype=None):
+        dtype = dtype or self.dt
+        w = conv.weight
+        if w.dim() == 2:
+            Cout, Cin, kh, kw = w.shape[0], w.shape[1], 1, 1
+        else:
+            Cout, Cin, kh, kw = w.shape
+        ntaps = 16 if mode == L.PACK_UPDGRAD else kh * kw
+        rows = Cout if mode == L.PACK_FWD else Cin
+
+        def make_buf():
+            return torch.empty(rows * ntaps * Kc, dtype=dtype, device=w.device)
+
+        return self.packs.get((id(conv), mode, Kc, dtype), (w,), make_buf,
+                              lambda buf: [(w, buf, 0, mode, Cout, Cin, kh, kw, Kc, -1)])
+
+    def _conv(self, srcs, conv, taps, OH, OW, Cout, mode=L.MODE_NORMAL, stride=1, pro=None, drop=None,
+              bias=None, addvec=None, ld_add=0, resid=None, out=None, out_f32=False, out_nchw=False,
+              dtype=None, packmode=L.PACK_FWD, w=None, Kc=None, silu_pre=None, ld_silu=0, split=None):
+        """Generic implicit-GEMM conv over 1-2 NHWC sources. pro = (kind, scale, shift)."""
+        dtype = dtype or self.dt
+        a = srcs[0]
+        C1 = a.C
+        C2 = srcs[1].C if len(srcs) > 1 else 0
+        ld1 = a.t.shape[-1]
+        ld2 = srcs[1].t.shape[-1] if len(srcs) > 1 else 0
+        N = a.t.shape[0]
+        if Kc is None:
+            Kc = L.kc_for(C1 + C2, dtype)
+        if w is None:
+            w = self._wpack(conv, packmode, Kc, dtype)
+        d = K.make_desc(dtype, N, a.H, a.W, C1, C2, ld1, ld2, Kc, OH, OW, Cout, taps, mode, stride)
+        if pro is not None:
+            K.set_prologue(d, pro[0], pro[1], pro[2], C1 + C2, drop, C1 + C2)
+        elif drop is not None:
+            raise ValueError("dropout needs a prologue")
+        ldy2 = 0
+        y2 = None
+        if split is not None:
+            (y1, ldy1), (y2, ldy2), csplit = split
+        else:
+            y1 = out
+            ldy1 = 0 if out_nchw else out.shape[-1]
+            csplit = None
+        K.set_epilogue(d, bias=bias, addvec=addvec, ld_add=ld_add, resid=resid,
+                       ld_res=(0 if resid is None or out_nchw else resid.shape[-1]), silu_pre=silu_pre,
+                       ld_silu=ld_silu, ldy1=ldy1, ldy2=ldy2, Csplit=csplit, out_f32=out_f32, out_nchw=out_nchw)
+        K.conv(d, a.t, srcs[1].t if len(srcs) > 1 else None, w, y1, y2)
+        return d
+
+    def _wgrad(self, srcs, dy, ld_dy, taps, OH, OW, Cout, dw, mode=L.MODE_NORMAL, stride=1, pro=None, drop=None,
+               dtype=None):
+        dtype = dtype or self.dt
+        a = srcs[0]
+        C1 = a.C
+        C2 = srcs[1].C if len(srcs) > 1 else 0
+        N = a.t.shape[0]
+        Kc = L.kc_for(C1 + C2, dtype)
+        d = K.make_desc(dtype, N, a.H, a.W, C1, C2, a.t.shape[-1], srcs[1].t.shape[-1] if len(srcs) > 1 else 0, Kc,
+                        OH, OW, Cout, taps, mode, stride)
+        if pro is not None:
+            K.set_prologue(d, pro[0], pro[1], pro[2], C1 + C2, drop, C1 + C2)
+        K.wgrad(d, dy, ld_dy, a.t, srcs[1].t if len(srcs) > 1 else None, dw, self.training_grad_scale)
+
+    def _new(self, N, H, W, C, dtype=None):
+        return Act(torch.empty(N, H, W, C, dtype=dtype or self.dt, device=self.device), H, W, C)
+
+
+
+class UNetExecutor(ExecCore):
     def __init__(self, model):
         self.m = model
         self.dt = model.compute_dtype
@@ -150,28 +230,6 @@ class UNetExecutor:
         self.temb_b_off = self.goff[self.pindex[id(tail[len(rbs)])]]
         self.temb_l_off = self.goff[self.pindex[id(tail[2 * len(rbs)])]] if m.num_classes is not None else None
 
-    def _gview(self, flat, p):
-        i = self.pindex[id(p)]
-        o = self.goff[i]
-        return flat[o:o + p.numel()].view(p.shape)
-
-    # ---------------------------------------------------------------------------------------
-    def _wpack(self, conv, mode, Kc, dtype=None):
-        dtype = dtype or self.dt
-        w = conv.weight
-        if w.dim() == 2:
-            Cout, Cin, kh, kw = w.shape[0], w.shape[1], 1, 1
-        else:
-            Cout, Cin, kh, kw = w.shape
-        ntaps = 16 if mode == L.PACK_UPDGRAD else kh * kw
-        rows = Cout if mode == L.PACK_FWD else Cin
-
-        def make_buf():
-            return torch.empty(rows * ntaps * Kc, dtype=dtype, device=w.device)
-
-        return self.packs.get((id(conv), mode, Kc, dtype), (w,), make_buf,
-                              lambda buf: [(w, buf, 0, mode, Cout, Cin, kh, kw, Kc, -1)])
-
     def _temb_lins(self, which):
         return [(rb.time_mlp[1] if which == 0 else rb.label_proj[1]) for rb in self.res_blocks]
 
@@ -229,54 +287,6 @@ class UNetExecutor:
                               jobs)
 
     # ---------------------------------------------------------------------------------------
-    def _conv(self, srcs, conv, taps, OH, OW, Cout, mode=L.MODE_NORMAL, stride=1, pro=None, drop=None,
-              bias=None, addvec=None, ld_add=0, resid=None, out=None, out_f32=False, out_nchw=False,
-              dtype=None, packmode=L.PACK_FWD, w=None, Kc=None, silu_pre=None, ld_silu=0, split=None):
-        """Generic implicit-GEMM conv over 1-2 NHWC sources. pro = (kind, scale, shift)."""
-        dtype = dtype or self.dt
-        a = srcs[0]
-        C1 = a.C
-        C2 = srcs[1].C if len(srcs) > 1 else 0
-        ld1 = a.t.shape[-1]
-        ld2 = srcs[1].t.shape[-1] if len(srcs) > 1 else 0
-        N = a.t.shape[0]
-        if Kc is None:
-            Kc = L.kc_for(C1 + C2, dtype)
-        if w is None:
-            w = self._wpack(conv, packmode, Kc, dtype)
-        d = K.make_desc(dtype, N, a.H, a.W, C1, C2, ld1, ld2, Kc, OH, OW, Cout, taps, mode, stride)
-        if pro is not None:
-            K.set_prologue(d, pro[0], pro[1], pro[2], C1 + C2, drop, C1 + C2)
-        elif drop is not None:
-            raise ValueError("dropout needs a prologue")
-        ldy2 = 0
-        y2 = None
-        if split is not None:
-            (y1, ldy1), (y2, ldy2), csplit = split
-        else:
-            y1 = out
-            ldy1 = 0 if out_nchw else out.shape[-1]
-            csplit = None
-        K.set_epilogue(d, bias=bias, addvec=addvec, ld_add=ld_add, resid=resid,
-                       ld_res=(0 if resid is None or out_nchw else resid.shape[-1]), silu_pre=silu_pre,
-                       ld_silu=ld_silu, ldy1=ldy1, ldy2=ldy2, Csplit=csplit, out_f32=out_f32, out_nchw=out_nchw)
-        K.conv(d, a.t, srcs[1].t if len(srcs) > 1 else None, w, y1, y2)
-        return d
-
-    def _wgrad(self, srcs, dy, ld_dy, taps, OH, OW, Cout, dw, mode=L.MODE_NORMAL, stride=1, pro=None, drop=None,
-               dtype=None):
-        dtype = dtype or self.dt
-        a = srcs[0]
-        C1 = a.C
-        C2 = srcs[1].C if len(srcs) > 1 else 0
-        N = a.t.shape[0]
-        Kc = L.kc_for(C1 + C2, dtype)
-        d = K.make_desc(dtype, N, a.H, a.W, C1, C2, a.t.shape[-1], srcs[1].t.shape[-1] if len(srcs) > 1 else 0, Kc,
-                        OH, OW, Cout, taps, mode, stride)
-        if pro is not None:
-            K.set_prologue(d, pro[0], pro[1], pro[2], C1 + C2, drop, C1 + C2)
-        K.wgrad(d, dy, ld_dy, a.t, srcs[1].t if len(srcs) > 1 else None, dw, self.training_grad_scale)
-
     def _gn(self, srcs, gn, dtype=None):
         dtype = dtype or self.dt
         a = srcs[0]
@@ -313,9 +323,6 @@ class UNetExecutor:
             K.set_prologue(d, L.PRO_AFFINE_SILU, st[0], st[1], C1 + C2)
             ok = self._halo_pro_cache[key] = K.conv_halo_prologue(d)
         return ok
-
-    def _new(self, N, H, W, C, dtype=None):
-        return Act(torch.empty(N, H, W, C, dtype=dtype or self.dt, device=self.device), H, W, C)
 
     def _grad_target(self, act):
         """(buffer, accumulate) for writing a gradient contribution into act.grad."""

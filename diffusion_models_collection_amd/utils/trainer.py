@@ -29,8 +29,9 @@ from .. import kernels as K
 from .helpers import resolve_image_size
 
 
-def _is_dmc_unet(m):
-    return type(m).__name__ == "UNet" and hasattr(m, "executor") and type(m).__module__.startswith(
+def _is_dmc_model(m):
+    """A backbone run by one of this package's executors (UNet, DiT): flat gradients, fused optimizer, graphs."""
+    return type(m).__name__ in ("UNet", "DiT") and hasattr(m, "executor") and type(m).__module__.startswith(
         "diffusion_models_collection_amd")
 
 
@@ -247,7 +248,7 @@ class GraphedTrainStep:
         return (os.environ.get("DMC_GRAPH", "1") != "0"
                 and (not trainer.is_distributed or trainer.grad_sync is not None)
                 and trainer._flat is not None and trainer.gradient_accumulation_steps == 1
-                and _is_dmc_unet(trainer._raw_model))
+                and _is_dmc_model(trainer._raw_model))
 
     def _key(self, images, y):
         return (tuple(images.shape), images.device, None if y is None else tuple(y.shape))
@@ -443,7 +444,7 @@ class DiffusionTrainer:
         self._raw_model = self.model
         self.grad_sync = None
         if self.is_distributed:
-            if _is_dmc_unet(self.model):
+            if _is_dmc_model(self.model):
                 # DDP's init broadcast, then gradient averaging from inside the HIP backward
                 with torch.no_grad():
                     for t in list(self.model.parameters()) + list(self.model.buffers()):
@@ -493,8 +494,8 @@ class DiffusionTrainer:
         self._ema_refs = None
         self._clip_refs = None
         self._flat = None
-        if _is_dmc_unet(self._module) and FlatAdamW.supported(self._module, optimizer) and (
-                self.ema_model is None or _is_dmc_unet(self.ema_model)):
+        if _is_dmc_model(self._module) and FlatAdamW.supported(self._module, optimizer) and (
+                self.ema_model is None or _is_dmc_model(self.ema_model)):
             self._flat = FlatAdamW(self._module, optimizer, self.ema_model)
         self._graph = GraphedTrainStep(self) if GraphedTrainStep.supported(self) else None
 

@@ -249,6 +249,44 @@ int dmc_unpack_output(int dtype, const void* src, int ld, int N, int C, int H, i
                       void* stream);
 int dmc_add(int dtype, void* y, const void* x, long n, void* stream);
 
+
+/* ---- DiT backbone (models/dit.py of the reference; dmc_dit.hip) ----------------------------------------------
+ * Token rows [T = B*L][C]; the residual stream x is fp32, GEMM operands (h, branch) are in `dtype`.
+ * Modulation vectors (shift / scale / gate) are rows of the stacked adaLN GEMM output [B][ld_mod].
+ * ln_mod_fwd: DiTBlock.forward (dit.py:113-130): x_new = x + gate * dropout(br) when br != NULL (x_out = x_new),
+ *   then h = LayerNorm(x_new; eps, no affine) * (1 + scale) + shift; saves the row mean / rstd.
+ * ln_mod_bwd: dx += d/dx of that LayerNorm + modulation for upstream dh; dscale / dshift = sums over each image's
+ *   L rows (written).  gate_bwd: dbr = dy * gate (* dropout mask); dgate = per-image row sums of dy * dropout(br).
+ * gelu_fwd / gelu_bwd: nn.GELU() (erf) + nn.Dropout between the MLP Linears (dit.py:100-104).
+ * timestep_embedding: TimestepEmbedder.timestep_embedding (dit.py:38-47) -> [B][dim] = [cos | sin].
+ * unpatchify: DiT.unpatchify (dit.py:248-261) [B*ht*wt][ld_src >= p*p*C] -> NCHW; patchify_grad is its adjoint.
+ * add_bcast: x[r][i] += v[i] (pos_embed broadcast over the batch, dit.py:274). */
+int dmc_ln_mod_fwd(int dtype, const float* x, const void* br, int ld_br, const float* gate, const float* shift,
+                   const float* scale, int ld_mod, int T, int C, int L, float eps, uint32_t drop_seed,
+                   const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, float* x_out, void* h,
+                   int ld_h, float* mean, float* rstd, void* stream);
+int dmc_ln_mod_bwd(int dtype, const void* dh, int ld_dh, const float* x, const float* mean, const float* rstd,
+                   const float* scale, int ld_mod, int T, int C, int L, float* dx, float* dscale, float* dshift,
+                   void* stream);
+int dmc_gate_bwd(int dtype, const float* dy, const void* br, int ld_br, const float* gate, int ld_mod, int T, int C,
+                 int L, uint32_t drop_seed, const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale,
+                 void* dbr, int ld_dbr, float* dgate, void* stream);
+int dmc_gelu_fwd(int dtype, const void* u, long rows, int C, int ld, uint32_t drop_seed, const uint32_t* drop_seed_base,
+                 uint32_t drop_thresh, float drop_scale, void* a, void* stream);
+int dmc_gelu_bwd(int dtype, const void* da, const void* u, long rows, int C, int ld, uint32_t drop_seed,
+                 const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* du, void* stream);
+int dmc_timestep_embedding(const int64_t* t, int B, int dim, float max_period, float* out, void* stream);
+int dmc_unpatchify(const float* src, int ld_src, int B, int ht, int wt, int p, int C, float* dst, void* stream);
+int dmc_patchify_grad(int dtype, const float* dout, int B, int ht, int wt, int p, int C, void* dst, int ld_dst,
+                      void* stream);
+int dmc_add_bcast(float* x, const float* v, long rows, long n, void* stream);
+/* batch_sum: out[i] = sum_r x[r][i] (fp32, rows summed in order): the pos_embed gradient.
+ * patch_dgrad: input gradient of the patch embedding Conv2d(k=p, s=p) (dit.py:21): dx[B][C][ht*p][wt*p] from the
+ * fp32 token gradient dtok[B*ht*wt][ld] and the fp32 weight [H][C][p][p]. */
+int dmc_batch_sum(const float* x, long rows, long n, float* out, void* stream);
+int dmc_patch_dgrad(const float* dtok, int ld, const float* w, int B, int ht, int wt, int p, int C, int H, float* dx,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

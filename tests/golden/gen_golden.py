@@ -30,6 +30,11 @@ Fixture list (every array is float32 / int64 data, loaded with numpy.load(allow_
                      strings and the config dict only: loads with torch.load(weights_only=True))
   ckpt_resume.npz    the inputs of a 3rd step and the reference's loss / parameters / EMA after resuming
                      from trainer_ckpt.pth and running it
+  dit_tiny_*.npz     tiny DiTs (models/dit.py; patch 2 conditional, patch 4 unconditional), parameters
+                     perturbed away from the zero adaLN init, input, output (and the y=None output), the
+                     gradients of sum(out * cot) w.r.t. every parameter and x
+  dit_s2.npz         DiT-S/2 at 32x32 (BASELINE config #4): weights NOT stored (seed + perturbation are
+                     reproduced, per-tensor checksums pin them), output, grad_x, gradient summaries
 """
 import os
 import sys
@@ -383,10 +388,87 @@ def gen_checkpoint():
     npz(OUT / "ckpt_resume.npz", **arrs)
 
 
+DIT_CFGS = {
+    # 8x8 tokens of 2x2 patches, 2 heads of 32, conditional (label 0 = null, 11 exercises the clamp)
+    "dit_tiny_cond": dict(img_size=(16, 16), patch_size=2, in_channels=3, hidden_size=64, depth=2, num_heads=2,
+                          mlp_ratio=4.0, num_classes=10, dropout=0.0),
+    # 4x4 patches (16 taps), 1 channel, 4 heads of 16, unconditional, non-square image
+    "dit_tiny_p4": dict(img_size=(16, 32), patch_size=4, in_channels=1, hidden_size=64, depth=2, num_heads=4,
+                        mlp_ratio=2.0, num_classes=None, dropout=0.0),
+}
+# BASELINE config #4: DiT-S/2 at 32x32, 10 classes
+DIT_S2 = dict(img_size=(32, 32), patch_size=2, in_channels=3, hidden_size=384, depth=12, num_heads=6, mlp_ratio=4.0,
+              num_classes=10, dropout=0.0)
+
+
+def perturb_dit(m, std, seed=11):
+    """The reference zero-initialises every adaLN projection and the final linear (models/dit.py:239-247), which
+    makes a fresh DiT output exactly 0 and most gradients vanish: add seeded N(0, std) to every parameter (in
+    named_parameters order) so that the fixture exercises every path. The build's DiT applies the same
+    perturbation (tests/test_oracle.py: perturb_dit)."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for _, p in m.named_parameters():
+            p.add_(std * torch.randn(p.shape, generator=g))
+
+
+def _dit_inputs(cfg, B):
+    g = torch.Generator().manual_seed(7)
+    C, (H, W) = cfg["in_channels"], cfg["img_size"]
+    x = torch.randn(B, C, H, W, generator=g).requires_grad_(True)
+    t = torch.tensor([17, 903, 500, 0][:B], dtype=torch.long)
+    y = torch.tensor([0, 11, 3, 10][:B], dtype=torch.long) if cfg["num_classes"] is not None else None
+    return g, x, t, y
+
+
+def gen_dit(name, cfg, B=2):
+    from models.dit import DiT
+    torch.manual_seed(1234)
+    m = DiT(**cfg).float()
+    perturb_dit(m, 0.05)
+    m.train()   # dropout 0.0 -> deterministic
+    g, x, t, y = _dit_inputs(cfg, B)
+    out = m(x, t, y)
+    cot = torch.randn(out.shape, generator=g)
+    (out * cot).sum().backward()
+    arrs = {"x": x.detach(), "t": t, "out": out.detach(), "cot": cot, "grad_x": x.grad}
+    if y is not None:
+        arrs["y"] = y
+        with torch.no_grad():
+            arrs["out_ynone"] = m(x.detach(), t, None)
+    for k, v in m.state_dict().items():
+        arrs["param/" + k] = v
+    for k, p in m.named_parameters():
+        arrs["grad/" + k] = p.grad
+    npz(OUT / f"{name}.npz", **arrs)
+
+
+def gen_dit_s2(B=2):
+    """Weights not stored: torch.manual_seed(1234) + perturb_dit(std 0.02) is reproduced by the tests and pinned by
+    the per-tensor checksums."""
+    from models.dit import DiT
+    torch.manual_seed(1234)
+    m = DiT(**DIT_S2).float()
+    perturb_dit(m, 0.02)
+    m.train()
+    g, x, t, y = _dit_inputs(DIT_S2, B)
+    out = m(x, t, y)
+    cot = torch.randn(out.shape, generator=g)
+    (out * cot).sum().backward()
+    arrs = {"x": x.detach(), "t": t, "y": y, "out": out.detach(), "cot": cot, "grad_x": x.grad}
+    for k, v in m.state_dict().items():
+        arrs[f"psum/{k}"] = v.double().sum().reshape(1)
+        arrs[f"pabs/{k}"] = v.double().abs().sum().reshape(1)
+    for k, p in m.named_parameters():
+        grad_summary(k, p.grad, arrs, "g")
+    npz(OUT / "dit_s2.npz", **arrs)
+
+
 GENERATORS = {"schedules": gen_schedules, "tiny": lambda: [gen_unet(n, c) for n, c in TINY_CFGS.items()],
               "diffusion_ops": gen_diffusion_ops, "trainer_traj": gen_trainer_traj,
               "ddpm_sample": gen_ddpm_sample, "big": lambda: [gen_big_unet(n, c) for n, c in BIG_CFGS.items()],
-              "checkpoint": gen_checkpoint}
+              "checkpoint": gen_checkpoint, "dit": lambda: [gen_dit(n, c) for n, c in DIT_CFGS.items()],
+              "dit_s2": gen_dit_s2}
 
 
 if __name__ == "__main__":
