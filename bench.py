@@ -22,6 +22,8 @@ The JSON line also carries:
                 UNet (10 classes), B=128 per GPU as one 256-row forward per step
   celeba64      BASELINE config #5 on one GPU: the same network at 64x64, train img/s and DDIM-100 img/s
   fp32          the headline train step in the reference's own arithmetic (fp32 parity mode)
+  dit_s2_ddim50_cfg  BASELINE config #4: DiT-S/2 conditional DDIM-50 + CFG 3.0 sampling img/s (replicas) with
+                its MFMA roofline, and the DiT train step img/s (--no-dit skips it)
 (celeba64 / fp32 only at N=1; --no-extra skips them.) `--image-size 64 --sample-steps 100` makes config #5 the
 headline line instead.
 """
@@ -235,6 +237,53 @@ def sample_rate(fn, world):
     return max_over_ranks(el, world)
 
 
+DIT_S2 = dict(img_size=(32, 32), patch_size=2, in_channels=3, hidden_size=384, depth=12, num_heads=6, mlp_ratio=4.0)
+
+
+def dit_lines(args, dev, rank, world, B):
+    """BASELINE config #4: DiT-S/2 (conditional, 10 classes) DDIM-50 + CFG 3.0 sampling img/s, replicas (each rank
+    samples its own B images; the cond and null-label rows run as ONE 2B forward per step). The roofline is the
+    whole sampling loop's MFMA work: DiT forward FLOPs (linears, patch conv, attention matmuls) x 2B rows x 50
+    steps / measured seconds, vs the dense bf16 peak. Also the DiT train step img/s (dropout 0: attention-
+    probability dropout is not implemented on the HIP path, see models/dit.py)."""
+    from diffusion_models_collection_amd.models import DiT
+    from diffusion_models_collection_amd.models._dit_exec import dit_flops_per_image
+    from diffusion_models_collection_amd.diffusion import DDIM, DDPM
+    from diffusion_models_collection_amd.utils.trainer import DiffusionTrainer
+    torch.manual_seed(44 + rank)
+    m = DiT(**DIT_S2, num_classes=10, dropout=0.0, compute_dtype=args.dtype).to(dev).eval()
+    ddim = DDIM(1000, 50, device=dev)
+    yl = torch.arange(B, device=dev) % 10 + 1
+    el = sample_rate(lambda: ddim.sample_with_cfg(m, (B, 3, 32, 32), yl, cfg_scale=3.0), world)
+    gf = dit_flops_per_image(m) / 1e9
+    tfs = 2 * B * 50 * gf / el / 1e3
+    res = {"value": round(world * B / el, 2), "unit": "img/s", "batch_per_gpu": B, "steps": 50, "cfg_scale": 3.0,
+           "p_threshold": 0.995, "forward_batch": 2 * B, "seconds": round(el, 3), "scaling": "replicas",
+           "model": "DiT-S/2 (hidden 384, depth 12, 6 heads, patch 2, 256 tokens), 10 classes",
+           "gflop_per_forward_img": round(gf, 3),
+           "roofline": {"bound": "mfma", "achieved": round(tfs, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(tfs / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+                        "scope": "whole DDIM-50 CFG loop per GPU"}}
+    if not args.no_train:
+        mt = DiT(**DIT_S2, num_classes=10, dropout=0.0, compute_dtype=args.dtype).to(dev)
+        opt = torch.optim.AdamW(mt.parameters(), lr=1e-4, weight_decay=1e-4)
+        cfg = {"epochs": 1, "save_dir": "/tmp/dmc_bench_ckpt", "sample_dir": "/tmp/dmc_bench_smp", "loss_type": "l2",
+               "use_ema": True, "ema_decay": 0.9999, "model_type": "dit", "conditional": True, "num_classes": 10,
+               "cfg_dropout_prob": 0.2, "model_params": dict(DIT_S2, dropout=0.0)}
+        tr = DiffusionTrainer(mt, DDPM(device=dev), None, opt, None, device=dev, config=cfg, rank=rank,
+                              world_size=world)
+        gen = torch.Generator(device=dev).manual_seed(77 + rank)
+        pool = [(torch.rand(B, 3, 32, 32, device=dev, generator=gen) * 2 - 1,
+                 torch.randint(0, 10, (B,), device=dev, generator=gen)) for _ in range(2)]
+        mt.train()
+        et, _ = train_rate(tr, pool, 10, 3, world)
+        res["train_img_s"] = round(world * B * 10 / et, 2)
+        res["train_ms_per_step"] = round(et / 10 * 1e3, 3)
+        res["train_tflops_per_gpu"] = round(B * 10 / et * 3 * gf / 1e3, 2)
+        res["train_note"] = "conditional, CFG label dropout 0.2, EMA, dropout 0 (fwd+bwd = 3x forward FLOPs)"
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -254,7 +303,13 @@ def main():
     ap.add_argument("--image-size", type=int, default=32, help="32 (CIFAR-10, headline) or 64 (CelebA, config #5)")
     ap.add_argument("--no-extra", dest="extra", action="store_false",
                     help="skip the 64x64 (config #5) and fp32 side lines")
+    ap.add_argument("--no-dit", dest="dit", action="store_false", help="skip the DiT-S/2 (config #4) line")
+    ap.add_argument("--dit-only", action="store_true", help="only the DiT-S/2 line (profiling)")
     args = ap.parse_args()
+    if args.dit_only:
+        torch.cuda.set_device(0)
+        print(json.dumps(dit_lines(args, torch.device("cuda", 0), 0, 1, args.batch)), flush=True)
+        return
     if args.roofline_only:
         print(json.dumps(conv_roofline(torch.bfloat16 if args.dtype == "bf16" else torch.float32)), flush=True)
         return
@@ -331,6 +386,9 @@ def main():
                                                    "p_threshold": 0.995, "forward_batch": 2 * B,
                                                    "seconds": round(cel, 3), "scaling": "replicas"}
             del cmodel
+    if args.dit and S == 32:
+        model = trainer = None          # free the UNet's HBM before the DiT runs
+        out["dit_s2_ddim50_cfg"] = dit_lines(args, dev, rank, world, B)
     if args.extra and S == 32 and not args.no_train and world == 1:
         # BASELINE config #5 beside the headline: the same network at 64x64 (CelebA), train + DDIM-100
         del model, trainer
