@@ -470,6 +470,19 @@ DMC_DEV void glds_issue_buf(const ConvK& a, char* base, int c0, unsigned k2, int
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (LDS_AS void*)(base + BM * 128 + (wave * BI + j) * 1024), 16, ob[j] + k2, 0, 0, 0);
 }
 
+// XCD-aware tile order of a 1-D grid over MB x NB output tiles. Workgroups are dealt to the 8 XCDs round-robin
+// (block b -> XCD b % 8) and each XCD has its own L2: XCD x gets the contiguous tile range [x*per, (x+1)*per)
+// with the NB output-channel tiles of one pixel tile adjacent, so the blocks that share an activation tile
+// run together on one XCD and read it from that XCD's L2 once (with blockIdx.y = channel tile, every round of
+// 256 blocks streamed ALL the activations again for ONE weight tile: the DiT's 1536-wide linear read its
+// 50 MB input 12 times). The tail (total % 8 blocks) keeps its own index; the map is a bijection.
+DMC_DEV void xcd_tile(int NB, int& mb, int& nb) {
+  const int total = gridDim.x, bid = blockIdx.x, per = total >> 3;
+  const int t = bid < (per << 3) ? (bid & 7) * per + (bid >> 3) : bid;
+  mb = t / NB;
+  nb = t - mb * NB;
+}
+
 // BUF = true: all operands through buffer resources (raw_ptr_buffer_load_lds), zero padding by the
 // hardware range check, per-row offsets precomputed once per tap -> one VALU add per DMA instruction.
 // Requires C1 % 64 == 0, C2 % 64 == 0, Kc == C1 + C2 (a stage never straddles the concat boundary).
@@ -489,8 +502,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave % WM, wn = wave / WM;
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  int mb = blockIdx.x, nb = blockIdx.y;
+  if (!a.sk) xcd_tile((a.Cout + BN - 1) / BN, mb, nb);   // 1-D grid (split-K launches keep the 3-D grid)
+  const int m0 = mb * BM;
+  const int n0 = nb * BN;
   const int lrow = lane >> 3;
   const int lc = (lane & 7) ^ lrow;             // logical 16-byte chunk this lane fetches
 
@@ -728,7 +743,9 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave % WM, wn = wave / WM;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  int mb = blockIdx.x, nb = blockIdx.y;
+  if (gridDim.y == 1) xcd_tile((a.Cout + BN - 1) / BN, mb, nb);   // 1-D launch: XCD-aware tile order
+  const int m0 = mb * BM, n0 = nb * BN;
   const int lrow = lane >> 3;
   const int lc = (lane & 7) ^ lrow;
   const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
@@ -2347,11 +2364,11 @@ void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
     const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
     conv_splitk_epilogue_kernel<bf16_t><<<blocks, 256, 0, s>>>(k, p.splits, Cpad);
   } else if (p.cfg == 0) {
-    conv_fwd_glds_kernel<4, 2, BUF><<<dim3(dmc::cdiv(k.M, 256), dmc::cdiv(k.Cout, 128)), 512, 0, s>>>(k);
+    conv_fwd_glds_kernel<4, 2, BUF><<<dmc::cdiv(k.M, 256) * dmc::cdiv(k.Cout, 128), 512, 0, s>>>(k);
   } else if (p.cfg == 1) {
-    conv_fwd_glds_kernel<2, 2, BUF><<<dim3(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128)), 256, 0, s>>>(k);
+    conv_fwd_glds_kernel<2, 2, BUF><<<dmc::cdiv(k.M, 128) * dmc::cdiv(k.Cout, 128), 256, 0, s>>>(k);
   } else {
-    conv_fwd_glds_kernel<1, 2, BUF><<<dim3(dmc::cdiv(k.M, 64), dmc::cdiv(k.Cout, 128)), 128, 0, s>>>(k);
+    conv_fwd_glds_kernel<1, 2, BUF><<<dmc::cdiv(k.M, 64) * dmc::cdiv(k.Cout, 128), 128, 0, s>>>(k);
   }
 }
 
@@ -2371,9 +2388,9 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
   if (sizeof(T) == 2 && k.prologue == DMC_PRO_AFFINE_SILU) {
     int R, nimg;
     const int hp = halo_pro_plan(k, &R, &nimg);
-    const dim3 hg(k.M / 256, dmc::cdiv(k.Cout, 128));
-    if (hp == 6) { conv3x3_halo_kernel<6, 3, true><<<hg, 512, 0, s>>>(k, R, nimg); return dmc::check_launch("dmc_conv2d"); }
-    if (hp == 7) { conv3x3_halo_kernel<7, 3, true><<<hg, 512, 0, s>>>(k, R, nimg); return dmc::check_launch("dmc_conv2d"); }
+    const int hg1 = k.M / 256 * dmc::cdiv(k.Cout, 128);   // 1-D: the kernel maps it XCD-aware
+    if (hp == 6) { conv3x3_halo_kernel<6, 3, true><<<hg1, 512, 0, s>>>(k, R, nimg); return dmc::check_launch("dmc_conv2d"); }
+    if (hp == 7) { conv3x3_halo_kernel<7, 3, true><<<hg1, 512, 0, s>>>(k, R, nimg); return dmc::check_launch("dmc_conv2d"); }
   }
   if (sizeof(T) == 2 && k.prologue == DMC_PRO_NONE && !dmc::opt(dmc::OPT_NO_GLDS)) {
     // bf16, plain operands: LDS-DMA pipelined kernel
@@ -2429,11 +2446,11 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
       if (hp == 6) conv3x3_halo_rw_kernel<6><<<hg, 512, 0, s>>>(k, R, nimg);
       else conv3x3_halo_rw_kernel<7><<<hg, 512, 0, s>>>(k, R, nimg);
     } else if (hp == 6 && dmc::opt(dmc::OPT_HALO_WS4))
-      conv3x3_halo_kernel<6, 4><<<hg, 512, 0, s>>>(k, R, nimg);
+      conv3x3_halo_kernel<6, 4><<<hg.x * hg.y, 512, 0, s>>>(k, R, nimg);
     else if (hp == 6)
-      conv3x3_halo_kernel<6, 3><<<hg, 512, 0, s>>>(k, R, nimg);
+      conv3x3_halo_kernel<6, 3><<<hg.x * hg.y, 512, 0, s>>>(k, R, nimg);
     else if (hp == 7)
-      conv3x3_halo_kernel<7, 3><<<hg, 512, 0, s>>>(k, R, nimg);
+      conv3x3_halo_kernel<7, 3><<<hg.x * hg.y, 512, 0, s>>>(k, R, nimg);
     else if (buf) launch_glds<true>(k, p, s);
     else launch_glds<false>(k, p, s);
     return dmc::check_launch("dmc_conv2d");
