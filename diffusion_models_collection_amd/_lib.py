@@ -23,6 +23,9 @@ _c_int, _c_p, _c_f, _c_u32, _c_long, _c_size = (ctypes.c_int, ctypes.c_void_p, c
                                                 ctypes.c_long, ctypes.c_size_t)
 
 
+ACT_NONE, ACT_GELU = 0, 1   # include/dmc.h DMC_ACT_*
+
+
 class ConvDesc(ctypes.Structure):
     _fields_ = [
         ("dtype", _c_int), ("N", _c_int), ("H", _c_int), ("W", _c_int),
@@ -34,7 +37,7 @@ class ConvDesc(ctypes.Structure):
         ("drop_seed_base", _c_p),
         ("bias", _c_p), ("addvec", _c_p), ("ld_add", _c_int), ("resid", _c_p), ("ld_res", _c_int),
         ("silu_pre", _c_p), ("ld_silu", _c_int), ("Csplit", _c_int), ("ldy1", _c_int), ("ldy2", _c_int),
-        ("out_f32", _c_int), ("out_nchw", _c_int),
+        ("out_f32", _c_int), ("out_nchw", _c_int), ("act", _c_int), ("y_pre", _c_p), ("ld_pre", _c_int),
     ]
 
 

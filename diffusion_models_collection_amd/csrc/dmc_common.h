@@ -133,6 +133,8 @@ template <> DMC_DEV v4i lds_frag_tr<bf16_t>(const char* base, int pitch, int k0,
 // backward passes recompute SiLU' per element and were VALU-bound on the division. exp(-z) = inf gives 0.
 DMC_DEV float sigmoid_f(float z) { return __builtin_amdgcn_rcpf(1.0f + __expf(-z)); }
 DMC_DEV float silu_f(float z) { return z * sigmoid_f(z); }
+// nn.GELU() (exact): 0.5 u (1 + erf(u / sqrt 2)) -- the DiT MLP activation (dmc_dit.hip, the conv epilogue)
+DMC_DEV float gelu_f(float u) { return 0.5f * u * (1.0f + erff(u * 0.70710678118654752f)); }
 
 // Counter-based hash for dropout masks: recomputable in backward from (seed, element index).
 DMC_DEV uint32_t hash_u32(uint32_t x, uint32_t seed) {

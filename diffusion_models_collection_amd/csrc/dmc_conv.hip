@@ -24,6 +24,7 @@ struct ConvK {
   const float* bias; const float* addvec; int ld_add;
   const char* resid; int ld_res; const float* silu_pre; int ld_silu;
   int Csplit, ldy1, ldy2, out_f32, out_nchw;
+  int act; char* ypre; int ldpre;   // DMC_ACT_GELU epilogue (+ optional pre-activation copy)
   int M;      // N*OH*OW output pixels
   int OHW;    // OH*OW
   float* sk;  // split-K partial slab (nullptr: no split)
@@ -261,6 +262,18 @@ DMC_DEV void conv_epilogue(const ConvK& a, v4f (&acc)[TN][TM], int pix_base, int
     for (int i = 0; i < TN; ++i) conv_store_tile<T>(a, acc[i][j], pix_base + j * 16 + fr, co_base + i * 16 + fh * 4);
 }
 
+// GELU epilogue on 4 channels: the pre-activation is stored (if asked) in the output dtype, and the activation
+// is taken of that stored (rounded) value, so the fused result is bitwise gelu_fwd of the stored tensor.
+template <typename T>
+DMC_DEV void apply_act(const ConvK& a, float* v, int pix, int co, bool of32) {
+  if (a.ypre) store4<T>(a.ypre, (size_t)pix * a.ldpre + co, v, of32);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float u = (sizeof(T) == 2 && !of32) ? bf2f(f2bf(v[e])) : v[e];
+    v[e] = gelu_f(u);
+  }
+}
+
 template <typename T>
 DMC_DEV void conv_store_tile(const ConvK& a, const v4f accv, const int pix, const int co) {
   const bool of32 = a.out_f32 != 0;
@@ -278,6 +291,7 @@ DMC_DEV void conv_store_tile(const ConvK& a, const v4f accv, const int pix, cons
           for (int e = 0; e < 4; ++e) { float sg = sigmoid_f(z[e]); v[e] *= sg * (1.f + z[e] * (1.f - sg)); }
         }
         if (a.resid) { float r[4]; load4<T>(a.resid, (size_t)pix * a.ld_res + co, r, of32); v[0] += r[0]; v[1] += r[1]; v[2] += r[2]; v[3] += r[3]; }
+        if (a.act) apply_act<T>(a, v, pix, co, of32);
         if (co < a.Csplit) store4<T>(a.y1, (size_t)pix * a.ldy1 + co, v, of32);
         else store4<T>(a.y2, (size_t)pix * a.ldy2 + (co - a.Csplit), v, of32);
       } else {
@@ -357,6 +371,13 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] += r[e];
       }
+      if (a.act) {   // GELU of the rounded pre-activation (see apply_act)
+        const v4i pre = Chunk<bf16_t>::pack(f);
+        if (a.ypre) *(v4i*)(a.ypre + ((size_t)pix * a.ldpre + co) * 2) = pre;
+        Chunk<bf16_t>::unpack(pre, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = gelu_f(f[e]);
+      }
       *(v4i*)(y + ((size_t)pix * ldy + cy) * 2) = Chunk<bf16_t>::pack(f);
     }
   }
@@ -402,6 +423,7 @@ DMC_DEV void tile_epilogue(const ConvK& a, const char* lds, int EP, int m0, int 
       load4<T>(a.resid, (size_t)pix * a.ld_res + co, r, of32);
       f[0] += r[0]; f[1] += r[1]; f[2] += r[2]; f[3] += r[3];
     }
+    if (a.act) apply_act<T>(a, f, pix, co, of32);
     store4<T>(y, (size_t)pix * ldy + cy, f, of32);
   }
 }
@@ -1432,7 +1454,7 @@ int halo5_plan(const ConvK& k, int* R, int* nimg) {
 
 // Whether the round-2 halo kernel's register epilogue covers this descriptor's epilogue
 bool halo4_epilogue_ok(const ConvK& k) {
-  return !k.out_f32 && !k.out_nchw && !k.silu_pre && k.Csplit >= k.Cout && (k.Cout & 3) == 0 &&
+  return !k.out_f32 && !k.out_nchw && !k.silu_pre && !k.act && k.Csplit >= k.Cout && (k.Cout & 3) == 0 &&
          (k.ldy1 & 3) == 0 && (!k.resid || (k.ld_res & 3) == 0) && (k.OHW % 32) == 0 &&
          (!k.addvec || (k.ld_add & 3) == 0);
 }
@@ -2266,6 +2288,10 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
   k.bias = d->bias; k.addvec = d->addvec; k.ld_add = d->ld_add; k.resid = (const char*)d->resid; k.ld_res = d->ld_res;
   k.silu_pre = d->silu_pre; k.ld_silu = d->ld_silu;
   k.Csplit = d->Csplit; k.ldy1 = d->ldy1; k.ldy2 = d->ldy2; k.out_f32 = d->out_f32; k.out_nchw = d->out_nchw;
+  DMC_REQUIRE(d->act == DMC_ACT_NONE || (d->act == DMC_ACT_GELU && d->Csplit == d->Cout && !d->out_nchw &&
+                                         !d->silu_pre && d->Cout % 4 == 0 && (!d->y_pre || d->ld_pre % 4 == 0)),
+              "conv: act %d needs a single NHWC output, Cout %% 4 == 0, no silu'", d->act);
+  k.act = d->act; k.ypre = (char*)d->y_pre; k.ldpre = d->ld_pre;
   k.M = d->N * d->OH * d->OW; k.OHW = d->OH * d->OW;
   k.sk = nullptr; k.sk_per = 0;
   {

@@ -260,7 +260,6 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(const float* dy, const vo
     dgate[(size_t)b * ld_mod + c] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
 }
 
-DMC_DEV float gelu_f(float u) { return 0.5f * u * (1.0f + erff(u * 0.70710678118654752f)); }
 DMC_DEV float gelu_grad(float u) {
   return 0.5f * (1.0f + erff(u * 0.70710678118654752f)) + u * 0.39894228040143268f * __expf(-0.5f * u * u);
 }

@@ -73,8 +73,11 @@ def set_prologue(d, kind=L.PRO_NONE, scale=None, shift=None, ld=0, drop=None, dr
 
 
 def set_epilogue(d, bias=None, addvec=None, ld_add=0, resid=None, ld_res=0, silu_pre=None, ld_silu=0,
-                 ldy1=0, ldy2=0, Csplit=None, out_f32=False, out_nchw=False):
-    d._keep_epi = (bias, addvec, resid, silu_pre)   # keep the tensors behind the raw pointers alive
+                 ldy1=0, ldy2=0, Csplit=None, out_f32=False, out_nchw=False, act=L.ACT_NONE, y_pre=None, ld_pre=0):
+    d._keep_epi = (bias, addvec, resid, silu_pre, y_pre)   # keep the tensors behind the raw pointers alive
+    d.act = act
+    d.y_pre = ptr(y_pre)
+    d.ld_pre = ld_pre
     d.bias = ptr(bias)
     d.addvec = ptr(addvec)
     d.ld_add = ld_add

@@ -240,11 +240,16 @@ class DiTExecutor(ExecCore):
             self._conv([o], blk.attn.out_proj, K.TAPS1, ht, wt, H, bias=blk.attn.out_proj.bias, out=ao.t)
             x_mid, h2, mean2, rstd2 = ln(x_in, ao.t, mo_ + 2 * H, mo_ + 3 * H, mo_ + 4 * H, None)
             Hm = blk.mlp[0].out_features
-            u = self._new(B, ht, wt, Hm)
-            self._conv([Act(h2, ht, wt, H)], blk.mlp[0], K.TAPS1, ht, wt, Hm, bias=blk.mlp[0].bias, out=u.t)
-            a = self._new(B, ht, wt, Hm)
             d1 = self._drop(2 * i)
-            K.gelu_fwd(dt, u.t, T, Hm, Hm, a.t, drop=d1)
+            a = self._new(B, ht, wt, Hm)
+            u = self._new(B, ht, wt, Hm) if keep or d1 is not None else None
+            if d1 is None:
+                # GELU in fc1's epilogue; the pre-activation is stored only when the backward needs it
+                self._conv([Act(h2, ht, wt, H)], blk.mlp[0], K.TAPS1, ht, wt, Hm, bias=blk.mlp[0].bias, out=a.t,
+                           act=L.ACT_GELU, y_pre=None if u is None else u.t)
+            else:
+                self._conv([Act(h2, ht, wt, H)], blk.mlp[0], K.TAPS1, ht, wt, Hm, bias=blk.mlp[0].bias, out=u.t)
+                K.gelu_fwd(dt, u.t, T, Hm, Hm, a.t, drop=d1)
             mo = self._new(B, ht, wt, H)
             self._conv([a], blk.mlp[3], K.TAPS1, ht, wt, H, bias=blk.mlp[3].bias, out=mo.t)
             d2 = self._drop(2 * i + 1)

@@ -120,7 +120,8 @@ class ExecCore:
 
     def _conv(self, srcs, conv, taps, OH, OW, Cout, mode=L.MODE_NORMAL, stride=1, pro=None, drop=None,
               bias=None, addvec=None, ld_add=0, resid=None, out=None, out_f32=False, out_nchw=False,
-              dtype=None, packmode=L.PACK_FWD, w=None, Kc=None, silu_pre=None, ld_silu=0, split=None):
+              dtype=None, packmode=L.PACK_FWD, w=None, Kc=None, silu_pre=None, ld_silu=0, split=None,
+              act=L.ACT_NONE, y_pre=None):
         """Generic implicit-GEMM conv over 1-2 NHWC sources. pro = (kind, scale, shift)."""
         dtype = dtype or self.dt
         a = srcs[0]
@@ -148,7 +149,8 @@ class ExecCore:
             csplit = None
         K.set_epilogue(d, bias=bias, addvec=addvec, ld_add=ld_add, resid=resid,
                        ld_res=(0 if resid is None or out_nchw else resid.shape[-1]), silu_pre=silu_pre,
-                       ld_silu=ld_silu, ldy1=ldy1, ldy2=ldy2, Csplit=csplit, out_f32=out_f32, out_nchw=out_nchw)
+                       ld_silu=ld_silu, ldy1=ldy1, ldy2=ldy2, Csplit=csplit, out_f32=out_f32, out_nchw=out_nchw,
+                       act=act, y_pre=y_pre, ld_pre=0 if y_pre is None else y_pre.shape[-1])
         K.conv(d, a.t, srcs[1].t if len(srcs) > 1 else None, w, y1, y2)
         return d
 

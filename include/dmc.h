@@ -75,7 +75,11 @@ typedef struct dmc_conv_desc {
   int ldy1, ldy2;
   int out_f32;               /* output stored fp32 even in bf16 mode */
   int out_nchw;              /* y1 is NCHW fp32 [N][Cout][OH][OW] */
+  int act;                   /* DMC_ACT_*: activation applied last (after bias / addvec / resid) */
+  void* y_pre;               /* with act: the pre-activation value is also stored here ([pix][ld_pre], output dtype) */
+  int ld_pre;
 } dmc_conv_desc;
+enum { DMC_ACT_NONE = 0, DMC_ACT_GELU = 1 };   /* GELU (exact): the DiT MLP (dit.py:98-99) */
 
 /* y = conv(x) with fused prologue/epilogue. w = packed [Cout][ntaps][Kc] (dtype).
  * workspace (dmc_conv2d_workspace() bytes, may be 0) enables split-K for small-M shapes; with a NULL
