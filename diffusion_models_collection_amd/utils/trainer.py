@@ -56,12 +56,20 @@ class GradSync:
         self.world = dist.get_world_size(process_group)
         executor.grad_hook = self.hook
 
+    TAIL = 256 * 1024      # elements: once at most this much is unfinished, flush what is finished
+
+    def cut(self, hi, done, total, final):
+        """Whether the finished prefix [done, hi) is issued now: a full bucket, the end of the backward, or all but
+        a small tail finished (so the bucket left for after the backward is only that tail -- the UNet's input
+        conv, whose gradient comes last)."""
+        return hi > done and (hi - done >= self.bucket or final or total - hi <= self.TAIL)
+
     def wants(self, hi, final):
         """Whether hook(flat, hi, final) will issue an all-reduce (the executor then joins its side stream)."""
-        return hi - self.done >= self.bucket or (final and hi > self.done) or final
+        return final or self.cut(hi, self.done, self.ex.gtotal, final)
 
     def hook(self, flat, hi, final):
-        if hi - self.done >= self.bucket or (final and hi > self.done):
+        if self.cut(hi, self.done, flat.numel(), final):
             seg = flat[self.done:hi]
             op = dist.ReduceOp.AVG if self.native_avg else dist.ReduceOp.SUM
             self.works.append((seg, dist.all_reduce(seg, op=op, group=self.pg, async_op=True)))
@@ -324,7 +332,7 @@ class GraphedTrainStep:
             segs.append((state["g"], bucket))
 
         def hook(flat, hi, final):
-            if hi - state["done"] >= gs.bucket or (final and hi > state["done"]):
+            if gs.cut(hi, state["done"], flat.numel(), final):
                 end((state["done"], hi))
                 state["done"] = hi
                 begin()

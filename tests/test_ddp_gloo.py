@@ -13,6 +13,7 @@ import torch.multiprocessing as mp
 
 class FakeExecutor:
     grad_hook = None
+    gtotal = 10007
 
 
 def _free_port():
@@ -30,6 +31,7 @@ def _worker(rank, world, port, q):
     from diffusion_models_collection_amd.utils.trainer import GradSync
     ex = FakeExecutor()
     gs = GradSync(ex, bucket_bytes=4 * 1000)
+    gs.TAIL = 0          # bucket boundaries only (the tail rule has its own test)
     n = 10007
     g = torch.Generator().manual_seed(100 + rank)
     results = []
@@ -60,3 +62,20 @@ def test_gradsync_two_rank_gloo():
         p.join(timeout=60)
     assert all(ok for _, ok, _ in out), out
     assert all(pending == 0 for _, _, pending in out)
+
+
+def test_gradsync_cut_rule():
+    """A bucket is issued when >= bucket elements are finished, at the end of the backward, or as soon as all but
+    a small tail is finished (so only that tail is left for after the backward)."""
+    from diffusion_models_collection_amd.utils.trainer import GradSync
+
+    class S:
+        bucket, TAIL = 1000, 100
+
+    cut = GradSync.cut
+    assert not cut(S, 500, 0, 10000, False)
+    assert cut(S, 1000, 0, 10000, False)
+    assert cut(S, 9950, 9000, 10000, False)       # 50 elements unfinished <= TAIL: flush the 950 now
+    assert not cut(S, 9000, 9000, 10000, False)   # nothing new
+    assert cut(S, 10000, 9950, 10000, True)
+    assert not cut(S, 10000, 10000, 10000, True)
