@@ -38,6 +38,7 @@ class ConvDesc(ctypes.Structure):
         ("bias", _c_p), ("addvec", _c_p), ("ld_add", _c_int), ("resid", _c_p), ("ld_res", _c_int),
         ("silu_pre", _c_p), ("ld_silu", _c_int), ("Csplit", _c_int), ("ldy1", _c_int), ("ldy2", _c_int),
         ("out_f32", _c_int), ("out_nchw", _c_int), ("act", _c_int), ("y_pre", _c_p), ("ld_pre", _c_int),
+        ("gn_part", _c_p),
     ]
 
 
@@ -73,6 +74,8 @@ def _load():
         "dmc_gn_workspace": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
         "dmc_gn_stats": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_f,
                                   _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+        "dmc_gn_finalize": (_c_int, [_c_p, _c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_f, _c_p, _c_p, _c_p, _c_p,
+                                     _c_p, _c_p]),
         "dmc_gn_apply": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p,
                                   _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_int, _c_p]),
         "dmc_gn_silu_bwd": (_c_int, [_c_int, _c_p, _c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int,

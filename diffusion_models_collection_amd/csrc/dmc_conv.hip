@@ -25,6 +25,7 @@ struct ConvK {
   const char* resid; int ld_res; const float* silu_pre; int ld_silu;
   int Csplit, ldy1, ldy2, out_f32, out_nchw;
   int act; char* ypre; int ldpre;   // DMC_ACT_GELU epilogue (+ optional pre-activation copy)
+  float* gst;  // GroupNorm partials from the epilogue: [M/64][Cout/8] x (mean, M2) (nullptr: off)
   int M;      // N*OH*OW output pixels
   int OHW;    // OH*OW
   float* sk;  // split-K partial slab (nullptr: no split)
@@ -326,12 +327,27 @@ DMC_DEV void conv_store_tile(const ConvK& a, const v4f accv, const int pix, cons
 // every residual load issued up front, and the embedding row is reloaded only when the image changes, so the
 // store phase pays one global round trip instead of one per row (it runs with no other block on the CU to
 // hide it).
+// Chan's combination of two (mean, M2) partials of equal count n: the count doubles.
+DMC_DEV void chan_eq(float& m, float& q, float mb, float qb, float n) {
+  const float d = mb - m;
+  q = q + qb + d * d * (0.5f * n);
+  m = 0.5f * (m + mb);
+}
+
 template <int BM, int BN, int NT>
 DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int n0) {
   constexpr int CG = BN / 8, RS = NT / CG, IT = BM / RS;
+  constexpr int SEG = 64, NSEG = BM / SEG, KPS = SEG / RS;   // GroupNorm partial segments of 64 pixels
+  static_assert(CG == 16 && SEG % RS == 0 && BM % SEG == 0, "GroupNorm partial geometry");
   const int cg = threadIdx.x % CG, r0 = threadIdx.x / CG;
   const int co = n0 + cg * 8;
   if (co >= a.Cout) return;
+  // GroupNorm statistics of the stored tile (a.gst): per (64-pixel segment, 8-channel chunk) the mean and M2 of
+  // the bf16 values as stored. Row k of this thread lies in segment k / KPS for every thread (r0 < RS), so the
+  // partials combine in a fixed order: rows within a thread, then lanes (xor 16, 32), then waves through LDS.
+  float gm[NSEG], gq[NSEG];
+#pragma unroll
+  for (int j = 0; j < NSEG; ++j) { gm[j] = 0.f; gq[j] = 0.f; }
   v4f b0 = {0.f, 0.f, 0.f, 0.f}, b1 = {0.f, 0.f, 0.f, 0.f};
   if (a.bias) { b0 = *(const v4f*)(a.bias + co); b1 = *(const v4f*)(a.bias + co + 4); }
   const bool first = co < a.Csplit;
@@ -378,7 +394,67 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] = gelu_f(f[e]);
       }
-      *(v4i*)(y + ((size_t)pix * ldy + cy) * 2) = Chunk<bf16_t>::pack(f);
+      const v4i out = Chunk<bf16_t>::pack(f);
+      *(v4i*)(y + ((size_t)pix * ldy + cy) * 2) = out;
+      if (a.gst) {
+        float g[8];
+        Chunk<bf16_t>::unpack(out, g);
+        float mb = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) mb += g[e];
+        mb *= 0.125f;
+        float qb = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qb = fmaf(g[e] - mb, g[e] - mb, qb);
+        const int kk = k % KPS;                       // row k's index within its segment k / KPS
+#pragma unroll
+        for (int j = 0; j < NSEG; ++j) {
+          if (j != k / KPS) continue;                 // resolved at compile time (k, j unrolled)
+          if (kk == 0) { gm[j] = mb; gq[j] = qb; }
+          else {                                      // fold one row (8 values) into kk rows (8 kk values)
+            const float d = mb - gm[j], nn = 8.f * kk;
+            gm[j] += d * (8.f / (nn + 8.f));
+            gq[j] += qb + d * d * (nn * 8.f / (nn + 8.f));
+          }
+        }
+      }
+    }
+  }
+  if (a.gst) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int NW = NT / 64;
+    float cnt = 8.f * KPS;
+#pragma unroll
+    for (int sh = 16; sh < 64; sh <<= 1) {          // the lanes of this wave with the same chunk
+#pragma unroll
+      for (int j = 0; j < NSEG; ++j) {
+        const float mb = __shfl_xor(gm[j], sh), qb = __shfl_xor(gq[j], sh);
+        chan_eq(gm[j], gq[j], mb, qb, cnt);
+      }
+      cnt *= 2.f;
+    }
+    float* red = (float*)(lds + BM * EP);            // [NW][NSEG][CG][2], past the epilogue tile
+    if (lane < CG) {
+#pragma unroll
+      for (int j = 0; j < NSEG; ++j) {
+        red[((wave * NSEG + j) * CG + lane) * 2] = gm[j];
+        red[((wave * NSEG + j) * CG + lane) * 2 + 1] = gq[j];
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < NSEG * CG) {
+      const int j = threadIdx.x / CG, c = threadIdx.x % CG;
+      float m = red[(j * CG + c) * 2], q = red[(j * CG + c) * 2 + 1];
+      for (int w = 1; w < NW; ++w) {                 // equal counts: fold wave w into waves [0, w)
+        const float mb = red[((w * NSEG + j) * CG + c) * 2], qb = red[((w * NSEG + j) * CG + c) * 2 + 1];
+        const float na = cnt * w, nb = cnt;
+        const float d = mb - m;
+        m += d * (nb / (na + nb));
+        q += qb + d * d * (na * nb / (na + nb));
+      }
+      const size_t o = ((size_t)(m0 / SEG + j) * (a.Cout / 8) + (n0 / 8 + c)) * 2;
+      a.gst[o] = m;
+      a.gst[o + 1] = q;
     }
   }
 }
@@ -525,7 +601,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave % WM, wn = wave / WM;
   int mb = blockIdx.x, nb = blockIdx.y;
-  if (!a.sk) xcd_tile((a.Cout + BN - 1) / BN, mb, nb);   // 1-D grid (split-K launches keep the 3-D grid)
+  if (!a.sk && gridDim.y == 1) xcd_tile((a.Cout + BN - 1) / BN, mb, nb);   // 1-D grid: XCD-aware tile order
   const int m0 = mb * BM;
   const int n0 = nb * BN;
   const int lrow = lane >> 3;
@@ -2292,6 +2368,7 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
                                          !d->silu_pre && d->Cout % 4 == 0 && (!d->y_pre || d->ld_pre % 4 == 0)),
               "conv: act %d needs a single NHWC output, Cout %% 4 == 0, no silu'", d->act);
   k.act = d->act; k.ypre = (char*)d->y_pre; k.ldpre = d->ld_pre;
+  k.gst = nullptr;   // set by dmc_conv2d when the chosen kernel emits the GroupNorm partials
   k.M = d->N * d->OH * d->OW; k.OHW = d->OH * d->OW;
   k.sk = nullptr; k.sk_per = 0;
   {
@@ -2389,13 +2466,57 @@ void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
     const long total = (long)k.M * Cpad / 4;
     const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
     conv_splitk_epilogue_kernel<bf16_t><<<blocks, 256, 0, s>>>(k, p.splits, Cpad);
-  } else if (p.cfg == 0) {
-    conv_fwd_glds_kernel<4, 2, BUF><<<dmc::cdiv(k.M, 256) * dmc::cdiv(k.Cout, 128), 512, 0, s>>>(k);
-  } else if (p.cfg == 1) {
-    conv_fwd_glds_kernel<2, 2, BUF><<<dmc::cdiv(k.M, 128) * dmc::cdiv(k.Cout, 128), 256, 0, s>>>(k);
   } else {
-    conv_fwd_glds_kernel<1, 2, BUF><<<dmc::cdiv(k.M, 64) * dmc::cdiv(k.Cout, 128), 128, 0, s>>>(k);
+    // 1-D grid: the kernel orders its tiles XCD-aware (xcd_tile); DMC_NO_XCD=1 keeps the 2-D grid (A/B)
+    const int bm = p.cfg == 0 ? 256 : p.cfg == 1 ? 128 : 64;
+    const int nb = dmc::cdiv(k.Cout, 128);
+    const dim3 g = dmc::opt(dmc::OPT_NO_XCD) ? dim3(dmc::cdiv(k.M, bm), nb) : dim3(dmc::cdiv(k.M, bm) * nb);
+    if (p.cfg == 0) conv_fwd_glds_kernel<4, 2, BUF><<<g, 512, 0, s>>>(k);
+    else if (p.cfg == 1) conv_fwd_glds_kernel<2, 2, BUF><<<g, 256, 0, s>>>(k);
+    else conv_fwd_glds_kernel<1, 2, BUF><<<g, 128, 0, s>>>(k);
   }
+}
+
+// GroupNorm partials of a stored NHWC output, for the conv paths whose epilogue does not emit them (fp32, split-K,
+// narrow, register-staged): one wave per (64-pixel segment, 8-channel chunk), (mean, M2) by an exact two-pass.
+template <typename T>
+__global__ __launch_bounds__(256) void gn_part_kernel(const char* y, int ldy, int nseg, int nch, float* out) {
+  const int lane = threadIdx.x & 63;
+  const long w = blockIdx.x * 4L + (threadIdx.x >> 6);
+  if (w >= (long)nseg * nch) return;
+  const int seg = (int)(w / nch), ch = (int)(w - (long)seg * nch);
+  const size_t row = ((size_t)seg * 64 + lane) * ldy + ch * 8;
+  float f[8];
+  load4<T>(y, row, f, false);
+  load4<T>(y, row + 4, f + 4, false);
+  float t = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t += f[e];
+  const float m = wave_sum(t) * (1.0f / 512.0f);
+  float q = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) q = fmaf(f[e] - m, f[e] - m, q);
+  q = wave_sum(q);
+  if (lane == 0) { out[w * 2] = m; out[w * 2 + 1] = q; }
+}
+
+// Whether dmc_conv2d's chosen kernel emits the GroupNorm partials in its epilogue (tile_epilogue8: the round-1
+// halo kernel and the non-split LDS-DMA kernel, bf16, one NHWC output, whole 256-pixel tiles, 128-channel tiles).
+bool epi_stats_ok(const ConvK& k, const void* ws, size_t ws_bytes) {
+  if (k.dtype_bytes != 2 || k.out_f32 || k.out_nchw || k.silu_pre || k.Csplit != k.Cout || k.Cout % 128 ||
+      k.M % 256 || k.OHW % 64 || ((k.Cout | k.ldy1 | k.ld_res) & 7))
+    return false;
+  if (!dmc::opt(dmc::OPT_NO_NARROW) && ((k.C2 == 0 && k.C1 <= 8 && k.Cout >= 16) || k.Cout <= 8)) return false;
+  if (dmc::opt(dmc::OPT_NO_GLDS) || dmc::opt(dmc::OPT_HALO_VER) != 1 || dmc::opt(dmc::OPT_HALO_RW) ||
+      dmc::opt(dmc::OPT_NO_EPI_STATS))
+    return false;
+  if (k.prologue == DMC_PRO_AFFINE_SILU) {
+    int R, nimg;
+    return halo_pro_plan(k, &R, &nimg) != 0;
+  }
+  if (k.prologue != DMC_PRO_NONE) return false;
+  const FwdPlan p = plan_glds(k);
+  return p.splits == 1 || ws == nullptr || ws_bytes < p.ws || dmc::opt(dmc::OPT_NO_SPLITK);
 }
 
 template <typename T>
@@ -2414,7 +2535,8 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
   if (sizeof(T) == 2 && k.prologue == DMC_PRO_AFFINE_SILU) {
     int R, nimg;
     const int hp = halo_pro_plan(k, &R, &nimg);
-    const int hg1 = k.M / 256 * dmc::cdiv(k.Cout, 128);   // 1-D: the kernel maps it XCD-aware
+    const dim3 hg1 = dmc::opt(dmc::OPT_NO_XCD) ? dim3(k.M / 256, dmc::cdiv(k.Cout, 128))
+                                               : dim3(k.M / 256 * dmc::cdiv(k.Cout, 128));   // 1-D: XCD-aware
     if (hp == 6) { conv3x3_halo_kernel<6, 3, true><<<hg1, 512, 0, s>>>(k, R, nimg); return dmc::check_launch("dmc_conv2d"); }
     if (hp == 7) { conv3x3_halo_kernel<7, 3, true><<<hg1, 512, 0, s>>>(k, R, nimg); return dmc::check_launch("dmc_conv2d"); }
   }
@@ -2428,6 +2550,7 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     int R, nimg;
     const int hp = (buf && p.splits == 1 && !dmc::opt(dmc::OPT_NO_HALO)) ? halo_plan(k, &R, &nimg) : 0;
     const dim3 hg(k.M / 256, dmc::cdiv(k.Cout, 128));
+    const dim3 hgx = dmc::opt(dmc::OPT_NO_XCD) ? hg : dim3(hg.x * hg.y);   // 1-D: XCD-aware tile order
     int R5, nimg5;
     const long hver = dmc::opt(dmc::OPT_HALO_VER);   // 1: round-1 8-wave kernel (default), 4 / 5: round-2 variants
     const int hp5 = (buf && p.splits == 1 && !dmc::opt(dmc::OPT_NO_HALO) && !dmc::opt(dmc::OPT_HALO_V1) &&
@@ -2472,11 +2595,11 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
       if (hp == 6) conv3x3_halo_rw_kernel<6><<<hg, 512, 0, s>>>(k, R, nimg);
       else conv3x3_halo_rw_kernel<7><<<hg, 512, 0, s>>>(k, R, nimg);
     } else if (hp == 6 && dmc::opt(dmc::OPT_HALO_WS4))
-      conv3x3_halo_kernel<6, 4><<<hg.x * hg.y, 512, 0, s>>>(k, R, nimg);
+      conv3x3_halo_kernel<6, 4><<<hgx, 512, 0, s>>>(k, R, nimg);
     else if (hp == 6)
-      conv3x3_halo_kernel<6, 3><<<hg.x * hg.y, 512, 0, s>>>(k, R, nimg);
+      conv3x3_halo_kernel<6, 3><<<hgx, 512, 0, s>>>(k, R, nimg);
     else if (hp == 7)
-      conv3x3_halo_kernel<7, 3><<<hg.x * hg.y, 512, 0, s>>>(k, R, nimg);
+      conv3x3_halo_kernel<7, 3><<<hgx, 512, 0, s>>>(k, R, nimg);
     else if (buf) launch_glds<true>(k, p, s);
     else launch_glds<false>(k, p, s);
     return dmc::check_launch("dmc_conv2d");
@@ -2536,8 +2659,23 @@ extern "C" int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2
   if (fill_convk(d, x1, x2, w, y1, y2, k)) return 1;
   hipStream_t s = dmc::as_stream(stream);
   if (k.M == 0 || k.Cout == 0) return 0;
-  return d->dtype == DMC_F32 ? launch_fwd<float>(k, workspace, ws_bytes, s)
-                             : launch_fwd<bf16_t>(k, workspace, ws_bytes, s);
+  float* const part = d->gn_part;
+  if (part) {
+    DMC_REQUIRE(k.OHW % 64 == 0 && k.Cout % 8 == 0 && k.Csplit == k.Cout && !k.out_nchw && k.ldy1 % 4 == 0,
+                "conv: GroupNorm partials need OH*OW %% 64 == 0, Cout %% 8 == 0 and one NHWC output");
+    k.gst = epi_stats_ok(k, workspace, ws_bytes) ? part : nullptr;
+  }
+  const int rc = d->dtype == DMC_F32 ? launch_fwd<float>(k, workspace, ws_bytes, s)
+                                     : launch_fwd<bf16_t>(k, workspace, ws_bytes, s);
+  if (rc || !part || k.gst) return rc;
+  // the chosen kernel's epilogue does not emit them: one pass over the stored output
+  const int nseg = k.M / 64, nch = k.Cout / 8;
+  const int blocks = (int)(((long)nseg * nch + 3) / 4);
+  if (k.out_f32 || d->dtype == DMC_F32)
+    gn_part_kernel<float><<<blocks, 256, 0, s>>>(k.y1, k.ldy1, nseg, nch, part);
+  else
+    gn_part_kernel<bf16_t><<<blocks, 256, 0, s>>>(k.y1, k.ldy1, nseg, nch, part);
+  return dmc::check_launch("dmc_conv2d (GroupNorm partials)");
 }
 
 // Halo weight-gradient plan: applies to bf16 3x3 stride-1 convs the halo forward kernel handles, with

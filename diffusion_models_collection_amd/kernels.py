@@ -73,8 +73,10 @@ def set_prologue(d, kind=L.PRO_NONE, scale=None, shift=None, ld=0, drop=None, dr
 
 
 def set_epilogue(d, bias=None, addvec=None, ld_add=0, resid=None, ld_res=0, silu_pre=None, ld_silu=0,
-                 ldy1=0, ldy2=0, Csplit=None, out_f32=False, out_nchw=False, act=L.ACT_NONE, y_pre=None, ld_pre=0):
-    d._keep_epi = (bias, addvec, resid, silu_pre, y_pre)   # keep the tensors behind the raw pointers alive
+                 ldy1=0, ldy2=0, Csplit=None, out_f32=False, out_nchw=False, act=L.ACT_NONE, y_pre=None, ld_pre=0,
+                 gn_part=None):
+    d._keep_epi = (bias, addvec, resid, silu_pre, y_pre, gn_part)   # keep the tensors behind the raw pointers alive
+    d.gn_part = ptr(gn_part)
     d.act = act
     d.y_pre = ptr(y_pre)
     d.ld_pre = ld_pre
@@ -219,6 +221,18 @@ def gn_stats(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, G, eps, gamma, beta):
     ws = SCRATCH.get(LIB.dmc_gn_workspace(N, C, G, HW), dev)
     check(LIB.dmc_gn_stats(L.dtype_code(dtype), ptr(x1), ptr(x2), N, HW, C1, C2, ld1, ld2, G, eps, ptr(gamma),
                            ptr(beta), ptr(ws), ptr(mr), ptr(sc), ptr(sh), L.stream()), "dmc_gn_stats")
+    return sc, sh, mr
+
+
+def gn_finalize(p1, C1, p2, C2, N, HW, G, eps, gamma, beta):
+    """GroupNorm (scale, shift, mean_rstd) from the producing convs' partials (dmc_conv_desc.gn_part)."""
+    dev = p1.device
+    C = C1 + C2
+    mr = torch.empty(N * G * 2, dtype=torch.float32, device=dev)
+    sc = torch.empty(N * C, dtype=torch.float32, device=dev)
+    sh = torch.empty(N * C, dtype=torch.float32, device=dev)
+    check(LIB.dmc_gn_finalize(ptr(p1), C1, ptr(p2), C2, N, HW, G, eps, ptr(gamma), ptr(beta), ptr(mr), ptr(sc),
+                              ptr(sh), L.stream()), "dmc_gn_finalize")
     return sc, sh, mr
 
 

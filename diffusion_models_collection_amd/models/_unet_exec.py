@@ -31,11 +31,16 @@ from .. import kernels as K
 class Act:
     """An NHWC activation [N, H, W, C] (contiguous, pitch C) plus its gradient buffer."""
 
-    __slots__ = ("t", "H", "W", "C", "grad")
+    __slots__ = ("t", "H", "W", "C", "grad", "part")
 
     def __init__(self, t, H, W, C):
         self.t, self.H, self.W, self.C = t, H, W, C
         self.grad = None
+        self.part = None    # GroupNorm partials written by the conv that produced t (dmc_conv_desc.gn_part)
+
+
+# GroupNorm statistics from the conv epilogues (A/B: DMC_GN_PARTIALS=0 computes them with dmc_gn_stats passes)
+_GN_PARTIALS = os.environ.get("DMC_GN_PARTIALS", "1") not in ("", "0")
 
 
 def _seed_from_torch():
@@ -121,9 +126,17 @@ class ExecCore:
     def _conv(self, srcs, conv, taps, OH, OW, Cout, mode=L.MODE_NORMAL, stride=1, pro=None, drop=None,
               bias=None, addvec=None, ld_add=0, resid=None, out=None, out_f32=False, out_nchw=False,
               dtype=None, packmode=L.PACK_FWD, w=None, Kc=None, silu_pre=None, ld_silu=0, split=None,
-              act=L.ACT_NONE, y_pre=None):
-        """Generic implicit-GEMM conv over 1-2 NHWC sources. pro = (kind, scale, shift)."""
+              act=L.ACT_NONE, y_pre=None, stats=None):
+        """Generic implicit-GEMM conv over 1-2 NHWC sources. pro = (kind, scale, shift). stats = the output Act:
+        in bf16 mode it gets the GroupNorm partials of the stored output (the next GroupNorm then needs no
+        statistics pass over it, see _gn)."""
         dtype = dtype or self.dt
+        gn_part = None
+        if (stats is not None and _GN_PARTIALS and dtype == torch.bfloat16 and (OH * OW) % 64 == 0 and Cout % 8 == 0
+                and split is None and not out_nchw and not out_f32):
+            gn_part = torch.empty(srcs[0].t.shape[0] * OH * OW // 64 * (Cout // 8) * 2, dtype=torch.float32,
+                                  device=srcs[0].t.device)
+            stats.part = gn_part
         a = srcs[0]
         C1 = a.C
         C2 = srcs[1].C if len(srcs) > 1 else 0
@@ -150,7 +163,7 @@ class ExecCore:
         K.set_epilogue(d, bias=bias, addvec=addvec, ld_add=ld_add, resid=resid,
                        ld_res=(0 if resid is None or out_nchw else resid.shape[-1]), silu_pre=silu_pre,
                        ld_silu=ld_silu, ldy1=ldy1, ldy2=ldy2, Csplit=csplit, out_f32=out_f32, out_nchw=out_nchw,
-                       act=act, y_pre=y_pre, ld_pre=0 if y_pre is None else y_pre.shape[-1])
+                       act=act, y_pre=y_pre, ld_pre=0 if y_pre is None else y_pre.shape[-1], gn_part=gn_part)
         K.conv(d, a.t, srcs[1].t if len(srcs) > 1 else None, w, y1, y2)
         return d
 
@@ -294,6 +307,12 @@ class UNetExecutor(ExecCore):
         a = srcs[0]
         b = srcs[1] if len(srcs) > 1 else None
         N = a.t.shape[0]
+        C = a.C + (b.C if b else 0)
+        if (all(s.part is not None for s in srcs) and (a.H * a.W) % 64 == 0 and C % gn.num_groups == 0
+                and (C // gn.num_groups) % 8 == 0):
+            # statistics from the producing convs' epilogue partials: no pass over the activation
+            return K.gn_finalize(a.part, a.C, b.part if b else None, b.C if b else 0, N, a.H * a.W, gn.num_groups,
+                                 gn.eps, gn.weight, gn.bias)
         return K.gn_stats(dtype, a.t, b.t if b else None, N, a.H * a.W, a.C, b.C if b else 0, a.t.shape[-1],
                           b.t.shape[-1] if b else 0, gn.num_groups, gn.eps, gn.weight, gn.bias)
 
@@ -435,7 +454,7 @@ class UNetExecutor(ExecCore):
         ldx = (Cin + self.chunk - 1) // self.chunk * self.chunk
         xin = Act(K.pack_input(dt, x, ldx), H, W, Cin)
         h = self._new(N, H, W, m.model_channels)
-        self._conv([xin], m.input_conv, K.TAPS3, H, W, m.model_channels, bias=m.input_conv.bias, out=h.t)
+        self._conv([xin], m.input_conv, K.TAPS3, H, W, m.model_channels, bias=m.input_conv.bias, out=h.t, stats=h)
         if keep:
             tape.append(("conv_in", xin, h, x.requires_grad))
         hs = [h]
@@ -472,7 +491,7 @@ class UNetExecutor(ExecCore):
             a = srcs[0]
             OH, OW = (a.H + 2 - 3) // 2 + 1, (a.W + 2 - 3) // 2 + 1
             out = self._new(a.t.shape[0], OH, OW, a.C)
-            self._conv([a], layer.conv, K.TAPS3, OH, OW, a.C, stride=2, bias=layer.conv.bias, out=out.t)
+            self._conv([a], layer.conv, K.TAPS3, OH, OW, a.C, stride=2, bias=layer.conv.bias, out=out.t, stats=out)
             if tape is not None:
                 tape.append(("down", layer, a, out))
             return out
@@ -480,7 +499,7 @@ class UNetExecutor(ExecCore):
             a = srcs[0]
             out = self._new(a.t.shape[0], 2 * a.H, 2 * a.W, a.C)
             self._conv([a], layer.conv, K.TAPS3, 2 * a.H, 2 * a.W, a.C, mode=L.MODE_UPSAMPLE, bias=layer.conv.bias,
-                       out=out.t)
+                       out=out.t, stats=out)
             if tape is not None:
                 tape.append(("up", layer, a, out))
             return out
@@ -500,11 +519,11 @@ class UNetExecutor(ExecCore):
         if tape is None and self._halo_pro_ok(srcs, Cout, st1):
             a1 = None
             self._conv(srcs, conv1, K.TAPS3, H, W, Cout, pro=(L.PRO_AFFINE_SILU, st1[0], st1[1]), bias=conv1.bias,
-                       addvec=self.addvec.view(N, -1)[:, off:], ld_add=self.temb_total, out=h1.t)
+                       addvec=self.addvec.view(N, -1)[:, off:], ld_add=self.temb_total, out=h1.t, stats=h1)
         else:
             a1 = self._apply(srcs, st1, silu=True)
             self._conv([a1], conv1, K.TAPS3, H, W, Cout, bias=conv1.bias,
-                       addvec=self.addvec.view(N, -1)[:, off:], ld_add=self.temb_total, out=h1.t)
+                       addvec=self.addvec.view(N, -1)[:, off:], ld_add=self.temb_total, out=h1.t, stats=h1)
         st2 = self._gn([h1], gn2)
         if isinstance(rb.shortcut, torch.nn.Conv2d):
             s = torch.empty(N, H, W, Cout, dtype=self.dt, device=self.device)
@@ -522,10 +541,10 @@ class UNetExecutor(ExecCore):
         if tape is None and drop is None and self._halo_pro_ok([h1], Cout, st2):
             a2 = None
             self._conv([h1], conv2, K.TAPS3, H, W, Cout, pro=(L.PRO_AFFINE_SILU, st2[0], st2[1]), bias=conv2.bias,
-                       resid=resid, out=out.t)
+                       resid=resid, out=out.t, stats=out)
         else:
             a2 = self._apply([h1], st2, silu=True, drop=drop)
-            self._conv([a2], conv2, K.TAPS3, H, W, Cout, bias=conv2.bias, resid=resid, out=out.t)
+            self._conv([a2], conv2, K.TAPS3, H, W, Cout, bias=conv2.bias, resid=resid, out=out.t, stats=out)
         st1 = (st1, a1)
         st2 = (st2, a2)
         if tape is not None:
@@ -546,7 +565,7 @@ class UNetExecutor(ExecCore):
         lse = torch.empty(N * heads * Lq, dtype=torch.float32, device=self.device)
         K.attn_fwd(self.dt, qkv.t, 3 * C, N, Lq, heads, hd, o.t, C, lse)
         out = self._new(N, H, W, C)
-        self._conv([o], ab.proj, K.TAPS1, H, W, C, bias=ab.proj.bias, resid=a.t, out=out.t)
+        self._conv([o], ab.proj, K.TAPS1, H, W, C, bias=ab.proj.bias, resid=a.t, out=out.t, stats=out)
         if tape is not None:
             tape.append(("attn", ab, a, st, qkv, o, lse, out))
         return out

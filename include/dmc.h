@@ -78,6 +78,10 @@ typedef struct dmc_conv_desc {
   int act;                   /* DMC_ACT_*: activation applied last (after bias / addvec / resid) */
   void* y_pre;               /* with act: the pre-activation value is also stored here ([pix][ld_pre], output dtype) */
   int ld_pre;
+  float* gn_part;            /* if set: GroupNorm partial statistics of the stored output y1 (the input of the next
+                              * GroupNorm, models/unet.py:34/:84), [M/64][Cout/8][2] = (mean, M2) over 64 pixels x 8
+                              * channels, from the kernel's epilogue where it can, else one pass over y1. Needs
+                              * OH*OW % 64 == 0, Cout % 8 == 0, one NHWC output. Finalised by dmc_gn_finalize. */
 } dmc_conv_desc;
 enum { DMC_ACT_NONE = 0, DMC_ACT_GELU = 1 };   /* GELU (exact): the DiT MLP (dit.py:98-99) */
 
@@ -127,6 +131,13 @@ size_t dmc_gn_workspace(int N, int C, int G, int HW);
 int dmc_gn_stats(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1,
                  int ld2, int G, float eps, const float* gamma, const float* beta, void* workspace,
                  float* mean_rstd, float* scale, float* shift, void* stream);
+
+/* The same statistics from the GroupNorm partials of the convs that produced x1 / x2 (dmc_conv_desc.gn_part,
+ * [N*HW/64][C/8][2]): one tiny launch instead of a pass over the activation. Needs HW % 64 == 0 and groups made of
+ * whole 8-channel chunks; the partials are folded in a fixed order (deterministic). */
+int dmc_gn_finalize(const float* part1, int C1, const float* part2, int C2, int N, int HW, int G, float eps,
+                    const float* gamma, const float* beta, float* mean_rstd, float* scale, float* shift,
+                    void* stream);
 
 /* a = dropout(SiLU(x*scale[n,c] + shift[n,c])) (silu=1) or the affine alone (silu=0), materialised once
  * (dtype, [pix][ld_out]); dropout keeps element (pix, c) iff hash(seed, pix*C + c) >= drop_thresh. */

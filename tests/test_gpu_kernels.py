@@ -608,3 +608,44 @@ def test_conv_fp32_gemm_splitk_silu_pre(Cin, Cout):
     K.conv(d, xd, None, wp, y)
     torch.cuda.synchronize()
     assert rel_err(y.view(N, Cout).cpu(), ref) < 1e-5
+
+
+@pytest.mark.parametrize("case", ["halo3x3", "glds1x1", "splitk_small", "fp32_reg", "concat_two"])
+def test_conv_epilogue_groupnorm_partials(case):
+    """dmc_conv_desc.gn_part + dmc_gn_finalize (the conv epilogue's GroupNorm partials: in-kernel on the halo and
+    LDS-DMA paths, one pass over the output elsewhere) give the statistics dmc_gn_stats computes over the stored
+    output: mean / rstd and the folded scale / shift within 2e-5 (fp32 summation order)."""
+    from diffusion_models_collection_amd import _lib as L, kernels as K
+    gen = torch.Generator().manual_seed(11)
+    dt = torch.float32 if case == "fp32_reg" else torch.bfloat16
+    N, H, W, Cin, Cout, taps = {"halo3x3": (4, 32, 32, 128, 128, K.TAPS3), "glds1x1": (8, 16, 16, 256, 256, K.TAPS1),
+                                "splitk_small": (2, 8, 8, 256, 256, K.TAPS3), "fp32_reg": (2, 16, 16, 64, 128, K.TAPS3),
+                                "concat_two": (4, 16, 16, 128, 128, K.TAPS3)}[case]
+    G = 8
+
+    def conv_with_part(cout, seed):
+        g = torch.Generator().manual_seed(seed)
+        x = (torch.randn(N, H, W, Cin, generator=g) + 0.5).to(DEV).to(dt)
+        w = (torch.randn(cout, Cin, int(len(taps) ** 0.5), int(len(taps) ** 0.5), generator=g) * 0.05).to(DEV)
+        b = (torch.randn(cout, generator=g) + 2.0).to(DEV)        # a large mean: tests the M2 form
+        Kc = L.kc_for(Cin, dt)
+        wp = K.pack_weight(L.PACK_FWD, dt, w, Kc)
+        y = torch.empty(N, H, W, cout, dtype=dt, device=DEV)
+        part = torch.empty(N * H * W // 64 * (cout // 8) * 2, device=DEV)
+        d = K.make_desc(dt, N, H, W, Cin, 0, Cin, 0, Kc, H, W, cout, taps)
+        K.set_epilogue(d, bias=b, ldy1=cout, gn_part=part)
+        K.conv(d, x, None, wp, y)
+        return y, part
+
+    y1, p1 = conv_with_part(Cout, 1)
+    y2, p2, C2 = (None, None, 0)
+    if case == "concat_two":
+        y2, p2 = conv_with_part(256, 2)
+        C2 = 256
+    gamma = torch.randn(Cout + C2, generator=gen).to(DEV)
+    beta = torch.randn(Cout + C2, generator=gen).to(DEV)
+    sc, sh, mr = K.gn_finalize(p1, Cout, p2, C2, N, H * W, G, 1e-5, gamma, beta)
+    rsc, rsh, rmr = K.gn_stats(dt, y1, y2, N, H * W, Cout, C2, Cout, C2, G, 1e-5, gamma, beta)
+    torch.cuda.synchronize()
+    for got, ref in ((mr, rmr), (sc, rsc), (sh, rsh)):
+        assert rel_err(got, ref) < 2e-5, (case, rel_err(got, ref))
