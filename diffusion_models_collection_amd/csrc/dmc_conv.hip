@@ -2446,8 +2446,9 @@ RegPlan plan_reg(const ConvK& k) {
 // normalised activation is not needed for a weight gradient). Returns the DMA pieces (6/7) or 0.
 int halo_pro_plan(const ConvK& k, int* R, int* nimg) {
   if (k.dtype_bytes != 2 || k.prologue != DMC_PRO_AFFINE_SILU || k.dthresh != 0 || k.ldp < k.C1 + k.C2) return 0;
-  // opt-in (DMC_HALO_PRO=1): measured neutral for DDIM-50 at B=128 on MI355X (the saved GN-apply pass is
-  // paid back by a ~17 % slower conv: the halo rewrite's VALU work and its vmcnt(0) drains)
+  // default since round 2 (DMC_HALO_PRO=0 turns it off): with the GroupNorm statistics taken from the producing
+  // conv's epilogue the activation is not read at all before this conv; DDIM-50 645 -> 658 img/s, CFG 379 -> 389
+  // (round 1, with a statistics pass still in front of it, it was neutral: the halo rewrite costs ~17 % conv time)
   if (!dmc::opt(dmc::OPT_HALO_PRO) || dmc::opt(dmc::OPT_NO_HALO) || dmc::opt(dmc::OPT_NO_GLDS) ||
       dmc::opt(dmc::OPT_NO_BUFLDS))
     return 0;

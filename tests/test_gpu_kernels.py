@@ -130,7 +130,7 @@ def test_conv3x3_halo_gn_silu_prologue(case, monkeypatch, dmc_opt):
     conv (same op sequence and bf16 rounding), and the fp32 torch reference within bf16 tolerance."""
     L, K = _lib()
     dmc_opt("DMC_NO_SPLITK", 1)   # small N: keep the planner on the halo kernel
-    dmc_opt("DMC_HALO_PRO", 1)    # opt-in path
+    dmc_opt("DMC_HALO_PRO", 1)    # the halo prologue path (default on)
     dt = torch.bfloat16
     torch.manual_seed(11)
     N, H, C1, C2, Cout = {"c32_two_sources": (2, 32, 128, 64, 128), "c16_wide": (3, 16, 256, 0, 256),

@@ -84,7 +84,7 @@ def test_cifar_unet_matches_oracle(dtype):
 
 
 def test_cifar_unet_inference_halo_prologue_bitwise(monkeypatch, dmc_opt):
-    """bf16 inference at B=128 with the opt-in DMC_HALO_PRO=1: the ResBlock convs that take the GN+SiLU
+    """bf16 inference at B=128 with DMC_HALO_PRO=1 (the default): the ResBlock convs that take the GN+SiLU
     prologue on the halo kernel (dmc_conv_halo_prologue) give bitwise the output of the materialised path."""
     from diffusion_models_collection_amd.models import UNet
     torch.manual_seed(42)
