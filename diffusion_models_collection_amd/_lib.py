@@ -114,9 +114,10 @@ def _load():
         "dmc_ln_mod_fwd": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_p, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_f,
                                     _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_p, _c_int, _c_p, _c_p, _c_p]),
         "dmc_ln_mod_bwd": (_c_int, [_c_int, _c_p, _c_int, _c_p, _c_p, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_p,
-                                    _c_p, _c_p, _c_p]),
+                                    _c_p, _c_p, _c_p, _c_p]),
+        "dmc_dit_rowsum_workspace": (_c_size, [_c_int, _c_int, _c_int]),
         "dmc_gate_bwd": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_u32, _c_p, _c_u32,
-                                  _c_f, _c_p, _c_int, _c_p, _c_p]),
+                                  _c_f, _c_p, _c_int, _c_p, _c_p, _c_p]),
         "dmc_gelu_fwd": (_c_int, [_c_int, _c_p, _c_long, _c_int, _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_p]),
         "dmc_gelu_bwd": (_c_int, [_c_int, _c_p, _c_p, _c_long, _c_int, _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_p]),
         "dmc_timestep_embedding": (_c_int, [_c_p, _c_int, _c_int, _c_f, _c_p, _c_p]),

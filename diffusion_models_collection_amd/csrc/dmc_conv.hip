@@ -1869,7 +1869,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvK a, const char* dy, int ld_dy, float* slab,
                                                          int KK, int pix_per_split) {
   constexpr int EPC = TT<T>::KPL;
-  constexpr int SP = 128 / sizeof(T);      // pixels per stage
+  constexpr int SP = 64 / sizeof(T);       // pixels per stage (32 KB of LDS per block: 3 blocks per CU)
   constexpr int ROWB = 128 * sizeof(T);    // bytes per image row (128 columns)
   constexpr int CPR = ROWB / 16;           // chunks per row
   constexpr int NCH = SP * CPR / 256;      // chunks per thread per operand (=4)
@@ -1892,6 +1892,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvK a, const char* dy
   const bool kk_ok = kk < KK;
   const int co_c = co0 + chk * EPC;
 
+  // 1x1 stride-1 taps without a prologue (the DiT linears, the UNet's 1x1 convs): the source pixel is the output
+  // pixel, no per-load index arithmetic
+  const bool direct = a.ntaps == 1 && a.stride == 1 && a.mode == DMC_MODE_NORMAL && a.tdy0 == 0 && a.tdx0 == 0 &&
+                      a.H == a.OH && a.W == a.OW && a.prologue == DMC_PRO_NONE;
+  const char* xsrc = cch < a.C1 ? a.x1 + (size_t)cch * sizeof(T) : a.x2 + (size_t)(cch - a.C1) * sizeof(T);
+  const int xld = cch < a.C1 ? a.ld1 : a.ld2;
+  const bool x_in = cch < a.C1 + a.C2;
   v4i rd[NCH], rx[NCH];
   auto load_stage = [&](int p0) {
 #pragma unroll
@@ -1901,11 +1908,15 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvK a, const char* dy
       if (pix < p_end) {
         if (co_c < a.Cout) d = *(const v4i*)(dy + ((size_t)pix * ld_dy + co_c) * sizeof(T));
         if (kk_ok) {
-          const int n = pix / a.OHW;
-          const int rem = pix - n * a.OHW;
-          const int oy = rem / a.OW, ox = rem - (rem / a.OW) * a.OW;
-          const int sp = src_pixel(a, n, oy, ox, tap);
-          x = load_act_chunk<T>(a, n, sp, cch);
+          if (direct) {
+            if (x_in) x = *(const v4i*)(xsrc + (size_t)pix * xld * sizeof(T));
+          } else {
+            const int n = pix / a.OHW;
+            const int rem = pix - n * a.OHW;
+            const int oy = rem / a.OW, ox = rem - (rem / a.OW) * a.OW;
+            const int sp = src_pixel(a, n, oy, ox, tap);
+            x = load_act_chunk<T>(a, n, sp, cch);
+          }
         }
       }
       rd[j] = d; rx[j] = x;

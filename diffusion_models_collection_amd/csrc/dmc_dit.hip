@@ -123,13 +123,16 @@ __global__ __launch_bounds__(256) void ln_mod_fwd_kernel(const float* x, const v
 // One block (4 waves) per image: waves take rows w, w+4, ... of the image. Per row: dxhat = dh * (1 + scale),
 // dx += rstd * (dxhat - mean(dxhat) - xhat * mean(dxhat * xhat)); per channel (lane-owned, summed over the image's
 // rows in registers, then across waves in LDS): dscale = sum dh * xhat, dshift = sum dh.
+// The image's rows are split over gridDim.y blocks (so that B x splits blocks fill the chip); with more than one
+// split each block writes its channel sums to ws[b][split][2][C] and split_sum_kernel adds them in split order.
 template <typename T>
 __global__ __launch_bounds__(256) void ln_mod_bwd_kernel(const void* dh, int ld_dh, const float* x, const float* mean,
                                                          const float* rstd, const float* scale, int ld_mod, int C, int L,
-                                                         float* dx, float* dscale, float* dshift) {
+                                                         float* dx, float* dscale, float* dshift, float* ws) {
   __shared__ float red[4][2][512];   // [wave][dscale | dshift][channel]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int b = blockIdx.x;
+  const int b = blockIdx.x, S = gridDim.y, sp = blockIdx.y;
+  const int l0 = (int)((long)L * sp / S), l1 = (int)((long)L * (sp + 1) / S);
   float as[kMaxV][4], ah[kMaxV][4], sc1[kMaxV][4];
 #pragma unroll
   for (int k = 0; k < kMaxV; ++k)
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(256) void ln_mod_bwd_kernel(const void* dh, int ld_
       for (int e = 0; e < 4; ++e) sc1[k][e] = 1.0f + s[e];
     }
   }
-  for (int l = wave; l < L; l += 4) {
+  for (int l = l0 + wave; l < l1; l += 4) {
     const int row = b * L + l;
     const float mu = mean[row], rs = rstd[row];
     float g[kMaxV][4], xh[kMaxV][4];
@@ -200,8 +203,25 @@ __global__ __launch_bounds__(256) void ln_mod_bwd_kernel(const void* dh, int ld_
     float s = 0.f, t = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) { s += rs_[w * stride + c]; t += rs_[w * stride + 512 + c]; }
-    dscale[(size_t)b * ld_mod + c] = s;
-    dshift[(size_t)b * ld_mod + c] = t;
+    if (S == 1) {
+      dscale[(size_t)b * ld_mod + c] = s;
+      dshift[(size_t)b * ld_mod + c] = t;
+    } else {
+      ws[((size_t)(b * S + sp) * 2) * C + c] = s;
+      ws[((size_t)(b * S + sp) * 2 + 1) * C + c] = t;
+    }
+  }
+}
+
+// o_k[b * ld + c] = sum over splits s (in order) of ws[b][s][k][C]
+__global__ void split_sum_kernel(const float* ws, int B, int S, int C, int nout, float* o0, float* o1, int ld) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B * C; i += gridDim.x * blockDim.x) {
+    const int b = i / C, c = i - b * C;
+    for (int k = 0; k < nout; ++k) {
+      float v = 0.f;
+      for (int sp = 0; sp < S; ++sp) v += ws[((size_t)(b * S + sp) * nout + k) * C + c];
+      (k == 0 ? o0 : o1)[(size_t)b * ld + c] = v;
+    }
   }
 }
 
@@ -210,10 +230,11 @@ __global__ __launch_bounds__(256) void ln_mod_bwd_kernel(const void* dh, int ld_
 template <typename T>
 __global__ __launch_bounds__(256) void gate_bwd_kernel(const float* dy, const void* br, int ld_br, const float* gate,
                                                        int ld_mod, int C, int L, Drop drop, void* dbr, int ld_dbr,
-                                                       float* dgate) {
+                                                       float* dgate, float* ws) {
   __shared__ float red[4][512];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int b = blockIdx.x;
+  const int b = blockIdx.x, S = gridDim.y, sp = blockIdx.y;
+  const int l0 = (int)((long)L * sp / S), l1 = (int)((long)L * (sp + 1) / S);
   const uint32_t seed = drop.thresh ? drop.s() : 0u;
   float acc[kMaxV][4], gv[kMaxV][4];
 #pragma unroll
@@ -227,7 +248,7 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(const float* dy, const vo
       for (int e = 0; e < 4; ++e) gv[k][e] = g[e];
     }
   }
-  for (int l = wave; l < L; l += 4) {
+  for (int l = l0 + wave; l < l1; l += 4) {
     const int row = b * L + l;
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
@@ -256,8 +277,11 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(const float* dy, const vo
     }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256)
-    dgate[(size_t)b * ld_mod + c] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float v = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+    if (S == 1) dgate[(size_t)b * ld_mod + c] = v;
+    else ws[(size_t)(b * S + sp) * C + c] = v;
+  }
 }
 
 DMC_DEV float gelu_grad(float u) {
@@ -417,30 +441,52 @@ extern "C" int dmc_ln_mod_fwd(int dtype, const float* x, const void* br, int ld_
   return dmc::check_launch("dmc_ln_mod_fwd");
 }
 
+namespace {
+// row splits per image for the per-image channel sums: enough blocks to fill the chip, >= 16 rows per split
+int row_splits(int B, int L) {
+  int S = (1024 + B - 1) / B;
+  if (S > L / 16) S = L / 16;
+  return S < 1 ? 1 : (S > 64 ? 64 : S);
+}
+}  // namespace
+
+extern "C" size_t dmc_dit_rowsum_workspace(int B, int C, int L) {
+  const int S = row_splits(B, L);
+  return S > 1 ? (size_t)B * S * 2 * C * sizeof(float) : 0;
+}
+
 extern "C" int dmc_ln_mod_bwd(int dtype, const void* dh, int ld_dh, const float* x, const float* mean,
                               const float* rstd, const float* scale, int ld_mod, int T, int C, int L, float* dx,
-                              float* dscale, float* dshift, void* stream) {
+                              float* dscale, float* dshift, void* workspace, void* stream) {
   DMC_REQUIRE(C % 4 == 0 && C <= 512 && T % L == 0 && L > 0, "ln_mod_bwd: C %d (<= 512) T %d L %d", C, T, L);
   hipStream_t s = dmc::as_stream(stream);
   const int B = T / L;
+  const int S = workspace ? row_splits(B, L) : 1;
+  float* ws = (float*)workspace;
+  const dim3 g(B, S);
   if (dtype == DMC_F32)
-    ln_mod_bwd_kernel<float><<<B, 256, 0, s>>>(dh, ld_dh, x, mean, rstd, scale, ld_mod, C, L, dx, dscale, dshift);
+    ln_mod_bwd_kernel<float><<<g, 256, 0, s>>>(dh, ld_dh, x, mean, rstd, scale, ld_mod, C, L, dx, dscale, dshift, ws);
   else
-    ln_mod_bwd_kernel<bf16_t><<<B, 256, 0, s>>>(dh, ld_dh, x, mean, rstd, scale, ld_mod, C, L, dx, dscale, dshift);
+    ln_mod_bwd_kernel<bf16_t><<<g, 256, 0, s>>>(dh, ld_dh, x, mean, rstd, scale, ld_mod, C, L, dx, dscale, dshift, ws);
+  if (S > 1) split_sum_kernel<<<grid_for((long)B * C), 256, 0, s>>>(ws, B, S, C, 2, dscale, dshift, ld_mod);
   return dmc::check_launch("dmc_ln_mod_bwd");
 }
 
 extern "C" int dmc_gate_bwd(int dtype, const float* dy, const void* br, int ld_br, const float* gate, int ld_mod, int T,
                             int C, int L, uint32_t drop_seed, const uint32_t* drop_seed_base, uint32_t drop_thresh,
-                            float drop_scale, void* dbr, int ld_dbr, float* dgate, void* stream) {
+                            float drop_scale, void* dbr, int ld_dbr, float* dgate, void* workspace, void* stream) {
   DMC_REQUIRE(C % 4 == 0 && C <= 512 && T % L == 0 && L > 0, "gate_bwd: C %d (<= 512) T %d L %d", C, T, L);
   const Drop d = make_drop(drop_seed, drop_seed_base, drop_thresh, drop_scale);
   hipStream_t s = dmc::as_stream(stream);
   const int B = T / L;
+  const int S = workspace ? row_splits(B, L) : 1;
+  float* ws = (float*)workspace;
+  const dim3 g(B, S);
   if (dtype == DMC_F32)
-    gate_bwd_kernel<float><<<B, 256, 0, s>>>(dy, br, ld_br, gate, ld_mod, C, L, d, dbr, ld_dbr, dgate);
+    gate_bwd_kernel<float><<<g, 256, 0, s>>>(dy, br, ld_br, gate, ld_mod, C, L, d, dbr, ld_dbr, dgate, ws);
   else
-    gate_bwd_kernel<bf16_t><<<B, 256, 0, s>>>(dy, br, ld_br, gate, ld_mod, C, L, d, dbr, ld_dbr, dgate);
+    gate_bwd_kernel<bf16_t><<<g, 256, 0, s>>>(dy, br, ld_br, gate, ld_mod, C, L, d, dbr, ld_dbr, dgate, ws);
+  if (S > 1) split_sum_kernel<<<grid_for((long)B * C), 256, 0, s>>>(ws, B, S, C, 1, dgate, nullptr, ld_mod);
   return dmc::check_launch("dmc_gate_bwd");
 }
 

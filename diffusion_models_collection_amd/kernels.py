@@ -463,17 +463,24 @@ def ln_mod_fwd(dtype, x, T, C, L_, mod, ld_mod, off_shift, off_scale, eps, h, ld
                              ptr(rstd), L.stream()), "dmc_ln_mod_fwd")
 
 
+def _rowsum_ws(T, C, L_, dev):
+    n = LIB.dmc_dit_rowsum_workspace(T // L_, C, L_)
+    return SCRATCH.get(n, dev) if n else None
+
+
 def ln_mod_bwd(dtype, dh, ld_dh, x, mean, rstd, mod, ld_mod, off_scale, T, C, L_, dx, dmod, off_dscale, off_dshift):
+    ws = _rowsum_ws(T, C, L_, dx.device)
     check(LIB.dmc_ln_mod_bwd(L.dtype_code(dtype), ptr(dh), ld_dh, ptr(x), ptr(mean), ptr(rstd),
                              _mod_ptr(mod, off_scale), ld_mod, T, C, L_, ptr(dx), _mod_ptr(dmod, off_dscale),
-                             _mod_ptr(dmod, off_dshift), L.stream()), "dmc_ln_mod_bwd")
+                             _mod_ptr(dmod, off_dshift), ptr(ws), L.stream()), "dmc_ln_mod_bwd")
 
 
 def gate_bwd(dtype, dy, br, ld_br, mod, ld_mod, off_gate, T, C, L_, dbr, ld_dbr, dmod, off_dgate, drop=None):
     seed, seed_base, thresh, scale = drop_args(drop)
+    ws = _rowsum_ws(T, C, L_, dy.device)
     check(LIB.dmc_gate_bwd(L.dtype_code(dtype), ptr(dy), ptr(br), ld_br, _mod_ptr(mod, off_gate), ld_mod, T, C, L_,
-                           seed, seed_base, thresh, scale, ptr(dbr), ld_dbr, _mod_ptr(dmod, off_dgate), L.stream()),
-          "dmc_gate_bwd")
+                           seed, seed_base, thresh, scale, ptr(dbr), ld_dbr, _mod_ptr(dmod, off_dgate), ptr(ws),
+                           L.stream()), "dmc_gate_bwd")
 
 
 def gelu_fwd(dtype, u, rows, C, ld, a, drop=None):

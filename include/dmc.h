@@ -280,12 +280,15 @@ int dmc_ln_mod_fwd(int dtype, const float* x, const void* br, int ld_br, const f
                    const float* scale, int ld_mod, int T, int C, int L, float eps, uint32_t drop_seed,
                    const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, float* x_out, void* h,
                    int ld_h, float* mean, float* rstd, void* stream);
+/* workspace (dmc_dit_rowsum_workspace bytes, may be NULL = one block per image): the image's rows are split over
+ * several blocks whose per-image channel sums are added in split order (deterministic). */
+size_t dmc_dit_rowsum_workspace(int B, int C, int L);
 int dmc_ln_mod_bwd(int dtype, const void* dh, int ld_dh, const float* x, const float* mean, const float* rstd,
                    const float* scale, int ld_mod, int T, int C, int L, float* dx, float* dscale, float* dshift,
-                   void* stream);
+                   void* workspace, void* stream);
 int dmc_gate_bwd(int dtype, const float* dy, const void* br, int ld_br, const float* gate, int ld_mod, int T, int C,
                  int L, uint32_t drop_seed, const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale,
-                 void* dbr, int ld_dbr, float* dgate, void* stream);
+                 void* dbr, int ld_dbr, float* dgate, void* workspace, void* stream);
 int dmc_gelu_fwd(int dtype, const void* u, long rows, int C, int ld, uint32_t drop_seed, const uint32_t* drop_seed_base,
                  uint32_t drop_thresh, float drop_scale, void* a, void* stream);
 int dmc_gelu_bwd(int dtype, const void* da, const void* u, long rows, int C, int ld, uint32_t drop_seed,
