@@ -52,7 +52,8 @@ def log(*a):
 
 def conv_roofline(dtype, B=128):
     """Time the dominant kernel (the ResBlock 3x3 conv 128->128 @32x32, B=128, bias + time-embedding epilogue;
-    its GN+SiLU input is materialised by the GN-apply pass, as in training) with HIP events on the stream it is
+    its GN+SiLU input is materialised by the GN-apply pass, as in training; the halo kernel the library picks by
+    default: conv3x3_halo2_kernel, two 128-pixel blocks per CU) with HIP events on the stream it is
     launched on. `achieved` uses per-launch events (an event before and after every launch, so launches do not
     overlap: the same isolation rocprofv3's kernel trace gives, whose average the committed profile holds);
     `back_to_back_ms` is the average of 50 launches issued back to back (tails overlap)."""
@@ -88,7 +89,9 @@ def conv_roofline(dtype, B=128):
     b2b_ms = e0.elapsed_time(e1) / n
     flops = 2.0 * B * H * W * C * C * 9
     achieved = flops / (avg_ms * 1e-3) / 1e12
-    return {"kernel": "conv3x3_halo_kernel bf16 implicit GEMM (ResBlock 3x3 128->128 @32x32, B=128, "
+    ver = L.get_option("DMC_HALO_VER")
+    kname = "conv3x3_halo2_kernel" if ver == 2 else "conv3x3_halo_kernel"
+    return {"kernel": f"{kname} bf16 implicit GEMM (ResBlock 3x3 128->128 @32x32, B=128, "
                       "bias+temb epilogue)" if dtype == torch.bfloat16 else "conv_fwd_kernel<f32,128,128>",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic(),

@@ -983,6 +983,139 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
 }
 
 // ---------------------------------------------------------------------------------------------
+// Two-blocks-per-CU halo conv. The 8-wave kernel above holds 144 KB of LDS (double-buffered 64-channel halo +
+// 3-slot weight ring) for a 256-pixel tile, so one block owns a CU: every tile's prologue (halo + first weight
+// slices from HBM/L2), its chunk switches and its store burst stall the whole CU. Here a block is 4 waves on a
+// 128-pixel x 128-channel tile (each wave 64 x 64, the same fragments and MFMAs), with ONE halo buffer (<= 36 KB)
+// and a WS-slot weight ring: <= 78 KB, two blocks per CU, so one block's prologue / chunk reload / epilogue
+// overlaps the other's tap loop. At a chunk switch the block waits for its own next-chunk halo (the other block
+// keeps the CU busy). Tile geometry: R = 128 / OW rows of one image, or 128 / (OH*OW) whole images.
+template <int HP, int WS, bool PRO = false>
+__global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int nimg) {
+  using T = bf16_t;
+  constexpr int NW = 4, WM = 2, BM = 128, BN = 128;
+  constexpr int HB = HP * NW * 1024;             // bytes of the halo buffer
+  constexpr int WB = BN * 128;                   // bytes per weight slot
+  constexpr int EP = BN * 4 + 16;                // epilogue row pitch (fp32)
+  constexpr int STATS = NW * (BM / 64) * 16 * 8; // GroupNorm partial scratch past the epilogue tile
+  constexpr int LDS_BYTES = (HB + WS * WB) > BM * EP + STATS ? (HB + WS * WB) : BM * EP + STATS;
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  char* const wring = lds + HB;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  int mb = blockIdx.x, nb = blockIdx.y;
+  if (gridDim.y == 1) xcd_tile((a.Cout + BN - 1) / BN, mb, nb);
+  const int m0 = mb * BM, n0 = nb * BN;
+  const int lrow = lane >> 3;
+  const int lc = (lane & 7) ^ lrow;
+  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
+  const int n_first = m0 / a.OHW;
+  const int r0 = (m0 - n_first * a.OHW) / OW;
+
+  unsigned h1[HP], h2[HP];
+#pragma unroll
+  for (int p = 0; p < HP; ++p) {
+    const int h = (wave * HP + p) * 8 + lrow;
+    h1[p] = kOOB; h2[p] = kOOB;
+    if (h < npix) {
+      const int img = h / segpix, rem = h - img * segpix;
+      const int hr = rem / HW, hc = rem - hr * HW;
+      const int iy = r0 + hr - 1, ix = hc - 1;
+      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
+        const unsigned sp = (unsigned)(((n_first + img) * a.H + iy) * a.W + ix);
+        h1[p] = (sp * a.ld1 + lc * 8) * 2u;
+        h2[p] = (sp * a.ld2 + lc * 8) * 2u;
+      }
+    }
+  }
+  const unsigned wrow = (unsigned)(a.ntaps * a.Kc);
+  unsigned ob[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int co = n0 + (wave * 4 + j) * 8 + lrow;
+    ob[j] = co < a.Cout ? ((unsigned)co * wrow + lc * 8) * 2u : kOOB;
+  }
+  const int fr = lane & 15, fh = lane >> 4;
+  int hb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = wm * 64 + j * 16 + fr;
+    const int img = m / (R * OW), rem = m - img * (R * OW);
+    const int r = rem / OW, col = rem - r * OW;
+    hb[j] = img * segpix + (r + 1) * HW + col + 1;
+  }
+
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int nch = a.Kc / 64, nst = nch * 9;
+  auto issue_w = [&](int s) {
+    const int c = s / 9, t = s - c * 9;
+    const unsigned koff = (unsigned)(t * a.Kc + c * 64) * 2u;
+    dma_pieces<4>(a.w, a.w_bytes, wring + (s % WS) * WB + wave * 4 * 1024, ob, koff, 0, 4);
+  };
+  v4f pst[4];
+  for (int s = 0; s < nst; ++s) {
+    const int c = s / 9, t = s - c * 9;
+    if (t == 0) {
+      // chunk c's halo into the single buffer: every wave is done with chunk c-1's taps
+      if (c > 0) __syncthreads();
+      if (PRO) halo_pro_load(a, n_first, c * 64, pst);
+      halo_issue<HP>(a, lds, c * 64, wave, 0, HP, h1, h2);
+      if (c == 0)
+        for (int q = 0; q < WS - 1 && q < nst; ++q) issue_w(q);
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+      if (PRO) halo_affine_silu<HP>(lds, wave, h1, pst);
+    } else {
+      // weight slice s has landed once at most the slices issued after it are in flight
+      const int after = min(nst - 1, s + WS - 2) - s;
+      wait_vm_dyn(4 * (after > 0 ? after : 0));
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    if (s + WS - 1 < nst) issue_w(s + WS - 1);
+    const char* Bw = wring + (s % WS) * WB;
+    const int ty = t / 3, tx = t - ty * 3;
+    const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = ks * 4 + fh;
+      v4i fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wn * 64 + i * 16 + fr;
+        fa[i] = *(const v4i*)(Bw + r * 128 + ((chunk ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int h = hb[j] + delta;
+        fb[j] = *(const v4i*)(lds + h * 128 + ((chunk ^ (h & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *(v4f*)(lds + (wm * 64 + j * 16 + fr) * EP + (wn * 64 + i * 16 + fh * 4) * 4) = acc[i][j];
+  __syncthreads();
+  tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Round-2 halo conv: 4 waves (one per SIMD), v_mfma_f32_32x32x16_bf16, epilogue straight from registers.
 //
 // Same block tile (128 output channels x 256 output pixels), the same LDS-resident halo per 64-channel chunk
@@ -1693,6 +1826,21 @@ int halo_plan(const ConvK& k, int* R, int* nimg) {
   else return 0;
   const int npix = *nimg * (*R + 2) * (k.OW + 2);
   return npix <= 6 * 64 ? 6 : npix <= 7 * 64 ? 7 : 0;
+}
+
+// Geometry of the two-blocks-per-CU halo kernel (128-pixel tiles): halo pieces per wave (6, 7 or 9), 0 if it
+// does not apply.
+int halo2_plan(const ConvK& k, int* R, int* nimg) {
+  if (k.mode != DMC_MODE_NORMAL || k.stride != 1 || k.ntaps != 9 || k.tkw != 3) return 0;
+  if (!((k.tdy0 == -1 && k.tsy == 1) || (k.tdy0 == 1 && k.tsy == -1))) return 0;
+  if (!((k.tdx0 == -1 && k.tsx == 1) || (k.tdx0 == 1 && k.tsx == -1))) return 0;
+  if (k.OH != k.H || k.OW != k.W) return 0;
+  const int ohw = k.OH * k.OW;
+  if (ohw % 128 == 0 && 128 % k.OW == 0) { *nimg = 1; *R = 128 / k.OW; }
+  else if (128 % ohw == 0 && k.N % (128 / ohw) == 0) { *nimg = 128 / ohw; *R = k.OH; }
+  else return 0;
+  const int npix = *nimg * (*R + 2) * (k.OW + 2);
+  return npix <= 6 * 32 ? 6 : npix <= 7 * 32 ? 7 : npix <= 9 * 32 ? 9 : 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2470,6 +2618,28 @@ int halo_pro_plan(const ConvK& k, int* R, int* nimg) {
   return *nimg == 1 ? hp : 0;   // one image per tile: a lane's scale/shift row is the same in every piece
 }
 
+// halo_pro_plan for the two-blocks-per-CU kernel (DMC_HALO_VER=2)
+int halo2_pro_plan(const ConvK& k, int* R, int* nimg) {
+  if (k.dtype_bytes != 2 || k.prologue != DMC_PRO_AFFINE_SILU || k.dthresh != 0 || k.ldp < k.C1 + k.C2) return 0;
+  if (!dmc::opt(dmc::OPT_HALO_PRO) || dmc::opt(dmc::OPT_NO_HALO) || dmc::opt(dmc::OPT_NO_GLDS) ||
+      dmc::opt(dmc::OPT_NO_BUFLDS) || dmc::opt(dmc::OPT_HALO_VER) != 2)
+    return 0;
+  const bool buf = k.C1 % 64 == 0 && k.C2 % 64 == 0 && k.Kc == k.C1 + k.C2 && k.x1_bytes > 0 &&
+                   (k.C2 == 0 || k.x2_bytes > 0) && k.w_bytes > 0;
+  if (!buf) return 0;
+  const int hp = halo2_plan(k, R, nimg);
+  return *nimg == 1 ? hp : 0;
+}
+
+template <bool PRO>
+void launch_halo2(const ConvK& k, int hp, int R, int nimg, hipStream_t s) {
+  const dim3 g = dmc::opt(dmc::OPT_NO_XCD) ? dim3(k.M / 128, dmc::cdiv(k.Cout, 128))
+                                          : dim3(k.M / 128 * dmc::cdiv(k.Cout, 128));
+  if (hp == 6) conv3x3_halo2_kernel<6, 3, PRO><<<g, 256, 0, s>>>(k, R, nimg);
+  else if (hp == 7) conv3x3_halo2_kernel<7, 3, PRO><<<g, 256, 0, s>>>(k, R, nimg);
+  else conv3x3_halo2_kernel<9, 2, PRO><<<g, 256, 0, s>>>(k, R, nimg);
+}
+
 template <bool BUF>
 void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
   if (p.splits > 1) {
@@ -2519,12 +2689,13 @@ bool epi_stats_ok(const ConvK& k, const void* ws, size_t ws_bytes) {
       k.M % 256 || k.OHW % 64 || ((k.Cout | k.ldy1 | k.ld_res) & 7))
     return false;
   if (!dmc::opt(dmc::OPT_NO_NARROW) && ((k.C2 == 0 && k.C1 <= 8 && k.Cout >= 16) || k.Cout <= 8)) return false;
-  if (dmc::opt(dmc::OPT_NO_GLDS) || dmc::opt(dmc::OPT_HALO_VER) != 1 || dmc::opt(dmc::OPT_HALO_RW) ||
+  if (dmc::opt(dmc::OPT_NO_GLDS) || (dmc::opt(dmc::OPT_HALO_VER) != 1 && dmc::opt(dmc::OPT_HALO_VER) != 2) ||
+      dmc::opt(dmc::OPT_HALO_RW) ||
       dmc::opt(dmc::OPT_NO_EPI_STATS))
     return false;
   if (k.prologue == DMC_PRO_AFFINE_SILU) {
     int R, nimg;
-    return halo_pro_plan(k, &R, &nimg) != 0;
+    return halo2_pro_plan(k, &R, &nimg) != 0 || halo_pro_plan(k, &R, &nimg) != 0;
   }
   if (k.prologue != DMC_PRO_NONE) return false;
   const FwdPlan p = plan_glds(k);
@@ -2546,6 +2717,8 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
   }
   if (sizeof(T) == 2 && k.prologue == DMC_PRO_AFFINE_SILU) {
     int R, nimg;
+    const int hp2 = halo2_pro_plan(k, &R, &nimg);
+    if (hp2) { launch_halo2<true>(k, hp2, R, nimg, s); return dmc::check_launch("dmc_conv2d"); }
     const int hp = halo_pro_plan(k, &R, &nimg);
     const dim3 hg1 = dmc::opt(dmc::OPT_NO_XCD) ? dim3(k.M / 256, dmc::cdiv(k.Cout, 128))
                                                : dim3(k.M / 256 * dmc::cdiv(k.Cout, 128));   // 1-D: XCD-aware
@@ -2564,7 +2737,10 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     const dim3 hg(k.M / 256, dmc::cdiv(k.Cout, 128));
     const dim3 hgx = dmc::opt(dmc::OPT_NO_XCD) ? hg : dim3(hg.x * hg.y);   // 1-D: XCD-aware tile order
     int R5, nimg5;
-    const long hver = dmc::opt(dmc::OPT_HALO_VER);   // 1: round-1 8-wave kernel (default), 4 / 5: round-2 variants
+    const long hver = dmc::opt(dmc::OPT_HALO_VER);   // 1: 8-wave kernel, 2: two blocks per CU, 4 / 5: experiments
+    int R2, nimg2;
+    const int hp2 = (buf && p.splits == 1 && !dmc::opt(dmc::OPT_NO_HALO) && hver == 2) ? halo2_plan(k, &R2, &nimg2) : 0;
+    if (hp2) { launch_halo2<false>(k, hp2, R2, nimg2, s); return dmc::check_launch("dmc_conv2d"); }
     const int hp5 = (buf && p.splits == 1 && !dmc::opt(dmc::OPT_NO_HALO) && !dmc::opt(dmc::OPT_HALO_V1) &&
                      !dmc::opt(dmc::OPT_HALO_RW) && !dmc::opt(dmc::OPT_HALO_WS4) && hver == 5 &&
                      halo4_epilogue_ok(k)) ? halo5_plan(k, &R5, &nimg5) : 0;

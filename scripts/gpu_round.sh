@@ -55,5 +55,5 @@ if [[ $STAGES == *m* ]]; then
   P="python3 bench.py --roofline-only"
   timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d "$O/fetch" -o fetch --output-format csv -- $P > /dev/null
   timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d "$O/write" -o write --output-format csv -- $P > /dev/null
-  python3 scripts/pmc_to_json.py "$O/fetch" "$O/write" conv3x3_halo_kernel "$O/pmc_roofline_conv.json"
+  python3 scripts/pmc_to_json.py "$O/fetch" "$O/write" conv3x3_halo2_kernel "$O/pmc_roofline_conv.json"
 fi

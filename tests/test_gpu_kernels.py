@@ -123,14 +123,16 @@ def test_upsample2x_nhwc_bitwise(dt):
     assert torch.equal(y.permute(0, 3, 1, 2).float(), ref)
 
 
+@pytest.mark.parametrize("ver", [1, 2])
 @pytest.mark.parametrize("case", ["c32_two_sources", "c16_wide", "c32_384", "c8_multi_image"])
-def test_conv3x3_halo_gn_silu_prologue(case, monkeypatch, dmc_opt):
+def test_conv3x3_halo_gn_silu_prologue(case, ver, monkeypatch, dmc_opt):
     """Inference prologue on the halo kernel: conv(SiLU(x*scale+shift)) with the GroupNorm affine + SiLU
     applied to the LDS-resident halo equals, BITWISE, dmc_gn_apply materialisation followed by the plain halo
     conv (same op sequence and bf16 rounding), and the fp32 torch reference within bf16 tolerance."""
     L, K = _lib()
     dmc_opt("DMC_NO_SPLITK", 1)   # small N: keep the planner on the halo kernel
     dmc_opt("DMC_HALO_PRO", 1)    # the halo prologue path (default on)
+    dmc_opt("DMC_HALO_VER", ver)  # 1: 256-pixel 8-wave kernel, 2: 128-pixel two-blocks-per-CU kernel
     dt = torch.bfloat16
     torch.manual_seed(11)
     N, H, C1, C2, Cout = {"c32_two_sources": (2, 32, 128, 64, 128), "c16_wide": (3, 16, 256, 0, 256),
@@ -225,14 +227,16 @@ def test_conv_dgrad_wgrad(dt, case):
     assert e1 < lim and e2 < (1e-5 if dt == torch.float32 else 1e-2), (e1, e2)
 
 
-@pytest.mark.parametrize("variant", ["ring3", "ring4", "regw"])
+@pytest.mark.parametrize("variant", ["ring3", "ring4", "regw", "halo2"])
 @pytest.mark.parametrize("case", ["fwd32_concat", "fwd16_ragged_cout", "dgrad32", "fwd8_multi_image", "fallback_4x4",
                                   "fwd8_concat_b128", "fwd64_rows"])
 def test_conv3x3_halo_kernel(case, variant, monkeypatch, dmc_opt):
     """bf16 3x3 stride-1 convs on the LDS-halo kernel (whole-row 256-pixel tiles) vs an fp32 reference and
     vs the per-tap kernel (DMC_NO_HALO) on the same inputs. Variants: 3- or 4-slot LDS-DMA weight ring
-    (DMC_HALO_WS4), register-staged weights (DMC_HALO_RW)."""
+    (DMC_HALO_WS4), register-staged weights (DMC_HALO_RW), the two-blocks-per-CU 128-pixel kernel
+    (DMC_HALO_VER=2)."""
     L, K = _lib()
+    dmc_opt("DMC_HALO_VER", 2 if variant == "halo2" else 1)
     dmc_opt("DMC_HALO_WS4", 1 if variant == "ring4" else 0)
     dmc_opt("DMC_HALO_RW", 1 if variant == "regw" else 0)
     # at these small M the planner would split K over the LDS-DMA kernel instead; the halo kernel is what the
@@ -610,15 +614,17 @@ def test_conv_fp32_gemm_splitk_silu_pre(Cin, Cout):
     assert rel_err(y.view(N, Cout).cpu(), ref) < 1e-5
 
 
-@pytest.mark.parametrize("case", ["halo3x3", "glds1x1", "splitk_small", "fp32_reg", "concat_two"])
-def test_conv_epilogue_groupnorm_partials(case):
+@pytest.mark.parametrize("case", ["halo3x3", "halo2_3x3", "glds1x1", "splitk_small", "fp32_reg", "concat_two"])
+def test_conv_epilogue_groupnorm_partials(case, dmc_opt):
     """dmc_conv_desc.gn_part + dmc_gn_finalize (the conv epilogue's GroupNorm partials: in-kernel on the halo and
     LDS-DMA paths, one pass over the output elsewhere) give the statistics dmc_gn_stats computes over the stored
     output: mean / rstd and the folded scale / shift within 2e-5 (fp32 summation order)."""
     from diffusion_models_collection_amd import _lib as L, kernels as K
     gen = torch.Generator().manual_seed(11)
     dt = torch.float32 if case == "fp32_reg" else torch.bfloat16
+    dmc_opt("DMC_HALO_VER", 2 if case == "halo2_3x3" else 1)
     N, H, W, Cin, Cout, taps = {"halo3x3": (4, 32, 32, 128, 128, K.TAPS3), "glds1x1": (8, 16, 16, 256, 256, K.TAPS1),
+                                "halo2_3x3": (4, 32, 32, 128, 128, K.TAPS3),
                                 "splitk_small": (2, 8, 8, 256, 256, K.TAPS3), "fp32_reg": (2, 16, 16, 64, 128, K.TAPS3),
                                 "concat_two": (4, 16, 16, 128, 128, K.TAPS3)}[case]
     G = 8
