@@ -990,7 +990,7 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
 // and a WS-slot weight ring: <= 78 KB, two blocks per CU, so one block's prologue / chunk reload / epilogue
 // overlaps the other's tap loop. At a chunk switch the block waits for its own next-chunk halo (the other block
 // keeps the CU busy). Tile geometry: R = 128 / OW rows of one image, or 128 / (OH*OW) whole images.
-template <int HP, int WS, bool PRO = false>
+template <int HP, int WS, bool PRO = false, bool SCHED = true>
 __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int nimg) {
   using T = bf16_t;
   constexpr int NW = 4, WM = 2, BM = 128, BN = 128;
@@ -1085,24 +1085,38 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
     const char* Bw = wring + (s % WS) * WB;
     const int ty = t / 3, tx = t - ty * 3;
     const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
+    // both k-steps' fragments read up front into distinct registers; the schedule below issues the second
+    // k-step's reads between the first k-step's MFMAs (left alone, hipcc re-reads fragments into the same
+    // registers and waits for each read right before its MFMA)
+    v4i fa[2][4], fb[2][4];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int chunk = ks * 4 + fh;
-      v4i fa[4], fb[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = wn * 64 + i * 16 + fr;
-        fa[i] = *(const v4i*)(Bw + r * 128 + ((chunk ^ (r & 7)) << 4));
+        fa[ks][i] = *(const v4i*)(Bw + r * 128 + ((chunk ^ (r & 7)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int h = hb[j] + delta;
-        fb[j] = *(const v4i*)(lds + h * 128 + ((chunk ^ (h & 7)) << 4));
+        fb[ks][j] = *(const v4i*)(lds + h * 128 + ((chunk ^ (h & 7)) << 4));
       }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[ks][i], fb[ks][j]);
+    if (SCHED) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);    // k-step 0 reads
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // two k-step-0 MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one k-step-1 read
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);   // k-step 1 MFMAs
     }
   }
   __syncthreads();
@@ -2635,6 +2649,12 @@ template <bool PRO>
 void launch_halo2(const ConvK& k, int hp, int R, int nimg, hipStream_t s) {
   const dim3 g = dmc::opt(dmc::OPT_NO_XCD) ? dim3(k.M / 128, dmc::cdiv(k.Cout, 128))
                                           : dim3(k.M / 128 * dmc::cdiv(k.Cout, 128));
+  if (dmc::opt(dmc::OPT_HALO_NOSCHED)) {   // A/B: the compiler's own fragment-read schedule
+    if (hp == 6) conv3x3_halo2_kernel<6, 3, PRO, false><<<g, 256, 0, s>>>(k, R, nimg);
+    else if (hp == 7) conv3x3_halo2_kernel<7, 3, PRO, false><<<g, 256, 0, s>>>(k, R, nimg);
+    else conv3x3_halo2_kernel<9, 2, PRO, false><<<g, 256, 0, s>>>(k, R, nimg);
+    return;
+  }
   if (hp == 6) conv3x3_halo2_kernel<6, 3, PRO><<<g, 256, 0, s>>>(k, R, nimg);
   else if (hp == 7) conv3x3_halo2_kernel<7, 3, PRO><<<g, 256, 0, s>>>(k, R, nimg);
   else conv3x3_halo2_kernel<9, 2, PRO><<<g, 256, 0, s>>>(k, R, nimg);
