@@ -686,25 +686,36 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
     if (s + 2 < ns) DMC_GLDS_ISSUE(s + 2);
     const char* A = lds + (s % STAGES) * SB;
     const char* B = A + BM * 128;
+    // fragment reads of both k-steps into distinct registers, the second k-step's between the first's MFMAs
+    // (the schedule of conv3x3_halo2_kernel)
+    v4i fa[2][4], fb[2][4];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int chunk = ks * 4 + fh;
-      v4i fa[4], fb[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = wn * 64 + i * 16 + fr;
-        fa[i] = *(const v4i*)(B + r * 128 + ((chunk ^ (r & 7)) << 4));
+        fa[ks][i] = *(const v4i*)(B + r * 128 + ((chunk ^ (r & 7)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int r = wm * 64 + j * 16 + fr;
-        fb[j] = *(const v4i*)(A + r * 128 + ((chunk ^ (r & 7)) << 4));
+        fb[ks][j] = *(const v4i*)(A + r * 128 + ((chunk ^ (r & 7)) << 4));
       }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[ks][i], fb[ks][j]);
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
+    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
   }
 #undef DMC_GLDS_ISSUE
   // Epilogue through LDS: the block's fp32 tile is parked in the (now free) staging ring, then every
