@@ -585,17 +585,20 @@ DMC_DEV void xcd_tile(int NB, int& mb, int& nb) {
 // hardware range check, per-row offsets precomputed once per tap -> one VALU add per DMA instruction.
 // Requires C1 % 64 == 0, C2 % 64 == 0, Kc == C1 + C2 (a stage never straddles the concat boundary).
 // BUF = false: generic (any channel split) with flat global_load_lds and a zero page.
-template <int WM, int WN, bool BUF>
+// STAGES = LDS ring depth: 3 (one block per CU for the 256x128 tile), or 2 for the 128x128 tile so that two
+// blocks share a CU (one's prologue / epilogue overlaps the other's K loop).
+template <int WM, int WN, bool BUF, int STAGES = 3>
 __global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
   using T = bf16_t;
   constexpr int NW = WM * WN;
   constexpr int BM = 64 * WM, BN = 64 * WN;
-  constexpr int STAGES = 3;
   constexpr int SB = (BM + BN) * 128;           // bytes per stage
   constexpr int AI = BM / 8 / NW;               // A glds instructions per wave per stage
   constexpr int BI = BN / 8 / NW;               // B glds instructions per wave per stage
   static_assert(AI >= 1 && BI >= 1, "tile too small for the wave count");
-  __shared__ __attribute__((aligned(16))) char lds[STAGES * SB];
+  constexpr int EPB = BM * (BN * 4 + 16) + NW * (BM / 64) * 16 * 8;   // epilogue tile + GroupNorm partials
+  constexpr int LDS_BYTES = STAGES * SB > EPB ? STAGES * SB : EPB;
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -670,20 +673,19 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
     if (is_c0 == a.Kc) { is_c0 = 0; ++is_tap; if (is_tap < a.ntaps) tap_rows(); }
   };
 #define DMC_GLDS_ISSUE(S) issue(S)
-  if (ns > 0) DMC_GLDS_ISSUE(0);
-  if (ns > 1) DMC_GLDS_ISSUE(1);
+  for (int q = 0; q < STAGES - 1 && q < ns; ++q) DMC_GLDS_ISSUE(q);
   const int fr = lane & 15, fh = lane >> 4;
   for (int s = 0; s < ns; ++s) {
-    // stage s has landed once at most the next stage's instructions are still outstanding
-    if (s + 1 < ns) __builtin_amdgcn_s_waitcnt(waitcnt_vm(AI + BI));
+    // stage s has landed once at most the later stages' instructions are still outstanding
+    if (STAGES > 2 && s + STAGES - 2 < ns) __builtin_amdgcn_s_waitcnt(waitcnt_vm((STAGES - 2) * (AI + BI)));
     else __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
-    // every wave has finished reading stage s-1's buffer: refill it with stage s+2
-    if (s + 2 < ns) DMC_GLDS_ISSUE(s + 2);
+    // every wave has finished reading stage s-1's buffer: refill it with stage s+STAGES-1
+    if (s + STAGES - 1 < ns) DMC_GLDS_ISSUE(s + STAGES - 1);
     const char* A = lds + (s % STAGES) * SB;
     const char* B = A + BM * 128;
     // fragment reads of both k-steps into distinct registers, the second k-step's between the first's MFMAs
@@ -722,7 +724,6 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
   // thread finishes 4-channel groups of consecutive channels (coalesced NHWC stores; the epilogue loop is
   // a runtime loop, which keeps hipcc from spilling the accumulators to scratch).
   constexpr int EP = BN * 4 + 16;
-  static_assert(BM * EP <= STAGES * SB, "epilogue tile must fit the staging ring");
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -2684,7 +2685,11 @@ void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
     const int bm = p.cfg == 0 ? 256 : p.cfg == 1 ? 128 : 64;
     const int nb = dmc::cdiv(k.Cout, 128);
     const dim3 g = dmc::opt(dmc::OPT_NO_XCD) ? dim3(dmc::cdiv(k.M, bm), nb) : dim3(dmc::cdiv(k.M, bm) * nb);
-    if (p.cfg == 0) conv_fwd_glds_kernel<4, 2, BUF><<<g, 512, 0, s>>>(k);
+    if (p.cfg == 0 && dmc::opt(dmc::OPT_GLDS_2B)) {
+      // A/B: 128x128 tiles, 2-stage ring, two blocks per CU
+      const dim3 g2 = dmc::opt(dmc::OPT_NO_XCD) ? dim3(dmc::cdiv(k.M, 128), nb) : dim3(dmc::cdiv(k.M, 128) * nb);
+      conv_fwd_glds_kernel<2, 2, BUF, 2><<<g2, 256, 0, s>>>(k);
+    } else if (p.cfg == 0) conv_fwd_glds_kernel<4, 2, BUF><<<g, 512, 0, s>>>(k);
     else if (p.cfg == 1) conv_fwd_glds_kernel<2, 2, BUF><<<g, 256, 0, s>>>(k);
     else conv_fwd_glds_kernel<1, 2, BUF><<<g, 128, 0, s>>>(k);
   }
