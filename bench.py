@@ -43,7 +43,7 @@ CIFAR = dict(image_size=(32, 32), in_channels=3, model_channels=128, out_channel
              attention_resolutions=(16, 8), dropout=0.1, channel_mult=(1, 2, 2, 2), use_attention=True)
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense, MI355X_MICROARCH.md
 TRAIN_GFLOP_PER_IMG = 37.890     # fwd + bwd, = 3 x 12.632 forward
-PMC_FILE = "r1_pmc_roofline_conv.json"
+PMC_FILE = "r2_pmc_roofline_conv.json"
 
 
 def log(*a):
@@ -54,9 +54,9 @@ def conv_roofline(dtype, B=128):
     """Time the dominant kernel (the ResBlock 3x3 conv 128->128 @32x32, B=128, bias + time-embedding epilogue;
     its GN+SiLU input is materialised by the GN-apply pass, as in training; the halo kernel the library picks by
     default: conv3x3_halo2_kernel, two 128-pixel blocks per CU) with HIP events on the stream it is
-    launched on. `achieved` uses per-launch events (an event before and after every launch, so launches do not
-    overlap: the same isolation rocprofv3's kernel trace gives, whose average the committed profile holds);
-    `back_to_back_ms` is the average of 50 launches issued back to back (tails overlap)."""
+    launched on. `achieved` / `avg_launch_ms`: the average of 50 launches issued back to back between two events
+    (agrees with the rocprofv3 kernel-trace average, profiles/r2_roofline_kernel_stats.csv);
+    `per_launch_events_ms`: an event pair around every launch (includes the events' own overhead)."""
     from diffusion_models_collection_amd import _lib as L, kernels as K
     H = W = 32
     C = 128
@@ -88,14 +88,17 @@ def conv_roofline(dtype, B=128):
     avg_ms = sum(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(n)) / n
     b2b_ms = e0.elapsed_time(e1) / n
     flops = 2.0 * B * H * W * C * C * 9
-    achieved = flops / (avg_ms * 1e-3) / 1e12
+    # the launch duration is taken from the 50 back-to-back launches between two events: it agrees with the
+    # rocprofv3 kernel-trace average of the same command within ~1 % (profiles/r2_roofline_*), whereas an event
+    # pair around every launch adds its own ~4 us
+    achieved = flops / (b2b_ms * 1e-3) / 1e12
     ver = L.get_option("DMC_HALO_VER")
     kname = "conv3x3_halo2_kernel" if ver == 2 else "conv3x3_halo_kernel"
     return {"kernel": f"{kname} bf16 implicit GEMM (ResBlock 3x3 128->128 @32x32, B=128, "
                       "bias+temb epilogue)" if dtype == torch.bfloat16 else "conv_fwd_kernel<f32,128,128>",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic(),
-            "flops_per_launch": flops, "avg_launch_ms": round(avg_ms, 4), "back_to_back_ms": round(b2b_ms, 4),
+            "flops_per_launch": flops, "avg_launch_ms": round(b2b_ms, 4), "per_launch_events_ms": round(avg_ms, 4),
             "algorithmic_bytes_per_launch": 2 * (2 * B * H * W * C) + 2 * C * 9 * C}
 
 
