@@ -84,10 +84,11 @@ def _load():
         "dmc_channel_sum_workspace": (_c_size, [_c_int, _c_int, _c_int]),
         "dmc_channel_sum": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_p, _c_int, _c_p, _c_f, _c_p,
                                      _c_p]),
-        "dmc_attn_fwd": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_int, _c_p, _c_p]),
+        "dmc_attn_fwd": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_int, _c_p, _c_u32,
+                                  _c_p, _c_u32, _c_f, _c_p]),
         "dmc_attn_workspace": (_c_size, [_c_int, _c_int, _c_int]),
         "dmc_attn_bwd": (_c_int, [_c_int, _c_p, _c_int, _c_p, _c_p, _c_int, _c_p, _c_int, _c_int, _c_int, _c_int,
-                                  _c_p, _c_int, _c_p, _c_p]),
+                                  _c_p, _c_int, _c_p, _c_u32, _c_p, _c_u32, _c_f, _c_p]),
         "dmc_time_embed": (_c_int, [_c_p, _c_int, _c_int, _c_p, _c_p]),
         "dmc_embed_fwd": (_c_int, [_c_p, _c_int, _c_int, _c_p, _c_int, _c_p, _c_p]),
         "dmc_embed_bwd": (_c_int, [_c_p, _c_int, _c_int, _c_p, _c_int, _c_p, _c_p]),

@@ -36,7 +36,16 @@ struct AttnK {
   float* lse_out;
   int N, L, heads, hd;
   float scale;                  // 1/sqrt(hd)
+  // attention-probability dropout (nn.MultiheadAttention(dropout=p) in training, the DiT's blocks): the
+  // probability P[q][key] of head row nh is kept iff hash(seed, (nh*L + q)*L + key) >= dthresh and scaled by
+  // dscale = 1/(1-p); the softmax statistics (lse) are those of the undropped P, as in torch
+  uint32_t dseed, dthresh; float dscale; const uint32_t* dseed_base;
 };
+
+DMC_DEV uint32_t attn_seed(const AttnK& a) { return a.dthresh ? a.dseed + (a.dseed_base ? *a.dseed_base : 0u) : 0u; }
+DMC_DEV float attn_keep(const AttnK& a, uint32_t seed, size_t idx) {
+  return drop_keep(idx, seed, a.dthresh) ? a.dscale : 0.f;
+}
 
 // B-operand fragments (rows = token, k = d) straight from global memory: lane holds token row
 // `tok` (its column) and 16 bytes of d starting at dc*4*KPL + h*KPL.
@@ -143,7 +152,7 @@ DMC_DEV void store_d4(char* base, size_t idx, const float* v) {
 // Forward: online-softmax update of (m, lsum, o) with keys [k0, k0+64).
 template <typename T, int HDP>
 DMC_DEV void fwd_keys(const AttnK& a, const char* sK, const char* sV, int k0, const v4i* qf, float sl2, float& m,
-                      float& lsum, v4f* o) {
+                      float& lsum, v4f* o, size_t mrow = 0, uint32_t seed = 0) {
   constexpr int KPL = TT<T>::KPL;
   constexpr int DC = HDP / (4 * KPL);
   constexpr int DT = HDP / 16;
@@ -177,6 +186,12 @@ DMC_DEV void fwd_keys(const AttnK& a, const char* sK, const char* sV, int k0, co
   rs += __shfl_xor(rs, 32, 64);
   lsum = lsum * alpha + rs;
   m = mn;
+  if (a.dthresh) {   // dropout on the probabilities that multiply V (the row sum above is of the undropped P)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) p[t][i] *= attn_keep(a, seed, mrow + (size_t)(k0 + 16 * t + 4 * h + i));
+  }
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) {
     o[dt] *= alpha;
@@ -235,7 +250,7 @@ DMC_DEV float dq_delta(const AttnK& a, int n, int hh, int q) {
 // dQ += dS K over keys [k0, k0+64), P recomputed from the log-sum-exp, dS = P (dP - delta)
 template <typename T, int HDP>
 DMC_DEV void dq_keys(const AttnK& a, const char* sK, const char* sV, int k0, const v4i* qf, const v4i* df, float sl2,
-                     float lse2, float dl, v4f* dq) {
+                     float lse2, float dl, v4f* dq, size_t mrow = 0, uint32_t seed = 0) {
   constexpr int KPL = TT<T>::KPL;
   constexpr int DC = HDP / (4 * KPL);
   constexpr int DT = HDP / 16;
@@ -255,7 +270,9 @@ DMC_DEV void dq_keys(const AttnK& a, const char* sK, const char* sV, int k0, con
     for (int i = 0; i < 4; ++i) {
       const int key = k0 + 16 * t + 4 * h + i;
       const float pv = key < a.L ? exp2f(s[i] * sl2 - lse2) : 0.f;
-      ds[t][i] = pv * (dp[i] - dl);
+      // with dropout O = (P*M) V: dP = (dO V^T) * M, and delta = rowsum(dO * O) still equals rowsum(P * dP)
+      const float dpv = a.dthresh ? dp[i] * attn_keep(a, seed, mrow + (size_t)key) : dp[i];
+      ds[t][i] = pv * (dpv - dl);
     }
   }
 #pragma unroll
@@ -281,8 +298,9 @@ DMC_DEV void dq_store(const AttnK& a, int n, int hh, int q, const v4f* dq) {
 
 // dK/dV of the lane's key over queries [q0, q0+64): sL = log2-scaled lse (+inf past L -> P = 0), sDl = delta
 template <typename T, int HDP>
-DMC_DEV void dkdv_queries(const char* sQ, const char* sD, const float* sL, const float* sDl, const v4i* kf,
-                          const v4i* vf, float sl2, v4f* dk, v4f* dv) {
+DMC_DEV void dkdv_queries(const AttnK& a, const char* sQ, const char* sD, const float* sL, const float* sDl,
+                          const v4i* kf, const v4i* vf, float sl2, v4f* dk, v4f* dv, size_t ibase = 0,
+                          uint32_t seed = 0) {
   constexpr int KPL = TT<T>::KPL;
   constexpr int DC = HDP / (4 * KPL);
   constexpr int DT = HDP / 16;
@@ -302,8 +320,14 @@ DMC_DEV void dkdv_queries(const char* sQ, const char* sD, const float* sL, const
     for (int i = 0; i < 4; ++i) {
       const int qi = 16 * t + 4 * h + i;   // query (row) within the tile
       const float pv = exp2f(s[i] * sl2 - sL[qi]);
-      p[t][i] = pv;
-      ds[t][i] = pv * (dp[i] - sDl[qi]);
+      if (a.dthresh) {   // ibase = index of (tile query 0, this key): query qi adds qi * L
+        const float mk = attn_keep(a, seed, ibase + (size_t)qi * a.L);
+        p[t][i] = pv * mk;
+        ds[t][i] = pv * (dp[i] * mk - sDl[qi]);
+      } else {
+        p[t][i] = pv;
+        ds[t][i] = pv * (dp[i] - sDl[qi]);
+      }
     }
   }
 #pragma unroll
@@ -348,6 +372,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnK a) {
   const int nh = blockIdx.y, n = nh / a.heads, hh = nh % a.heads;
   const int C = a.heads * a.hd;
   const int q = blockIdx.x * 64 + wave * 16 + (threadIdx.x & 15);
+  const uint32_t seed = attn_seed(a);
   v4i qf[DC];
   load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, q, hh * a.hd, qf);
   float m = -INFINITY, lsum = 0.f;
@@ -359,7 +384,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnK a) {
     stage_tile<T, HDP>(a, a.qkv, a.ld_qkv, n, k0, C + hh * a.hd, sK);
     stage_tile<T, HDP>(a, a.qkv, a.ld_qkv, n, k0, 2 * C + hh * a.hd, sV);
     __syncthreads();
-    fwd_keys<T, HDP>(a, sK, sV, k0, qf, a.scale * kLog2e, m, lsum, o);
+    fwd_keys<T, HDP>(a, sK, sV, k0, qf, a.scale * kLog2e, m, lsum, o, ((size_t)nh * a.L + q) * a.L, seed);
   }
   fwd_store<T, HDP>(a, n, hh, q, m, lsum, o);
 }
@@ -375,6 +400,7 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnK a) {
   const int nh = blockIdx.y, n = nh / a.heads, hh = nh % a.heads;
   const int C = a.heads * a.hd;
   const int q = blockIdx.x * 64 + wave * 16 + (threadIdx.x & 15);
+  const uint32_t seed = attn_seed(a);
   v4i qf[DC], df[DC];
   load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, q, hh * a.hd, qf);
   load_tok_frags<T, DC>(a, a.dout, a.ld_o, n, q, hh * a.hd, df);
@@ -388,7 +414,7 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(AttnK a) {
     stage_tile<T, HDP>(a, a.qkv, a.ld_qkv, n, k0, C + hh * a.hd, sK);
     stage_tile<T, HDP>(a, a.qkv, a.ld_qkv, n, k0, 2 * C + hh * a.hd, sV);
     __syncthreads();
-    dq_keys<T, HDP>(a, sK, sV, k0, qf, df, a.scale * kLog2e, lse2, dl, dq);
+    dq_keys<T, HDP>(a, sK, sV, k0, qf, df, a.scale * kLog2e, lse2, dl, dq, ((size_t)nh * a.L + q) * a.L, seed);
   }
   dq_store<T, HDP>(a, n, hh, q, dq);
 }
@@ -405,6 +431,7 @@ __global__ __launch_bounds__(256) void attn_dkdv_kernel(AttnK a) {
   const int nh = blockIdx.y, n = nh / a.heads, hh = nh % a.heads;
   const int C = a.heads * a.hd;
   const int key = blockIdx.x * 64 + wave * 16 + (threadIdx.x & 15);
+  const uint32_t seed = attn_seed(a);
   v4i kf[DC], vf[DC];
   load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, key, C + hh * a.hd, kf);
   load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, key, 2 * C + hh * a.hd, vf);
@@ -421,7 +448,8 @@ __global__ __launch_bounds__(256) void attn_dkdv_kernel(AttnK a) {
       sDl[threadIdx.x] = qq < a.L ? a.delta[(size_t)nh * a.L + qq] : 0.f;
     }
     __syncthreads();
-    dkdv_queries<T, HDP>(sQ, sD, sL, sDl, kf, vf, a.scale * kLog2e, dk, dv);
+    dkdv_queries<T, HDP>(a, sQ, sD, sL, sDl, kf, vf, a.scale * kLog2e, dk, dv,
+                         ((size_t)nh * a.L + q0) * a.L + key, seed);
   }
   dkdv_store<T, HDP>(a, n, hh, key, dk, dv);
 }
@@ -443,6 +471,7 @@ __global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnK a, int HG, int 
   const int C = a.heads * a.hd;
   stage_rows2<T, HDP>(a, a.qkv, a.ld_qkv, C, a.qkv, a.ld_qkv, 2 * C, n, h0, HG, Lp, sK, sV);
   __syncthreads();
+  const uint32_t seed = attn_seed(a);
   const int tph = (a.L + 15) / 16;
   for (int tile = wave; tile < HG * tph; tile += 8) {
     const int g = tile / tph, hh = h0 + g;
@@ -455,8 +484,10 @@ __global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnK a, int HG, int 
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) o[dt] = v4f{0.f, 0.f, 0.f, 0.f};
     const size_t base = (size_t)g * Lp * PITCH;
+    const size_t mrow = (((size_t)n * a.heads + hh) * a.L + q) * a.L;
     for (int k0 = 0; k0 < a.L; k0 += 64)
-      fwd_keys<T, HDP>(a, sK + base + k0 * PITCH, sV + base + k0 * PITCH, k0, qf, a.scale * kLog2e, m, lsum, o);
+      fwd_keys<T, HDP>(a, sK + base + k0 * PITCH, sV + base + k0 * PITCH, k0, qf, a.scale * kLog2e, m, lsum, o, mrow,
+                       seed);
     fwd_store<T, HDP>(a, n, hh, q, m, lsum, o);
   }
 }
@@ -475,6 +506,7 @@ __global__ __launch_bounds__(512) void attn_dq_res_kernel(AttnK a, int HG, int L
   const int C = a.heads * a.hd;
   stage_rows2<T, HDP>(a, a.qkv, a.ld_qkv, C, a.qkv, a.ld_qkv, 2 * C, n, h0, HG, Lp, sK, sV);
   __syncthreads();
+  const uint32_t seed = attn_seed(a);
   const int tph = (a.L + 15) / 16;
   for (int tile = wave; tile < HG * tph; tile += 8) {
     const int g = tile / tph, hh = h0 + g;
@@ -491,7 +523,8 @@ __global__ __launch_bounds__(512) void attn_dq_res_kernel(AttnK a, int HG, int L
     for (int dt = 0; dt < DT; ++dt) dq[dt] = v4f{0.f, 0.f, 0.f, 0.f};
     const size_t base = (size_t)g * Lp * PITCH;
     for (int k0 = 0; k0 < a.L; k0 += 64)
-      dq_keys<T, HDP>(a, sK + base + k0 * PITCH, sV + base + k0 * PITCH, k0, qf, df, a.scale * kLog2e, lse2, dl, dq);
+      dq_keys<T, HDP>(a, sK + base + k0 * PITCH, sV + base + k0 * PITCH, k0, qf, df, a.scale * kLog2e, lse2, dl, dq,
+                      (nh * a.L + q) * a.L, seed);
     dq_store<T, HDP>(a, n, hh, q, dq);
   }
 }
@@ -511,6 +544,7 @@ __global__ __launch_bounds__(512) void attn_dkdv_res_kernel(AttnK a, int HG, int
   const int n = blockIdx.x / groups, h0 = (blockIdx.x - n * groups) * HG;
   const int C = a.heads * a.hd;
   stage_rows2<T, HDP>(a, a.qkv, a.ld_qkv, 0, a.dout, a.ld_o, 0, n, h0, HG, Lp, sQ, sD);
+  const uint32_t seed = attn_seed(a);
   if (threadIdx.x < kResRows) {
     const int g = threadIdx.x / Lp, tok = threadIdx.x - g * Lp;
     const bool ok = g < HG && h0 + g < a.heads && tok < a.L;
@@ -531,9 +565,10 @@ __global__ __launch_bounds__(512) void attn_dkdv_res_kernel(AttnK a, int HG, int
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) { dk[dt] = v4f{0.f, 0.f, 0.f, 0.f}; dv[dt] = v4f{0.f, 0.f, 0.f, 0.f}; }
     const int row0 = g * Lp;
+    const size_t nhl = ((size_t)n * a.heads + hh) * a.L;
     for (int q0 = 0; q0 < a.L; q0 += 64)
-      dkdv_queries<T, HDP>(sQ + (size_t)(row0 + q0) * PITCH, sD + (size_t)(row0 + q0) * PITCH, sL + row0 + q0,
-                           sDl + row0 + q0, kf, vf, a.scale * kLog2e, dk, dv);
+      dkdv_queries<T, HDP>(a, sQ + (size_t)(row0 + q0) * PITCH, sD + (size_t)(row0 + q0) * PITCH, sL + row0 + q0,
+                           sDl + row0 + q0, kf, vf, a.scale * kLog2e, dk, dv, (nhl + q0) * a.L + key, seed);
     dkdv_store<T, HDP>(a, n, hh, key, dk, dv);
   }
 }
@@ -594,11 +629,13 @@ int check(int dtype, int ld_qkv, int heads, int hd, int ld_out) {
 }  // namespace
 
 extern "C" int dmc_attn_fwd(int dtype, const void* qkv, int ld_qkv, int N, int L, int heads, int hd, void* out, int ld_out,
-                            float* lse, void* stream) {
+                            float* lse, uint32_t drop_seed, const uint32_t* drop_seed_base, uint32_t drop_thresh,
+                            float drop_scale, void* stream) {
   if (check(dtype, ld_qkv, heads, hd, ld_out)) return 1;
   AttnK a{};
   a.qkv = (const char*)qkv; a.ld_qkv = ld_qkv; a.out = (char*)out; a.ld_out = ld_out; a.lse_out = lse;
   a.N = N; a.L = L; a.heads = heads; a.hd = hd; a.scale = 1.0f / sqrtf((float)hd);
+  a.dseed = drop_seed; a.dseed_base = drop_seed_base; a.dthresh = drop_thresh; a.dscale = drop_scale;
   if (N == 0 || L == 0) return 0;
   hipStream_t s = dmc::as_stream(stream);
   return dtype == DMC_F32 ? dispatch<float>(true, a, nullptr, s) : dispatch<bf16_t>(true, a, nullptr, s);
@@ -608,13 +645,15 @@ extern "C" size_t dmc_attn_workspace(int N, int L, int heads) { return (size_t)N
 
 extern "C" int dmc_attn_bwd(int dtype, const void* qkv, int ld_qkv, const void* out, const void* dout, int ld_out,
                             const float* lse, int N, int L, int heads, int hd, void* dqkv, int ld_dqkv, void* workspace,
-                            void* stream) {
+                            uint32_t drop_seed, const uint32_t* drop_seed_base, uint32_t drop_thresh,
+                            float drop_scale, void* stream) {
   if (check(dtype, ld_qkv, heads, hd, ld_out)) return 1;
   DMC_REQUIRE(ld_dqkv >= 3 * heads * hd, "attn_bwd: ld_dqkv");
   AttnK a{};
   a.qkv = (const char*)qkv; a.ld_qkv = ld_qkv; a.o = (const char*)out; a.dout = (const char*)dout; a.ld_o = ld_out;
   a.lse = lse; a.out = (char*)dqkv; a.ld_out = ld_dqkv;
   a.N = N; a.L = L; a.heads = heads; a.hd = hd; a.scale = 1.0f / sqrtf((float)hd);
+  a.dseed = drop_seed; a.dseed_base = drop_seed_base; a.dthresh = drop_thresh; a.dscale = drop_scale;
   if (N == 0 || L == 0) return 0;
   hipStream_t s = dmc::as_stream(stream);
   return dtype == DMC_F32 ? dispatch<float>(false, a, (float*)workspace, s)

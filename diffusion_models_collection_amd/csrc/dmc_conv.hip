@@ -2311,12 +2311,20 @@ __global__ __launch_bounds__(512) void wgrad3x3_halo_kernel(ConvK a, const char*
       v4i fa[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) fa[i] = tr_frag<256, true>(D, ks * 32 + 8 * fh, wm * 4 + i);
+      // x fragments one n tile ahead: tile u+1's two transposed reads are in flight while tile u's four MFMAs
+      // run (left alone, hipcc waits for each fragment right before its MFMAs: lgkmcnt(0) every 4 MFMAs)
+      v4i fb = tr_frag<128, false>(X, hb0 + hj + dl[0], (wq * 9) & 3);
 #pragma unroll
       for (int u = 0; u < 9; ++u) {
-        const int nt = wq * 9 + u;
-        const v4i fb = tr_frag<128, false>(X, hb0 + hj + dl[u], nt & 3);
+        v4i fn = fb;
+        if (u + 1 < 9) fn = tr_frag<128, false>(X, hb0 + hj + dl[u + 1], (wq * 9 + u + 1) & 3);
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i][u] = mma16<T>(acc[i][u], fa[i], fb);
+        if (u + 1 < 9) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the next tile's reads
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // this tile's MFMAs
+        }
+        fb = fn;
       }
     }
   }

@@ -273,15 +273,18 @@ def channel_sum(dtype, dy, N, HW, C, ld, out_nc=None, ld_out=0, out_c=None, scal
                                   scale, ptr(ws), L.stream()), "dmc_channel_sum")
 
 
-def attn_fwd(dtype, qkv, ld_qkv, N, Lq, heads, hd, out, ld_out, lse):
-    check(LIB.dmc_attn_fwd(L.dtype_code(dtype), ptr(qkv), ld_qkv, N, Lq, heads, hd, ptr(out), ld_out, ptr(lse),
-                           L.stream()), "dmc_attn_fwd")
+def attn_fwd(dtype, qkv, ld_qkv, N, Lq, heads, hd, out, ld_out, lse, drop=None):
+    """drop = (seed, thresh, scale[, seed_base]): attention-probability dropout (kernels.drop_args)."""
+    seed, base, thresh, scale = drop_args(drop)
+    check(LIB.dmc_attn_fwd(L.dtype_code(dtype), ptr(qkv), ld_qkv, N, Lq, heads, hd, ptr(out), ld_out, ptr(lse), seed,
+                           base, thresh, scale, L.stream()), "dmc_attn_fwd")
 
 
-def attn_bwd(dtype, qkv, ld_qkv, out, dout, ld_out, lse, N, Lq, heads, hd, dqkv, ld_dqkv):
+def attn_bwd(dtype, qkv, ld_qkv, out, dout, ld_out, lse, N, Lq, heads, hd, dqkv, ld_dqkv, drop=None):
     ws = SCRATCH.get(LIB.dmc_attn_workspace(N, Lq, heads), qkv.device)
+    seed, base, thresh, scale = drop_args(drop)
     check(LIB.dmc_attn_bwd(L.dtype_code(dtype), ptr(qkv), ld_qkv, ptr(out), ptr(dout), ld_out, ptr(lse), N, Lq, heads,
-                           hd, ptr(dqkv), ld_dqkv, ptr(ws), L.stream()), "dmc_attn_bwd")
+                           hd, ptr(dqkv), ld_dqkv, ptr(ws), seed, base, thresh, scale, L.stream()), "dmc_attn_bwd")
 
 
 def time_embed(t, dim, out):

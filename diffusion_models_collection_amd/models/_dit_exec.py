@@ -8,7 +8,7 @@ implicit-GEMM conv (dmc_conv2d, MFMA) and the patch embedding the 2x2 stride-2 c
   patch conv (fp32) + pos_embed                                                          = x   (fp32 stream)
   per block:  h1 = LN(x) * (1 + scale_msa) + shift_msa            (dmc_ln_mod_fwd, fused with the previous
                                                                    block's gated MLP residual)
-              qkv = h1 W_in^T + b -> flash attention -> o W_out^T + b = ao
+              qkv = h1 W_in^T + b -> flash attention (probability dropout in training) -> o W_out^T + b = ao
               x_mid = x + gate_msa * ao;  h2 = LN(x_mid) * (1 + scale_mlp) + shift_mlp   (one fused kernel)
               u = h2 W1^T + b1 -> a = Dropout(GELU(u)) -> mo = a W2^T + b2   (x_out = x_mid + gate_mlp * drop(mo)
                                                                               folded into the next LayerNorm)
@@ -235,7 +235,8 @@ class DiTExecutor(ExecCore):
             self._conv([A], self.in_proj[i], K.TAPS1, ht, wt, 3 * H, bias=blk.attn.in_proj_bias, out=qkv.t)
             o = self._new(B, ht, wt, H)
             lse = torch.empty(B * heads * Lt, dtype=f32, device=x.device)
-            K.attn_fwd(dt, qkv.t, 3 * H, B, Lt, heads, hd, o.t, H, lse)
+            d0 = self._drop(2 * len(self.blocks) + i)      # attention-probability dropout (MHA dropout=p)
+            K.attn_fwd(dt, qkv.t, 3 * H, B, Lt, heads, hd, o.t, H, lse, drop=d0)
             ao = self._new(B, ht, wt, H)
             self._conv([o], blk.attn.out_proj, K.TAPS1, ht, wt, H, bias=blk.attn.out_proj.bias, out=ao.t)
             x_mid, h2, mean2, rstd2 = ln(x_in, ao.t, mo_ + 2 * H, mo_ + 3 * H, mo_ + 4 * H, None)
@@ -255,7 +256,7 @@ class DiTExecutor(ExecCore):
             d2 = self._drop(2 * i + 1)
             if keep:
                 tape.append(("block", i, x_in, h1, mean1, rstd1, qkv, o, lse, ao, x_mid, h2, mean2, rstd2, u, a, mo,
-                             d1, d2))
+                             d1, d2, d0))
             xcur = x_mid
             pend = (mo.t, mo_ + 5 * H, d2)
         # ---- final layer ----
@@ -325,7 +326,7 @@ class DiTExecutor(ExecCore):
 
         # ---- blocks, last to first ----
         for rec in reversed(tape[1:-1]):
-            (_, i, x_in, h1, mean1, rstd1, qkv, o, lse, ao, x_mid, h2, mean2, rstd2, u, a, mo, d1, d2) = rec
+            (_, i, x_in, h1, mean1, rstd1, qkv, o, lse, ao, x_mid, h2, mean2, rstd2, u, a, mo, d1, d2, d0) = rec
             blk = self.blocks[i]
             mo_ = self.ada_off[i]
             Hm = blk.mlp[0].out_features
@@ -353,7 +354,7 @@ class DiTExecutor(ExecCore):
             do = torch.empty(B, ht, wt, H, dtype=dt, device=dev)
             self._conv([Act(dao, ht, wt, H)], op, K.TAPS1, ht, wt, H, out=do, packmode=L.PACK_DGRAD)
             dqkv = torch.empty(B, ht, wt, 3 * H, dtype=dt, device=dev)
-            K.attn_bwd(dt, qkv.t, 3 * H, o.t, do, H, lse, B, Lt, heads, hd, dqkv, 3 * H)
+            K.attn_bwd(dt, qkv.t, 3 * H, o.t, do, H, lse, B, Lt, heads, hd, dqkv, 3 * H, drop=d0)
             self._wgrad([Act(h1, ht, wt, H)], dqkv, 3 * H, K.TAPS1, ht, wt, 3 * H, gv(blk.attn.in_proj_weight))
             K.channel_sum(dt, dqkv, B, Lt, 3 * H, 3 * H, out_c=gv(blk.attn.in_proj_bias))
             dh1 = torch.empty(B, ht, wt, H, dtype=dt, device=dev)

@@ -13,8 +13,9 @@ layer's stacked into one GEMM) on the implicit-GEMM kernels, the attention on th
 gated residuals + LayerNorm + modulation, GELU, timestep embedding and unpatchify in fused token-wise kernels.
 
 Extra (optional) constructor argument: compute_dtype = "fp32" | "bf16" (as models/unet.py).
-Attention-probability dropout (nn.MultiheadAttention(dropout=...) in training mode) is not implemented on the HIP
-path: a DiT in training mode with dropout > 0 raises (in eval mode every dropout is inactive, as in the reference).
+Dropout in training mode: the attention-probability dropout of nn.MultiheadAttention (inside the flash-attention
+kernels, dmc_attn_fwd/bwd) and the two MLP dropouts (in the GELU and gated-residual kernels), each with a counter-hash
+mask recomputed in the backward; the masks are not torch's RNG stream (statistically equivalent, not bitwise).
 """
 import math
 from typing import Tuple
@@ -190,10 +191,6 @@ class DiT(nn.Module):
     def forward(self, x, t, y=None):
         if not x.is_cuda:
             raise RuntimeError("DiT runs on the MI355X HIP kernels only: move the model and inputs to a cuda device")
-        if self.training and self.dropout > 0:
-            raise NotImplementedError(
-                "DiT: attention-probability dropout (nn.MultiheadAttention dropout > 0 in training mode) is not "
-                "implemented on the HIP path; construct DiT(dropout=0.0) for training, or call model.eval()")
         return self.executor.run(x, t, y if self.num_classes is not None else None)
 
     def __getstate__(self):

@@ -170,12 +170,18 @@ int dmc_channel_sum(int dtype, const void* dy, int N, int HW, int C, int ld, flo
  * which*C + head*hd + d (reshape(B,3,heads,hd,HW)), softmax(QK^T/sqrt(hd))V -> out [N][L][ld_out]
  * channel head*hd + d; lse [N][heads][L] fp32 saved for backward. */
 int dmc_attn_fwd(int dtype, const void* qkv, int ld_qkv, int N, int L, int heads, int hd, void* out,
-                 int ld_out, float* lse, void* stream);
-/* dqkv [N][L][ld_dqkv] (overwritten). workspace: dmc_attn_workspace() bytes. */
+                 int ld_out, float* lse, uint32_t drop_seed, const uint32_t* drop_seed_base,
+                 uint32_t drop_thresh, float drop_scale, void* stream);
+/* dqkv [N][L][ld_dqkv] (overwritten). workspace: dmc_attn_workspace() bytes.
+ * Attention-probability dropout (nn.MultiheadAttention(dropout=p) in training; the DiT blocks, dit.py:94):
+ * drop_thresh != 0 keeps P[n,h][q][key] iff hash(seed, ((n*heads + h)*L + q)*L + key) >= drop_thresh and scales it
+ * by drop_scale = 1/(1-p) in O = P V (lse stays that of the undropped softmax); the backward takes the same
+ * arguments and recomputes the mask. drop_thresh = 0: no dropout (the UNet). */
 size_t dmc_attn_workspace(int N, int L, int heads);
 int dmc_attn_bwd(int dtype, const void* qkv, int ld_qkv, const void* out, const void* dout,
                  int ld_out, const float* lse, int N, int L, int heads, int hd, void* dqkv,
-                 int ld_dqkv, void* workspace, void* stream);
+                 int ld_dqkv, void* workspace, uint32_t drop_seed, const uint32_t* drop_seed_base,
+                 uint32_t drop_thresh, float drop_scale, void* stream);
 
 /* Sinusoidal TimeEmbedding (models/unet.py:18-25): out [B][dim] fp32 = [sin(t f_i) | cos(t f_i)]. */
 int dmc_time_embed(const int64_t* t, int B, int dim, float* out, void* stream);

@@ -41,7 +41,7 @@ def test_descriptor_validation_errors():
         L.check(L.LIB.dmc_conv2d(__import__("ctypes").byref(d), None, None, None, None, None, None, 0, None),
                     "conv")
     with pytest.raises(L.DMCError, match="head dim"):
-        L.check(L.LIB.dmc_attn_fwd(0, None, 768, 1, 16, 4, 100, None, 256, None, None), "attn")
+        L.check(L.LIB.dmc_attn_fwd(0, None, 768, 1, 16, 4, 100, None, 256, None, 0, None, 0, 1.0, None), "attn")
 
 
 def test_schedule_op_sequence_reproduces_fixture():

@@ -179,13 +179,67 @@ def test_dit_train_step_grads_match_oracle():
         assert rel(p.grad, sd[k].grad) < 5e-4, (k, rel(p.grad, sd[k].grad))
 
 
-def test_dit_training_mode_attention_dropout_raises():
+def test_dit_training_with_dropout_graphed_matches_eager(monkeypatch):
+    """The reference DiT config trains with dropout 0.1 (configs/cifar10_dit.py): attention-probability dropout in
+    the flash kernels plus both MLP dropouts. Over 4 DiffusionTrainer steps (bf16, conditional, EMA) the losses are
+    finite and the HIP-graph step (dropout seed read from device memory per replay) equals the eager step bitwise;
+    eval mode switches every dropout off (deterministic output)."""
     from diffusion_models_collection_amd.models import DiT
-    m = DiT(**{**DIT["dit_tiny_cond"], "dropout": 0.1}).to(DEV).train()
+    from diffusion_models_collection_amd.diffusion import DDPM
+    from diffusion_models_collection_amd.utils.trainer import DiffusionTrainer
+    mp = dict(DIT["dit_tiny_cond"], dropout=0.1)
+    mp.pop("num_classes")
+
+    def run(graph):
+        monkeypatch.setenv("DMC_GRAPH", "1" if graph else "0")
+        torch.manual_seed(0)
+        torch.cuda.manual_seed(0)
+        m = DiT(**mp, num_classes=10, compute_dtype="bf16").to(DEV)
+        opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4)
+        cfg = {"epochs": 1, "save_dir": "/tmp/dmc_ditd_ckpt", "sample_dir": "/tmp/dmc_ditd_smp", "loss_type": "l2",
+               "use_ema": True, "ema_decay": 0.99, "conditional": True, "num_classes": 10, "cfg_dropout_prob": 0.2,
+               "model_type": "dit", "model_params": dict(mp)}
+        tr = DiffusionTrainer(m, DDPM(device=DEV), None, opt, None, device=DEV, config=cfg)
+        m.train()
+        gen = torch.Generator().manual_seed(5)
+        losses = []
+        for i in range(4):
+            x = (torch.rand(8, 3, 16, 16, generator=gen) * 2 - 1).to(DEV)
+            losses.append(tr.train_step((x, torch.randint(0, 10, (8,), generator=gen).to(DEV)), i).detach().float()
+                          .cpu().reshape(()))
+        torch.cuda.synchronize()
+        return torch.stack(losses), {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}, m, tr
+
+    le, se, m, _ = run(False)
+    lg, sg, _, trg = run(True)
+    assert torch.isfinite(le).all()
+    assert trg._graph is not None and trg._graph.graph is not None and not trg._graph.failed
+    assert torch.equal(le, lg), (le, lg)
+    for k in se:
+        assert torch.equal(se[k], sg[k]), k
+    m.eval()
     x = torch.randn(2, 3, 16, 16, device=DEV)
     t = torch.tensor([1, 2], device=DEV)
-    with pytest.raises(NotImplementedError):
-        m(x, t, None)
-    m.eval()
     with torch.no_grad():
-        assert torch.isfinite(m(x, t, None)).all()      # eval: every dropout inactive
+        assert torch.equal(m(x, t, None), m(x, t, None))
+
+
+def test_dit_dropout_mask_matches_eval_when_zero():
+    """With dropout active the training-mode forward differs from eval mode, and the two MLP masks and the
+    attention mask change with the torch seed (torch.manual_seed drives the per-step mask seed)."""
+    from diffusion_models_collection_amd.models import DiT
+    torch.manual_seed(1)
+    m = DiT(**{**DIT["dit_tiny_cond"], "dropout": 0.3}).to(DEV)
+    x = torch.randn(2, 3, 16, 16, device=DEV)
+    t = torch.tensor([5, 600], device=DEV)
+    with torch.no_grad():
+        m.eval()
+        e = m(x, t, None)
+        m.train()
+        torch.manual_seed(7)
+        a = m(x, t, None)
+        torch.manual_seed(7)
+        b = m(x, t, None)
+        torch.manual_seed(8)
+        c = m(x, t, None)
+    assert torch.equal(a, b) and not torch.equal(a, c) and not torch.equal(a, e)

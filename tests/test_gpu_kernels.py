@@ -464,6 +464,65 @@ def test_attention_fwd_bwd(dt, Lq, hd, path, monkeypatch, dmc_opt):
     assert rel_err(dq.float().cpu(), qkv.grad) < (2e-4 if dt == torch.float32 else 5e-2)
 
 
+def _hash_u32(x, seed):
+    """csrc/dmc_common.h hash_u32 in numpy uint32 arithmetic (test-side reconstruction of the dropout mask)."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        x = (x ^ np.uint32(seed)).astype(np.uint32)
+        x = (x * np.uint32(0x9E3779B1)).astype(np.uint32); x ^= x >> np.uint32(16)
+        x = (x * np.uint32(0x85EBCA6B)).astype(np.uint32); x ^= x >> np.uint32(13)
+        x = (x * np.uint32(0xC2B2AE35)).astype(np.uint32); x ^= x >> np.uint32(16)
+    return x
+
+
+def drop_keep_np(idx, seed, thresh):
+    """dmc_common.h drop_keep over an int64 index array (low 32 bits, seed mix of drop_seed_mix)."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        mix = _hash_u32(np.zeros(1, np.uint32), np.uint32((seed * 0x27d4eb2f + 1) & 0xFFFFFFFF))[0]
+    return _hash_u32((idx.astype(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.uint32) ^ mix, seed) >= np.uint32(thresh)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("path", ["auto", "staged"])
+@pytest.mark.parametrize("Lq", [64, 256, 320])
+def test_attention_probability_dropout(dt, path, Lq, dmc_opt):
+    """Attention-probability dropout (dmc_attn_fwd/bwd drop_* arguments, the DiT's nn.MultiheadAttention(dropout=p)):
+    O = (softmax(QK^T/sqrt(hd)) * M / (1-p)) V with the counter-hash mask M[(n*heads+h)*L+q)*L+key] rebuilt on the
+    host, forward and the q/k/v gradients vs torch autograd of that formula."""
+    import numpy as np
+    L, K = _lib()
+    dmc_opt("DMC_ATTN_STAGED", 1 if path == "staged" else 0)
+    torch.manual_seed(4)
+    N, heads, hd = 2, 3, 64
+    C = heads * hd
+    p_drop, seed = 0.25, 12345
+    thresh = int(round(p_drop * 4294967296.0))
+    scale = 1.0 / (1.0 - p_drop)
+    idx = np.arange(N * heads * Lq * Lq, dtype=np.int64)
+    mask = torch.from_numpy(drop_keep_np(idx, seed, thresh).reshape(N, heads, Lq, Lq).astype(np.float32))
+    assert 0.7 < mask.mean().item() < 0.8
+    qkv = q(torch.randn(N, Lq, 3 * C), dt).requires_grad_(True)
+    t = qkv.view(N, Lq, 3, heads, hd).permute(2, 0, 3, 1, 4)
+    qq, kk, vv = t[0], t[1], t[2]
+    pr = torch.softmax(qq @ kk.transpose(-2, -1) / math.sqrt(hd), -1)
+    o = ((pr * mask * scale) @ vv).permute(0, 2, 1, 3).reshape(N, Lq, C)
+    do = q(torch.randn_like(o), dt)
+    o.backward(do)
+    qd = qkv.detach().to(dt).to(DEV).contiguous()
+    od = torch.empty(N, Lq, C, dtype=dt, device=DEV)
+    lse = torch.empty(N * heads * Lq, device=DEV)
+    drop = (seed, thresh, scale)
+    K.attn_fwd(dt, qd, 3 * C, N, Lq, heads, hd, od, C, lse, drop=drop)
+    dq = torch.empty_like(qd)
+    K.attn_bwd(dt, qd, 3 * C, od, do.to(dt).to(DEV), C, lse, N, Lq, heads, hd, dq, 3 * C, drop=drop)
+    torch.cuda.synchronize()
+    lim = 1e-4 if dt == torch.float32 else 3e-2
+    assert rel_err(od.float().cpu(), o.detach()) < lim, rel_err(od.float().cpu(), o.detach())
+    assert rel_err(dq.float().cpu(), qkv.grad) < (2e-4 if dt == torch.float32 else 5e-2), rel_err(dq.float().cpu(),
+                                                                                                      qkv.grad)
+
+
 def test_elementwise_and_multitensor():
     L, K = _lib()
     torch.manual_seed(4)
