@@ -250,8 +250,8 @@ def dit_lines(args, dev, rank, world, B):
     """BASELINE config #4: DiT-S/2 (conditional, 10 classes) DDIM-50 + CFG 3.0 sampling img/s, replicas (each rank
     samples its own B images; the cond and null-label rows run as ONE 2B forward per step). The roofline is the
     whole sampling loop's MFMA work: DiT forward FLOPs (linears, patch conv, attention matmuls) x 2B rows x 50
-    steps / measured seconds, vs the dense bf16 peak. Also the DiT train step img/s (dropout 0: attention-
-    probability dropout is not implemented on the HIP path, see models/dit.py)."""
+    steps / measured seconds, vs the dense bf16 peak. Also the DiT train step img/s with the reference config's
+    dropout 0.1."""
     from diffusion_models_collection_amd.models import DiT
     from diffusion_models_collection_amd.models._dit_exec import dit_flops_per_image
     from diffusion_models_collection_amd.diffusion import DDIM, DDPM
@@ -271,11 +271,11 @@ def dit_lines(args, dev, rank, world, B):
                         "frac": round(tfs / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
                         "scope": "whole DDIM-50 CFG loop per GPU"}}
     if not args.no_train:
-        mt = DiT(**DIT_S2, num_classes=10, dropout=0.0, compute_dtype=args.dtype).to(dev)
+        mt = DiT(**DIT_S2, num_classes=10, dropout=0.1, compute_dtype=args.dtype).to(dev)
         opt = torch.optim.AdamW(mt.parameters(), lr=1e-4, weight_decay=1e-4)
         cfg = {"epochs": 1, "save_dir": "/tmp/dmc_bench_ckpt", "sample_dir": "/tmp/dmc_bench_smp", "loss_type": "l2",
                "use_ema": True, "ema_decay": 0.9999, "model_type": "dit", "conditional": True, "num_classes": 10,
-               "cfg_dropout_prob": 0.2, "model_params": dict(DIT_S2, dropout=0.0)}
+               "cfg_dropout_prob": 0.2, "model_params": dict(DIT_S2, dropout=0.1)}
         tr = DiffusionTrainer(mt, DDPM(device=dev), None, opt, None, device=dev, config=cfg, rank=rank,
                               world_size=world)
         gen = torch.Generator(device=dev).manual_seed(77 + rank)
@@ -286,7 +286,8 @@ def dit_lines(args, dev, rank, world, B):
         res["train_img_s"] = round(world * B * 10 / et, 2)
         res["train_ms_per_step"] = round(et / 10 * 1e3, 3)
         res["train_tflops_per_gpu"] = round(B * 10 / et * 3 * gf / 1e3, 2)
-        res["train_note"] = "conditional, CFG label dropout 0.2, EMA, dropout 0 (fwd+bwd = 3x forward FLOPs)"
+        res["train_note"] = ("configs/cifar10_dit.py dropout 0.1 (attention-probability + MLP dropouts), conditional, "
+                             "CFG label dropout 0.2, EMA (fwd+bwd = 3x forward FLOPs)")
     return res
 
 
