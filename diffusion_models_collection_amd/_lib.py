@@ -24,6 +24,7 @@ _c_int, _c_p, _c_f, _c_u32, _c_long, _c_size = (ctypes.c_int, ctypes.c_void_p, c
 
 
 ACT_NONE, ACT_GELU = 0, 1   # include/dmc.h DMC_ACT_*
+FUSED_GN_STATS, FUSED_GN_BWD = 1, 2   # dmc_conv2d_fused_epilogue bits
 
 
 class ConvDesc(ctypes.Structure):
@@ -38,7 +39,17 @@ class ConvDesc(ctypes.Structure):
         ("bias", _c_p), ("addvec", _c_p), ("ld_add", _c_int), ("resid", _c_p), ("ld_res", _c_int),
         ("silu_pre", _c_p), ("ld_silu", _c_int), ("Csplit", _c_int), ("ldy1", _c_int), ("ldy2", _c_int),
         ("out_f32", _c_int), ("out_nchw", _c_int), ("act", _c_int), ("y_pre", _c_p), ("ld_pre", _c_int),
-        ("gn_part", _c_p),
+        ("gnb", _c_p), ("gn_part", _c_p),
+    ]
+
+
+class GnBwdEpi(ctypes.Structure):
+    """include/dmc.h dmc_gn_bwd_epi: GroupNorm-backward partial sums from an input-gradient conv's epilogue."""
+    _fields_ = [
+        ("x1", _c_p), ("x2", _c_p), ("C1", _c_int), ("ld1", _c_int), ("ld2", _c_int),
+        ("mean_rstd", _c_p), ("gamma", _c_p), ("beta", _c_p), ("G", _c_int), ("silu", _c_int),
+        ("drop_seed", _c_u32), ("drop_seed_base", _c_p), ("drop_thresh", _c_u32), ("drop_scale", _c_f),
+        ("part", _c_p),
     ]
 
 
@@ -65,6 +76,7 @@ def _load():
         "dmc_last_error": (ctypes.c_char_p, []),
         "dmc_conv2d_workspace": (_c_size, [ctypes.POINTER(ConvDesc)]),
         "dmc_conv_halo_prologue": (_c_int, [ctypes.POINTER(ConvDesc)]),
+        "dmc_conv2d_fused_epilogue": (_c_int, [ctypes.POINTER(ConvDesc), ctypes.c_size_t]),
         "dmc_conv2d": (_c_int, [ctypes.POINTER(ConvDesc), _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_size, _c_p]),
         "dmc_conv2d_wgrad_workspace": (_c_size, [ctypes.POINTER(ConvDesc)]),
         "dmc_conv2d_wgrad": (_c_int, [ctypes.POINTER(ConvDesc), _c_p, _c_int, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p]),
@@ -80,7 +92,8 @@ def _load():
                                   _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_int, _c_p]),
         "dmc_gn_silu_bwd": (_c_int, [_c_int, _c_p, _c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int,
                                      _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_p,
-                                     _c_int, _c_int, _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_p, _c_p, _c_p]),
+                                     _c_int, _c_int, _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_p, _c_p, _c_p,
+                                     _c_p]),
         "dmc_channel_sum_workspace": (_c_size, [_c_int, _c_int, _c_int]),
         "dmc_channel_sum": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_p, _c_int, _c_p, _c_f, _c_p,
                                      _c_p]),

@@ -26,6 +26,8 @@ struct ConvK {
   int Csplit, ldy1, ldy2, out_f32, out_nchw;
   int act; char* ypre; int ldpre;   // DMC_ACT_GELU epilogue (+ optional pre-activation copy)
   float* gst;  // GroupNorm partials from the epilogue: [M/64][Cout/8] x (mean, M2) (nullptr: off)
+  int gb_on;   // GroupNorm-backward partials from the epilogue (dmc_gn_bwd_epi in gb)
+  dmc_gn_bwd_epi gb;
   int M;      // N*OH*OW output pixels
   int OHW;    // OH*OW
   float* sk;  // split-K partial slab (nullptr: no split)
@@ -327,6 +329,15 @@ DMC_DEV void conv_store_tile(const ConvK& a, const v4f accv, const int pix, cons
 // every residual load issued up front, and the embedding row is reloaded only when the image changes, so the
 // store phase pays one global round trip instead of one per row (it runs with no other block on the CU to
 // hide it).
+// dL/dz of one element of dropout(SiLU(GroupNorm(x))) from g = dL/d(output) (dmc_norm.hip gn_dz, same ops)
+DMC_DEV float gnb_dz(float x, float gv, float mean, float rstd, float gm, float bt, float& xhat, int silu) {
+  xhat = (x - mean) * rstd;
+  if (!silu) return gv;
+  const float z = fmaf(xhat, gm, bt);
+  const float sg = sigmoid_f(z);
+  return gv * sg * (1.f + z * (1.f - sg));
+}
+
 // Chan's combination of two (mean, M2) partials of equal count n: the count doubles.
 DMC_DEV void chan_eq(float& m, float& q, float mb, float qb, float n) {
   const float d = mb - m;
@@ -348,6 +359,35 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
   float gm[NSEG], gq[NSEG];
 #pragma unroll
   for (int j = 0; j < NSEG; ++j) { gm[j] = 0.f; gq[j] = 0.f; }
+  // GroupNorm backward (a.gb_on): per (segment, channel) sums of dz and dz * xhat, dz recomputed from the GroupNorm
+  // input x (loaded up front, one 16-byte chunk per row) exactly as dmc_gn_silu_bwd does
+  float gs1[NSEG][8], gs2[NSEG][8];
+  v4i xr[IT];
+  float bgm[8], bbt[8];
+  int bG = 1, bcpg = 1;
+  if (a.gb_on) {
+#pragma unroll
+    for (int j = 0; j < NSEG; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { gs1[j][e] = 0.f; gs2[j][e] = 0.f; }
+    const bool in1 = co < a.gb.C1;
+    const char* xb = in1 ? (const char*)a.gb.x1 : (const char*)a.gb.x2;
+    const int xld = in1 ? a.gb.ld1 : a.gb.ld2, xc = in1 ? co : co - a.gb.C1;
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const int pix = min(m0 + r0 + k * RS, a.M - 1);
+      xr[k] = *(const v4i*)(xb + ((size_t)pix * xld + xc) * 2);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bgm[e] = a.gb.gamma ? a.gb.gamma[co + e] : 1.f;
+      bbt[e] = a.gb.beta ? a.gb.beta[co + e] : 0.f;
+    }
+    bG = a.gb.G;
+    bcpg = a.Cout / bG;
+  }
+  const uint32_t bseed = (a.gb_on && a.gb.drop_thresh)
+                             ? a.gb.drop_seed + (a.gb.drop_seed_base ? *a.gb.drop_seed_base : 0u) : 0u;
   v4f b0 = {0.f, 0.f, 0.f, 0.f}, b1 = {0.f, 0.f, 0.f, 0.f};
   if (a.bias) { b0 = *(const v4f*)(a.bias + co); b1 = *(const v4f*)(a.bias + co + 4); }
   const bool first = co < a.Csplit;
@@ -396,6 +436,28 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
       }
       const v4i out = Chunk<bf16_t>::pack(f);
       *(v4i*)(y + ((size_t)pix * ldy + cy) * 2) = out;
+      if (a.gb_on) {
+        float gv[8], xv[8];
+        Chunk<bf16_t>::unpack(out, gv);
+        Chunk<bf16_t>::unpack(xr[k], xv);
+        const int nimg = pix / a.OHW, grp = co / bcpg;
+        const float mean = a.gb.mean_rstd[((size_t)nimg * bG + grp) * 2];
+        const float rstd = a.gb.mean_rstd[((size_t)nimg * bG + grp) * 2 + 1];
+#pragma unroll
+        for (int j = 0; j < NSEG; ++j) {
+          if (j != k / KPS) continue;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float g = gv[e];
+            if (a.gb.drop_thresh)
+              g = drop_keep((uint64_t)pix * a.Cout + co + e, bseed, a.gb.drop_thresh) ? g * a.gb.drop_scale : 0.f;
+            float xh;
+            const float dz = gnb_dz(xv[e], g, mean, rstd, bgm[e], bbt[e], xh, a.gb.silu);
+            gs1[j][e] += dz;
+            gs2[j][e] = fmaf(dz, xh, gs2[j][e]);
+          }
+        }
+      }
       if (a.gst) {
         float g[8];
         Chunk<bf16_t>::unpack(out, g);
@@ -420,10 +482,45 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
       }
     }
   }
+  if (a.gb_on) {
+    // lanes with the same chunk (xor 16, 32), then waves through LDS past the epilogue tile, in fixed order
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int NW = NT / 64;
+#pragma unroll
+    for (int sh = 16; sh < 64; sh <<= 1)
+#pragma unroll
+      for (int j = 0; j < NSEG; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { gs1[j][e] += __shfl_xor(gs1[j][e], sh); gs2[j][e] += __shfl_xor(gs2[j][e], sh); }
+    float* red = (float*)(lds + BM * EP);            // [NW][NSEG][CG][16]
+    if (lane < CG) {
+#pragma unroll
+      for (int j = 0; j < NSEG; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          red[((wave * NSEG + j) * CG + lane) * 16 + e] = gs1[j][e];
+          red[((wave * NSEG + j) * CG + lane) * 16 + 8 + e] = gs2[j][e];
+        }
+    }
+    __syncthreads();
+    // the thread of chunk cg (live: co < Cout) finishes (segment, channel) items r0, r0 + RS, ... of that chunk
+    for (int q = r0; q < NSEG * 8; q += RS) {
+      const int j = q / 8, c = cg, e = q % 8;
+      float v1 = 0.f, v2 = 0.f;
+      for (int w = 0; w < NW; ++w) {
+        v1 += red[((w * NSEG + j) * CG + c) * 16 + e];
+        v2 += red[((w * NSEG + j) * CG + c) * 16 + 8 + e];
+      }
+      const size_t o = ((size_t)(m0 / SEG + j) * a.Cout + n0 + c * 8 + e) * 2;
+      a.gb.part[o] = v1;
+      a.gb.part[o + 1] = v2;
+    }
+  }
   if (a.gst) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int NW = NT / 64;
     float cnt = 8.f * KPS;
+    if (a.gb_on) __syncthreads();                    // the scratch below is shared with the sums above
 #pragma unroll
     for (int sh = 16; sh < 64; sh <<= 1) {          // the lanes of this wave with the same chunk
 #pragma unroll
@@ -596,7 +693,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
   constexpr int AI = BM / 8 / NW;               // A glds instructions per wave per stage
   constexpr int BI = BN / 8 / NW;               // B glds instructions per wave per stage
   static_assert(AI >= 1 && BI >= 1, "tile too small for the wave count");
-  constexpr int EPB = BM * (BN * 4 + 16) + NW * (BM / 64) * 16 * 8;   // epilogue tile + GroupNorm partials
+  // epilogue tile + GroupNorm partial scratch (4-wave tiles also hold the GroupNorm-backward sums)
+  constexpr int EPB = BM * (BN * 4 + 16) + NW * (BM / 64) * 16 * (NW <= 4 ? 64 : 8);
   constexpr int LDS_BYTES = STAGES * SB > EPB ? STAGES * SB : EPB;
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
 
@@ -1009,7 +1107,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
   constexpr int HB = HP * NW * 1024;             // bytes of the halo buffer
   constexpr int WB = BN * 128;                   // bytes per weight slot
   constexpr int EP = BN * 4 + 16;                // epilogue row pitch (fp32)
-  constexpr int STATS = NW * (BM / 64) * 16 * 8; // GroupNorm partial scratch past the epilogue tile
+  constexpr int STATS = NW * (BM / 64) * 16 * 64; // GroupNorm (backward) partial scratch past the epilogue tile
   constexpr int LDS_BYTES = (HB + WS * WB) > BM * EP + STATS ? (HB + WS * WB) : BM * EP + STATS;
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   char* const wring = lds + HB;
@@ -2562,6 +2660,7 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
               "conv: act %d needs a single NHWC output, Cout %% 4 == 0, no silu'", d->act);
   k.act = d->act; k.ypre = (char*)d->y_pre; k.ldpre = d->ld_pre;
   k.gst = nullptr;   // set by dmc_conv2d when the chosen kernel emits the GroupNorm partials
+  k.gb_on = 0;       // likewise for the GroupNorm-backward partials
   k.M = d->N * d->OH * d->OW; k.OHW = d->OH * d->OW;
   k.sk = nullptr; k.sk_per = 0;
   {
@@ -2726,6 +2825,48 @@ __global__ __launch_bounds__(256) void gn_part_kernel(const char* y, int ldy, in
   if (lane == 0) { out[w * 2] = m; out[w * 2 + 1] = q; }
 }
 
+// GroupNorm-backward partials of a stored input gradient g for the paths whose epilogue does not emit them: one
+// wave per (64-pixel segment, 8-channel chunk), the sums over the segment's pixels per channel.
+template <typename T>
+__global__ __launch_bounds__(256) void gn_bwd_part_kernel(const char* gy, int ldy, int nseg, int C, int OHW,
+                                                          dmc_gn_bwd_epi gb) {
+  const int lane = threadIdx.x & 63;
+  const int nch = C / 8;
+  const long w = blockIdx.x * 4L + (threadIdx.x >> 6);
+  if (w >= (long)nseg * nch) return;
+  const int seg = (int)(w / nch), ch = (int)(w - (long)seg * nch);
+  const int pix = seg * 64 + lane, c0 = ch * 8;
+  const int n = pix / OHW, cpg = C / gb.G, grp = c0 / cpg;
+  const float mean = gb.mean_rstd[((size_t)n * gb.G + grp) * 2], rstd = gb.mean_rstd[((size_t)n * gb.G + grp) * 2 + 1];
+  const bool in1 = c0 < gb.C1;
+  const char* xb = in1 ? (const char*)gb.x1 : (const char*)gb.x2;
+  const int xld = in1 ? gb.ld1 : gb.ld2, xc = in1 ? c0 : c0 - gb.C1;
+  float gv[8], xv[8];
+  load4<T>(gy, (size_t)pix * ldy + c0, gv, false);
+  load4<T>(gy, (size_t)pix * ldy + c0 + 4, gv + 4, false);
+  load4<T>(xb, (size_t)pix * xld + xc, xv, false);
+  load4<T>(xb, (size_t)pix * xld + xc + 4, xv + 4, false);
+  const uint32_t seed = gb.drop_thresh ? gb.drop_seed + (gb.drop_seed_base ? *gb.drop_seed_base : 0u) : 0u;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float g = gv[e];
+    if (gb.drop_thresh) g = drop_keep((uint64_t)pix * C + c0 + e, seed, gb.drop_thresh) ? g * gb.drop_scale : 0.f;
+    const float gm = gb.gamma ? gb.gamma[c0 + e] : 1.f, bt = gb.beta ? gb.beta[c0 + e] : 0.f;
+    float xh;
+    const float dz = gnb_dz(xv[e], g, mean, rstd, gm, bt, xh, gb.silu);
+    s1[e] = wave_sum(dz);
+    s2[e] = wave_sum(dz * xh);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      gb.part[((size_t)seg * C + c0 + e) * 2] = s1[e];
+      gb.part[((size_t)seg * C + c0 + e) * 2 + 1] = s2[e];
+    }
+  }
+}
+
 // Whether dmc_conv2d's chosen kernel emits the GroupNorm partials in its epilogue (tile_epilogue8: the round-1
 // halo kernel and the non-split LDS-DMA kernel, bf16, one NHWC output, whole 256-pixel tiles, 128-channel tiles).
 bool epi_stats_ok(const ConvK& k, const void* ws, size_t ws_bytes) {
@@ -2744,6 +2885,21 @@ bool epi_stats_ok(const ConvK& k, const void* ws, size_t ws_bytes) {
   if (k.prologue != DMC_PRO_NONE) return false;
   const FwdPlan p = plan_glds(k);
   return p.splits == 1 || ws == nullptr || ws_bytes < p.ws || dmc::opt(dmc::OPT_NO_SPLITK);
+}
+
+// ... and the GroupNorm-backward sums: only the 4-wave tiles have the LDS for their cross-wave reduction (the
+// halo2 kernel, the 128x128 / 64x128 LDS-DMA tiles), never with a prologue (input-gradient convs have none).
+bool epi_gnb_ok(const ConvK& k, const void* ws, size_t ws_bytes) {
+  if (k.prologue != DMC_PRO_NONE || !epi_stats_ok(k, ws, ws_bytes)) return false;
+  const bool buf = k.C1 % 64 == 0 && k.C2 % 64 == 0 && k.Kc == k.C1 + k.C2 && k.x1_bytes > 0 &&
+                   (k.C2 == 0 || k.x2_bytes > 0) && k.w_bytes > 0 && !dmc::opt(dmc::OPT_NO_BUFLDS);
+  const FwdPlan p = plan_glds(k);
+  const bool split = p.splits > 1 && !(ws == nullptr || ws_bytes < p.ws || dmc::opt(dmc::OPT_NO_SPLITK));
+  if (split) return false;
+  int R, nimg;
+  if (buf && !dmc::opt(dmc::OPT_NO_HALO) && dmc::opt(dmc::OPT_HALO_VER) == 2 && halo2_plan(k, &R, &nimg)) return true;
+  if (buf && !dmc::opt(dmc::OPT_NO_HALO) && halo_plan(k, &R, &nimg)) return false;   // the 8-wave halo kernel
+  return p.splits > 1 || p.cfg != 0 || dmc::opt(dmc::OPT_GLDS_2B);
 }
 
 template <typename T>
@@ -2885,12 +3041,30 @@ extern "C" size_t dmc_conv2d_workspace(const dmc_conv_desc* d) {
   return plan_glds(k).ws;
 }
 
+extern "C" int dmc_conv2d_fused_epilogue(const dmc_conv_desc* d, size_t ws_bytes) {
+  ConvK k;
+  if (fill_convk(d, nullptr, nullptr, nullptr, nullptr, nullptr, k) || k.M == 0 || k.Cout == 0) return 0;
+  // the planners only ask whether a workspace of ws_bytes is present
+  const void* ws = ws_bytes ? (const void*)d : nullptr;
+  int f = 0;
+  if (k.OHW % 64 == 0 && k.Cout % 8 == 0 && epi_stats_ok(k, ws, ws_bytes)) f |= DMC_FUSED_GN_STATS;
+  if (k.OHW % 64 == 0 && k.Cout % 8 == 0 && epi_gnb_ok(k, ws, ws_bytes)) f |= DMC_FUSED_GN_BWD;
+  return f;
+}
+
 extern "C" int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2, const void* w, void* y1,
                           void* y2, void* workspace, size_t ws_bytes, void* stream) {
   ConvK k;
   if (fill_convk(d, x1, x2, w, y1, y2, k)) return 1;
   hipStream_t s = dmc::as_stream(stream);
   if (k.M == 0 || k.Cout == 0) return 0;
+  if (d->gnb) {
+    DMC_REQUIRE(k.OHW % 64 == 0 && k.Cout % 8 == 0 && k.Csplit == k.Cout && !k.out_nchw && !k.out_f32 &&
+                    d->gnb->G > 0 && (k.Cout / d->gnb->G) % 8 == 0 && d->gnb->part,
+                "conv: GroupNorm-backward partials need OH*OW %% 64 == 0, one NHWC output, 8-channel chunks per group");
+    k.gb = *d->gnb;
+    k.gb_on = epi_gnb_ok(k, workspace, ws_bytes) ? 1 : 0;
+  }
   float* const part = d->gn_part;
   if (part) {
     DMC_REQUIRE(k.OHW % 64 == 0 && k.Cout % 8 == 0 && k.Csplit == k.Cout && !k.out_nchw && k.ldy1 % 4 == 0,
@@ -2899,7 +3073,18 @@ extern "C" int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2
   }
   const int rc = d->dtype == DMC_F32 ? launch_fwd<float>(k, workspace, ws_bytes, s)
                                      : launch_fwd<bf16_t>(k, workspace, ws_bytes, s);
-  if (rc || !part || k.gst) return rc;
+  if (rc) return rc;
+  if (d->gnb && !k.gb_on) {   // the chosen kernel's epilogue does not emit them: one pass over (g, x)
+    const int nseg = k.M / 64, nch = k.Cout / 8;
+    const int blocks = (int)(((long)nseg * nch + 3) / 4);
+    if (d->dtype == DMC_F32)
+      gn_bwd_part_kernel<float><<<blocks, 256, 0, s>>>(k.y1, k.ldy1, nseg, k.Cout, k.OHW, *d->gnb);
+    else
+      gn_bwd_part_kernel<bf16_t><<<blocks, 256, 0, s>>>(k.y1, k.ldy1, nseg, k.Cout, k.OHW, *d->gnb);
+    const int rc2 = dmc::check_launch("dmc_conv2d (GroupNorm-backward partials)");
+    if (rc2) return rc2;
+  }
+  if (!part || k.gst) return 0;
   // the chosen kernel's epilogue does not emit them: one pass over the stored output
   const int nseg = k.M / 64, nch = k.Cout / 8;
   const int blocks = (int)(((long)nseg * nch + 3) / 4);

@@ -882,8 +882,8 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
                                const float* beta, int silu, uint32_t drop_seed, const uint32_t* drop_seed_base,
                                uint32_t drop_thresh, float drop_scale, void* dx1,
                                void* dx2, int ld_dx1, int ld_dx2, int accumulate1, int accumulate2, float* dgamma,
-                               float* dbeta, float* dx_sum_nc, int ld_sum_nc, float* dx_sum_c, void* workspace,
-                               void* stream) {
+                               float* dbeta, float* dx_sum_nc, int ld_sum_nc, float* dx_sum_c, const float* part,
+                               void* workspace, void* stream) {
   const int epc = dtype == DMC_F32 ? 4 : 8;
   const int C = C1 + C2;
   DMC_REQUIRE(C % G == 0 && C <= 1024 && G <= 64, "gn_bwd: C %d / G %d", C, G);
@@ -905,7 +905,12 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
   const bool want_sums = dx_sum_nc || dx_sum_c;
   dim3 gr(N, b.splits);
   const long one_max = dmc::opt(dmc::OPT_GN_BWD_ONE_MAX);   // A/B knob
-  if (dtype != DMC_F32 && N >= 64 && (long)HW * C <= one_max && !dmc::opt(dmc::OPT_GN_BWD_SPLIT)) {
+  if (part) {
+    // the per-(64-pixel segment, channel) sums came from the input-gradient conv's epilogue (dmc_gn_bwd_epi):
+    // [n][HW/64][C][2] is gn_bwd_final's partial layout with HW/64 splits
+    DMC_REQUIRE(HW % 64 == 0, "gn_bwd: partials need HW %% 64 == 0");
+    gn_bwd_final<<<N, 256, 0, s>>>(C, G, HW, HW / 64, part, mean_rstd, gamma, beta, A, cf);
+  } else if (dtype != DMC_F32 && N >= 64 && (long)HW * C <= one_max && !dmc::opt(dmc::OPT_GN_BWD_SPLIT)) {
     gn_bwd_one<bf16_t><<<N, 1024, 0, s>>>(b, A, cf);
   } else {
     if (dtype == DMC_F32) gn_bwd_partial<float><<<gr, 256, 0, s>>>(b, partial);

@@ -74,9 +74,10 @@ def set_prologue(d, kind=L.PRO_NONE, scale=None, shift=None, ld=0, drop=None, dr
 
 def set_epilogue(d, bias=None, addvec=None, ld_add=0, resid=None, ld_res=0, silu_pre=None, ld_silu=0,
                  ldy1=0, ldy2=0, Csplit=None, out_f32=False, out_nchw=False, act=L.ACT_NONE, y_pre=None, ld_pre=0,
-                 gn_part=None):
-    d._keep_epi = (bias, addvec, resid, silu_pre, y_pre, gn_part)   # keep the tensors behind the raw pointers alive
+                 gn_part=None, gnb=None):
+    d._keep_epi = (bias, addvec, resid, silu_pre, y_pre, gn_part, gnb)   # keep what the raw pointers point at alive
     d.gn_part = ptr(gn_part)
+    d.gnb = None if gnb is None else ctypes.addressof(gnb)
     d.act = act
     d.y_pre = ptr(y_pre)
     d.ld_pre = ld_pre
@@ -140,6 +141,12 @@ def conv(d, x1, x2, w, y1, y2=None):
     ws = SCRATCH.get(nbytes, y1.device) if nbytes else None
     PROF.wrap("conv", d, lambda: check(LIB.dmc_conv2d(ctypes.byref(d), ptr(x1), ptr(x2), ptr(w), ptr(y1), ptr(y2),
                                                       ptr(ws), nbytes, L.stream()), "dmc_conv2d"))
+
+
+def conv_fused(d):
+    """include/dmc.h dmc_conv2d_fused_epilogue: which optional outputs (L.FUSED_*) the kernel dmc_conv2d would run
+    for `d` (with the workspace conv() passes) produces in its epilogue."""
+    return LIB.dmc_conv2d_fused_epilogue(ctypes.byref(d), LIB.dmc_conv2d_workspace(ctypes.byref(d)))
 
 
 def upsample2x(dtype, x, C):
@@ -248,16 +255,30 @@ def gn_apply(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, scale, shift, silu=True, dr
 
 
 def gn_bwd(dtype, g, ld_g, x1, x2, N, HW, C1, C2, ld1, ld2, G, mr, gamma, beta, silu, drop, dx1, dx2, ld_dx1,
-           ld_dx2, acc1, acc2, dgamma, dbeta, dx_sum_nc=None, ld_sum_nc=0, dx_sum_c=None):
+           ld_dx2, acc1, acc2, dgamma, dbeta, dx_sum_nc=None, ld_sum_nc=0, dx_sum_c=None, part=None):
     """GroupNorm(+SiLU+dropout) backward; optionally also the per-(n,c) / per-c pixel sums of dx (the bias and
-    time-embedding gradients of the layer that produced x), fused into the dx pass."""
+    time-embedding gradients of the layer that produced x), fused into the dx pass. part: the (sum dz,
+    sum dz*xhat) partials the input-gradient conv that produced g wrote (gn_bwd_epi), skipping the reduction."""
     ws = SCRATCH.get(LIB.dmc_gn_workspace(N, C1 + C2, G, HW), g.device)
     seed, base, thresh, scale = drop_args(drop)
     check(LIB.dmc_gn_silu_bwd(L.dtype_code(dtype), ptr(g), ld_g, ptr(x1), ptr(x2), N, HW, C1, C2, ld1, ld2, G, ptr(mr),
                               ptr(gamma), ptr(beta), int(silu), seed, base, thresh, scale, ptr(dx1), ptr(dx2), ld_dx1,
                               ld_dx2, int(acc1), int(acc2), ptr(dgamma), ptr(dbeta), ptr(dx_sum_nc), ld_sum_nc,
-                              ptr(dx_sum_c),
-                              ptr(ws), L.stream()), "dmc_gn_silu_bwd")
+                              ptr(dx_sum_c), ptr(part), ptr(ws), L.stream()), "dmc_gn_silu_bwd")
+
+
+def gn_bwd_epi(x1, x2, C1, ld1, ld2, mr, gamma, beta, G, silu, drop, M, C):
+    """The dmc_gn_bwd_epi of an input-gradient conv whose output feeds gn_bwd: returns (struct, partials tensor
+    [M/64][C][2]); pass the struct to set_epilogue(gnb=...) and the tensor to gn_bwd(part=...)."""
+    part = torch.empty(M // 64 * C * 2, dtype=torch.float32, device=x1.device)
+    e = L.GnBwdEpi()
+    seed, base, thresh, scale = drop_args(drop)
+    e.x1, e.x2, e.C1, e.ld1, e.ld2 = ptr(x1), ptr(x2), C1, ld1, ld2
+    e.mean_rstd, e.gamma, e.beta, e.G, e.silu = ptr(mr), ptr(gamma), ptr(beta), G, int(silu)
+    e.drop_seed, e.drop_seed_base, e.drop_thresh, e.drop_scale = seed, base, thresh, scale
+    e.part = ptr(part)
+    e._keep = (x1, x2, mr, gamma, beta, part)
+    return e, part
 
 
 def channel_sum(dtype, dy, N, HW, C, ld, out_nc=None, ld_out=0, out_c=None, scale=1.0):

@@ -18,6 +18,7 @@ into one flat fp32 buffer (views are handed to autograd), which is also what the
 all-reduce works on.
 """
 import contextlib
+import ctypes
 import math
 import os
 from typing import List, Optional
@@ -41,6 +42,19 @@ class Act:
 
 # GroupNorm statistics from the conv epilogues (A/B: DMC_GN_PARTIALS=0 computes them with dmc_gn_stats passes)
 _GN_PARTIALS = os.environ.get("DMC_GN_PARTIALS", "1") not in ("", "0")
+# GroupNorm-backward sums from the input-gradient convs' epilogues (opt-in, DMC_GNB_PARTIALS=1). Measured on the
+# B=128 train step: the dz recompute (sigmoid, dropout hash) in the MFMA kernels' epilogue costs what the removed
+# gn_bwd_one / gn_bwd_partial passes saved (halo2 <7,3> 56 -> 66 us; train 8253 vs 8284 img/s, 8256 vs 8290)
+_GNB_PARTIALS = _GN_PARTIALS and os.environ.get("DMC_GNB_PARTIALS", "0") not in ("", "0")
+_GNB_DROP = os.environ.get("DMC_GNB_DROP", "1") not in ("", "0")   # ... also at the dropout sites
+
+
+class GnbReq:
+    """A request for the GroupNorm-backward sums from an input-gradient conv (ExecCore._gnb_epi): epi is the
+    include/dmc.h dmc_gn_bwd_epi, part the sums; _conv sets part to None when its kernel would not fuse them."""
+
+    def __init__(self, epi, part):
+        self.epi, self.part = epi, part
 
 
 def _seed_from_torch():
@@ -126,10 +140,11 @@ class ExecCore:
     def _conv(self, srcs, conv, taps, OH, OW, Cout, mode=L.MODE_NORMAL, stride=1, pro=None, drop=None,
               bias=None, addvec=None, ld_add=0, resid=None, out=None, out_f32=False, out_nchw=False,
               dtype=None, packmode=L.PACK_FWD, w=None, Kc=None, silu_pre=None, ld_silu=0, split=None,
-              act=L.ACT_NONE, y_pre=None, stats=None):
+              act=L.ACT_NONE, y_pre=None, stats=None, gnb=None):
         """Generic implicit-GEMM conv over 1-2 NHWC sources. pro = (kind, scale, shift). stats = the output Act:
         in bf16 mode it gets the GroupNorm partials of the stored output (the next GroupNorm then needs no
-        statistics pass over it, see _gn)."""
+        statistics pass over it, see _gn). gnb = the dmc_gn_bwd_epi from _gnb_epi when the output is the gradient
+        a GroupNorm backward consumes: the conv also writes that backward's reduction sums."""
         dtype = dtype or self.dt
         gn_part = None
         if (stats is not None and _GN_PARTIALS and dtype == torch.bfloat16 and (OH * OW) % 64 == 0 and Cout % 8 == 0
@@ -164,8 +179,25 @@ class ExecCore:
                        ld_res=(0 if resid is None or out_nchw else resid.shape[-1]), silu_pre=silu_pre,
                        ld_silu=ld_silu, ldy1=ldy1, ldy2=ldy2, Csplit=csplit, out_f32=out_f32, out_nchw=out_nchw,
                        act=act, y_pre=y_pre, ld_pre=0 if y_pre is None else y_pre.shape[-1], gn_part=gn_part)
+        if gnb is not None:
+            if K.conv_fused(d) & L.FUSED_GN_BWD:
+                d.gnb = ctypes.addressof(gnb.epi)
+                d._keep_gnb = gnb
+            else:
+                gnb.part = None
         K.conv(d, a.t, srcs[1].t if len(srcs) > 1 else None, w, y1, y2)
         return d
+
+    def _gnb_epi(self, x1, x2, C1, C2, ld1, ld2, mr, gn, silu, drop, N, HW):
+        """(dmc_gn_bwd_epi, partials) for the input-gradient conv whose output g feeds gn_bwd over x = [x1 | x2]:
+        the conv's epilogue (or one pass over g where its kernel cannot) writes gn_bwd's per-(64-pixel segment,
+        channel) sums, so gn_bwd skips its reduction pass. None where gn_bwd reduces by itself; _conv also drops
+        the request (req.part = None) where its kernel would need an extra pass for them."""
+        C, G = C1 + C2, gn.num_groups
+        if not (_GNB_PARTIALS and self.dt == torch.bfloat16 and HW % 64 == 0 and C % 8 == 0 and (C // G) % 8 == 0
+                and (drop is None or _GNB_DROP)):
+            return None
+        return GnbReq(*K.gn_bwd_epi(x1, x2, C1, ld1, ld2, mr, gn.weight, gn.bias, G, silu, drop, N * HW, C))
 
     def _wgrad(self, srcs, dy, ld_dy, taps, OH, OW, Cout, dw, mode=L.MODE_NORMAL, stride=1, pro=None, drop=None,
                dtype=None):
@@ -659,11 +691,12 @@ class UNetExecutor(ExecCore):
                     K.channel_sum(dt, dy, N, H * W, Co, ldo, out_c=gv(convo.bias))
                 g = torch.empty(N, H, W, h.C, dtype=dt, device=dout.device)
                 dya = Act(dy, H, W, Co)
+                gnb = self._gnb_epi(h.t, None, h.C, 0, h.t.shape[-1], 0, mr, gno, True, None, N, H * W)
                 self._conv([dya], convo, K.TAPS3_DGRAD, H, W, h.C, out=g, packmode=L.PACK_DGRAD,
-                           Kc=L.kc_for(Co, dt))
+                           Kc=L.kc_for(Co, dt), gnb=gnb)
                 buf, acc = self._grad_target(h)
                 K.gn_bwd(dt, g, h.C, h.t, None, N, H * W, h.C, 0, h.t.shape[-1], 0, gno.num_groups, mr, gno.weight,
-                         gno.bias, True, None, buf, None, h.C, 0, acc, 0, gv(gno.weight), gv(gno.bias))
+                         gno.bias, True, None, buf, None, h.C, 0, acc, 0, gv(gno.weight), gv(gno.bias), part=gnb and gnb.part)
             elif kind == "res":
                 self._res_bwd(rec, gv)
             elif kind == "attn":
@@ -732,7 +765,9 @@ class UNetExecutor(ExecCore):
             self._wgrad([a2], dout, Cout, K.TAPS3, H, W, Cout, gv(conv2.weight))
             K.channel_sum(dt, dout, N, HW, Cout, Cout, out_c=gv(conv2.bias))
         g2 = torch.empty(N, H, W, Cout, dtype=dt, device=dout.device)
-        self._conv([Act(dout, H, W, Cout)], conv2, K.TAPS3_DGRAD, H, W, Cout, out=g2, packmode=L.PACK_DGRAD)
+        gnb2 = self._gnb_epi(h1.t, None, Cout, 0, Cout, 0, st2[2], gn2, True, drop, N, HW)
+        self._conv([Act(dout, H, W, Cout)], conv2, K.TAPS3_DGRAD, H, W, Cout, out=g2, packmode=L.PACK_DGRAD,
+                   gnb=gnb2)
         # shortcut
         if isinstance(rb.shortcut, torch.nn.Conv2d):
             sc = rb.shortcut
@@ -771,12 +806,16 @@ class UNetExecutor(ExecCore):
         dh1 = torch.empty(N, H, W, Cout, dtype=dt, device=dout.device)
         K.gn_bwd(dt, g2, Cout, h1.t, None, N, HW, Cout, 0, Cout, 0, gn2.num_groups, st2[2], gn2.weight, gn2.bias, True,
                  drop, dh1, None, Cout, 0, 0, 0, gv(gn2.weight), gv(gn2.bias), dx_sum_nc=self.daddvec[:, off:],
-                 ld_sum_nc=self.temb_total, dx_sum_c=gv(conv1.bias))
+                 ld_sum_nc=self.temb_total, dx_sum_c=gv(conv1.bias), part=gnb2 and gnb2.part)
         # conv1
         with self._side(a1.t, dh1):
             self._wgrad([a1], dh1, Cout, K.TAPS3, H, W, Cout, gv(conv1.weight))
         g1 = torch.empty(N, H, W, C1 + C2, dtype=dt, device=dout.device)
-        self._conv([Act(dh1, H, W, Cout)], conv1, K.TAPS3_DGRAD, H, W, C1 + C2, out=g1, packmode=L.PACK_DGRAD)
+        x2 = srcs[1].t if len(srcs) > 1 else None
+        gnb1 = self._gnb_epi(a.t, x2, C1, C2, a.t.shape[-1], 0 if x2 is None else x2.shape[-1], st1[2], gn1,
+                                    True, None, N, HW)
+        self._conv([Act(dh1, H, W, Cout)], conv1, K.TAPS3_DGRAD, H, W, C1 + C2, out=g1, packmode=L.PACK_DGRAD,
+                   gnb=gnb1)
         b1, acc1 = self._grad_target(a)
         if len(srcs) > 1:
             b2, acc2 = self._grad_target(srcs[1])
@@ -785,7 +824,7 @@ class UNetExecutor(ExecCore):
             b2, acc2, ld2 = None, 0, 0
         K.gn_bwd(dt, g1, C1 + C2, a.t, srcs[1].t if len(srcs) > 1 else None, N, HW, C1, C2, a.t.shape[-1], ld2,
                  gn1.num_groups, st1[2], gn1.weight, gn1.bias, True, None, b1, b2, a.t.shape[-1], ld2, acc1, acc2,
-                 gv(gn1.weight), gv(gn1.bias))
+                 gv(gn1.weight), gv(gn1.bias), part=gnb1 and gnb1.part)
 
     def _scatter_add_concat(self, tmp, b1, acc1, b2, acc2, C1, C2):
         t1 = tmp[..., :C1].contiguous()
@@ -825,9 +864,10 @@ class UNetExecutor(ExecCore):
             self._wgrad([an], dqkv, 3 * C, K.TAPS1, H, W, 3 * C, gv(ab.qkv.weight))
             K.channel_sum(dt, dqkv, N, HW, 3 * C, 3 * C, out_c=gv(ab.qkv.bias))
         g = torch.empty(N, H, W, C, dtype=dt, device=dout.device)
-        self._conv([Act(dqkv, H, W, 3 * C)], ab.qkv, K.TAPS1, H, W, C, out=g, packmode=L.PACK_DGRAD)
+        gnb = self._gnb_epi(a.t, None, C, 0, C, 0, st[2], ab.norm, False, None, N, HW)
+        self._conv([Act(dqkv, H, W, 3 * C)], ab.qkv, K.TAPS1, H, W, C, out=g, packmode=L.PACK_DGRAD, gnb=gnb)
         K.gn_bwd(dt, g, C, a.t, None, N, HW, C, 0, C, 0, ab.norm.num_groups, st[2], ab.norm.weight, ab.norm.bias,
-                 False, None, a.grad, None, C, 0, 1, 0, gv(ab.norm.weight), gv(ab.norm.bias))
+                 False, None, a.grad, None, C, 0, 1, 0, gv(ab.norm.weight), gv(ab.norm.bias), part=gnb and gnb.part)
 
     def _temb_bwd(self, rec, daddvec, gv):
         _, t, y, A0, A1, A2, Ay, addvec = rec

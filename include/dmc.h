@@ -47,6 +47,26 @@ void dmc_reset_options(int from_env);
  * then mode UPSAMPLE: valid in [0,2H) and >>1 (nearest x2); DILATE: valid iff even, /2 (the
  * transposed stride-2 conv of a dgrad); NORMAL: valid in [0,H). Invalid taps read zero.
  */
+/* GroupNorm-backward partials from an input-gradient conv (models/unet.py:35/:51, the backward of
+ * dropout(SiLU(GroupNorm(x)))): the conv's output y1 is g = dL/d(GN+SiLU output); per 64-pixel segment and channel
+ * the epilogue (or one pass over y1 where the kernel has no such epilogue) writes part[seg][c] = (sum dz,
+ * sum dz * xhat), dz = dL/dz recomputed from x exactly as dmc_gn_silu_bwd does; dmc_gn_silu_bwd(..., part, ...)
+ * then skips its own reduction pass over (g, x). */
+typedef struct dmc_gn_bwd_epi {
+  const void* x1;            /* GroupNorm input x (virtual concat x1 | x2), same dtype as the conv */
+  const void* x2;
+  int C1, ld1, ld2;
+  const float* mean_rstd;    /* forward statistics [N][G][2] */
+  const float* gamma;
+  const float* beta;
+  int G, silu;
+  uint32_t drop_seed;        /* dropout after the SiLU (the forward's mask, index pix * C + c) */
+  const uint32_t* drop_seed_base;
+  uint32_t drop_thresh;
+  float drop_scale;
+  float* part;               /* out: [M/64][Cout][2] */
+} dmc_gn_bwd_epi;
+
 typedef struct dmc_conv_desc {
   int dtype;
   int N, H, W;               /* source batch and spatial size */
@@ -78,6 +98,7 @@ typedef struct dmc_conv_desc {
   int act;                   /* DMC_ACT_*: activation applied last (after bias / addvec / resid) */
   void* y_pre;               /* with act: the pre-activation value is also stored here ([pix][ld_pre], output dtype) */
   int ld_pre;
+  const struct dmc_gn_bwd_epi* gnb;  /* if set: GroupNorm-backward partial sums of the stored output (see below) */
   float* gn_part;            /* if set: GroupNorm partial statistics of the stored output y1 (the input of the next
                               * GroupNorm, models/unet.py:34/:84), [M/64][Cout/8][2] = (mean, M2) over 64 pixels x 8
                               * channels, from the kernel's epilogue where it can, else one pass over y1. Needs
@@ -93,8 +114,15 @@ size_t dmc_conv2d_workspace(const dmc_conv_desc* d);
  * with SiLU(x*scale+shift) applied to the LDS-resident activation halo, so the caller need not materialise the
  * GroupNorm output first (inference; replaces the GroupNorm -> SiLU -> Conv2d chain of models/unet.py:34-37,
  * :55-60 without the intermediate tensor). 0 otherwise (dmc_conv2d then uses the register-staged kernel).
- * Opt-in: only with DMC_HALO_PRO=1 in the environment (measured neutral for DDIM-50 at B=128). */
+ * Default since round 2 (DMC_HALO_PRO=0 turns it off): with the GroupNorm statistics from the producing conv's
+ * epilogue the activation is not read before this conv at all. */
 int dmc_conv_halo_prologue(const dmc_conv_desc* d);
+/* Which of the optional outputs dmc_conv2d(d, ..., ws_bytes) produces inside its kernel's epilogue (bit mask), as
+ * opposed to one extra pass over the stored output: DMC_FUSED_GN_STATS (gn_part), DMC_FUSED_GN_BWD (gnb). The
+ * executor asks before it records a layer, and asks for the GroupNorm-backward sums only where they come fused
+ * (the extra pass costs more than dmc_gn_silu_bwd's own reduction). */
+int dmc_conv2d_fused_epilogue(const dmc_conv_desc* d, size_t ws_bytes);
+enum { DMC_FUSED_GN_STATS = 1, DMC_FUSED_GN_BWD = 2 };
 int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2, const void* w,
                void* y1, void* y2, void* workspace, size_t ws_bytes, void* stream);
 
@@ -158,7 +186,8 @@ int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x1, const vo
                     const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* dx1, void* dx2,
                     int ld_dx1,
                     int ld_dx2, int accumulate1, int accumulate2, float* dgamma, float* dbeta,
-                    float* dx_sum_nc, int ld_sum_nc, float* dx_sum_c, void* workspace, void* stream);
+                    float* dx_sum_nc, int ld_sum_nc, float* dx_sum_c, const float* part, void* workspace,
+                    void* stream);
 
 /* Per-(n,c) pixel sums of dy [N][HW][ld] -> out_nc [N][ld_out] (may be NULL) and per-c
  * sums over n -> out_c [C] (may be NULL); both fp32, scaled by `scale`. Bias / embedding grads. */

@@ -682,8 +682,9 @@ def test_conv_epilogue_groupnorm_partials(case, dmc_opt):
     gen = torch.Generator().manual_seed(11)
     dt = torch.float32 if case == "fp32_reg" else torch.bfloat16
     dmc_opt("DMC_HALO_VER", 2 if case == "halo2_3x3" else 1)
-    N, H, W, Cin, Cout, taps = {"halo3x3": (4, 32, 32, 128, 128, K.TAPS3), "glds1x1": (8, 16, 16, 256, 256, K.TAPS1),
-                                "halo2_3x3": (4, 32, 32, 128, 128, K.TAPS3),
+    # (the halo cases need >= 240 256x128 tiles: fewer take the split-K path, whose partials come from one pass)
+    N, H, W, Cin, Cout, taps = {"halo3x3": (32, 32, 32, 128, 256, K.TAPS3), "glds1x1": (8, 16, 16, 256, 256, K.TAPS1),
+                                "halo2_3x3": (32, 32, 32, 128, 256, K.TAPS3),
                                 "splitk_small": (2, 8, 8, 256, 256, K.TAPS3), "fp32_reg": (2, 16, 16, 64, 128, K.TAPS3),
                                 "concat_two": (4, 16, 16, 128, 128, K.TAPS3)}[case]
     G = 8
@@ -703,6 +704,10 @@ def test_conv_epilogue_groupnorm_partials(case, dmc_opt):
         return y, part
 
     y1, p1 = conv_with_part(Cout, 1)
+    if case in ("halo3x3", "halo2_3x3"):
+        d = K.make_desc(dt, N, H, W, Cin, 0, Cin, 0, L.kc_for(Cin, dt), H, W, Cout, taps)
+        K.set_epilogue(d, ldy1=Cout)
+        assert K.conv_fused(d) & L.FUSED_GN_STATS, case
     y2, p2, C2 = (None, None, 0)
     if case == "concat_two":
         y2, p2 = conv_with_part(256, 2)
@@ -714,3 +719,82 @@ def test_conv_epilogue_groupnorm_partials(case, dmc_opt):
     torch.cuda.synchronize()
     for got, ref in ((mr, rmr), (sc, rsc), (sh, rsh)):
         assert rel_err(got, ref) < 2e-5, (case, rel_err(got, ref))
+
+
+@pytest.mark.parametrize("case", ["halo2_3x3", "glds1x1_2b", "glds1x1_8wave", "halo1_3x3", "splitk_small",
+                                  "concat_two", "cfg2_small"])
+@pytest.mark.parametrize("silu,dropout", [(True, False), (True, True), (False, False)])
+def test_conv_epilogue_groupnorm_backward_partials(case, silu, dropout, dmc_opt):
+    """dmc_conv_desc.gnb: the conv that produces the gradient g of dropout(SiLU(GroupNorm(x))) also writes the
+    GroupNorm backward's per-(64-pixel segment, channel) sums of dz and dz * xhat (in its epilogue on the 4-wave
+    halo / LDS-DMA tiles, one pass over g on the other paths). The sums match an fp64 host restatement from the
+    stored g (with the counter-hash dropout mask), and gn_bwd(part=...) gives the dx / dgamma / dbeta of its own
+    reduction (summation order only)."""
+    import numpy as np
+    from diffusion_models_collection_amd import _lib as L, kernels as K
+    dmc_opt("DMC_HALO_VER", 1 if case == "halo1_3x3" else 2)
+    dmc_opt("DMC_GLDS_2B", 0 if case == "glds1x1_8wave" else 1)
+    N, H, W, Cin, C1, C2, taps = {
+        "halo2_3x3": (32, 32, 32, 128, 256, 0, K.TAPS3), "glds1x1_2b": (128, 16, 16, 256, 256, 0, K.TAPS1),
+        "glds1x1_8wave": (128, 16, 16, 256, 256, 0, K.TAPS1), "halo1_3x3": (32, 32, 32, 128, 256, 0, K.TAPS3),
+        "splitk_small": (2, 8, 8, 256, 256, 0, K.TAPS3), "concat_two": (64, 16, 16, 128, 128, 128, K.TAPS3),
+        "cfg2_small": (2, 16, 16, 128, 128, 0, K.TAPS1)}[case]
+    C, G, dt, HW = C1 + C2, 8, torch.bfloat16, H * W
+    gen = torch.Generator().manual_seed(21)
+    # the GroupNorm input x = [x1 | x2] and its statistics
+    xs = (torch.randn(N, H, W, C, generator=gen) * 1.3 + 0.4).to(dt).to(DEV)
+    x1 = xs[..., :C1].contiguous()
+    x2 = xs[..., C1:].contiguous() if C2 else None
+    gamma = (torch.rand(C, generator=gen) + 0.5).to(DEV)
+    beta = torch.randn(C, generator=gen).to(DEV)
+    _, _, mr = K.gn_stats(dt, x1, x2, N, HW, C1, C2, C1, C2, G, 1e-5, gamma, beta)
+    drop = (7, 1 << 30, 4.0 / 3.0) if dropout else None
+    # the conv producing g (C output channels)
+    dy = (torch.randn(N, H, W, Cin, generator=gen)).to(dt).to(DEV)
+    kk = int(len(taps) ** 0.5)
+    w = (torch.randn(C, Cin, kk, kk, generator=gen) * 0.05).to(DEV)
+    Kc = L.kc_for(Cin, dt)
+    wp = K.pack_weight(L.PACK_FWD, dt, w, Kc)
+    gnb, part = K.gn_bwd_epi(x1, x2, C1, C1, C2, mr, gamma, beta, G, silu, drop, N * HW, C)
+    g = torch.empty(N, H, W, C, dtype=dt, device=DEV)
+    d = K.make_desc(dt, N, H, W, Cin, 0, Cin, 0, Kc, H, W, C, taps)
+    K.set_epilogue(d, ldy1=C, gnb=gnb)
+    fused = case in ("halo2_3x3", "glds1x1_2b", "concat_two", "cfg2_small")
+    assert bool(K.conv_fused(d) & L.FUSED_GN_BWD) == fused, case
+    K.conv(d, dy, None, wp, g)
+    g_ref = torch.empty_like(g)
+    d0 = K.make_desc(dt, N, H, W, Cin, 0, Cin, 0, Kc, H, W, C, taps)
+    K.set_epilogue(d0, ldy1=C)
+    K.conv(d0, dy, None, wp, g_ref)
+    torch.cuda.synchronize()
+    assert torch.equal(g, g_ref)          # the epilogue's extra work leaves the stored output unchanged
+    # fp64 host restatement of the sums (dmc_norm.hip gn_dz)
+    gv = g.double().cpu().view(N * HW, C)
+    if dropout:
+        idx = np.arange(N * HW * C, dtype=np.int64)
+        keep = torch.from_numpy(drop_keep_np(idx, 7, 1 << 30).reshape(N * HW, C))
+        gv = torch.where(keep, gv * (4.0 / 3.0), torch.zeros_like(gv))
+    xv = xs.double().cpu().view(N, HW, C)
+    m = mr.double().cpu().view(N, G, 2)
+    mean = m[..., 0].repeat_interleave(C // G, 1).unsqueeze(1)
+    rstd = m[..., 1].repeat_interleave(C // G, 1).unsqueeze(1)
+    xh = ((xv - mean) * rstd).view(N * HW, C)
+    dz = gv
+    if silu:
+        z = xh * gamma.double().cpu() + beta.double().cpu()
+        sg = torch.sigmoid(z)
+        dz = gv * sg * (1 + z * (1 - sg))
+    ref = torch.stack([dz.view(-1, 64, C).sum(1), (dz * xh).view(-1, 64, C).sum(1)], -1)
+    got = part.double().cpu().view(-1, C, 2)
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())
+    # gn_bwd with the partials == gn_bwd with its own reduction
+    outs = []
+    for pp in (part, None):
+        dx1, dx2 = torch.empty_like(x1), (torch.empty_like(x2) if C2 else None)
+        dg, db = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        K.gn_bwd(dt, g, C, x1, x2, N, HW, C1, C2, C1, C2, G, mr, gamma, beta, silu, drop, dx1, dx2, C1, C2, 0, 0,
+                 dg, db, part=pp)
+        outs.append((torch.cat([dx1, dx2], -1) if C2 else dx1, dg, db))
+    torch.cuda.synchronize()
+    for a, b in zip(outs[0], outs[1]):
+        assert rel_err(a.float(), b.float()) < (2e-3 if a.dtype == dt else 1e-5), (case, rel_err(a.float(), b.float()))
