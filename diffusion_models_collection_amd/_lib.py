@@ -39,7 +39,7 @@ class ConvDesc(ctypes.Structure):
         ("bias", _c_p), ("addvec", _c_p), ("ld_add", _c_int), ("resid", _c_p), ("ld_res", _c_int),
         ("silu_pre", _c_p), ("ld_silu", _c_int), ("Csplit", _c_int), ("ldy1", _c_int), ("ldy2", _c_int),
         ("out_f32", _c_int), ("out_nchw", _c_int), ("act", _c_int), ("y_pre", _c_p), ("ld_pre", _c_int),
-        ("gnb", _c_p), ("gn_part", _c_p),
+        ("gnb", _c_p), ("gn_part", _c_p), ("wg_bias", _c_p),
     ]
 
 

@@ -28,6 +28,7 @@ struct ConvK {
   float* gst;  // GroupNorm partials from the epilogue: [M/64][Cout/8] x (mean, M2) (nullptr: off)
   int gb_on;   // GroupNorm-backward partials from the epilogue (dmc_gn_bwd_epi in gb)
   dmc_gn_bwd_epi gb;
+  float* wgb;  // wgrad: per-split bias partials [split][Cpad] = sum over the split's pixels of dy (nullptr: off)
   int M;      // N*OH*OW output pixels
   int OHW;    // OH*OW
   float* sk;  // split-K partial slab (nullptr: no split)
@@ -1240,559 +1241,6 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Round-2 halo conv: 4 waves (one per SIMD), v_mfma_f32_32x32x16_bf16, epilogue straight from registers.
-//
-// Same block tile (128 output channels x 256 output pixels), the same LDS-resident halo per 64-channel chunk
-// (double-buffered, the next chunk's halo DMA'd in three parts during taps 0-2) and the same 3-slot LDS-DMA
-// weight ring as conv3x3_halo_kernel, but:
-//   * each wave owns a 64 co x 128 pixel tile (2 x 4 tiles of 32x32x16): per 16-deep k-step it reads 2 weight +
-//     4 halo fragments (ds_read_b128) for 8 MFMAs, i.e. 0.75 reads per 32 MFMA-cycles -- the 8-wave 64x64 tiling
-//     read 1 per 16 cycles per wave, which at two waves per SIMD is the full LDS bandwidth (256 B/clk/CU) with
-//     nothing left for the DMA writes;
-//   * the fragments of k-step s+1 are read while the MFMAs of step s run, and the barrier of stage g+1 sits
-//     inside stage g, between the last fragment reads and the last 8 MFMAs of g, so those MFMAs cover the read
-//     latency of stage g+1's first fragments (the weight slot the next DMA overwrites is free by then);
-//   * no fp32 LDS staging of the output tile: lane l holds 4 consecutive channels of pixel l&31 per register
-//     group, stored as one 8-byte bf16 write with bias / time-embedding / residual applied on the way (the LDS
-//     staging needed 135 KB and two block barriers);
-//   * LDS images swizzled by (row >> 1) & 7 (16-byte chunk c of row r at c ^ ((r >> 1) & 7)): conflict-free for
-//     the 32-row fragment reads of the weights and of 32- and 64-wide halo rows (2-way at 16-wide rows, 3-way
-//     for 8x8 images; brute-forced over every tap shift with the ds_read_b128 lane groups of the guide).
-// HP = DMA pieces per wave of the 8-wave layout (6: <= 384 halo pixels, 7: <= 448); here 2*HP per wave.
-typedef float v16f __attribute__((ext_vector_type(16)));
-DMC_DEV v16f mma32(v16f acc, const v4i& a, const v4i& b) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8s, a), __builtin_bit_cast(v8s, b), acc, 0, 0, 0);
-}
-DMC_DEV int swz2(int row) { return (row >> 1) & 7; }
-
-// PROBE (measurement builds only, never the production instantiation PROBE = 0): 1 = no MFMAs, 2 = no epilogue
-// stores, 4 = no DMA after the prologue, 8 = no barriers in the loop
-template <int HP, int PROBE = 0>
-__global__ __launch_bounds__(256) void conv3x3_halo4_kernel(ConvK a, int R, int nimg) {
-  constexpr int NW = 4, HPW = 2 * HP, WPW = 4;
-  constexpr int HB = HPW * NW * 1024;            // bytes per halo buffer
-  constexpr int WB = 128 * 128;                  // bytes per weight slot: 128 co x 64 ch
-  constexpr int WS = 3;
-  __shared__ __attribute__((aligned(16))) char lds[2 * HB + WS * WB];
-  char* const wring = lds + 2 * HB;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wco = wave & 1, wpx = wave >> 1;
-  const int m0 = blockIdx.x * 256, n0 = blockIdx.y * 128;
-  const int lrow = lane >> 3;
-  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
-  const int n_first = m0 / a.OHW;
-  const int r0 = (m0 - n_first * a.OHW) / OW;
-
-  // halo DMA: piece p of this wave = halo rows 8*(wave*HPW + p) + lrow; the lane fetches the logical chunk that
-  // lands on physical chunk lane&7 under the row swizzle
-  unsigned h1[HPW], h2[HPW];
-#pragma unroll
-  for (int p = 0; p < HPW; ++p) {
-    const int h = (wave * HPW + p) * 8 + lrow;
-    const int lc = (lane & 7) ^ swz2(h);
-    h1[p] = kOOB; h2[p] = kOOB;
-    if (h < npix) {
-      const int img = h / segpix, rem = h - img * segpix;
-      const int hr = rem / HW, hc = rem - hr * HW;
-      const int iy = r0 + hr - 1, ix = hc - 1;
-      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
-        const unsigned sp = (unsigned)(((n_first + img) * a.H + iy) * a.W + ix);
-        h1[p] = (sp * a.ld1 + lc * 8) * 2u;
-        h2[p] = (sp * a.ld2 + lc * 8) * 2u;
-      }
-    }
-  }
-  // weight slice: 4 pieces per wave per stage, rows 8*(wave*4 + j) + lrow
-  const unsigned wrow = (unsigned)(a.ntaps * a.Kc);
-  unsigned ob[WPW];
-#pragma unroll
-  for (int j = 0; j < WPW; ++j) {
-    const int r = (wave * WPW + j) * 8 + lrow;
-    const int co = n0 + r;
-    const int lc = (lane & 7) ^ swz2(r);
-    ob[j] = co < a.Cout ? ((unsigned)co * wrow + lc * 8) * 2u : kOOB;
-  }
-  // fragment rows: weights (A) rows wco*64 + 32i + (lane&31); halo rows of pixels wpx*128 + 32j + (lane&31)
-  const int fr = lane & 31, fh = lane >> 5;
-  int wr[2], hb[4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) wr[i] = wco * 64 + i * 32 + fr;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int m = wpx * 128 + j * 32 + fr;
-    const int img = m / (R * OW), rem = m - img * (R * OW);
-    const int r = rem / OW, col = rem - r * OW;
-    hb[j] = img * segpix + (r + 1) * HW + col + 1;
-  }
-
-  v16f acc[2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-  const int nch = a.Kc / 64, nst = nch * 9;
-  auto issue_w = [&](int st) {
-    const int c = st / 9, t = st - c * 9;
-    const unsigned koff = (unsigned)(t * a.Kc + c * 64) * 2u;
-    dma_pieces<WPW>(a.w, a.w_bytes, wring + (st % WS) * WB + wave * WPW * 1024, ob, koff, 0, WPW);
-  };
-  auto part_b = [](int k) { return k * HPW / 3; };
-  auto halo_count = [&](int st) {
-    const int c = st / 9, k = st - c * 9;
-    return (k < 3 && c + 1 < nch) ? part_b(k + 1) - part_b(k) : 0;
-  };
-  // slot st (issued right after the barrier of stage st): weight slice st+2, then a part of the next chunk's halo
-  auto issue_slot = [&](int st) {
-    if (PROBE & 4) return;
-    if (st + 2 < nst) issue_w(st + 2);
-    const int c = st / 9, k = st - c * 9;
-    if (k < 3 && c + 1 < nch)
-      halo_issue<HPW>(a, lds + ((c + 1) & 1) * HB, (c + 1) * 64, wave, part_b(k), part_b(k + 1), h1, h2);
-  };
-  auto slot_count = [&](int st) { return (PROBE & 4) ? 0 : (st + 2 < nst ? WPW : 0) + halo_count(st); };
-  auto load_frags = [&](int st, int s, v4i* fa, v4i* fb) {
-    if (PROBE & 16) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = v4i{st, s, 1, 2};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = v4i{s, st, 3, j};
-      return;
-    }
-    const int c = st / 9, t = st - c * 9;
-    const char* A = lds + (c & 1) * HB;
-    const char* Bw = wring + (st % WS) * WB;
-    const int ty = t / 3, tx = t - ty * 3;
-    const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
-    const int chunk = 2 * s + fh;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = wr[i];
-      fa[i] = *(const v4i*)(Bw + r * 128 + ((chunk ^ swz2(r)) << 4));
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int h = hb[j] + delta;
-      fb[j] = *(const v4i*)(A + h * 128 + ((chunk ^ swz2(h)) << 4));
-    }
-  };
-  auto barrier = [&]() {
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("" ::: "memory");
-  };
-
-  // prologue: chunk 0's halo and weight slices 0, 1; stage 0 needs all but slice 1
-  halo_issue<HPW>(a, lds, 0, wave, 0, HPW, h1, h2);
-  issue_w(0);
-  if (nst > 1) issue_w(1);
-  wait_vm_dyn(nst > 1 ? WPW : 0);
-  barrier();
-  issue_slot(0);
-  v4i fa[2][2], fb[2][4];
-  load_frags(0, 0, fa[0], fb[0]);
-  // One k-step = 8 MFMAs (32 cycles each on the SIMD); the 6 fragment reads of the next step are interleaved
-  // one per MFMA (sched_group_barrier pins the order) so each read's latency hides under the following MFMAs.
-  // At the stage's last step the barrier of stage st+1 is taken after the first two MFMAs are issued (the
-  // matrix pipe keeps running through the wait), then the next slot's DMA and stage st+1's first reads are
-  // interleaved with the remaining six.
-  constexpr int kMfma = 0x008, kDsRead = 0x100;
-  for (int st = 0; st < ((PROBE & 32) ? 0 : nst); ++st) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      v4i* ca = fa[s & 1];
-      v4i* cb = fb[s & 1];
-      v4i* na = fa[(s + 1) & 1];
-      v4i* nb = fb[(s + 1) & 1];
-      if (s < 3) {
-        load_frags(st, s + 1, na, nb);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (PROBE & 1) acc[i][j][0] += __builtin_bit_cast(float, ca[i][0] ^ cb[j][0]);
-            else acc[i][j] = mma32(acc[i][j], ca[i], cb[j]);
-        // reads front-loaded: the last of them still has 6 MFMAs (~190 cycles) to land before its use
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          __builtin_amdgcn_sched_group_barrier(kDsRead, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(kMfma, 1, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(kMfma, 5, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (PROBE & 1) acc[0][j][0] += __builtin_bit_cast(float, ca[0][0] ^ cb[j][0]);
-          else acc[0][j] = mma32(acc[0][j], ca[0], cb[j]);
-        __builtin_amdgcn_sched_barrier(0);
-        // this wave's fragment reads of stage st have returned (unconditional, so the compiler's counter model
-        // knows it on every path); stage st+1's DMA (all but slot st) has landed
-        __builtin_amdgcn_s_waitcnt(waitcnt_lgkm0());
-        if (st + 1 < nst) {
-          wait_vm_dyn(slot_count(st));
-          if (!(PROBE & 8)) barrier();
-          issue_slot(st + 1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        // stage st+1's first fragments (on the last stage: harmless reads of in-bounds LDS, never used)
-        load_frags(st + 1, 0, na, nb);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (PROBE & 1) acc[1][j][0] += __builtin_bit_cast(float, ca[1][0] ^ cb[j][0]);
-          else acc[1][j] = mma32(acc[1][j], ca[1], cb[j]);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          __builtin_amdgcn_sched_group_barrier(kDsRead, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(kMfma, 1, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(kMfma, 1, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  }
-
-  // epilogue from registers: acc[i][j] reg e -> co = 32i + (e&3) + 8(e>>2) + 4fh, pixel = 32j + fr
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int co = n0 + wco * 64 + i * 32 + 8 * g + 4 * fh;
-      if (co >= a.Cout) continue;
-      const v4f b = a.bias ? *(const v4f*)(a.bias + co) : v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int pbase = m0 + wpx * 128 + j * 32;        // 32 pixels of one image (OHW % 32 == 0)
-        const int pix = pbase + fr;
-        v4f v = v4f{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]} + b;
-        if (a.addvec) {
-          const int n = __builtin_amdgcn_readfirstlane(pbase / a.OHW);
-          v += *(const v4f*)(a.addvec + (size_t)n * a.ld_add + co);
-        }
-        if (a.resid) {
-          const v2i r = *(const v2i*)(a.resid + ((size_t)pix * a.ld_res + co) * 2);
-          v[0] += bf2f((uint32_t)r[0] & 0xffffu); v[1] += bf2f((uint32_t)r[0] >> 16);
-          v[2] += bf2f((uint32_t)r[1] & 0xffffu); v[3] += bf2f((uint32_t)r[1] >> 16);
-        }
-        v2i o;
-        o[0] = (int)f2bf2(v[0], v[1]);
-        o[1] = (int)f2bf2(v[2], v[3]);
-        if (!(PROBE & 2)) *(v2i*)(a.y1 + ((size_t)pix * a.ldy1 + co) * 2) = o;
-        else if (o[0] == 0x7fc07fc1) *(v2i*)(a.y1) = o;     // keep the math alive
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// conv3x3_halo5_kernel: the round-2 halo conv with 512-pixel blocks and 32-channel stages.
-//
-// Measured on conv3x3_halo4_kernel (PMC, scripts/pmc_halo4.sh): waves parked on s_waitcnt / barriers 44 % of
-// their lifetime and the matrix pipe busy 22 %: every block streams the whole weight tensor (16 KB per stage,
-// 151 MB per launch of the roofline layer) from L2 for only 256 pixels of work. Here a block owns 128 output
-// channels x 512 pixels (two 256-pixel halves, one grid round on 256 CUs for the B=128 32x32 layers) and each
-// weight slice serves both halves: per stage (tap t, 32-channel chunk c) a wave runs 2 k-steps x 16 MFMAs
-// (64 co x 256 px, 256 accumulator registers -- one wave per SIMD has 512) on one 8 KB weight slice, half the
-// weight bytes per FLOP. 64-byte LDS rows (16-byte chunk q of row r at q ^ ((r >> 2) & 3): conflict-free for the
-// weight reads and 32- / 64-wide halo rows, 2-way at 16-wide rows, 3-way for 8x8 images), halo double-buffered
-// (the next chunk's halo in three parts during taps 0-2), 3-slot weight ring, and the epilogue straight from
-// registers: bias / time embedding / residual in fp32, bf16 pack, v_permlane32_swap pairs into 16-byte stores.
-// HPW = halo DMA pieces (16 rows x 64 B) per wave: 10 covers 640 halo pixels, 13 covers 832.
-DMC_DEV int swz64(int row) { return (row >> 2) & 3; }
-
-template <int NW, int HPW, int WS = 3, int PROBE = 0>
-__global__ __launch_bounds__(NW * 64) void conv3x3_halo5_kernel(ConvK a, int R, int nimg) {
-  constexpr int WPW = 8 / NW;                    // weight DMA pieces per wave per stage (8 KB slot)
-  constexpr int JT = 32 / NW;                    // 32-pixel tiles per wave (NW = 4: both halves, 8: one)
-  constexpr int HB = HPW * NW * 1024;            // bytes per halo buffer
-  constexpr int WB = 128 * 64;                   // bytes per weight slot: 128 co x 32 ch (WS-slot ring)
-  __shared__ __attribute__((aligned(16))) char lds[2 * HB + WS * WB];
-  char* const wring = lds + 2 * HB;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wco = wave & 1, wpx = (wave >> 1) & 1, whh = wave >> 2;
-  const int m0 = blockIdx.x * 512, n0 = blockIdx.y * 128;
-  const int lrow = lane >> 2, pch = lane & 3;    // DMA: lane -> (row in piece, physical 16-byte chunk)
-  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
-  const int n_first = m0 / a.OHW;
-  const int r0 = (m0 - n_first * a.OHW) / OW;
-
-  // halo DMA sources: source pixel * 4 + logical chunk per piece, -1 for zero padding / past the halo (the
-  // byte offset for either concat source is formed at issue time: one register per piece, not two)
-  int hs[HPW];
-#pragma unroll
-  for (int p = 0; p < HPW; ++p) {
-    const int h = (wave * HPW + p) * 16 + lrow;
-    const int lc = pch ^ swz64(h);
-    hs[p] = -1;
-    if (h < npix) {
-      const int img = h / segpix, rem = h - img * segpix;
-      const int hr = rem / HW, hc = rem - hr * HW;
-      const int iy = r0 + hr - 1, ix = hc - 1;
-      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) hs[p] = ((((n_first + img) * a.H + iy) * a.W + ix) << 2) | lc;
-    }
-  }
-  const unsigned wrow = (unsigned)(a.ntaps * a.Kc);
-  unsigned ob[WPW];
-#pragma unroll
-  for (int j = 0; j < WPW; ++j) {
-    const int r = (wave * WPW + j) * 16 + lrow;
-    const int co = n0 + r;
-    ob[j] = co < a.Cout ? ((unsigned)co * wrow + (pch ^ swz64(r)) * 8) * 2u : kOOB;
-  }
-  const int fr = lane & 31, fh = lane >> 5;
-  int wr[2], hb[JT];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) wr[i] = wco * 64 + i * 32 + fr;
-#pragma unroll
-  for (int j = 0; j < JT; ++j) {
-    const int hh = NW == 4 ? (j >> 2) : whh, jj = NW == 4 ? (j & 3) : j;
-    const int m = hh * 256 + wpx * 128 + jj * 32 + fr;
-    const int img = m / (R * OW), rem = m - img * (R * OW);
-    const int r = rem / OW, col = rem - r * OW;
-    hb[j] = img * segpix + (r + 1) * HW + col + 1;
-  }
-
-  v16f acc[2][JT];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < JT; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-  const int nch = a.Kc / 32, nst = nch * 9;
-  auto halo_issue5 = [&](char* buf, int c0, int pb, int pe) {
-    const bool first = c0 < a.C1;
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        first ? (void*)a.x1 : (void*)a.x2, (short)0, first ? a.x1_bytes : a.x2_bytes, 0x00020000);
-    const unsigned c2 = (unsigned)(first ? c0 : c0 - a.C1) * 2u;
-    const unsigned ld = (unsigned)(first ? a.ld1 : a.ld2);
-#pragma unroll
-    for (int p = 0; p < HPW; ++p)
-      if (p >= pb && p < pe) {
-        const unsigned off = hs[p] < 0 ? kOOB : (((unsigned)hs[p] >> 2) * ld + ((unsigned)hs[p] & 3u) * 8u) * 2u + c2;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(buf + (wave * HPW + p) * 1024), 16, off, 0, 0, 0);
-      }
-  };
-  auto issue_w = [&](int st) {
-    const int c = st / 9, t = st - c * 9;
-    const unsigned koff = (unsigned)(t * a.Kc + c * 32) * 2u;
-    dma_pieces<WPW>(a.w, a.w_bytes, wring + (st % WS) * WB + wave * WPW * 1024, ob, koff, 0, WPW);
-  };
-  auto part_b = [](int k) { return k * HPW / 3; };
-  auto halo_count = [&](int st) {
-    const int c = st / 9, k = st - c * 9;
-    return (k < 3 && c + 1 < nch) ? part_b(k + 1) - part_b(k) : 0;
-  };
-  auto issue_slot = [&](int st) {
-    if (PROBE & 4) return;
-    if (st + WS - 1 < nst) issue_w(st + WS - 1);
-    const int c = st / 9, k = st - c * 9;
-    if (k < 3 && c + 1 < nch) halo_issue5(lds + ((c + 1) & 1) * HB, (c + 1) * 32, part_b(k), part_b(k + 1));
-  };
-  auto slot_count = [&](int st) { return (PROBE & 4) ? 0 : (st + WS - 1 < nst ? WPW : 0) + halo_count(st); };
-  // what may still be in flight when stage st+1 starts: the slots issued after stage st+1's weight slice
-  auto after_w = [&](int st) {
-    int n = 0;
-    const int ws = st + 2 - WS;            // slot that issued stage st+1's weights (negative: the prologue)
-    if (ws >= 0) n += halo_count(ws);
-    else for (int q = st + 2; q < WS - 1 && q < nst; ++q) n += WPW;
-    for (int t = (ws >= 0 ? ws + 1 : 0); t <= st; ++t) n += slot_count(t);
-    return (PROBE & 4) ? 0 : n;
-  };
-  auto load_a = [&](int st, int s, v4i* fa) {
-    const char* Bw = wring + (st % WS) * WB;
-    const int chunk = 2 * s + fh;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = wr[i];
-      fa[i] = *(const v4i*)(Bw + r * 64 + ((chunk ^ swz64(r)) << 4));
-    }
-  };
-  auto load_b = [&](int st, int s, int j, v4i& fb) {
-    const int c = st / 9, t = st - c * 9;
-    const char* A = lds + (c & 1) * HB;
-    const int ty = t / 3, tx = t - ty * 3;
-    const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
-    const int h = hb[j] + delta;
-    fb = *(const v4i*)(A + h * 64 + (((2 * s + fh) ^ swz64(h)) << 4));
-  };
-  auto mma = [&](v16f& acc_, const v4i& x, const v4i& y) {
-    if (PROBE & 1) acc_[0] += __builtin_bit_cast(float, x[0] ^ y[0]);
-    else acc_ = mma32(acc_, x, y);
-  };
-  auto barrier = [&]() {
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("" ::: "memory");
-  };
-  constexpr int kMfma = 0x008, kDsRead = 0x100;
-  constexpr int NR = 2 + JT;                     // fragment reads per k-step
-  constexpr int NM = 2 * JT;                     // MFMAs per k-step
-  constexpr int NPRE = NW == 4 ? 4 : 2;          // MFMAs of k-step 1 issued before the stage barrier
-
-  // PROBE & 16: in-kernel s_memtime stamps (diagnostic build only): cycles in the prologue, in the stage waits
-  // (lgkmcnt + vmcnt + barrier), in the whole main loop and in the epilogue, per wave, written to y1 (the probe's
-  // output is not a result)
-  long t_start = 0, t_wait = 0, t_loop0 = 0, t_loop1 = 0;
-  if (PROBE & 16) t_start = __builtin_amdgcn_s_memtime();
-  // prologue: chunk 0's halo and the first WS-1 weight slices
-  halo_issue5(lds, 0, 0, HPW);
-  for (int q = 0; q < WS - 1 && q < nst; ++q) issue_w(q);
-  {
-    int pending = 0;   // stage 0 needs the halo and slice 0: the later prologue slices may stay in flight
-    for (int q = 1; q < WS - 1 && q < nst; ++q) pending += WPW;
-    wait_vm_dyn(pending);
-  }
-  barrier();
-  issue_slot(0);
-  // k-step = (stage, s in {0,1}): 2 weight + JT halo fragments, 2*JT MFMAs; fragments double-buffered across
-  // k-steps, the next k-step's reads spread over the first MFMAs of this one.
-  if (PROBE & 16) t_loop0 = __builtin_amdgcn_s_memtime();
-  v4i fa[2][2], fb[2][JT];
-  load_a(0, 0, fa[0]);
-#pragma unroll
-  for (int j = 0; j < JT; ++j) load_b(0, 0, j, fb[0][j]);
-  for (int st = 0; st < nst; ++st) {
-    load_a(st, 1, fa[1]);
-#pragma unroll
-    for (int j = 0; j < JT; ++j) load_b(st, 1, j, fb[1][j]);
-#pragma unroll
-    for (int j = 0; j < JT; ++j)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) mma(acc[i][j], fa[0][i], fb[0][j]);
-#pragma unroll
-    for (int q = 0; q < NR / 2; ++q) {
-      __builtin_amdgcn_sched_group_barrier(kDsRead, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(kMfma, 1, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(kMfma, NM - NR / 2, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    // k-step 1: NPRE MFMAs, then the barrier of stage st+1 (this wave's reads of stage st are back), the next
-    // slot's DMA, and stage st+1's k-step-0 reads spread over the remaining MFMAs
-#pragma unroll
-    for (int q = 0; q < NPRE; ++q) mma(acc[q & 1][q >> 1], fa[1][q & 1], fb[1][q >> 1]);
-    __builtin_amdgcn_sched_barrier(0);
-    long tw0 = 0;
-    if (PROBE & 16) tw0 = __builtin_amdgcn_s_memtime();
-    __builtin_amdgcn_s_waitcnt(waitcnt_lgkm0());
-    if (st + 1 < nst) {
-      wait_vm_dyn(after_w(st));
-      if (!(PROBE & 8)) barrier();
-    }
-    if (PROBE & 16) t_wait += __builtin_amdgcn_s_memtime() - tw0;
-    if (st + 1 < nst) issue_slot(st + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    load_a(st + 1, 0, fa[0]);        // last stage: in-bounds reads of a stale slot, never used
-#pragma unroll
-    for (int j = 0; j < JT; ++j) load_b(st + 1, 0, j, fb[0][j]);
-#pragma unroll
-    for (int q = NPRE; q < NM; ++q) mma(acc[q & 1][q >> 1], fa[1][q & 1], fb[1][q >> 1]);
-#pragma unroll
-    for (int q = 0; q < NR / 2; ++q) {
-      __builtin_amdgcn_sched_group_barrier(kDsRead, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(kMfma, 1, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(kMfma, NM - NPRE - NR / 2, 0);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-
-  if (PROBE & 16) t_loop1 = __builtin_amdgcn_s_memtime();
-  // epilogue: acc[i][j] reg e -> co = 32i + (e&3) + 8(e>>2) + 4fh, pixel = tile j. Per register group g the
-  // lane's 4 channels get bias / embedding / residual in fp32 and are packed to bf16; groups (g, g+1) are then
-  // exchanged across the half-waves (v_permlane32_swap) so each lane stores 8 consecutive channels (16 B).
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    v4f bsv[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int co = n0 + wco * 64 + i * 32 + 8 * g + 4 * fh;
-      bsv[g] = (a.bias && co < a.Cout) ? *(const v4f*)(a.bias + co) : v4f{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int j = 0; j < JT; ++j) {
-      const int hh = NW == 4 ? (j >> 2) : whh, jj = NW == 4 ? (j & 3) : j;
-      const int pbase = m0 + hh * 256 + wpx * 128 + jj * 32;   // 32 pixels of one image (OHW % 32 == 0)
-      const int pix = pbase + fr;
-      const int n = __builtin_amdgcn_readfirstlane(pbase / a.OHW);
-      uint32_t pk[4][2];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int co = n0 + wco * 64 + i * 32 + 8 * g + 4 * fh;
-        v4f v = v4f{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]} + bsv[g];
-        if (co < a.Cout) {
-          if (a.addvec) v += *(const v4f*)(a.addvec + (size_t)n * a.ld_add + co);
-          if (a.resid) {
-            const v2i r = *(const v2i*)(a.resid + ((size_t)pix * a.ld_res + co) * 2);
-            v[0] += bf2f((uint32_t)r[0] & 0xffffu); v[1] += bf2f((uint32_t)r[0] >> 16);
-            v[2] += bf2f((uint32_t)r[1] & 0xffffu); v[3] += bf2f((uint32_t)r[1] >> 16);
-          }
-        }
-        pk[g][0] = f2bf2(v[0], v[1]);
-        pk[g][1] = f2bf2(v[2], v[3]);
-      }
-#pragma unroll
-      for (int g = 0; g < 4; g += 2) {
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          const auto r = __builtin_amdgcn_permlane32_swap(pk[g][d], pk[g + 1][d], false, false);
-          pk[g][d] = r[0];
-          pk[g + 1][d] = r[1];
-        }
-        // lanes 0-31: channels 8g..8g+7; lanes 32-63: 8g+8..8g+15 (of this 32-channel tile)
-        const int co = n0 + wco * 64 + i * 32 + 8 * g + 8 * fh;
-        if (co < a.Cout && !(PROBE & 2)) {
-          const v4i o = {(int)pk[g][0], (int)pk[g][1], (int)pk[g + 1][0], (int)pk[g + 1][1]};
-          *(v4i*)(a.y1 + ((size_t)pix * a.ldy1 + co) * 2) = o;
-        } else if ((PROBE & 2) && pk[g][0] == 0x7fc07fc1u) {
-          *(int*)(a.y1) = (int)pk[g + 1][1];
-        }
-      }
-    }
-  }
-  if (PROBE & 16) {
-    __syncthreads();
-    const long t_end = __builtin_amdgcn_s_memtime();
-    if (lane == 0) {
-      long* o = (long*)a.y1 + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * NW + wave) * 4;
-      o[0] = t_loop0 - t_start; o[1] = t_wait; o[2] = t_loop1 - t_loop0; o[3] = t_end - t_loop1;
-    }
-  }
-}
-
-// Geometry of the 512-pixel halo kernel: HPW (halo pieces per wave), 0 if it does not apply
-int halo5_plan(const ConvK& k, int* R, int* nimg) {
-  if (k.mode != DMC_MODE_NORMAL || k.stride != 1 || k.ntaps != 9 || k.tkw != 3) return 0;
-  if (!((k.tdy0 == -1 && k.tsy == 1) || (k.tdy0 == 1 && k.tsy == -1))) return 0;
-  if (!((k.tdx0 == -1 && k.tsx == 1) || (k.tdx0 == 1 && k.tsx == -1))) return 0;
-  if (k.OH != k.H || k.OW != k.W || k.M % 512) return 0;
-  if (k.C1 % 32 || k.C2 % 32 || k.Kc != k.C1 + k.C2 || k.Kc % 32) return 0;
-  const int ohw = k.OH * k.OW;
-  if (ohw % 512 == 0 && 512 % k.OW == 0) { *nimg = 1; *R = 512 / k.OW; }
-  else if (512 % ohw == 0 && k.N % (512 / ohw) == 0) { *nimg = 512 / ohw; *R = k.OH; }
-  else return 0;
-  const int npix = *nimg * (*R + 2) * (k.OW + 2);
-  return npix <= 640 ? 40 : npix <= 896 ? 56 : 0;    // halo DMA pieces (16 rows each) the kernel issues
-}
-
-// Whether the round-2 halo kernel's register epilogue covers this descriptor's epilogue
-bool halo4_epilogue_ok(const ConvK& k) {
-  return !k.out_f32 && !k.out_nchw && !k.silu_pre && !k.act && k.Csplit >= k.Cout && (k.Cout & 3) == 0 &&
-         (k.ldy1 & 3) == 0 && (!k.resid || (k.ld_res & 3) == 0) && (k.OHW % 32) == 0 &&
-         (!k.addvec || (k.ld_add & 3) == 0);
-}
-
-// ---------------------------------------------------------------------------------------------
 // Register-weight variant of conv3x3_halo_kernel (same tile, halo image and fragment reads). Each wave
 // loads its own 64x64 weight fragments of tap stage s+1 straight into VGPRs while stage s computes (the
 // four waves sharing a slice hit the same L1 lines), and the next chunk's halo is staged through VGPRs
@@ -2194,6 +1642,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvK a, const char* dy
       rd[j] = d; rx[j] = x;
     }
   };
+  // bias gradient (a.wgb, the first kk block only): this thread's dy chunks summed per channel as they are stored
+  const bool bias_on = a.wgb != nullptr && blockIdx.x == 0;
+  float bsum[EPC];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) bsum[e] = 0.f;
   auto store_stage = [&](int buf) {
     char* D = lds[buf];
     char* X = lds[buf] + SP * ROWB;
@@ -2202,6 +1655,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvK a, const char* dy
       const int r = rb0 + RSTEP * j;
       *(v4i*)(D + r * ROWB + wg_phys<T>(r, chk)) = rd[j];
       *(v4i*)(X + r * ROWB + wg_phys<T>(r, chk)) = rx[j];
+      if (bias_on) {
+        float f[EPC];
+        Chunk<T>::unpack(rd[j], f);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) bsum[e] += f[e];
+      }
     }
   };
 
@@ -2240,6 +1699,21 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvK a, const char* dy
   // slab [z][Cpad][KK], Cpad = Cout rounded up to 128 (co is the row of C: co = 4h+i, kk = col r):
   // for each register i, 16 lanes store 16 consecutive kk of one co row (64-byte segments)
   const int Cpad = gridDim.y * 128;
+  if (bias_on) {   // fixed order: rows within a thread, lanes of the same chunk (xor CPR ...), then the 4 waves
+#pragma unroll
+    for (int sh = CPR; sh < 64; sh <<= 1)
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) bsum[e] += __shfl_xor(bsum[e], sh);
+    float* red = (float*)lds[0];                   // [4][CPR][EPC]; the loop ended with a barrier
+    if (lane < CPR)
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) red[(wave * CPR + lane) * EPC + e] = bsum[e];
+    __syncthreads();
+    if (tid < CPR * EPC) {
+      const float v = red[tid] + red[CPR * EPC + tid] + red[2 * CPR * EPC + tid] + red[3 * CPR * EPC + tid];
+      a.wgb[(size_t)blockIdx.z * Cpad + co0 + tid] = v;   // tid = chunk * EPC + e: channel co0 + tid
+    }
+  }
   float* out = slab + (size_t)blockIdx.z * KK * Cpad;
   const int fr = lane & 15, fh = lane >> 4;
 #pragma unroll
@@ -2371,6 +1845,11 @@ __global__ __launch_bounds__(512) void wgrad3x3_halo_kernel(ConvK a, const char*
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int u = 0; u < 9; ++u) acc[i][u] = v4f{0.f, 0.f, 0.f, 0.f};
+  // bias gradient (a.wgb, the first channel chunk's blocks): dy fragment i = wq times an all-ones B fragment, one
+  // extra MFMA per k-step per wave; every column of the 16x16 result is the pixel sum of its co row
+  const bool bias_on = a.wgb != nullptr && blockIdx.x == 0;
+  const v4i ones = {0x3F803F80, 0x3F803F80, 0x3F803F80, 0x3F803F80};   // bf16 1.0 pairs
+  v4f accb = {0.f, 0.f, 0.f, 0.f};
 
   const int nt_blk = t_end - t_begin, nst = nt_blk * 4;
   // the next tile's halo goes out in three parts (slots k = 0, 1, 2 of a tile): pieces [part_b(k), part_b(k+1))
@@ -2424,7 +1903,17 @@ __global__ __launch_bounds__(512) void wgrad3x3_halo_kernel(ConvK a, const char*
         }
         fb = fn;
       }
+      if (bias_on) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (i == wq) accb = mma16<T>(accb, fa[i], ones);
+      }
     }
+  }
+  if (bias_on && (lane & 15) == 0) {   // column 0: rows co = 4 fh + e of dy fragment wq
+    const int co = co0 + wm * 64 + wq * 16 + fh * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) a.wgb[(size_t)blockIdx.z * (gridDim.y * 128) + co + e] = accb[e];
   }
   // partial dW -> slab [z][Cpad][9*Kc]: C[co = 4h+e][n = r]
   const int Cpad = gridDim.y * 128;
@@ -2445,11 +1934,23 @@ __global__ __launch_bounds__(512) void wgrad3x3_halo_kernel(ConvK a, const char*
 }
 
 // dw[co][c][t] = scale * sum_z slab[z][co][t*Kc + c]; threads walk the slab contiguously (k fastest)
+// ... and with bslab: dbias[co] = scale * sum_z bslab[z][co], one wave per co in the blocks past wblocks (lanes
+// take z = lane, lane + 64, ...; fixed xor tree: deterministic)
 __global__ void wgrad_reduce_kernel(const float* slab, int splits, int KK, int Cpad, int Cout, int Ctot,
-                                    int ntaps, int Kc, float scale, float* dw) {
+                                    int ntaps, int Kc, float scale, float* dw, const float* bslab, float* dbias,
+                                    int wblocks) {
+  if ((int)blockIdx.x >= wblocks) {
+    const int co = ((int)blockIdx.x - wblocks) * (blockDim.x / 64) + (int)(threadIdx.x >> 6);
+    if (co >= Cout) return;
+    float s = 0.f;
+    for (int z = threadIdx.x & 63; z < splits; z += 64) s += bslab[(size_t)z * Cpad + co];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) dbias[co] = s * scale;
+    return;
+  }
   const int total = Cout * KK;   // < 2^31: weights of one conv
   const size_t zstride = (size_t)Cpad * KK;
-  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += wblocks * blockDim.x) {
     const int co = o / KK;
     const int k = o - co * KK;
     const int t = k / Kc, c = k - t * Kc;
@@ -2661,6 +2162,7 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
   k.act = d->act; k.ypre = (char*)d->y_pre; k.ldpre = d->ld_pre;
   k.gst = nullptr;   // set by dmc_conv2d when the chosen kernel emits the GroupNorm partials
   k.gb_on = 0;       // likewise for the GroupNorm-backward partials
+  k.wgb = nullptr;   // set by dmc_conv2d_wgrad when the bias gradient is requested
   k.M = d->N * d->OH * d->OW; k.OHW = d->OH * d->OW;
   k.sk = nullptr; k.sk_per = 0;
   {
@@ -2936,50 +2438,11 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     const int hp = (buf && p.splits == 1 && !dmc::opt(dmc::OPT_NO_HALO)) ? halo_plan(k, &R, &nimg) : 0;
     const dim3 hg(k.M / 256, dmc::cdiv(k.Cout, 128));
     const dim3 hgx = dmc::opt(dmc::OPT_NO_XCD) ? hg : dim3(hg.x * hg.y);   // 1-D: XCD-aware tile order
-    int R5, nimg5;
-    const long hver = dmc::opt(dmc::OPT_HALO_VER);   // 1: 8-wave kernel, 2: two blocks per CU, 4 / 5: experiments
+    const long hver = dmc::opt(dmc::OPT_HALO_VER);   // 1: the 8-wave kernel, 2: two blocks per CU
     int R2, nimg2;
     const int hp2 = (buf && p.splits == 1 && !dmc::opt(dmc::OPT_NO_HALO) && hver == 2) ? halo2_plan(k, &R2, &nimg2) : 0;
     if (hp2) { launch_halo2<false>(k, hp2, R2, nimg2, s); return dmc::check_launch("dmc_conv2d"); }
-    const int hp5 = (buf && p.splits == 1 && !dmc::opt(dmc::OPT_NO_HALO) && !dmc::opt(dmc::OPT_HALO_V1) &&
-                     !dmc::opt(dmc::OPT_HALO_RW) && !dmc::opt(dmc::OPT_HALO_WS4) && hver == 5 &&
-                     halo4_epilogue_ok(k)) ? halo5_plan(k, &R5, &nimg5) : 0;
-    if (hp5) {
-      const dim3 g5(k.M / 512, dmc::cdiv(k.Cout, 128));
-      const long probe = dmc::opt(dmc::OPT_HALO_PROBE);
-      const long nw = dmc::opt(dmc::OPT_HALO_WS) == 4 ? 4 : 8;   // A/B: 4-wave variant
-      if (hp5 == 40 && nw == 8) {
-        if (probe == 1) conv3x3_halo5_kernel<8, 5, 3, 1><<<g5, 512, 0, s>>>(k, R5, nimg5);
-        else if (probe == 2) conv3x3_halo5_kernel<8, 5, 3, 2><<<g5, 512, 0, s>>>(k, R5, nimg5);
-        else if (probe == 4) conv3x3_halo5_kernel<8, 5, 3, 4><<<g5, 512, 0, s>>>(k, R5, nimg5);
-        else if (probe == 18) conv3x3_halo5_kernel<8, 5, 3, 18><<<g5, 512, 0, s>>>(k, R5, nimg5);
-        else if (probe == 19) conv3x3_halo5_kernel<8, 5, 3, 19><<<g5, 512, 0, s>>>(k, R5, nimg5);
-        else conv3x3_halo5_kernel<8, 5><<<g5, 512, 0, s>>>(k, R5, nimg5);
-      } else if (hp5 == 40) {
-        conv3x3_halo5_kernel<4, 10><<<g5, 256, 0, s>>>(k, R5, nimg5);
-      } else if (nw == 8) {
-        conv3x3_halo5_kernel<8, 7><<<g5, 512, 0, s>>>(k, R5, nimg5);
-      } else {
-        conv3x3_halo5_kernel<4, 14><<<g5, 256, 0, s>>>(k, R5, nimg5);
-      }
-    } else if (hp && hver == 4 && !dmc::opt(dmc::OPT_HALO_V1) && !dmc::opt(dmc::OPT_HALO_RW) && !dmc::opt(dmc::OPT_HALO_WS4) &&
-        halo4_epilogue_ok(k)) {
-      const long probe = dmc::opt(dmc::OPT_HALO_PROBE);
-      if (hp == 6 && probe == 0) conv3x3_halo4_kernel<6><<<hg, 256, 0, s>>>(k, R, nimg);
-      else if (hp == 7 && probe == 0) conv3x3_halo4_kernel<7><<<hg, 256, 0, s>>>(k, R, nimg);
-      else if (hp == 6 && probe == 1) conv3x3_halo4_kernel<6, 1><<<hg, 256, 0, s>>>(k, R, nimg);
-      else if (hp == 6 && probe == 2) conv3x3_halo4_kernel<6, 2><<<hg, 256, 0, s>>>(k, R, nimg);
-      else if (hp == 6 && probe == 4) conv3x3_halo4_kernel<6, 4><<<hg, 256, 0, s>>>(k, R, nimg);
-      else if (hp == 6 && probe == 8) conv3x3_halo4_kernel<6, 8><<<hg, 256, 0, s>>>(k, R, nimg);
-      else if (hp == 6 && probe == 7) conv3x3_halo4_kernel<6, 7><<<hg, 256, 0, s>>>(k, R, nimg);
-      else if (hp == 6 && probe == 5) conv3x3_halo4_kernel<6, 5><<<hg, 256, 0, s>>>(k, R, nimg);
-      else if (hp == 6 && probe == 3) conv3x3_halo4_kernel<6, 3><<<hg, 256, 0, s>>>(k, R, nimg);
-      else if (hp == 6 && probe == 16) conv3x3_halo4_kernel<6, 16><<<hg, 256, 0, s>>>(k, R, nimg);
-      else if (hp == 6 && probe == 23) conv3x3_halo4_kernel<6, 23><<<hg, 256, 0, s>>>(k, R, nimg);
-      else if (hp == 6 && probe == 32) conv3x3_halo4_kernel<6, 32><<<hg, 256, 0, s>>>(k, R, nimg);
-      else if (hp == 6 && probe == 34) conv3x3_halo4_kernel<6, 34><<<hg, 256, 0, s>>>(k, R, nimg);
-      else conv3x3_halo4_kernel<7><<<hg, 256, 0, s>>>(k, R, nimg);
-    } else if (hp && dmc::opt(dmc::OPT_HALO_RW)) {
+    if (hp && dmc::opt(dmc::OPT_HALO_RW)) {
       if (hp == 6) conv3x3_halo_rw_kernel<6><<<hg, 512, 0, s>>>(k, R, nimg);
       else conv3x3_halo_rw_kernel<7><<<hg, 512, 0, s>>>(k, R, nimg);
     } else if (hp == 6 && dmc::opt(dmc::OPT_HALO_WS4))
@@ -3021,7 +2484,9 @@ int wgrad_splits(const dmc_conv_desc* d, int* pps) {
   const long tiles = (long)dmc::cdiv(KK, 128) * dmc::cdiv(d->Cout, 128);
   const long target = dmc::opt(dmc::OPT_WG_BLOCKS);   // A/B knob
   long splits = (target + tiles - 1) / tiles;
-  const long max_splits = (M + 4 * sp - 1) / (4 * sp);  // at least 4 stages per split
+  // at least DMC_WG_MINPIX pixels per split (>= 4 stages): the fp32 slab is splits x KK x Cout, written and read back
+  const long minpix = dmc::opt(dmc::OPT_WG_MINPIX) > 4 * sp ? dmc::opt(dmc::OPT_WG_MINPIX) : 4 * sp;
+  const long max_splits = (M + minpix - 1) / minpix;
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   long per = (M + splits - 1) / splits;
@@ -3128,7 +2593,7 @@ extern "C" size_t dmc_conv2d_wgrad_workspace(const dmc_conv_desc* d) {
   if (hp.ok && hp.splits > splits) splits = hp.splits;
   const size_t KK = (size_t)d->ntaps * d->Kc;
   const size_t Cpad = (size_t)dmc::cdiv(d->Cout, 128) * 128;
-  return (size_t)splits * KK * Cpad * sizeof(float);
+  return (size_t)splits * (KK + 1) * Cpad * sizeof(float);   // + the bias partials [splits][Cpad]
 }
 
 extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_dy, const void* x1, const void* x2,
@@ -3144,8 +2609,13 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   dim3 g(dmc::cdiv(KK, 128), dmc::cdiv(d->Cout, 128), splits);
   const WgHaloPlan hp = wgrad_halo_plan(d);
   const size_t dyb = (size_t)k.M * ld_dy * 2;
-  if (hp.ok && dyb < 0x7fff0000u) {
-    splits = hp.splits;
+  const bool halo = hp.ok && dyb < 0x7fff0000u;
+  if (halo) splits = hp.splits;
+  const size_t Cpad = (size_t)dmc::cdiv(d->Cout, 128) * 128;
+  // bias partials after the weight slab (dmc_conv2d_wgrad_workspace sized for the larger split count)
+  float* const bslab = d->wg_bias ? (float*)workspace + (size_t)splits * KK * Cpad : nullptr;
+  k.wgb = bslab;
+  if (halo) {
     g = dim3(d->Kc / 64, dmc::cdiv(d->Cout, 128), splits);
     if (hp.hp == 6)
       wgrad3x3_halo_kernel<6><<<g, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
@@ -3159,8 +2629,9 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   const int Ctot = d->C1 + d->C2;
   const long total = (long)d->Cout * KK;
   const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
-  wgrad_reduce_kernel<<<blocks, 256, 0, s>>>((const float*)workspace, splits, KK, (int)g.y * 128, d->Cout, Ctot,
-                                             d->ntaps, d->Kc, scale, dw);
+  const int bblocks = d->wg_bias ? dmc::cdiv(d->Cout, 4) : 0;   // one wave per bias channel
+  wgrad_reduce_kernel<<<blocks + bblocks, 256, 0, s>>>((const float*)workspace, splits, KK, (int)g.y * 128, d->Cout,
+                                                       Ctot, d->ntaps, d->Kc, scale, dw, bslab, d->wg_bias, blocks);
   return dmc::check_launch("dmc_conv2d_wgrad reduce");
 }
 

@@ -163,7 +163,10 @@ def conv_halo_prologue(d):
     return bool(LIB.dmc_conv_halo_prologue(ctypes.byref(d)))
 
 
-def wgrad(d, dy, ld_dy, x1, x2, dw, scale=1.0):
+def wgrad(d, dy, ld_dy, x1, x2, dw, scale=1.0, dbias=None):
+    """dmc_conv2d_wgrad: dw (and with dbias the bias gradient, the pixel sums of dy) from one pass over dy."""
+    d.wg_bias = ptr(dbias)
+    d._keep_wgb = dbias
     nbytes = LIB.dmc_conv2d_wgrad_workspace(ctypes.byref(d))
     ws = SCRATCH.get(nbytes, dy.device)
     PROF.wrap("wgrad", d, lambda: check(LIB.dmc_conv2d_wgrad(ctypes.byref(d), ptr(dy), ld_dy, ptr(x1), ptr(x2), ptr(ws),

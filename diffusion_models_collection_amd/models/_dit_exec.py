@@ -313,8 +313,7 @@ class DiTExecutor(ExecCore):
         ldq = (K_out + self.chunk - 1) // self.chunk * self.chunk
         dtok = torch.empty(B, ht, wt, ldq, dtype=dt, device=dev)
         K.patchify_grad(dt, dout.contiguous(), B, ht, wt, p, m.out_channels, dtok, ldq)
-        self._wgrad([Act(hf, ht, wt, H)], dtok, ldq, K.TAPS1, ht, wt, K_out, gv(fl.weight))
-        K.channel_sum(dt, dtok, B, Lt, K_out, ldq, out_c=gv(fl.bias))
+        self._wgrad([Act(hf, ht, wt, H)], dtok, ldq, K.TAPS1, ht, wt, K_out, gv(fl.weight), dbias=gv(fl.bias))
         dhf = torch.empty(B, ht, wt, H, dtype=dt, device=dev)
         self._conv([Act(dtok, ht, wt, K_out)], fl, K.TAPS1, ht, wt, H, out=dhf, packmode=L.PACK_DGRAD,
                    Kc=L.kc_for(K_out, dt))
@@ -333,14 +332,13 @@ class DiTExecutor(ExecCore):
             # MLP branch: x_out = x_mid + gate_mlp * drop(mo)
             dmo = torch.empty(B, ht, wt, H, dtype=dt, device=dev)
             K.gate_bwd(dt, dx, mo.t, H, mod2, ldm, mo_ + 5 * H, T, H, Lt, dmo, H, dmod, mo_ + 5 * H, drop=d2)
-            self._wgrad([a], dmo, H, K.TAPS1, ht, wt, H, gv(blk.mlp[3].weight))
-            K.channel_sum(dt, dmo, B, Lt, H, H, out_c=gv(blk.mlp[3].bias))
+            self._wgrad([a], dmo, H, K.TAPS1, ht, wt, H, gv(blk.mlp[3].weight), dbias=gv(blk.mlp[3].bias))
             da = torch.empty(B, ht, wt, Hm, dtype=dt, device=dev)
             self._conv([Act(dmo, ht, wt, H)], blk.mlp[3], K.TAPS1, ht, wt, Hm, out=da, packmode=L.PACK_DGRAD)
             du = torch.empty(B, ht, wt, Hm, dtype=dt, device=dev)
             K.gelu_bwd(dt, da, u.t, T, Hm, Hm, du, drop=d1)
-            self._wgrad([Act(h2, ht, wt, H)], du, Hm, K.TAPS1, ht, wt, Hm, gv(blk.mlp[0].weight))
-            K.channel_sum(dt, du, B, Lt, Hm, Hm, out_c=gv(blk.mlp[0].bias))
+            self._wgrad([Act(h2, ht, wt, H)], du, Hm, K.TAPS1, ht, wt, Hm, gv(blk.mlp[0].weight),
+                        dbias=gv(blk.mlp[0].bias))
             dh2 = torch.empty(B, ht, wt, H, dtype=dt, device=dev)
             self._conv([Act(du, ht, wt, Hm)], blk.mlp[0], K.TAPS1, ht, wt, H, out=dh2, packmode=L.PACK_DGRAD)
             K.ln_mod_bwd(dt, dh2, H, x_mid, mean2, rstd2, mod2, ldm, mo_ + 4 * H, T, H, Lt, dx, dmod, mo_ + 4 * H,
@@ -349,14 +347,13 @@ class DiTExecutor(ExecCore):
             dao = torch.empty(B, ht, wt, H, dtype=dt, device=dev)
             K.gate_bwd(dt, dx, ao.t, H, mod2, ldm, mo_ + 2 * H, T, H, Lt, dao, H, dmod, mo_ + 2 * H)
             op = blk.attn.out_proj
-            self._wgrad([o], dao, H, K.TAPS1, ht, wt, H, gv(op.weight))
-            K.channel_sum(dt, dao, B, Lt, H, H, out_c=gv(op.bias))
+            self._wgrad([o], dao, H, K.TAPS1, ht, wt, H, gv(op.weight), dbias=gv(op.bias))
             do = torch.empty(B, ht, wt, H, dtype=dt, device=dev)
             self._conv([Act(dao, ht, wt, H)], op, K.TAPS1, ht, wt, H, out=do, packmode=L.PACK_DGRAD)
             dqkv = torch.empty(B, ht, wt, 3 * H, dtype=dt, device=dev)
             K.attn_bwd(dt, qkv.t, 3 * H, o.t, do, H, lse, B, Lt, heads, hd, dqkv, 3 * H, drop=d0)
-            self._wgrad([Act(h1, ht, wt, H)], dqkv, 3 * H, K.TAPS1, ht, wt, 3 * H, gv(blk.attn.in_proj_weight))
-            K.channel_sum(dt, dqkv, B, Lt, 3 * H, 3 * H, out_c=gv(blk.attn.in_proj_bias))
+            self._wgrad([Act(h1, ht, wt, H)], dqkv, 3 * H, K.TAPS1, ht, wt, 3 * H, gv(blk.attn.in_proj_weight),
+                        dbias=gv(blk.attn.in_proj_bias))
             dh1 = torch.empty(B, ht, wt, H, dtype=dt, device=dev)
             self._conv([Act(dqkv, ht, wt, 3 * H)], self.in_proj[i], K.TAPS1, ht, wt, H, out=dh1,
                        packmode=L.PACK_DGRAD)
@@ -372,25 +369,24 @@ class DiTExecutor(ExecCore):
         if x_requires_grad:
             dxin = torch.empty(B, m.in_channels, ht * p, wt * p, dtype=f32, device=dev)
             K.patch_dgrad(dx, H, pe.weight.detach(), B, ht, wt, p, m.in_channels, H, dxin)
-        self._wgrad([xin], dx, H, self.patch_taps, ht, wt, H, gv(pe.weight), stride=p, dtype=f32)
-        K.channel_sum(f32, dx, B, Lt, H, H, out_c=gv(pe.bias))
+        self._wgrad([xin], dx, H, self.patch_taps, ht, wt, H, gv(pe.weight), stride=p, dtype=f32, dbias=gv(pe.bias))
         # ---- stacked adaLN: mod = SiLU(c) W_ada^T + b ----
         Ta = self.ada_total
         dw_a = flat[self.ada_w_off:self.ada_w_off + Ta * H]
-        self._wgrad([c], dmod, Ta, K.TAPS1, 1, 1, Ta, dw_a, pro=(L.PRO_SILU, None, None), dtype=f32)
-        K.channel_sum(f32, dmod, 1, B, Ta, Ta, out_c=flat[self.ada_b_off:self.ada_b_off + Ta])
+        self._wgrad([c], dmod, Ta, K.TAPS1, 1, 1, Ta, dw_a, pro=(L.PRO_SILU, None, None), dtype=f32,
+                    dbias=flat[self.ada_b_off:self.ada_b_off + Ta])
         dc = torch.empty(B, 1, 1, H, dtype=f32, device=dev)
         self._conv([Act(dmod.view(B, 1, 1, Ta), 1, 1, Ta)], None, K.TAPS1, 1, 1, H, out=dc, dtype=f32,
                    w=self._ada_pack_dgrad(f32), Kc=L.kc_for(Ta, f32), silu_pre=c.t, ld_silu=H)
         # ---- timestep MLP and label embedding: c = Linear2(SiLU(Linear1(tf))) + label_emb ----
         te = m.t_embedder
-        self._wgrad([A1], dc, H, K.TAPS1, 1, 1, H, gv(te.mlp[2].weight), pro=(L.PRO_SILU, None, None), dtype=f32)
-        K.channel_sum(f32, dc, 1, B, H, H, out_c=gv(te.mlp[2].bias))
+        self._wgrad([A1], dc, H, K.TAPS1, 1, 1, H, gv(te.mlp[2].weight), pro=(L.PRO_SILU, None, None), dtype=f32,
+                    dbias=gv(te.mlp[2].bias))
         de1 = torch.empty(B, 1, 1, H, dtype=f32, device=dev)
         self._conv([Act(dc, 1, 1, H)], te.mlp[2], K.TAPS1, 1, 1, H, out=de1, dtype=f32, packmode=L.PACK_DGRAD,
                    silu_pre=A1.t, ld_silu=H)
-        self._wgrad([Act(tf, 1, 1, tf.shape[-1])], de1, H, K.TAPS1, 1, 1, H, gv(te.mlp[0].weight), dtype=f32)
-        K.channel_sum(f32, de1, 1, B, H, H, out_c=gv(te.mlp[0].bias))
+        self._wgrad([Act(tf, 1, 1, tf.shape[-1])], de1, H, K.TAPS1, 1, 1, H, gv(te.mlp[0].weight), dtype=f32,
+                    dbias=gv(te.mlp[0].bias))
         if m.y_embedder is not None:
             tab = m.y_embedder.embedding_table.weight
             if ye is not None:

@@ -200,7 +200,9 @@ class ExecCore:
         return GnbReq(*K.gn_bwd_epi(x1, x2, C1, ld1, ld2, mr, gn.weight, gn.bias, G, silu, drop, N * HW, C))
 
     def _wgrad(self, srcs, dy, ld_dy, taps, OH, OW, Cout, dw, mode=L.MODE_NORMAL, stride=1, pro=None, drop=None,
-               dtype=None):
+               dtype=None, dbias=None):
+        """Weight gradient dw of a conv/linear; with dbias also its bias gradient (the pixel sums of dy), taken in
+        the same kernel (include/dmc.h dmc_conv_desc.wg_bias) instead of a separate channel-sum pass."""
         dtype = dtype or self.dt
         a = srcs[0]
         C1 = a.C
@@ -211,7 +213,7 @@ class ExecCore:
                         OH, OW, Cout, taps, mode, stride)
         if pro is not None:
             K.set_prologue(d, pro[0], pro[1], pro[2], C1 + C2, drop, C1 + C2)
-        K.wgrad(d, dy, ld_dy, a.t, srcs[1].t if len(srcs) > 1 else None, dw, self.training_grad_scale)
+        K.wgrad(d, dy, ld_dy, a.t, srcs[1].t if len(srcs) > 1 else None, dw, self.training_grad_scale, dbias=dbias)
 
     def _new(self, N, H, W, C, dtype=None):
         return Act(torch.empty(N, H, W, C, dtype=dtype or self.dt, device=self.device), H, W, C)
@@ -687,8 +689,7 @@ class UNetExecutor(ExecCore):
                 ldo = (Co + self.chunk - 1) // self.chunk * self.chunk
                 dy = K.pack_input(dt, dout.contiguous(), ldo)
                 with self._side(ao.t, dy):
-                    self._wgrad([ao], dy, ldo, K.TAPS3, H, W, Co, gv(convo.weight))
-                    K.channel_sum(dt, dy, N, H * W, Co, ldo, out_c=gv(convo.bias))
+                    self._wgrad([ao], dy, ldo, K.TAPS3, H, W, Co, gv(convo.weight), dbias=gv(convo.bias))
                 g = torch.empty(N, H, W, h.C, dtype=dt, device=dout.device)
                 dya = Act(dy, H, W, Co)
                 gnb = self._gnb_epi(h.t, None, h.C, 0, h.t.shape[-1], 0, mr, gno, True, None, N, H * W)
@@ -696,7 +697,8 @@ class UNetExecutor(ExecCore):
                            Kc=L.kc_for(Co, dt), gnb=gnb)
                 buf, acc = self._grad_target(h)
                 K.gn_bwd(dt, g, h.C, h.t, None, N, H * W, h.C, 0, h.t.shape[-1], 0, gno.num_groups, mr, gno.weight,
-                         gno.bias, True, None, buf, None, h.C, 0, acc, 0, gv(gno.weight), gv(gno.bias), part=gnb and gnb.part)
+                         gno.bias, True, None, buf, None, h.C, 0, acc, 0, gv(gno.weight), gv(gno.bias),
+                         part=gnb and gnb.part)
             elif kind == "res":
                 self._res_bwd(rec, gv)
             elif kind == "attn":
@@ -706,8 +708,8 @@ class UNetExecutor(ExecCore):
                 N = a.t.shape[0]
                 dy = out.grad
                 with self._side(a.t, dy):
-                    self._wgrad([a], dy, out.C, K.TAPS3, out.H, out.W, out.C, gv(layer.conv.weight), stride=2)
-                    K.channel_sum(dt, dy, N, out.H * out.W, out.C, out.C, out_c=gv(layer.conv.bias))
+                    self._wgrad([a], dy, out.C, K.TAPS3, out.H, out.W, out.C, gv(layer.conv.weight), stride=2,
+                                dbias=gv(layer.conv.bias))
                 buf, acc = self._grad_target(a)
                 dya = Act(dy, out.H, out.W, out.C)
                 self._conv([dya], layer.conv, K.TAPS3_DGRAD, a.H, a.W, a.C, mode=L.MODE_DILATE,
@@ -723,11 +725,10 @@ class UNetExecutor(ExecCore):
                         # and the 2x2 replication costs one streaming pass
                         up = K.upsample2x(dt, a.t, a.t.shape[-1])
                         self._wgrad([Act(up, 2 * a.H, 2 * a.W, a.C)], dy, out.C, K.TAPS3, out.H, out.W, out.C,
-                                    gv(layer.conv.weight))
+                                    gv(layer.conv.weight), dbias=gv(layer.conv.bias))
                     else:
                         self._wgrad([a], dy, out.C, K.TAPS3, out.H, out.W, out.C, gv(layer.conv.weight),
-                                    mode=L.MODE_UPSAMPLE)
-                    K.channel_sum(dt, dy, N, out.H * out.W, out.C, out.C, out_c=gv(layer.conv.bias))
+                                    mode=L.MODE_UPSAMPLE, dbias=gv(layer.conv.bias))
                 buf, acc = self._grad_target(a)
                 dya = Act(dy, out.H, out.W, out.C)
                 self._conv([dya], layer.conv, K.TAPS_UPDGRAD, a.H, a.W, a.C, stride=2, out=buf,
@@ -738,8 +739,7 @@ class UNetExecutor(ExecCore):
                 dy = h.grad
                 conv = m.input_conv
                 with self._side(xin.t, dy):
-                    self._wgrad([xin], dy, h.C, K.TAPS3, h.H, h.W, h.C, gv(conv.weight))
-                    K.channel_sum(dt, dy, N, h.H * h.W, h.C, h.C, out_c=gv(conv.bias))
+                    self._wgrad([xin], dy, h.C, K.TAPS3, h.H, h.W, h.C, gv(conv.weight), dbias=gv(conv.bias))
                 if xg:
                     ldx = xin.t.shape[-1]
                     g = torch.empty(N, h.H, h.W, ldx, dtype=dt, device=dout.device)
@@ -762,8 +762,7 @@ class UNetExecutor(ExecCore):
         HW = H * W
         # conv2 (weight, bias) and its input gradient; a2 = dropout(SiLU(GN2(h1))) was kept from forward
         with self._side(a2.t, dout):
-            self._wgrad([a2], dout, Cout, K.TAPS3, H, W, Cout, gv(conv2.weight))
-            K.channel_sum(dt, dout, N, HW, Cout, Cout, out_c=gv(conv2.bias))
+            self._wgrad([a2], dout, Cout, K.TAPS3, H, W, Cout, gv(conv2.weight), dbias=gv(conv2.bias))
         g2 = torch.empty(N, H, W, Cout, dtype=dt, device=dout.device)
         gnb2 = self._gnb_epi(h1.t, None, Cout, 0, Cout, 0, st2[2], gn2, True, drop, N, HW)
         self._conv([Act(dout, H, W, Cout)], conv2, K.TAPS3_DGRAD, H, W, Cout, out=g2, packmode=L.PACK_DGRAD,
@@ -772,10 +771,7 @@ class UNetExecutor(ExecCore):
         if isinstance(rb.shortcut, torch.nn.Conv2d):
             sc = rb.shortcut
             with self._side(*[x.t for x in srcs], dout):
-                self._wgrad(srcs, dout, Cout, K.TAPS1, H, W, Cout, gv(sc.weight))
-                # the shortcut's bias gradient is the same pixel sum of dout as conv2's (computed just above,
-                # in order on this stream): a copy instead of a second two-kernel channel sum
-                gv(sc.bias).copy_(gv(conv2.bias))
+                self._wgrad(srcs, dout, Cout, K.TAPS1, H, W, Cout, gv(sc.weight), dbias=gv(sc.bias))
             if len(srcs) == 1:
                 buf, acc = self._grad_target(a)
                 self._conv([Act(dout, H, W, Cout)], sc, K.TAPS1, H, W, C1, out=buf, resid=buf if acc else None,
@@ -848,8 +844,7 @@ class UNetExecutor(ExecCore):
         dout = out.grad
         # proj
         with self._side(o.t, dout):
-            self._wgrad([o], dout, C, K.TAPS1, H, W, C, gv(ab.proj.weight))
-            K.channel_sum(dt, dout, N, HW, C, C, out_c=gv(ab.proj.bias))
+            self._wgrad([o], dout, C, K.TAPS1, H, W, C, gv(ab.proj.weight), dbias=gv(ab.proj.bias))
         do = torch.empty(N, H, W, C, dtype=dt, device=dout.device)
         self._conv([Act(dout, H, W, C)], ab.proj, K.TAPS1, H, W, C, out=do, packmode=L.PACK_DGRAD)
         # residual: x gets dout
@@ -861,8 +856,7 @@ class UNetExecutor(ExecCore):
         dqkv = torch.empty(N, H, W, 3 * C, dtype=dt, device=dout.device)
         K.attn_bwd(dt, qkv.t, 3 * C, o.t, do, C, lse, N, HW, heads, hd, dqkv, 3 * C)
         with self._side(an.t, dqkv):
-            self._wgrad([an], dqkv, 3 * C, K.TAPS1, H, W, 3 * C, gv(ab.qkv.weight))
-            K.channel_sum(dt, dqkv, N, HW, 3 * C, 3 * C, out_c=gv(ab.qkv.bias))
+            self._wgrad([an], dqkv, 3 * C, K.TAPS1, H, W, 3 * C, gv(ab.qkv.weight), dbias=gv(ab.qkv.bias))
         g = torch.empty(N, H, W, C, dtype=dt, device=dout.device)
         gnb = self._gnb_epi(a.t, None, C, 0, C, 0, st[2], ab.norm, False, None, N, HW)
         self._conv([Act(dqkv, H, W, 3 * C)], ab.qkv, K.TAPS1, H, W, C, out=g, packmode=L.PACK_DGRAD, gnb=gnb)
@@ -881,8 +875,8 @@ class UNetExecutor(ExecCore):
         # stacked projection weights: dW[sumC][dim] -> the per-block slices are contiguous rows
         flat = self.flat
         dw_t = flat[self.temb_w_off:self.temb_w_off + T * tdim]
-        self._wgrad([A2], daddvec, T, K.TAPS1, 1, 1, T, dw_t, pro=(L.PRO_SILU, None, None), dtype=f32)
-        K.channel_sum(f32, daddvec, 1, N, T, T, out_c=flat[self.temb_b_off:self.temb_b_off + T])
+        self._wgrad([A2], daddvec, T, K.TAPS1, 1, 1, T, dw_t, pro=(L.PRO_SILU, None, None), dtype=f32,
+                    dbias=flat[self.temb_b_off:self.temb_b_off + T])
         # d(silu(e2)) * silu'(e2) -> de2 (fused in the dgrad epilogue)
         de2 = torch.empty(N, 1, 1, tdim, dtype=f32, device=daddvec.device)
         self._conv([dA], None, K.TAPS1, 1, 1, tdim, out=de2, dtype=f32, w=self._temb_pack_dgrad(0),
@@ -895,14 +889,13 @@ class UNetExecutor(ExecCore):
                        Kc=L.kc_for(T, f32), silu_pre=Ay.t, ld_silu=tdim)
             K.embed_bwd(y, m.label_embed.weight.shape[0], dye.view(N, tdim), gv(m.label_embed.weight))
         # Linear2 (te[3]) on silu(e1)
-        self._wgrad([A1], de2, tdim, K.TAPS1, 1, 1, tdim, gv(te[3].weight), pro=(L.PRO_SILU, None, None), dtype=f32)
-        K.channel_sum(f32, de2, 1, N, tdim, tdim, out_c=gv(te[3].bias))
+        self._wgrad([A1], de2, tdim, K.TAPS1, 1, 1, tdim, gv(te[3].weight), pro=(L.PRO_SILU, None, None), dtype=f32,
+                    dbias=gv(te[3].bias))
         de1 = torch.empty(N, 1, 1, tdim, dtype=f32, device=daddvec.device)
         self._conv([Act(de2, 1, 1, tdim)], te[3], K.TAPS1, 1, 1, tdim, out=de1, dtype=f32, packmode=L.PACK_DGRAD,
                    silu_pre=A1.t, ld_silu=tdim)
         # Linear1 (te[1]) on the sinusoid
-        self._wgrad([A0], de1, tdim, K.TAPS1, 1, 1, tdim, gv(te[1].weight), dtype=f32)
-        K.channel_sum(f32, de1, 1, N, tdim, tdim, out_c=gv(te[1].bias))
+        self._wgrad([A0], de1, tdim, K.TAPS1, 1, 1, tdim, gv(te[1].weight), dtype=f32, dbias=gv(te[1].bias))
 
 
 class _UNetFunction(torch.autograd.Function):

@@ -103,6 +103,8 @@ typedef struct dmc_conv_desc {
                               * GroupNorm, models/unet.py:34/:84), [M/64][Cout/8][2] = (mean, M2) over 64 pixels x 8
                               * channels, from the kernel's epilogue where it can, else one pass over y1. Needs
                               * OH*OW % 64 == 0, Cout % 8 == 0, one NHWC output. Finalised by dmc_gn_finalize. */
+  float* wg_bias;            /* dmc_conv2d_wgrad only: if set, also the bias gradient wg_bias[co] = scale * sum over
+                              * pixels of dy[pix][co] (nn.Conv2d bias), from the same pass over dy */
 } dmc_conv_desc;
 enum { DMC_ACT_NONE = 0, DMC_ACT_GELU = 1 };   /* GELU (exact): the DiT MLP (dit.py:98-99) */
 

@@ -219,12 +219,14 @@ def test_conv_dgrad_wgrad(dt, case):
     dw = torch.empty_like(w, device=DEV)
     dw_desc = K.make_desc(dt, N, H, W, Cin, 0, Cin, 0, L.kc_for(Cin, dt), OH, OW, Cout,
                           K.TAPS3 if k == 3 else K.TAPS1, mode, stride)
-    K.wgrad(dw_desc, gd, Cout, xd, None, dw)
+    db = torch.full((Cout,), float("nan"), device=DEV)
+    K.wgrad(dw_desc, gd, Cout, xd, None, dw, dbias=db)    # + the bias gradient from the same kernel
     torch.cuda.synchronize()
     e1 = rel_err(nchw(dx.float().cpu()), x.grad)
     e2 = rel_err(dw.cpu(), w.grad)
     lim = 1e-5 if dt == torch.float32 else 2e-2
     assert e1 < lim and e2 < (1e-5 if dt == torch.float32 else 1e-2), (e1, e2)
+    assert rel_err(db.cpu(), g.sum((0, 2, 3))) < 1e-5
 
 
 @pytest.mark.parametrize("variant", ["ring3", "ring4", "regw", "halo2"])
@@ -295,9 +297,12 @@ def test_conv3x3_halo_kernel(case, variant, monkeypatch, dmc_opt):
         for no_halo in ("0", "1"):
             dmc_opt("DMC_NO_HALO", int(no_halo))
             dw = torch.full(tuple(w.shape), float("nan"), device=DEV)
-            K.wgrad(d, gd, Cout, x1d, x2d, dw)
+            db = torch.full((Cout,), float("nan"), device=DEV)
+            K.wgrad(d, gd, Cout, x1d, x2d, dw, dbias=db)
             torch.cuda.synchronize()
             dws.append(dw.cpu())
+            # the bias gradient (halo kernel: dy fragments x an all-ones MFMA operand) = the pixel sums of dy
+            assert rel_err(db.cpu(), g.sum((0, 2, 3))) < 1e-5, (no_halo, rel_err(db.cpu(), g.sum((0, 2, 3))))
         assert rel_err(dws[0], wr) < 1e-2, rel_err(dws[0], wr)
         assert rel_err(dws[0], dws[1]) < 1e-3, rel_err(dws[0], dws[1])
 
