@@ -2478,7 +2478,7 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
 }
 
 int wgrad_splits(const dmc_conv_desc* d, int* pps) {
-  const int sp = d->dtype == DMC_F32 ? 32 : 64;
+  const int sp = d->dtype == DMC_F32 ? 16 : 32;   // conv_wgrad_kernel's pixels per stage (SP)
   const long M = (long)d->N * d->OH * d->OW;
   const long KK = (long)d->ntaps * d->Kc;
   const long tiles = (long)dmc::cdiv(KK, 128) * dmc::cdiv(d->Cout, 128);
