@@ -22,6 +22,8 @@ The JSON line also carries:
                 UNet (10 classes), B=128 per GPU as one 256-row forward per step
   celeba64      BASELINE config #5 on one GPU: the same network at 64x64, train img/s and DDIM-100 img/s
   fp32          the headline train step in the reference's own arithmetic (fp32 parity mode)
+  data_loader   the device-resident data path (datasets/loader.py): dmc_load_batch per batch, the train step
+                fed by it, and the oracle's per-sample transform on one host thread as its CPU baseline
   dit_s2_ddim50_cfg  BASELINE config #4: DiT-S/2 conditional DDIM-50 + CFG 3.0 sampling img/s (replicas) with
                 its MFMA roofline, and the DiT train step img/s (--no-dit skips it)
 (celeba64 / fp32 only at N=1; --no-extra skips them.) `--image-size 64 --sample-steps 100` makes config #5 the
@@ -243,6 +245,55 @@ def sample_rate(fn, world):
     return max_over_ranks(el, world)
 
 
+def data_line(trainer, dev, B, steps):
+    """The device-resident data path (datasets/loader.py): a synthetic CIFAR-shaped uint8 bank
+    (50,000 x 32 x 32 x 3) in HBM, the train transform (flip 0.5, Normalize 0.5/0.5). `kernel`: one epoch of
+    dmc_load_batch launches timed with HIP events; `train_with_loader_img_s`: the headline train step fed by the
+    loader instead of the resident synthetic pool (loader cost inside the timed region); `cpu_baseline`: the
+    oracle's per-sample transform (the reference's DataLoader worker path) on one host thread."""
+    import numpy as np
+    from diffusion_models_collection_amd.datasets import DiffusionDataset, from_arrays
+    from diffusion_models_collection_amd.datasets.loader import DeviceLoader
+    rng = np.random.default_rng(0)
+    imgs = rng.integers(0, 256, (50000, 32, 32, 3), dtype=np.uint8)
+    tr = DiffusionDataset.get_default_transform(32, "cifar10", train=True)
+    ld = DeviceLoader(from_arrays(imgs, transform=tr), B, shuffle=True, drop_last=True, device=dev)
+    it = iter(ld)
+    next(it)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    n = 0
+    for _ in it:
+        n += 1
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / max(n, 1)
+    nbytes = B * 3072 * (1 + 4)         # algorithmic: uint8 images in, fp32 NCHW out
+    # the train step fed by the loader (same timing rules as the headline)
+    it = iter(ld)
+    for _ in range(3):
+        trainer.train_step(next(it), 0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        trainer.train_step(next(it), 0)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    from oracle import data_oracle as O
+    k = 2048
+    t1 = time.perf_counter()
+    for i in range(k):
+        O.to_tensor_normalize(imgs[i], tr.mean, tr.std, flip=bool(i & 1))
+    cpu = k / (time.perf_counter() - t1)
+    return {"batch": B, "batches_timed": n, "kernel_us_per_batch": round(ms * 1e3, 2),
+            "kernel_img_s": round(B / (ms * 1e-3), 1), "kernel_gb_s": round(nbytes / (ms * 1e-3) / 1e9, 1),
+            "train_with_loader_img_s": round(B * steps / el, 2), "steps": steps,
+            "cpu_baseline": {"value": round(cpu, 1), "unit": "img/s", "cores": 1, "kind": "port",
+                             "sample": f"oracle per-sample flip+ToTensor+Normalize, {k} CIFAR images, one thread "
+                                       "(one reference DataLoader worker's transform work; the reference runs 4)"}}
+
+
 DIT_S2 = dict(img_size=(32, 32), patch_size=2, in_channels=3, hidden_size=384, depth=12, num_heads=6, mlp_ratio=4.0)
 
 
@@ -373,6 +424,8 @@ def main():
            "train_tflops_per_gpu": round(value / world * gflop / 1e3, 2)}
     if args.no_train:
         out["value"] = None
+    if args.extra and S == 32 and not args.no_train and world == 1:
+        out["data_loader"] = data_line(trainer, dev, B, args.steps)
 
     if not args.no_sample:
         model.eval()

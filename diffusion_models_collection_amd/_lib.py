@@ -140,6 +140,8 @@ def _load():
         "dmc_add_bcast": (_c_int, [_c_p, _c_p, _c_long, _c_long, _c_p]),
         "dmc_batch_sum": (_c_int, [_c_p, _c_long, _c_long, _c_p, _c_p]),
         "dmc_patch_dgrad": (_c_int, [_c_p, _c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p]),
+        "dmc_load_batch": (_c_int, [_c_p, _c_long, _c_int, _c_int, _c_int, _c_p, _c_int, _c_p, _c_u32, _c_u32, _c_long,
+                                    ctypes.POINTER(_c_f), ctypes.POINTER(_c_f), _c_p, _c_p, _c_p, _c_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

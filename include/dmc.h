@@ -342,6 +342,18 @@ int dmc_batch_sum(const float* x, long rows, long n, float* out, void* stream);
 int dmc_patch_dgrad(const float* dtok, int ld, const float* w, int B, int ht, int wt, int p, int C, int H, float* dx,
                     void* stream);
 
+/* ---- Device-resident data path (datasets/base_dataset.py:96-128, train.py:107-128) ----
+ * One training batch from a uint8 image bank [n_images][H][W][C] resident in device memory: out[b] =
+ * Normalize(ToTensor(RandomHorizontalFlip(bank[idx[b]]))) as NCHW fp32 [B][C][H][W], i.e.
+ * ((float)u / 255 - mean[c]) / std[c] with torchvision's op order (bit-exact). idx: device int32 [B], every entry
+ * in [0, n_images) (the caller validates: the kernel does not). Flip of sample b: flips[b] != 0 if flips (device
+ * uint8 [B]) is given, else hash(pos0 + b, flip_seed) < flip_thresh (flip_thresh = p * 2^32; 0 = no flip).
+ * mean/std: HOST arrays of C floats, C <= 4. labels_in (device int64 [n_images]) / labels_out (device int64 [B]):
+ * both NULL or both set; labels_out[b] = labels_in[idx[b]]. */
+int dmc_load_batch(const uint8_t* bank, long n_images, int H, int W, int C, const int32_t* idx, int B,
+                   const uint8_t* flips, uint32_t flip_seed, uint32_t flip_thresh, long pos0, const float* mean,
+                   const float* std, float* out, const int64_t* labels_in, int64_t* labels_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
