@@ -1933,6 +1933,116 @@ __global__ __launch_bounds__(512) void wgrad3x3_halo_kernel(ConvK a, const char*
   }
 }
 
+// Weight gradient of a 1x1 stride-1 conv / Linear (bf16; the DiT linears, the UNet's 1x1 convs):
+// dW[co][ci] = sum_p dy[p][co] * x[p][ci]. Block = 128 co x 128 ci over a pixel range (split-K over grid.z); 4
+// waves, 2 (co halves) x 2 (ci halves) of 64 x 64. Both operands stream as SPX-pixel x 128-channel stages DMA'd
+// straight into LDS (buffer_load ... lds; no register staging, no ds_write), 32-byte segments XOR-swizzled on the
+// source column (the dy image of wgrad3x3_halo_kernel), read transposed (ds_read_b64_tr_b16). STAGES-deep ring,
+// one barrier per stage. Requires M % SPX == 0 and whole-stage split ranges (the planner checks).
+template <int SPX, int STAGES>
+__global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char* dy, int ld_dy, int dy_bytes,
+                                                            float* slab, int KK, int pix_per_split) {
+  using T = bf16_t;
+  constexpr int OPB = SPX * 256;           // bytes per operand per stage (SPX rows of 128 bf16 channels)
+  constexpr int SB = 2 * OPB;              // stage: dy image then x image
+  constexpr int PW = SPX / 16;             // DMA pieces (4 rows x 256 B) per wave per operand per stage
+  constexpr int KS = SPX / 32;             // MFMA k-steps per stage
+  __shared__ __attribute__((aligned(16))) char lds[STAGES * SB];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave & 1, wn = wave >> 1;          // co half, ci half
+  const int ci0 = blockIdx.x * 128, co0 = blockIdx.y * 128;
+  const int p_begin = blockIdx.z * pix_per_split;
+  const int p_end = min(a.M, p_begin + pix_per_split);
+  const int nst = (p_end - p_begin) / SPX;
+  const bool first = ci0 < a.C1;
+  const char* xsrc = first ? a.x1 : a.x2;
+  const int xbytes = first ? a.x1_bytes : a.x2_bytes;
+  const int xld = first ? a.ld1 : a.ld2, xc0 = first ? ci0 : ci0 - a.C1, xcn = first ? a.C1 : a.C2;
+  // lane -> (row inside its piece, 16-byte chunk); the logical chunk comes from the row's segment swizzle
+  unsigned od[PW], ox[PW];
+#pragma unroll
+  for (int j = 0; j < PW; ++j) {
+    const int row = (wave * PW + j) * 4 + (lane >> 4);
+    const int pc = lane & 15;
+    const int col = ((((pc >> 1) ^ swz_dy(row)) << 1) | (pc & 1)) * 8;
+    od[j] = co0 + col < a.Cout ? ((unsigned)row * ld_dy + co0 + col) * 2u : kOOB;
+    ox[j] = xc0 + col < xcn ? ((unsigned)row * xld + xc0 + col) * 2u : kOOB;
+  }
+  // (kOOB + a stage offset < 2^31 stays past the buffer's num_records: still a zero read)
+  auto issue = [&](int st) {
+    char* base = lds + (st % STAGES) * SB;
+    const unsigned p0 = (unsigned)(p_begin + st * SPX);
+    dma_pieces<PW>(dy, dy_bytes, base + wave * PW * 1024, od, p0 * (unsigned)ld_dy * 2u, 0, PW);
+    dma_pieces<PW>(xsrc, xbytes, base + OPB + wave * PW * 1024, ox, p0 * (unsigned)xld * 2u, 0, PW);
+  };
+
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  // bias gradient (a.wgb, the first ci block): dy fragment times an all-ones fragment, waves split the co tiles
+  const bool bias_on = a.wgb != nullptr && blockIdx.x == 0;
+  const v4i ones = {0x3F803F80, 0x3F803F80, 0x3F803F80, 0x3F803F80};   // bf16 1.0 pairs
+  v4f accb[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  const int fh = lane >> 4, fr = lane & 15;
+
+  for (int q = 0; q < STAGES - 1 && q < nst; ++q) issue(q);
+  for (int st = 0; st < nst; ++st) {
+    // stage st has landed once only the later stages' pieces are outstanding
+    const int later = min(nst - 1, st + STAGES - 2) - st;
+    wait_vm_dyn(2 * PW * (later > 0 ? later : 0));
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    if (st + STAGES - 1 < nst) issue(st + STAGES - 1);
+    const char* D = lds + (st % STAGES) * SB;
+    const char* X = D + OPB;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      v4i fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = tr_frag<256, true>(D, ks * 32 + 8 * fh, wm * 4 + i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = tr_frag<256, true>(X, ks * 32 + 8 * fh, wn * 4 + j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
+      if (bias_on) {
+        accb[0] = mma16<T>(accb[0], fa[2 * wn], ones);
+        accb[1] = mma16<T>(accb[1], fa[2 * wn + 1], ones);
+      }
+    }
+  }
+  const int Cpad = gridDim.y * 128;
+  if (bias_on && fr == 0) {   // column 0 of the all-ones product: rows co = 4 fh + e of dy fragments 2wn, 2wn+1
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int co = co0 + wm * 64 + (2 * wn + u) * 16 + fh * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a.wgb[(size_t)blockIdx.z * Cpad + co + e] = accb[u][e];
+    }
+  }
+  // partial dW -> slab [z][Cpad][KK]: C[co = 4 fh + e][ci = fr]
+  float* out = slab + (size_t)blockIdx.z * KK * Cpad;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = ci0 + wn * 64 + j * 16 + fr;
+    if (k >= KK) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = co0 + wm * 64 + i * 16 + fh * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[(size_t)(co + e) * KK + k] = acc[i][j][e];
+    }
+  }
+}
+
 // dw[co][c][t] = scale * sum_z slab[z][co][t*Kc + c]; threads walk the slab contiguously (k fastest)
 // ... and with bslab: dbias[co] = scale * sum_z bslab[z][co], one wave per co in the blocks past wblocks (lanes
 // take z = lane, lane + 64, ...; fixed xor tree: deterministic)
@@ -2611,6 +2721,21 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   const size_t dyb = (size_t)k.M * ld_dy * 2;
   const bool halo = hp.ok && dyb < 0x7fff0000u;
   if (halo) splits = hp.splits;
+  // 1x1 stride-1 bf16 (Linear-shaped): both operands DMA'd into LDS (wgrad1x1_glds_kernel); splits are whole
+  // SPX-pixel stages, never more than wgrad_splits() counted (the workspace query's bound)
+  const long w1 = halo ? 0 : dmc::opt(dmc::OPT_WG_1X1);
+  const int spx = w1 == 2 ? 32 : 64;
+  const bool direct = d->ntaps == 1 && k.stride == 1 && k.mode == DMC_MODE_NORMAL && k.tdy0 == 0 && k.tdx0 == 0 &&
+                      k.H == k.OH && k.W == k.OW && k.prologue == DMC_PRO_NONE;
+  const bool w1x1 = w1 != 0 && d->dtype == DMC_BF16 && direct && k.M % spx == 0 && d->Cout % 8 == 0 &&
+                    ld_dy % 8 == 0 && k.C1 % 8 == 0 && k.C2 % 8 == 0 && (k.C2 == 0 || k.C1 % 128 == 0) &&
+                    k.ld1 % 8 == 0 && (k.C2 == 0 || k.ld2 % 8 == 0) && k.x1_bytes > 0 && (k.C2 == 0 || k.x2_bytes > 0) &&
+                    dyb < 0x7fff0000u;
+  int pps1 = 0;
+  if (w1x1) {
+    pps1 = dmc::cdiv(dmc::cdiv(k.M, splits), spx) * spx;
+    splits = dmc::cdiv(k.M, pps1);
+  }
   const size_t Cpad = (size_t)dmc::cdiv(d->Cout, 128) * 128;
   // bias partials after the weight slab (dmc_conv2d_wgrad_workspace sized for the larger split count)
   float* const bslab = d->wg_bias ? (float*)workspace + (size_t)splits * KK * Cpad : nullptr;
@@ -2621,6 +2746,11 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
       wgrad3x3_halo_kernel<6><<<g, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
     else
       wgrad3x3_halo_kernel<7><<<g, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
+  } else if (w1x1) {
+    g.z = splits;
+    if (w1 == 2) wgrad1x1_glds_kernel<32, 4><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1);
+    else if (w1 == 3) wgrad1x1_glds_kernel<64, 3><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1);
+    else wgrad1x1_glds_kernel<64, 2><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1);
   } else if (d->dtype == DMC_F32)
     conv_wgrad_kernel<float><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (float*)workspace, KK, pps);
   else

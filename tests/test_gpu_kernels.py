@@ -803,3 +803,32 @@ def test_conv_epilogue_groupnorm_backward_partials(case, silu, dropout, dmc_opt)
     torch.cuda.synchronize()
     for a, b in zip(outs[0], outs[1]):
         assert rel_err(a.float(), b.float()) < (2e-3 if a.dtype == dt else 1e-5), (case, rel_err(a.float(), b.float()))
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("case", ["linear", "concat", "ragged", "split_tail"])
+def test_wgrad1x1_glds(case, variant, dmc_opt):
+    """1x1 / Linear weight gradients (wgrad1x1_glds_kernel: both operands LDS-DMA'd, DMC_WG_1X1 = 1: 64-pixel
+    stages x 2, 2: 32 x 4, 3: 64 x 3; 0: the register-staged generic kernel) and the bias gradient from the same
+    launch vs an fp32 matmul of the same bf16 operands."""
+    L, K = _lib()
+    dmc_opt("DMC_WG_1X1", variant)
+    dt = torch.bfloat16
+    torch.manual_seed(7)
+    N, H, W, C1, C2, Cout = {"linear": (16, 16, 16, 384, 0, 1152), "concat": (8, 16, 16, 256, 128, 256),
+                             "ragged": (4, 8, 8, 96, 0, 200), "split_tail": (3, 8, 8, 64, 0, 64)}[case]
+    M = N * H * W
+    x1 = torch.randn(M, C1).to(dt)
+    x2 = torch.randn(M, C2).to(dt) if C2 else None
+    g = torch.randn(M, Cout).to(dt)
+    xs = torch.cat([x1, x2], 1) if C2 else x1
+    ref_w = (g.float().t() @ xs.float())                           # [Cout, Cin]
+    Cin = C1 + C2
+    d = K.make_desc(dt, N, H, W, C1, C2, C1, C2, L.kc_for(Cin, dt), H, W, Cout, K.TAPS1)
+    dw = torch.full((Cout, Cin, 1, 1), float("nan"), device=DEV)
+    db = torch.full((Cout,), float("nan"), device=DEV)
+    K.wgrad(d, g.to(DEV).view(N, H, W, Cout), Cout, x1.to(DEV).view(N, H, W, C1),
+            x2.to(DEV).view(N, H, W, C2) if C2 else None, dw, dbias=db)
+    torch.cuda.synchronize()
+    assert rel_err(dw.cpu().view(Cout, Cin), ref_w) < 1e-5
+    assert rel_err(db.cpu(), g.float().sum(0)) < 1e-5
