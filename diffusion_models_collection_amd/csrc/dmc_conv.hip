@@ -1941,7 +1941,8 @@ __global__ __launch_bounds__(512) void wgrad3x3_halo_kernel(ConvK a, const char*
 // one barrier per stage. Requires M % SPX == 0 and whole-stage split ranges (the planner checks).
 template <int SPX, int STAGES>
 __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char* dy, int ld_dy, int dy_bytes,
-                                                            float* slab, int KK, int pix_per_split) {
+                                                            float* slab, int KK, int pix_per_split, int nci, int nco,
+                                                            int xcd) {
   using T = bf16_t;
   constexpr int OPB = SPX * 256;           // bytes per operand per stage (SPX rows of 128 bf16 channels)
   constexpr int SB = 2 * OPB;              // stage: dy image then x image
@@ -1952,8 +1953,15 @@ __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char*
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave & 1, wn = wave >> 1;          // co half, ci half
-  const int ci0 = blockIdx.x * 128, co0 = blockIdx.y * 128;
-  const int p_begin = blockIdx.z * pix_per_split;
+  // 1-D grid over (ci tile, co tile, split), ci fastest. XCD-aware: workgroups are dealt to the 8 XCDs round-robin,
+  // so block b takes tile (b mod 8) * (n / 8) + b / 8 -- each XCD works on a contiguous tile range, and the blocks
+  // that share a dy slice (same co tile and split) or an x slice (same ci tile and split) read it through one L2
+  const int bid = blockIdx.x, per8 = (int)(gridDim.x >> 3);
+  const int t = (xcd && bid < (per8 << 3)) ? (bid & 7) * per8 + (bid >> 3) : bid;
+  const int zb = t / (nci * nco), rem = t - zb * nci * nco;
+  const int cob = rem / nci, cib = rem - cob * nci;
+  const int ci0 = cib * 128, co0 = cob * 128;
+  const int p_begin = zb * pix_per_split;
   const int p_end = min(a.M, p_begin + pix_per_split);
   const int nst = (p_end - p_begin) / SPX;
   const bool first = ci0 < a.C1;
@@ -1984,7 +1992,7 @@ __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char*
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
   // bias gradient (a.wgb, the first ci block): dy fragment times an all-ones fragment, waves split the co tiles
-  const bool bias_on = a.wgb != nullptr && blockIdx.x == 0;
+  const bool bias_on = a.wgb != nullptr && cib == 0;
   const v4i ones = {0x3F803F80, 0x3F803F80, 0x3F803F80, 0x3F803F80};   // bf16 1.0 pairs
   v4f accb[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   const int fh = lane >> 4, fr = lane & 15;
@@ -2019,17 +2027,17 @@ __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char*
       }
     }
   }
-  const int Cpad = gridDim.y * 128;
+  const int Cpad = nco * 128;
   if (bias_on && fr == 0) {   // column 0 of the all-ones product: rows co = 4 fh + e of dy fragments 2wn, 2wn+1
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int co = co0 + wm * 64 + (2 * wn + u) * 16 + fh * 4;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) a.wgb[(size_t)blockIdx.z * Cpad + co + e] = accb[u][e];
+      for (int e = 0; e < 4; ++e) a.wgb[(size_t)zb * Cpad + co + e] = accb[u][e];
     }
   }
   // partial dW -> slab [z][Cpad][KK]: C[co = 4 fh + e][ci = fr]
-  float* out = slab + (size_t)blockIdx.z * KK * Cpad;
+  float* out = slab + (size_t)zb * KK * Cpad;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int k = ci0 + wn * 64 + j * 16 + fr;
@@ -2748,9 +2756,17 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
       wgrad3x3_halo_kernel<7><<<g, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
   } else if (w1x1) {
     g.z = splits;
-    if (w1 == 2) wgrad1x1_glds_kernel<32, 4><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1);
-    else if (w1 == 3) wgrad1x1_glds_kernel<64, 3><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1);
-    else wgrad1x1_glds_kernel<64, 2><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1);
+    const dim3 g1(g.x * g.y * g.z);
+    const int xcd = (dmc::opt(dmc::OPT_NO_XCD) || w1 == 4) ? 0 : 1;   // DMC_WG_1X1=4: variant 1 without the XCD order
+    if (w1 == 2)
+      wgrad1x1_glds_kernel<32, 4><<<g1, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1,
+                                                    (int)g.x, (int)g.y, xcd);
+    else if (w1 == 3)
+      wgrad1x1_glds_kernel<64, 3><<<g1, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1,
+                                                    (int)g.x, (int)g.y, xcd);
+    else
+      wgrad1x1_glds_kernel<64, 2><<<g1, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1,
+                                                    (int)g.x, (int)g.y, xcd);
   } else if (d->dtype == DMC_F32)
     conv_wgrad_kernel<float><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (float*)workspace, KK, pps);
   else
