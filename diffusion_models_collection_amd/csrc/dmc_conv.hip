@@ -1933,6 +1933,167 @@ __global__ __launch_bounds__(512) void wgrad3x3_halo_kernel(ConvK a, const char*
   }
 }
 
+// Two-blocks-per-CU twin of wgrad3x3_halo_kernel (the step conv3x3_halo2_kernel made for the forward): block =
+// (64-channel chunk of x, 64 output channels, a range of 256-pixel tiles), 4 waves, each 64 co x 144 n (9 of the
+// 36 16-wide n tiles = taps x channel column tiles), ONE x halo buffer (reloaded per tile: the other block on
+// the CU computes meanwhile) and a 3-slot ring of 64-pixel x 64-co dy stages in 128-byte rows (swz_x images, read
+// with tr_frag<128, false>). LDS: HP x 8 KB + 24 KB <= 80 KB.
+template <int HP>
+__global__ __launch_bounds__(256, 2) void wgrad3x3_halo2_kernel(ConvK a, const char* dy, int ld_dy, int dy_bytes,
+                                                             float* slab, int R, int nimg, int tiles_per_split) {
+  using T = bf16_t;
+  constexpr int HB = HP * 8 * 1024;      // halo buffer bytes (8 * HP pieces of 8 pixels x 128 B)
+  constexpr int HPW = 2 * HP;            // halo pieces per wave
+  constexpr int DB = 64 * 128;           // dy stage: 64 pixels x 64 co
+  __shared__ __attribute__((aligned(16))) char lds[HB + 3 * DB];
+  char* const dring = lds + HB;
+
+  const int lane = threadIdx.x & 63;
+  const int wq = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // n quarter
+  const int c0 = blockIdx.x * 64, co0 = blockIdx.y * 64;
+  const int ntiles = a.M / 256;
+  const int t_begin = blockIdx.z * tiles_per_split, t_end = min(ntiles, t_begin + tiles_per_split);
+  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
+  const bool first = c0 < a.C1;
+  const int cs = first ? c0 : c0 - a.C1;
+  const int lds_x = first ? a.ld1 : a.ld2;
+
+  // dy DMA: 2 pieces per wave per stage, piece = 8 pixel rows x 128 B; chunk-level source swizzle
+  unsigned od[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = (wq * 2 + j) * 8 + (lane >> 3);
+    const int pc = lane & 7;
+    const int lc = (((pc >> 1) ^ swz_x(row)) << 1) | (pc & 1);
+    const int co = co0 + lc * 8;
+    od[j] = co < a.Cout ? ((unsigned)row * ld_dy + co) * 2u : kOOB;
+  }
+  unsigned hx[HPW];
+  auto halo_offsets = [&](int tile) {
+    const int m0 = tile * 256;
+    const int n_first = m0 / a.OHW;
+    const int r0 = (m0 - n_first * a.OHW) / OW;
+#pragma unroll
+    for (int p = 0; p < HPW; ++p) {
+      const int h = (wq * HPW + p) * 8 + (lane >> 3);
+      hx[p] = kOOB;
+      if (h < npix) {
+        const int img = h / segpix, rem = h - img * segpix;
+        const int hr = rem / HW, hc = rem - hr * HW;
+        const int iy = r0 + hr - 1, ix = hc - 1;
+        const int lc = ((((lane & 7) >> 1) ^ swz_x(h)) << 1) | (lane & 1);
+        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+          hx[p] = ((unsigned)(((n_first + img) * a.H + iy) * a.W + ix) * lds_x + cs + lc * 8) * 2u;
+      }
+    }
+  };
+  auto dy_issue = [&](int st) {  // global stage index -> pixels [st*64, st*64+64) of the block's tile range
+    const int tile = t_begin + (st >> 2);
+    const unsigned base = (unsigned)(tile * 256 + (st & 3) * 64) * (unsigned)ld_dy * 2u;
+    dma_pieces<2>(dy, dy_bytes, dring + (st % 3) * DB + wq * 2 * 1024, od, base, 0, 2);
+  };
+
+  const int fh = lane >> 4;
+  auto hrow = [&](int pl) {
+    const int img = pl / (R * OW), rem = pl - img * (R * OW);
+    const int r = rem / OW, col = rem - r * OW;
+    return img * segpix + (r + 1) * HW + col + 1;
+  };
+  const int hb0 = hrow(8 * fh), hz = hrow(0);
+  int dl[9];
+#pragma unroll
+  for (int u = 0; u < 9; ++u) {
+    const int nt = wq * 9 + u, t = nt >> 2;
+    const int ty = t / 3, tx = t - ty * 3;
+    dl[u] = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
+  }
+
+  v4f acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int u = 0; u < 9; ++u) acc[i][u] = v4f{0.f, 0.f, 0.f, 0.f};
+  const bool bias_on = a.wgb != nullptr && blockIdx.x == 0;
+  const v4i ones = {0x3F803F80, 0x3F803F80, 0x3F803F80, 0x3F803F80};   // bf16 1.0 pairs
+  v4f accb = {0.f, 0.f, 0.f, 0.f};
+
+  const int nt_blk = t_end - t_begin, nst = nt_blk * 4;
+  for (int st = 0; st < nst; ++st) {
+    const int tl = st >> 2, k = st & 3;
+    if (k == 0) {
+      // the tile's halo into the single buffer: every wave is done with the previous tile (its dy slots too)
+      if (st > 0) __syncthreads();
+      halo_offsets(t_begin + tl);
+      dma_pieces<HPW>(first ? (const void*)a.x1 : (const void*)a.x2, first ? a.x1_bytes : a.x2_bytes,
+                      lds + wq * HPW * 1024, hx, 0u, 0, HPW);
+      if (st == 0) {
+        dy_issue(0);
+        if (nst > 1) dy_issue(1);
+      }
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    } else {
+      // dy stage st has landed once only stage st+1 (issued one stage earlier) may be outstanding
+      wait_vm_dyn(st + 1 < nst ? 2 : 0);
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    if (st + 2 < nst) dy_issue(st + 2);
+    const char* X = lds;
+    const char* D = dring + (st % 3) * DB;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int j = k * 2 + ks;                          // 32-pixel group inside the tile
+      const int hj = __builtin_amdgcn_readfirstlane(hrow(32 * j) - hz);
+      v4i fa[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = tr_frag<128, false>(D, ks * 32 + 8 * fh, i);
+      v4i fb = tr_frag<128, false>(X, hb0 + hj + dl[0], (wq * 9) & 3);
+#pragma unroll
+      for (int u = 0; u < 9; ++u) {
+        v4i fn = fb;
+        if (u + 1 < 9) fn = tr_frag<128, false>(X, hb0 + hj + dl[u + 1], (wq * 9 + u + 1) & 3);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][u] = mma16<T>(acc[i][u], fa[i], fb);
+        if (u + 1 < 9) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the next tile's reads
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // this tile's MFMAs
+        }
+        fb = fn;
+      }
+      if (bias_on) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (i == wq) accb = mma16<T>(accb, fa[i], ones);
+      }
+    }
+  }
+  const int Cpad = (a.Cout + 127) / 128 * 128;   // the slab layout of wgrad3x3_halo_kernel
+  if (bias_on && (lane & 15) == 0) {   // column 0: rows co = 4 fh + e of dy fragment wq
+    const int co = co0 + wq * 16 + fh * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (co + e < a.Cout) a.wgb[(size_t)blockIdx.z * Cpad + co + e] = accb[e];
+  }
+  const int KK = 9 * a.Kc;
+  float* out = slab + (size_t)blockIdx.z * Cpad * KK;
+  const int fr = lane & 15;
+#pragma unroll
+  for (int u = 0; u < 9; ++u) {
+    const int nt = wq * 9 + u, t = nt >> 2;
+    const int kk = t * a.Kc + c0 + (nt & 3) * 16 + fr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = co0 + i * 16 + fh * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (co + e < Cpad) out[(size_t)(co + e) * KK + kk] = acc[i][u][e];
+    }
+  }
+}
+
 // Weight gradient of a 1x1 stride-1 conv / Linear (bf16; the DiT linears, the UNet's 1x1 convs):
 // dW[co][ci] = sum_p dy[p][co] * x[p][ci]. Block = 128 co x 128 ci over a pixel range (split-K over grid.z); 4
 // waves, 2 (co halves) x 2 (ci halves) of 64 x 64. Both operands stream as SPX-pixel x 128-channel stages DMA'd
@@ -2748,7 +2909,15 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   // bias partials after the weight slab (dmc_conv2d_wgrad_workspace sized for the larger split count)
   float* const bslab = d->wg_bias ? (float*)workspace + (size_t)splits * KK * Cpad : nullptr;
   k.wgb = bslab;
-  if (halo) {
+  if (halo && dmc::opt(dmc::OPT_WG_HALO_VER) == 2) {
+    // two blocks per CU: 64-co blocks, the same split count (twice the co tiles, half the block target's share)
+    g = dim3(d->Kc / 64, dmc::cdiv(d->Cout, 64), splits);
+    if (hp.hp == 6)
+      wgrad3x3_halo2_kernel<6><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
+    else
+      wgrad3x3_halo2_kernel<7><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
+    g.y = dmc::cdiv(d->Cout, 128);   // the reduce's slab pitch: Cout rounded to 128
+  } else if (halo) {
     g = dim3(d->Kc / 64, dmc::cdiv(d->Cout, 128), splits);
     if (hp.hp == 6)
       wgrad3x3_halo_kernel<6><<<g, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
