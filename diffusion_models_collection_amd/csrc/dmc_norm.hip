@@ -354,19 +354,22 @@ __global__ __launch_bounds__(256) void gn_bwd_final(int C, int G, int HW, int sp
 // sample n, reduces the per-channel sums in LDS (fixed order) and writes A and the apply coefficients exactly
 // as gn_bwd_final does. Used at N >= 64 where HW*C <= 64K (the 16x16 and smaller levels): there the two-kernel
 // form is launch-latency bound (~6 us for the final kernel alone).
+// grid.y = S channel slices (whole groups each): S blocks per sample so that the walk of a 16x16 level spreads over
+// S x N CUs (one 1024-thread block per sample used only half the chip at B = 128).
 template <typename T>
 __global__ __launch_bounds__(1024) void gn_bwd_one(GnBwd b, float* A /*[n][C][2]*/, float* cf /*[6][N][C]*/) {
   constexpr int EPC = TT<T>::KPL;
   const int n = blockIdx.x, N = gridDim.x;
   const uint32_t dseed = drop_seed(b.dseed, b.dseed_base);
   const int C = b.s.C1 + b.s.C2, cpg = C / b.G, G = b.G;
-  const int CPR = C / EPC, rpi = 1024 / CPR;
+  const int Cs = C / (int)gridDim.y, cb = (int)blockIdx.y * Cs, g0 = cb / cpg;   // this block's channel slice
+  const int CPR = Cs / EPC, rpi = 1024 / CPR;
   const int tid = threadIdx.x, col = tid % CPR, r0 = tid / CPR;
   const bool active = r0 < rpi;
   __shared__ float red[1024][2 * EPC];
   __shared__ float sA[1024][2];
   __shared__ float sm[64][2];
-  const int c0 = col * EPC;
+  const int c0 = cb + col * EPC;
   float mean[EPC], rstd[EPC], gm[EPC], bt[EPC], a1[EPC], a2[EPC];
 #pragma unroll
   for (int e = 0; e < EPC; ++e) {
@@ -410,28 +413,29 @@ __global__ __launch_bounds__(1024) void gn_bwd_one(GnBwd b, float* A /*[n][C][2]
 #pragma unroll
   for (int e = 0; e < EPC; ++e) { red[tid][2 * e] = active ? a1[e] : 0.f; red[tid][2 * e + 1] = active ? a2[e] : 0.f; }
   __syncthreads();
-  onecta_chan_totals<EPC>(red, C, CPR, rpi, sA);
+  onecta_chan_totals<EPC>(red, Cs, CPR, rpi, sA);   // sA[c - cb]
   __syncthreads();
-  for (int c = tid; c < C; c += 1024) {
+  for (int c = tid; c < Cs; c += 1024) {
     const float v1 = sA[c][0], v2 = sA[c][1];
-    A[((size_t)n * C + c) * 2] = v1;
-    A[((size_t)n * C + c) * 2 + 1] = v2;
+    A[((size_t)n * C + cb + c) * 2] = v1;
+    A[((size_t)n * C + cb + c) * 2 + 1] = v2;
   }
   const float cnt = (float)cpg * (float)b.HW;
   const int wv = tid >> 6, ln = tid & 63;
-  for (int g = wv; g < G; g += 16) {   // one wave per group: gamma-weighted channel totals
+  for (int gl = wv; gl < Cs / cpg; gl += 16) {   // one wave per group: gamma-weighted channel totals
+    const int g = g0 + gl;
     float m1 = 0.f, m2 = 0.f;
     for (int c = g * cpg + ln; c < (g + 1) * cpg; c += 64) {
       const float g_ = b.gamma ? b.gamma[c] : 1.f;
-      m1 = fmaf(sA[c][0], g_, m1); m2 = fmaf(sA[c][1], g_, m2);
+      m1 = fmaf(sA[c - cb][0], g_, m1); m2 = fmaf(sA[c - cb][1], g_, m2);
     }
     m1 = wave_sum(m1); m2 = wave_sum(m2);
-    if (ln == 0) { sm[g][0] = m1 / cnt; sm[g][1] = m2 / cnt; }
+    if (ln == 0) { sm[gl][0] = m1 / cnt; sm[gl][1] = m2 / cnt; }
   }
   __syncthreads();
   const size_t NC = (size_t)N * C;
-  for (int c = tid; c < C; c += 1024) {
-    const int g = c / cpg;
+  for (int cl = tid; cl < Cs; cl += 1024) {
+    const int c = cb + cl, g = c / cpg, gl = g - g0;
     const float mu = b.mr[((size_t)n * G + g) * 2], rs = b.mr[((size_t)n * G + g) * 2 + 1];
     const float g_ = b.gamma ? b.gamma[c] : 1.f, bb = b.beta ? b.beta[c] : 0.f;
     const size_t i = (size_t)n * C + c;
@@ -439,9 +443,9 @@ __global__ __launch_bounds__(1024) void gn_bwd_one(GnBwd b, float* A /*[n][C][2]
     cf[i] = sc;
     cf[NC + i] = bb - mu * sc;
     cf[2 * NC + i] = sc;
-    cf[3 * NC + i] = -rs * rs * sm[g][1];
+    cf[3 * NC + i] = -rs * rs * sm[gl][1];
     cf[4 * NC + i] = mu;
-    cf[5 * NC + i] = -rs * sm[g][0];
+    cf[5 * NC + i] = -rs * sm[gl][0];
   }
 }
 
@@ -911,7 +915,11 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
     DMC_REQUIRE(HW % 64 == 0, "gn_bwd: partials need HW %% 64 == 0");
     gn_bwd_final<<<N, 256, 0, s>>>(C, G, HW, HW / 64, part, mean_rstd, gamma, beta, A, cf);
   } else if (dtype != DMC_F32 && N >= 64 && (long)HW * C <= one_max && !dmc::opt(dmc::OPT_GN_BWD_SPLIT)) {
-    gn_bwd_one<bf16_t><<<N, 1024, 0, s>>>(b, A, cf);
+    // channel slices per sample (DMC_GN_BWD_SLICES): whole groups, whole 8-channel chunks
+    int S = (int)dmc::opt(dmc::OPT_GN_BWD_SLICES);
+    while (S > 1 && (C % S || (C / S) % (C / G) || (C / S) % epc)) --S;
+    if (S < 1) S = 1;
+    gn_bwd_one<bf16_t><<<dim3(N, S), 1024, 0, s>>>(b, A, cf);
   } else {
     if (dtype == DMC_F32) gn_bwd_partial<float><<<gr, 256, 0, s>>>(b, partial);
     else gn_bwd_partial<bf16_t><<<gr, 256, 0, s>>>(b, partial);
