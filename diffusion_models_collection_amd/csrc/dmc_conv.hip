@@ -2100,7 +2100,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_halo2_kernel(ConvK a, const c
 // straight into LDS (buffer_load ... lds; no register staging, no ds_write), 32-byte segments XOR-swizzled on the
 // source column (the dy image of wgrad3x3_halo_kernel), read transposed (ds_read_b64_tr_b16). STAGES-deep ring,
 // one barrier per stage. Requires M % SPX == 0 and whole-stage split ranges (the planner checks).
-template <int SPX, int STAGES>
+template <int SPX, int STAGES, bool TAPS = false>
 __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char* dy, int ld_dy, int dy_bytes,
                                                             float* slab, int KK, int pix_per_split, int nci, int nco,
                                                             int xcd) {
@@ -2125,10 +2125,13 @@ __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char*
   const int p_begin = zb * pix_per_split;
   const int p_end = min(a.M, p_begin + pix_per_split);
   const int nst = (p_end - p_begin) / SPX;
-  const bool first = ci0 < a.C1;
+  // TAPS: the block's 128 kk columns lie in one tap (Kc % 128 == 0): kk = tap * Kc + channel
+  const int tap = TAPS ? ci0 / a.Kc : 0;
+  const int cc0 = TAPS ? ci0 - tap * a.Kc : ci0;
+  const bool first = cc0 < a.C1;
   const char* xsrc = first ? a.x1 : a.x2;
   const int xbytes = first ? a.x1_bytes : a.x2_bytes;
-  const int xld = first ? a.ld1 : a.ld2, xc0 = first ? ci0 : ci0 - a.C1, xcn = first ? a.C1 : a.C2;
+  const int xld = first ? a.ld1 : a.ld2, xc0 = first ? cc0 : cc0 - a.C1, xcn = first ? a.C1 : a.C2;
   // lane -> (row inside its piece, 16-byte chunk); the logical chunk comes from the row's segment swizzle
   unsigned od[PW], ox[PW];
 #pragma unroll
@@ -2137,14 +2140,27 @@ __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char*
     const int pc = lane & 15;
     const int col = ((((pc >> 1) ^ swz_dy(row)) << 1) | (pc & 1)) * 8;
     od[j] = co0 + col < a.Cout ? ((unsigned)row * ld_dy + co0 + col) * 2u : kOOB;
-    ox[j] = xc0 + col < xcn ? ((unsigned)row * xld + xc0 + col) * 2u : kOOB;
+    ox[j] = xc0 + col < xcn ? ((unsigned)(TAPS ? 0 : row) * xld + xc0 + col) * 2u : kOOB;
   }
   // (kOOB + a stage offset < 2^31 stays past the buffer's num_records: still a zero read)
+  unsigned oxs[PW];   // TAPS: per-stage source offsets of the x rows (the tap's source pixel, or kOOB = zero)
   auto issue = [&](int st) {
     char* base = lds + (st % STAGES) * SB;
     const unsigned p0 = (unsigned)(p_begin + st * SPX);
     dma_pieces<PW>(dy, dy_bytes, base + wave * PW * 1024, od, p0 * (unsigned)ld_dy * 2u, 0, PW);
-    dma_pieces<PW>(xsrc, xbytes, base + OPB + wave * PW * 1024, ox, p0 * (unsigned)xld * 2u, 0, PW);
+    if constexpr (TAPS) {
+#pragma unroll
+      for (int j = 0; j < PW; ++j) {
+        const int pix = (int)p0 + (wave * PW + j) * 4 + (lane >> 4);
+        const int n = pix / a.OHW, rem = pix - n * a.OHW;
+        const int oy = rem / a.OW, oxx = rem - oy * a.OW;
+        const int sp = src_pixel(a, n, oy, oxx, tap);
+        oxs[j] = (sp >= 0 && ox[j] != kOOB) ? (unsigned)sp * (unsigned)xld * 2u + ox[j] : kOOB;
+      }
+      dma_pieces<PW>(xsrc, xbytes, base + OPB + wave * PW * 1024, oxs, 0u, 0, PW);
+    } else {
+      dma_pieces<PW>(xsrc, xbytes, base + OPB + wave * PW * 1024, ox, p0 * (unsigned)xld * 2u, 0, PW);
+    }
   };
 
   v4f acc[4][4];
@@ -2893,10 +2909,13 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   // 1x1 stride-1 bf16 (Linear-shaped): both operands DMA'd into LDS (wgrad1x1_glds_kernel); splits are whole
   // SPX-pixel stages, never more than wgrad_splits() counted (the workspace query's bound)
   const long w1 = halo ? 0 : dmc::opt(dmc::OPT_WG_1X1);
-  const int spx = w1 == 2 ? 32 : 64;
   const bool direct = d->ntaps == 1 && k.stride == 1 && k.mode == DMC_MODE_NORMAL && k.tdy0 == 0 && k.tdx0 == 0 &&
                       k.H == k.OH && k.W == k.OW && k.prologue == DMC_PRO_NONE;
-  const bool w1x1 = w1 != 0 && d->dtype == DMC_BF16 && direct && k.M % spx == 0 && d->Cout % 8 == 0 &&
+  const int spx = (w1 == 2 && direct) ? 32 : 64;
+  // any tap grid / stride / upsample mode (TAPS): a 128-wide kk block must stay inside one tap
+  const bool wtaps = !direct && w1 != 0 && k.prologue == DMC_PRO_NONE && d->Kc % 128 == 0 &&
+                     dmc::opt(dmc::OPT_WG_TAPS);
+  const bool w1x1 = w1 != 0 && d->dtype == DMC_BF16 && (direct || wtaps) && k.M % spx == 0 && d->Cout % 8 == 0 &&
                     ld_dy % 8 == 0 && k.C1 % 8 == 0 && k.C2 % 8 == 0 && (k.C2 == 0 || k.C1 % 128 == 0) &&
                     k.ld1 % 8 == 0 && (k.C2 == 0 || k.ld2 % 8 == 0) && k.x1_bytes > 0 && (k.C2 == 0 || k.x2_bytes > 0) &&
                     dyb < 0x7fff0000u;
@@ -2927,7 +2946,10 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
     g.z = splits;
     const dim3 g1(g.x * g.y * g.z);
     const int xcd = (dmc::opt(dmc::OPT_NO_XCD) || w1 == 4) ? 0 : 1;   // DMC_WG_1X1=4: variant 1 without the XCD order
-    if (w1 == 2)
+    if (!direct)
+      wgrad1x1_glds_kernel<64, 2, true><<<g1, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK,
+                                                          pps1, (int)g.x, (int)g.y, xcd);
+    else if (w1 == 2)
       wgrad1x1_glds_kernel<32, 4><<<g1, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1,
                                                     (int)g.x, (int)g.y, xcd);
     else if (w1 == 3)

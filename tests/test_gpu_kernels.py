@@ -832,3 +832,36 @@ def test_wgrad1x1_glds(case, variant, dmc_opt):
     torch.cuda.synchronize()
     assert rel_err(dw.cpu().view(Cout, Cin), ref_w) < 1e-5
     assert rel_err(db.cpu(), g.float().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("on", [0, 1])
+@pytest.mark.parametrize("case", ["s1_8", "s1_4_concat", "s2", "up"])
+def test_wgrad_glds_taps(case, on, dmc_opt):
+    """3x3 weight gradients on the LDS-DMA kernel with per-stage tap source rows (wgrad1x1_glds_kernel<.., TAPS>:
+    stride 1 at the 8x8 / 4x4 levels, stride 2, nearest-x2 upsample folded into the indexing; DMC_WG_TAPS=0: the
+    register-staged kernel) and the bias gradient, vs autograd of F.conv2d on the same bf16 values (fp32 CPU)."""
+    L, K = _lib()
+    dmc_opt("DMC_WG_TAPS", on)
+    dt = torch.bfloat16
+    torch.manual_seed(3)
+    N, H, W, C1, C2, Cout, stride, mode = {
+        "s1_8": (4, 8, 8, 256, 0, 256, 1, L.MODE_NORMAL), "s1_4_concat": (8, 4, 4, 128, 128, 256, 1, L.MODE_NORMAL),
+        "s2": (2, 16, 16, 128, 0, 128, 2, L.MODE_NORMAL), "up": (2, 8, 8, 128, 0, 128, 1, L.MODE_UPSAMPLE)}[case]
+    Cin = C1 + C2
+    x = q(torch.randn(N, Cin, H, W), dt).requires_grad_(True)
+    w = q(torch.randn(Cout, Cin, 3, 3) / math.sqrt(Cin * 9), dt).requires_grad_(True)
+    xi = F.interpolate(x, scale_factor=2, mode="nearest") if mode == L.MODE_UPSAMPLE else x
+    y = F.conv2d(xi, w, stride=stride, padding=1)
+    g = q(torch.randn_like(y), dt)
+    y.backward(g)
+    OH, OW = y.shape[2], y.shape[3]
+    gd = nhwc(g).to(dt).to(DEV)
+    xd = nhwc(x.detach()).to(dt).to(DEV)
+    x1, x2 = (xd[..., :C1].contiguous(), xd[..., C1:].contiguous()) if C2 else (xd, None)
+    d = K.make_desc(dt, N, H, W, C1, C2, C1, C2, L.kc_for(Cin, dt), OH, OW, Cout, K.TAPS3, mode, stride)
+    dw = torch.full_like(w, float("nan"), device=DEV)
+    db = torch.full((Cout,), float("nan"), device=DEV)
+    K.wgrad(d, gd, Cout, x1, x2, dw, dbias=db)
+    torch.cuda.synchronize()
+    assert rel_err(dw.cpu(), w.grad) < 1e-5
+    assert rel_err(db.cpu(), g.float().sum((0, 2, 3))) < 1e-5
