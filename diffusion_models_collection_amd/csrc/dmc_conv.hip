@@ -276,6 +276,12 @@ DMC_DEV void apply_act(const ConvK& a, float* v, int pix, int co, bool of32) {
     const float u = (sizeof(T) == 2 && !of32) ? bf2f(f2bf(v[e])) : v[e];
     v[e] = gelu_f(u);
   }
+  if (a.act == DMC_ACT_GELU_DROP && a.dthresh) {   // the MLP Dropout after the GELU (dmc_gelu_fwd's mask)
+    const uint32_t seed = a.dseed + (a.dseed_base ? *a.dseed_base : 0u);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      v[e] = drop_keep((uint64_t)pix * a.Cout + co + e, seed, a.dthresh) ? v[e] * a.dscale : 0.f;
+  }
 }
 
 template <typename T>
@@ -434,6 +440,12 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
         Chunk<bf16_t>::unpack(pre, f);
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] = gelu_f(f[e]);
+        if (a.act == DMC_ACT_GELU_DROP && a.dthresh) {   // the MLP Dropout after the GELU (dmc_gelu_fwd's mask)
+          const uint32_t seed = a.dseed + (a.dseed_base ? *a.dseed_base : 0u);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            f[e] = drop_keep((uint64_t)pix * a.Cout + co + e, seed, a.dthresh) ? f[e] * a.dscale : 0.f;
+        }
       }
       const v4i out = Chunk<bf16_t>::pack(f);
       *(v4i*)(y + ((size_t)pix * ldy + cy) * 2) = out;
@@ -2451,9 +2463,12 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
   k.bias = d->bias; k.addvec = d->addvec; k.ld_add = d->ld_add; k.resid = (const char*)d->resid; k.ld_res = d->ld_res;
   k.silu_pre = d->silu_pre; k.ld_silu = d->ld_silu;
   k.Csplit = d->Csplit; k.ldy1 = d->ldy1; k.ldy2 = d->ldy2; k.out_f32 = d->out_f32; k.out_nchw = d->out_nchw;
-  DMC_REQUIRE(d->act == DMC_ACT_NONE || (d->act == DMC_ACT_GELU && d->Csplit == d->Cout && !d->out_nchw &&
-                                         !d->silu_pre && d->Cout % 4 == 0 && (!d->y_pre || d->ld_pre % 4 == 0)),
+  DMC_REQUIRE(d->act == DMC_ACT_NONE ||
+                  ((d->act == DMC_ACT_GELU || d->act == DMC_ACT_GELU_DROP) && d->Csplit == d->Cout && !d->out_nchw &&
+                   !d->silu_pre && d->Cout % 4 == 0 && (!d->y_pre || d->ld_pre % 4 == 0)),
               "conv: act %d needs a single NHWC output, Cout %% 4 == 0, no silu'", d->act);
+  DMC_REQUIRE(d->act != DMC_ACT_GELU_DROP || d->prologue == DMC_PRO_NONE,
+              "conv: the GELU-dropout epilogue uses the drop_* fields, so no prologue");
   k.act = d->act; k.ypre = (char*)d->y_pre; k.ldpre = d->ld_pre;
   k.gst = nullptr;   // set by dmc_conv2d when the chosen kernel emits the GroupNorm partials
   k.gb_on = 0;       // likewise for the GroupNorm-backward partials

@@ -20,12 +20,16 @@ in the order the backward finishes them (data-parallel buckets, fused clip + Ada
 The residual stream stays fp32; GEMM operands are in the compute dtype (bf16 in perf mode).
 """
 import math
+import os
 
 import torch
 
 from .. import _lib as L
 from .. import kernels as K
 from ._unet_exec import Act, ExecCore, _PackCache, _seed_from_torch
+
+# training with MLP dropout: GELU + Dropout in fc1's epilogue (A/B: DMC_GELU_DROP_EPI=0 keeps dmc_gelu_fwd)
+_GELU_DROP_EPI = os.environ.get("DMC_GELU_DROP_EPI", "1") not in ("", "0")
 
 
 class _W:
@@ -248,6 +252,10 @@ class DiTExecutor(ExecCore):
                 # GELU in fc1's epilogue; the pre-activation is stored only when the backward needs it
                 self._conv([Act(h2, ht, wt, H)], blk.mlp[0], K.TAPS1, ht, wt, Hm, bias=blk.mlp[0].bias, out=a.t,
                            act=L.ACT_GELU, y_pre=None if u is None else u.t)
+            elif _GELU_DROP_EPI:
+                # GELU + the MLP Dropout in fc1's epilogue (bitwise dmc_gelu_fwd of the stored pre-activation)
+                self._conv([Act(h2, ht, wt, H)], blk.mlp[0], K.TAPS1, ht, wt, Hm, bias=blk.mlp[0].bias, out=a.t,
+                           act=L.ACT_GELU_DROP, y_pre=u.t, drop=d1)
             else:
                 self._conv([Act(h2, ht, wt, H)], blk.mlp[0], K.TAPS1, ht, wt, Hm, bias=blk.mlp[0].bias, out=u.t)
                 K.gelu_fwd(dt, u.t, T, Hm, Hm, a.t, drop=d1)

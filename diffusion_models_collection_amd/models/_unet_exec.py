@@ -166,7 +166,9 @@ class ExecCore:
         if pro is not None:
             K.set_prologue(d, pro[0], pro[1], pro[2], C1 + C2, drop, C1 + C2)
         elif drop is not None:
-            raise ValueError("dropout needs a prologue")
+            if act != L.ACT_GELU_DROP:
+                raise ValueError("dropout needs a prologue (or the GELU-dropout epilogue)")
+            K.set_prologue(d, L.PRO_NONE, drop=drop)    # the epilogue's dropout reads the drop_* fields
         ldy2 = 0
         y2 = None
         if split is not None:

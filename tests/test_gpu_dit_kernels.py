@@ -100,9 +100,11 @@ def test_conv_gelu_epilogue_bitwise(dt, M):
     Kc = L.kc_for(Cin, dt)
     wp = K.pack_weight(L.PACK_FWD, dt, w, Kc)
 
-    def run(act, y_pre=None):
+    def run(act, y_pre=None, drop=None):
         y = torch.empty(M, Cout, dtype=dt, device=DEV)
         d = K.make_desc(dt, M, 1, 1, Cin, 0, Cin, 0, Kc, 1, 1, Cout, K.TAPS1)
+        if drop is not None:
+            K.set_prologue(d, L.PRO_NONE, drop=drop)
         K.set_epilogue(d, bias=b, ldy1=Cout, act=act, y_pre=y_pre, ld_pre=Cout if y_pre is not None else 0)
         K.conv(d, x, None, wp, y)
         return y
@@ -117,6 +119,19 @@ def test_conv_gelu_epilogue_bitwise(dt, M):
     assert torch.equal(fused, ref)
     fused2 = run(L.ACT_GELU)          # without the pre-activation copy
     assert torch.equal(fused2, ref)
+    # GELU + the MLP Dropout (p = 0.1, a device seed base as in the graphed step): bitwise dmc_gelu_fwd with the
+    # same dropout of the stored pre-activation
+    base = torch.tensor([77], dtype=torch.int32, device=DEV)
+    drop = (1234, int(0.1 * 2 ** 32), 1.0 / 0.9, base.data_ptr())
+    pre_d = torch.empty_like(plain)
+    fused_d = run(L.ACT_GELU_DROP, pre_d, drop)
+    ref_d = torch.empty_like(plain)
+    K.gelu_fwd(dt, plain, M, Cout, Cout, ref_d, drop=drop)
+    torch.cuda.synchronize()
+    assert torch.equal(pre_d, plain)
+    assert torch.equal(fused_d, ref_d)
+    zero = (fused_d == 0).float().mean().item()
+    assert 0.07 < zero < 0.13, zero
 
 
 def test_timestep_embedding_batch_sum_patch_dgrad():
