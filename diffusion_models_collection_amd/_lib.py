@@ -23,7 +23,7 @@ _c_int, _c_p, _c_f, _c_u32, _c_long, _c_size = (ctypes.c_int, ctypes.c_void_p, c
                                                 ctypes.c_long, ctypes.c_size_t)
 
 
-ACT_NONE, ACT_GELU, ACT_GELU_DROP = 0, 1, 2   # include/dmc.h DMC_ACT_*
+ACT_NONE, ACT_GELU, ACT_GELU_DROP, ACT_DGELU = 0, 1, 2, 3   # include/dmc.h DMC_ACT_*
 FUSED_GN_STATS, FUSED_GN_BWD = 1, 2   # dmc_conv2d_fused_epilogue bits
 
 

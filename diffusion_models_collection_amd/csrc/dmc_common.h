@@ -135,6 +135,10 @@ DMC_DEV float sigmoid_f(float z) { return __builtin_amdgcn_rcpf(1.0f + __expf(-z
 DMC_DEV float silu_f(float z) { return z * sigmoid_f(z); }
 // nn.GELU() (exact): 0.5 u (1 + erf(u / sqrt 2)) -- the DiT MLP activation (dmc_dit.hip, the conv epilogue)
 DMC_DEV float gelu_f(float u) { return 0.5f * u * (1.0f + erff(u * 0.70710678118654752f)); }
+// d GELU / du (dmc_gelu_bwd, and the conv epilogue's DMC_ACT_DGELU)
+DMC_DEV float gelu_grad(float u) {
+  return 0.5f * (1.0f + erff(u * 0.70710678118654752f)) + u * 0.39894228040143268f * __expf(-0.5f * u * u);
+}
 
 // Counter-based hash for dropout masks: recomputable in backward from (seed, element index).
 DMC_DEV uint32_t hash_u32(uint32_t x, uint32_t seed) {

@@ -270,6 +270,19 @@ DMC_DEV void conv_epilogue(const ConvK& a, v4f (&acc)[TN][TM], int pix_base, int
 // is taken of that stored (rounded) value, so the fused result is bitwise gelu_fwd of the stored tensor.
 template <typename T>
 DMC_DEV void apply_act(const ConvK& a, float* v, int pix, int co, bool of32) {
+  if (a.act == DMC_ACT_DGELU) {   // dmc_gelu_bwd of the stored (rounded) input gradient
+    float u[4];
+    load4<T>(a.ypre, (size_t)pix * a.ldpre + co, u, of32);
+    const uint32_t seed = a.dthresh ? a.dseed + (a.dseed_base ? *a.dseed_base : 0u) : 0u;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float g = (sizeof(T) == 2 && !of32) ? bf2f(f2bf(v[e])) : v[e];
+      float m = 1.f;
+      if (a.dthresh) m = drop_keep((uint64_t)pix * a.Cout + co + e, seed, a.dthresh) ? a.dscale : 0.f;
+      v[e] = g * m * gelu_grad(u[e]);
+    }
+    return;
+  }
   if (a.ypre) store4<T>(a.ypre, (size_t)pix * a.ldpre + co, v, of32);
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -434,7 +447,18 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] += r[e];
       }
-      if (a.act) {   // GELU of the rounded pre-activation (see apply_act)
+      if (a.act == DMC_ACT_DGELU) {   // dmc_gelu_bwd of the rounded input gradient (see apply_act)
+        Chunk<bf16_t>::unpack(Chunk<bf16_t>::pack(f), f);
+        float u[8];
+        Chunk<bf16_t>::unpack(*(const v4i*)(a.ypre + ((size_t)pix * a.ldpre + co) * 2), u);
+        const uint32_t seed = a.dthresh ? a.dseed + (a.dseed_base ? *a.dseed_base : 0u) : 0u;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float m = 1.f;
+          if (a.dthresh) m = drop_keep((uint64_t)pix * a.Cout + co + e, seed, a.dthresh) ? a.dscale : 0.f;
+          f[e] = f[e] * m * gelu_grad(u[e]);
+        }
+      } else if (a.act) {   // GELU of the rounded pre-activation (see apply_act)
         const v4i pre = Chunk<bf16_t>::pack(f);
         if (a.ypre) *(v4i*)(a.ypre + ((size_t)pix * a.ldpre + co) * 2) = pre;
         Chunk<bf16_t>::unpack(pre, f);
@@ -2464,11 +2488,12 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
   k.silu_pre = d->silu_pre; k.ld_silu = d->ld_silu;
   k.Csplit = d->Csplit; k.ldy1 = d->ldy1; k.ldy2 = d->ldy2; k.out_f32 = d->out_f32; k.out_nchw = d->out_nchw;
   DMC_REQUIRE(d->act == DMC_ACT_NONE ||
-                  ((d->act == DMC_ACT_GELU || d->act == DMC_ACT_GELU_DROP) && d->Csplit == d->Cout && !d->out_nchw &&
+                  ((d->act >= DMC_ACT_GELU && d->act <= DMC_ACT_DGELU) && d->Csplit == d->Cout && !d->out_nchw &&
                    !d->silu_pre && d->Cout % 4 == 0 && (!d->y_pre || d->ld_pre % 4 == 0)),
               "conv: act %d needs a single NHWC output, Cout %% 4 == 0, no silu'", d->act);
-  DMC_REQUIRE(d->act != DMC_ACT_GELU_DROP || d->prologue == DMC_PRO_NONE,
-              "conv: the GELU-dropout epilogue uses the drop_* fields, so no prologue");
+  DMC_REQUIRE((d->act != DMC_ACT_GELU_DROP && d->act != DMC_ACT_DGELU) || d->prologue == DMC_PRO_NONE,
+              "conv: the GELU-dropout epilogues use the drop_* fields, so no prologue");
+  DMC_REQUIRE(d->act != DMC_ACT_DGELU || d->y_pre, "conv: DGELU reads the pre-activation y_pre");
   k.act = d->act; k.ypre = (char*)d->y_pre; k.ldpre = d->ld_pre;
   k.gst = nullptr;   // set by dmc_conv2d when the chosen kernel emits the GroupNorm partials
   k.gb_on = 0;       // likewise for the GroupNorm-backward partials

@@ -284,10 +284,6 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(const float* dy, const vo
   }
 }
 
-DMC_DEV float gelu_grad(float u) {
-  return 0.5f * (1.0f + erff(u * 0.70710678118654752f)) + u * 0.39894228040143268f * __expf(-0.5f * u * u);
-}
-
 template <typename T>
 __global__ void gelu_fwd_kernel(const void* u, long rows, int C, int ld, Drop drop, void* a) {
   const uint32_t seed = drop.thresh ? drop.s() : 0u;

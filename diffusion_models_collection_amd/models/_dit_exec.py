@@ -28,8 +28,15 @@ from .. import _lib as L
 from .. import kernels as K
 from ._unet_exec import Act, ExecCore, _PackCache, _seed_from_torch
 
-# training with MLP dropout: GELU + Dropout in fc1's epilogue (A/B: DMC_GELU_DROP_EPI=0 keeps dmc_gelu_fwd)
-_GELU_DROP_EPI = os.environ.get("DMC_GELU_DROP_EPI", "1") not in ("", "0")
+# GELU + Dropout in fc1's epilogue (training with MLP dropout) and their backward in fc2's input-gradient epilogue
+# (A/B: DMC_GELU_DROP_EPI=0 keeps dmc_gelu_fwd / dmc_gelu_bwd)
+# measured slower on the DiT train step (erf/exp in the GEMM epilogue cost more than the separate HBM-bound pass:
+# 6958 -> 6874 img/s forward, -> 6839 backward), so off by default
+_GELU_EPI_BITS = int(os.environ.get("DMC_GELU_DROP_EPI", "0") or 0)   # bit 0: forward, bit 1: backward
+# inference / dropout-free training: GELU in fc1's epilogue (DMC_GELU_EPI=0: conv + dmc_gelu_fwd, for A/B)
+_GELU_EPI = os.environ.get("DMC_GELU_EPI", "1") not in ("", "0")
+_GELU_DROP_EPI = bool(_GELU_EPI_BITS & 1)
+_DGELU_EPI = bool(_GELU_EPI_BITS & 2)
 
 
 class _W:
@@ -248,7 +255,11 @@ class DiTExecutor(ExecCore):
             d1 = self._drop(2 * i)
             a = self._new(B, ht, wt, Hm)
             u = self._new(B, ht, wt, Hm) if keep or d1 is not None else None
-            if d1 is None:
+            if d1 is None and not _GELU_EPI:
+                self._conv([Act(h2, ht, wt, H)], blk.mlp[0], K.TAPS1, ht, wt, Hm, bias=blk.mlp[0].bias,
+                           out=(u.t if u is not None else a.t))
+                K.gelu_fwd(dt, u.t if u is not None else a.t, T, Hm, Hm, a.t)
+            elif d1 is None:
                 # GELU in fc1's epilogue; the pre-activation is stored only when the backward needs it
                 self._conv([Act(h2, ht, wt, H)], blk.mlp[0], K.TAPS1, ht, wt, Hm, bias=blk.mlp[0].bias, out=a.t,
                            act=L.ACT_GELU, y_pre=None if u is None else u.t)
@@ -341,10 +352,15 @@ class DiTExecutor(ExecCore):
             dmo = torch.empty(B, ht, wt, H, dtype=dt, device=dev)
             K.gate_bwd(dt, dx, mo.t, H, mod2, ldm, mo_ + 5 * H, T, H, Lt, dmo, H, dmod, mo_ + 5 * H, drop=d2)
             self._wgrad([a], dmo, H, K.TAPS1, ht, wt, H, gv(blk.mlp[3].weight), dbias=gv(blk.mlp[3].bias))
-            da = torch.empty(B, ht, wt, Hm, dtype=dt, device=dev)
-            self._conv([Act(dmo, ht, wt, H)], blk.mlp[3], K.TAPS1, ht, wt, Hm, out=da, packmode=L.PACK_DGRAD)
             du = torch.empty(B, ht, wt, Hm, dtype=dt, device=dev)
-            K.gelu_bwd(dt, da, u.t, T, Hm, Hm, du, drop=d1)
+            if _DGELU_EPI:
+                # fc2's input gradient with the GELU (+ Dropout) backward in its epilogue (bitwise dmc_gelu_bwd)
+                self._conv([Act(dmo, ht, wt, H)], blk.mlp[3], K.TAPS1, ht, wt, Hm, out=du, packmode=L.PACK_DGRAD,
+                           act=L.ACT_DGELU, y_pre=u.t, drop=d1)
+            else:
+                da = torch.empty(B, ht, wt, Hm, dtype=dt, device=dev)
+                self._conv([Act(dmo, ht, wt, H)], blk.mlp[3], K.TAPS1, ht, wt, Hm, out=da, packmode=L.PACK_DGRAD)
+                K.gelu_bwd(dt, da, u.t, T, Hm, Hm, du, drop=d1)
             self._wgrad([Act(h2, ht, wt, H)], du, Hm, K.TAPS1, ht, wt, Hm, gv(blk.mlp[0].weight),
                         dbias=gv(blk.mlp[0].bias))
             dh2 = torch.empty(B, ht, wt, H, dtype=dt, device=dev)

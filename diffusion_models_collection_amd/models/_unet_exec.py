@@ -166,7 +166,7 @@ class ExecCore:
         if pro is not None:
             K.set_prologue(d, pro[0], pro[1], pro[2], C1 + C2, drop, C1 + C2)
         elif drop is not None:
-            if act != L.ACT_GELU_DROP:
+            if act not in (L.ACT_GELU_DROP, L.ACT_DGELU):
                 raise ValueError("dropout needs a prologue (or the GELU-dropout epilogue)")
             K.set_prologue(d, L.PRO_NONE, drop=drop)    # the epilogue's dropout reads the drop_* fields
         ldy2 = 0

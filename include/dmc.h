@@ -106,8 +106,11 @@ typedef struct dmc_conv_desc {
   float* wg_bias;            /* dmc_conv2d_wgrad only: if set, also the bias gradient wg_bias[co] = scale * sum over
                               * pixels of dy[pix][co] (nn.Conv2d bias), from the same pass over dy */
 } dmc_conv_desc;
-enum { DMC_ACT_NONE = 0, DMC_ACT_GELU = 1, DMC_ACT_GELU_DROP = 2 };
-/* GELU (exact): the DiT MLP (dit.py:98-99). GELU_DROP: GELU, then the MLP's Dropout with the descriptor's drop_*
+enum { DMC_ACT_NONE = 0, DMC_ACT_GELU = 1, DMC_ACT_GELU_DROP = 2, DMC_ACT_DGELU = 3 };
+/* DGELU: the backward of GELU_DROP / GELU on an input-gradient conv: out = round(acc) * mask * scale * gelu'(u) with
+ * u = y_pre[pix][ld_pre] READ (the stored pre-activation), the mask from the drop_* fields as for GELU_DROP (none if
+ * drop_thresh == 0) -- bitwise dmc_gelu_bwd of the conv's stored output.
+ * GELU (exact): the DiT MLP (dit.py:98-99). GELU_DROP: GELU, then the MLP's Dropout with the descriptor's drop_*
  * fields (prologue must be DMC_PRO_NONE): element (pix, co) kept iff hash(seed, pix*Cout + co) >= drop_thresh, kept
  * values scaled by drop_scale -- bitwise dmc_gelu_fwd with the same dropout of the stored pre-activation. */
 

@@ -1,12 +1,11 @@
 #!/bin/bash
-# DiT MLP: GELU + Dropout in fc1's epilogue vs dmc_gelu_fwd (DMC_GELU_DROP_EPI), tests first
 set -e -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/gde
+O=gpurun_out/ge2
 mkdir -p $O
-true
-true
-for cfg in "DMC_GELU_DROP_EPI=0" "DMC_GELU_DROP_EPI=1" "DMC_GELU_DROP_EPI=2" "DMC_GELU_DROP_EPI=0" "DMC_GELU_DROP_EPI=1" "DMC_GELU_DROP_EPI=2"; do
+timeout -k 10 300 python -u -m pytest tests/test_gpu_dit.py -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
+tail -1 $O/t.log
+for cfg in "DMC_GELU_EPI=1" "DMC_GELU_EPI=0" "DMC_GELU_EPI=1" "DMC_GELU_EPI=0"; do
   env $cfg timeout -k 10 300 python -u bench.py --dit-only > $O/dit.json 2>/dev/null
   python3 -c "import json; d=json.load(open('$O/dit.json')); print('$cfg'.ljust(24), 'dit train', d['train_img_s'], 'dit cfg', d['value'])"
 done

@@ -132,6 +132,13 @@ def test_conv_gelu_epilogue_bitwise(dt, M):
     assert torch.equal(fused_d, ref_d)
     zero = (fused_d == 0).float().mean().item()
     assert 0.07 < zero < 0.13, zero
+    # DGELU: an input-gradient-shaped conv whose epilogue applies dmc_gelu_bwd with the stored pre-activation
+    for dr in (None, drop):
+        dgel = run(L.ACT_DGELU, pre_d, dr)
+        ref_b = torch.empty_like(plain)
+        K.gelu_bwd(dt, plain, pre_d, M, Cout, Cout, ref_b, drop=dr)
+        torch.cuda.synchronize()
+        assert torch.equal(dgel, ref_b)
 
 
 def test_timestep_embedding_batch_sum_patch_dgrad():
