@@ -150,8 +150,14 @@ __global__ __launch_bounds__(256) void ln_mod_bwd_kernel(const void* dh, int ld_
   for (int l = l0 + wave; l < l1; l += 4) {
     const int row = b * L + l;
     const float mu = mean[row], rs = rstd[row];
-    float g[kMaxV][4], xh[kMaxV][4];
+    float g[kMaxV][4], xh[kMaxV][4], o[kMaxV][4];
     float s1 = 0.f, s2 = 0.f;
+    // the dx row is loaded with the operands (it does not depend on the row sums): one memory latency per row
+#pragma unroll
+    for (int k = 0; k < kMaxV; ++k) {
+      const int c = (lane + 64 * k) * 4;
+      if (c < C) ld4<float>(dx, (size_t)row * C + c, o[k]);
+    }
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
       const int c = (lane + 64 * k) * 4;
@@ -176,11 +182,9 @@ __global__ __launch_bounds__(256) void ln_mod_bwd_kernel(const void* dh, int ld_
     for (int k = 0; k < kMaxV; ++k) {
       const int c = (lane + 64 * k) * 4;
       if (c < C) {
-        float o[4];
-        ld4<float>(dx, (size_t)row * C + c, o);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] += rs * (g[k][e] - s1 - xh[k][e] * s2);
-        st4<float>(dx, (size_t)row * C + c, o);
+        for (int e = 0; e < 4; ++e) o[k][e] += rs * (g[k][e] - s1 - xh[k][e] * s2);
+        st4<float>(dx, (size_t)row * C + c, o[k]);
       }
     }
   }
