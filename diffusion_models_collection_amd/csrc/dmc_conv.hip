@@ -29,6 +29,8 @@ struct ConvK {
   int gb_on;   // GroupNorm-backward partials from the epilogue (dmc_gn_bwd_epi in gb)
   dmc_gn_bwd_epi gb;
   float* wgb;  // wgrad: per-split bias partials [split][Cpad] = sum over the split's pixels of dy (nullptr: off)
+  float* gsk;  // split-K launches: GroupNorm partials written by the split-K epilogue (nullptr: off)
+  int* gsk_done;  // host flag: set when the launch path emitted gsk
   int M;      // N*OH*OW output pixels
   int OHW;    // OH*OW
   float* sk;  // split-K partial slab (nullptr: no split)
@@ -1575,6 +1577,40 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvK a, int 
   }
 }
 
+// ... and the GroupNorm partials of the stored output in the same pass (the input of the next GroupNorm, as
+// tile_epilogue8 emits them for the unsplit kernels): one wave per (64-pixel segment, 8-channel chunk), lane =
+// pixel; the statistics are those gn_part_kernel computes from the stored values (bitwise: same reads, same
+// reduction). Needs M % 64 == 0, Cout % 8 == 0 and one NHWC output (the planner checks).
+template <typename T>
+__global__ __launch_bounds__(256) void conv_splitk_epi_gn_kernel(ConvK a, int splits, int Cpad) {
+  const int lane = threadIdx.x & 63;
+  const int nch = a.Cout / 8;
+  const long w = blockIdx.x * 4L + (threadIdx.x >> 6);
+  if (w >= (long)(a.M / 64) * nch) return;
+  const int seg = (int)(w / nch), ch = (int)(w - (long)seg * nch);
+  const int pix = seg * 64 + lane, co = ch * 8;
+  const size_t zs = (size_t)a.M * Cpad;
+  const float* p = a.sk + (size_t)pix * Cpad + co;
+  v4f v0 = *(const v4f*)p, v1 = *(const v4f*)(p + 4);
+  for (int z = 1; z < splits; ++z) { v0 += *(const v4f*)(p + z * zs); v1 += *(const v4f*)(p + 4 + z * zs); }
+  conv_store_tile<T>(a, v0, pix, co);
+  conv_store_tile<T>(a, v1, pix, co + 4);
+  // read back what this lane stored (its own writes) and reduce exactly as gn_part_kernel
+  const size_t row = (size_t)pix * a.ldy1 + co;
+  float f[8];
+  load4<T>(a.y1, row, f, false);
+  load4<T>(a.y1, row + 4, f + 4, false);
+  float t = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t += f[e];
+  const float m = wave_sum(t) * (1.0f / 512.0f);
+  float q = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) q = fmaf(f[e] - m, f[e] - m, q);
+  q = wave_sum(q);
+  if (lane == 0) { a.gsk[w * 2] = m; a.gsk[w * 2 + 1] = q; }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Weight-gradient kernel: C[co][kk] over a pixel range (split-K over grid.z), written as an fp32
 // slab [split][kk][co]. Tile 128 co x 128 kk, stage SP = 128/sizeof(T) pixels.
@@ -2498,6 +2534,7 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
   k.gst = nullptr;   // set by dmc_conv2d when the chosen kernel emits the GroupNorm partials
   k.gb_on = 0;       // likewise for the GroupNorm-backward partials
   k.wgb = nullptr;   // set by dmc_conv2d_wgrad when the bias gradient is requested
+  k.gsk = nullptr; k.gsk_done = nullptr;
   k.M = d->N * d->OH * d->OW; k.OHW = d->OH * d->OW;
   k.sk = nullptr; k.sk_per = 0;
   {
@@ -2621,6 +2658,12 @@ void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
   if (p.splits > 1) {
     conv_fwd_glds_kernel<2, 2, BUF><<<dim3(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128), p.splits), 256, 0, s>>>(k);
     const int Cpad = dmc::cdiv(k.Cout, 128) * 128;
+    if (k.gsk && k.M % 64 == 0 && k.Cout % 8 == 0 && !k.out_f32 && !k.out_nchw && k.Csplit == k.Cout) {
+      conv_splitk_epi_gn_kernel<bf16_t><<<(int)(((long)(k.M / 64) * (k.Cout / 8) + 3) / 4), 256, 0, s>>>(k, p.splits,
+                                                                                                       Cpad);
+      if (k.gsk_done) *k.gsk_done = 1;
+      return;
+    }
     const long total = (long)k.M * Cpad / 4;
     const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
     conv_splitk_epilogue_kernel<bf16_t><<<blocks, 256, 0, s>>>(k, p.splits, Cpad);
@@ -2871,6 +2914,9 @@ extern "C" int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2
                 "conv: GroupNorm partials need OH*OW %% 64 == 0, Cout %% 8 == 0 and one NHWC output");
     k.gst = epi_stats_ok(k, workspace, ws_bytes) ? part : nullptr;
   }
+  // split-K launches: the split-K epilogue emits the partials in its pass (DMC_NO_SKGN=1: a separate pass)
+  int gsk_done = 0;
+  if (part && !k.gst && !dmc::opt(dmc::OPT_NO_SKGN)) { k.gsk = part; k.gsk_done = &gsk_done; }
   const int rc = d->dtype == DMC_F32 ? launch_fwd<float>(k, workspace, ws_bytes, s)
                                      : launch_fwd<bf16_t>(k, workspace, ws_bytes, s);
   if (rc) return rc;
@@ -2884,7 +2930,7 @@ extern "C" int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2
     const int rc2 = dmc::check_launch("dmc_conv2d (GroupNorm-backward partials)");
     if (rc2) return rc2;
   }
-  if (!part || k.gst) return 0;
+  if (!part || k.gst || gsk_done) return 0;
   // the chosen kernel's epilogue does not emit them: one pass over the stored output
   const int nseg = k.M / 64, nch = k.Cout / 8;
   const int blocks = (int)(((long)nseg * nch + 3) / 4);
@@ -2912,7 +2958,8 @@ WgHaloPlan wgrad_halo_plan(const dmc_conv_desc* d) {
   if (!p.hp) return p;
   const int ntiles = k.M / 256;
   const int base = (k.Kc / 64) * dmc::cdiv(k.Cout, 128);
-  int sp = (256 + base - 1) / base;
+  const int target = (int)dmc::opt(dmc::OPT_WG_HALO_TARGET);   // blocks of 128 co (the 64-co kernel runs twice as many)
+  int sp = (target + base - 1) / base;
   if (sp > ntiles) sp = ntiles;
   if (sp < 1) sp = 1;
   p.tps = (ntiles + sp - 1) / sp;

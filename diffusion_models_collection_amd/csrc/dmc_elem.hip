@@ -40,7 +40,8 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"DMC_WG_BLOCKS", 512}, {"DMC_GN_STATS_ONE_MAX", 1l << 20}, {"DMC_GN_BWD_ONE_MAX", 65536}, {"DMC_HALO_VER", 2},
     {"DMC_NO_XCD", 0}, {"DMC_NO_EPI_STATS", 0}, {"DMC_HALO_NOSCHED", 0}, {"DMC_GLDS_2B", 1}, {"DMC_WG_MINPIX", 0},
     {"DMC_WG_1X1", 1}, {"DMC_WG_HALO_VER", 2}, {"DMC_GN_BWD_SLICES", 2},
-    {"DMC_WG_TAPS", 0},
+    {"DMC_WG_TAPS", 0}, {"DMC_NO_SKGN", 0},
+    {"DMC_WG_HALO_TARGET", 256},
 };
 struct OptTable {
   long v[OPT_COUNT];
