@@ -289,3 +289,45 @@ def test_trainer_epoch_on_device_loader_matches_oracle_batches(tmp_path, monkeyp
     l_ref, p_ref = run(ref_batches)
     assert np.isfinite(l_dev) and l_dev == l_ref
     assert torch.equal(p_dev, p_ref)
+
+
+def test_custom_image_dataset_subdirs_and_json(tmp_path):
+    """datasets/custom_dataset.py semantics: class subdirectories -> labels in sorted-name order; a JSON label file
+    -> labels remapped to consecutive indices; images decoded once through Resize + CenterCrop."""
+    from PIL import Image
+    from diffusion_models_collection_amd.datasets import CustomImageDataset
+    rng = np.random.default_rng(4)
+    for cls in ("zebra", "ant"):
+        (tmp_path / cls).mkdir()
+        for i in range(3):
+            Image.fromarray(rng.integers(0, 256, (40, 48, 3), dtype=np.uint8)).save(tmp_path / cls / f"{i}.png")
+    tr = CustomImageDataset.get_default_transform(32, "rgb", train=True)
+    ds = CustomImageDataset(str(tmp_path), transform=tr, conditional=True, use_subdirs=True)
+    assert len(ds) == 6 and ds.images.shape == (6, 32, 32, 3)
+    assert ds.class_to_idx == {"ant": 0, "zebra": 1} and ds.num_classes == 2
+    assert sorted(ds.labels.tolist()) == [0, 0, 0, 1, 1, 1]
+    img, y = ds[0]
+    assert img.shape == (3, 32, 32) and y in (0, 1)
+    flat = tmp_path / "flat"
+    flat.mkdir()
+    for i in range(2):
+        Image.fromarray(rng.integers(0, 256, (32, 32, 3), dtype=np.uint8)).save(flat / f"im{i}.png")
+    (tmp_path / "labels.json").write_text('{"im0.png": 7, "im1.png": 3}')
+    dj = CustomImageDataset(str(flat), conditional=True, label_file=str(tmp_path / "labels.json"))
+    assert sorted(dj.labels.tolist()) == [0, 1] and dj.class_to_idx == {3: 0, 7: 1}
+    with pytest.raises(ValueError, match="requires either"):
+        CustomImageDataset(str(flat), conditional=True)
+
+
+def test_get_dataset_from_config(tmp_path):
+    """train.py:84-104 get_dataset on the reference's config keys (dataset, data_root, image_size, conditional)."""
+    from diffusion_models_collection_amd.datasets.loader import get_dataset
+    d = tmp_path / "cifar-10-batches-bin"
+    d.mkdir()
+    rng = np.random.default_rng(6)
+    for name in [f"data_batch_{i}.bin" for i in range(1, 6)] + ["test_batch.bin"]:
+        _cifar_bin(d / name, rng.integers(0, 256, (2, 3, 32, 32), dtype=np.uint8), rng.integers(0, 10, 2))
+    ds = get_dataset({"dataset": "cifar10", "data_root": str(tmp_path), "image_size": 32, "conditional": True})
+    assert len(ds) == 10 and ds.conditional and ds.transform.flip_p == 0.5
+    dt = get_dataset({"dataset": "cifar10", "data_root": str(tmp_path), "image_size": (32, 32)}, train=False)
+    assert len(dt) == 2 and dt.transform.flip_p == 0.0
