@@ -210,13 +210,11 @@ __global__ void loss_bwd_kernel(int type, const float* pred, const float* target
 __global__ void ddim_step_kernel(const float* x, const float* eps, const float* x0_in, const int64_t* t,
                                  const int64_t* t_next, const float* ac, int N, int per, float eta, int clip,
                                  const float* z, float* out) {
-  __shared__ int any_neg;
-  if (threadIdx.x == 0) {
-    int neg = 0;
-    for (int b = 0; b < N; ++b) neg |= (t_next[b] < 0);
-    any_neg = neg;
-  }
-  __syncthreads();
+  // the final step of the loop (ddim.py:196-200: t_next < 0 for the batch): the block's threads test the entries
+  // in parallel (a single thread walking them serialised N dependent-latency loads in every block)
+  int neg = 0;
+  for (int b = threadIdx.x; b < N; b += blockDim.x) neg |= (t_next[b] < 0);
+  const int any_neg = __syncthreads_or(neg);
   const long total = (long)N * per;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int n = i / per;
