@@ -1278,6 +1278,147 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
   tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
 }
 
+template <int HP, int WS, bool PRO = false>
+__global__ __launch_bounds__(256, 2) void conv3x3_halo3_kernel(ConvK a, int R, int nimg) {
+  using T = bf16_t;
+  constexpr int NW = 4, BM = 128, BN = 128;
+  constexpr int HB = HP * NW * 1024;             // bytes of the halo buffer
+  constexpr int WB = BN * 128;                   // bytes per weight slot
+  constexpr int EP = BN * 4 + 16;                // epilogue row pitch (fp32)
+  constexpr int STATS = NW * (BM / 64) * 16 * 64; // GroupNorm (backward) partial scratch past the epilogue tile
+  constexpr int LDS_BYTES = (HB + WS * WB) > BM * EP + STATS ? (HB + WS * WB) : BM * EP + STATS;
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  char* const wring = lds + HB;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // wave-private weights: wave w computes all 128 pixels x output channels [32w, 32w+32) -- exactly the weight rows
+  // its own DMA pieces bring in, so within a chunk no wave reads another wave's slice and the per-tap block barrier
+  // of conv3x3_halo2_kernel is gone (one barrier per 64-channel chunk, for the shared halo)
+  int mb = blockIdx.x, nb = blockIdx.y;
+  if (gridDim.y == 1) xcd_tile((a.Cout + BN - 1) / BN, mb, nb);
+  const int m0 = mb * BM, n0 = nb * BN;
+  const int lrow = lane >> 3;
+  const int lc = (lane & 7) ^ lrow;
+  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
+  const int n_first = m0 / a.OHW;
+  const int r0 = (m0 - n_first * a.OHW) / OW;
+
+  unsigned h1[HP], h2[HP];
+#pragma unroll
+  for (int p = 0; p < HP; ++p) {
+    const int h = (wave * HP + p) * 8 + lrow;
+    h1[p] = kOOB; h2[p] = kOOB;
+    if (h < npix) {
+      const int img = h / segpix, rem = h - img * segpix;
+      const int hr = rem / HW, hc = rem - hr * HW;
+      const int iy = r0 + hr - 1, ix = hc - 1;
+      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
+        const unsigned sp = (unsigned)(((n_first + img) * a.H + iy) * a.W + ix);
+        h1[p] = (sp * a.ld1 + lc * 8) * 2u;
+        h2[p] = (sp * a.ld2 + lc * 8) * 2u;
+      }
+    }
+  }
+  const unsigned wrow = (unsigned)(a.ntaps * a.Kc);
+  unsigned ob[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int co = n0 + (wave * 4 + j) * 8 + lrow;
+    ob[j] = co < a.Cout ? ((unsigned)co * wrow + lc * 8) * 2u : kOOB;
+  }
+  const int fr = lane & 15, fh = lane >> 4;
+  int hb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int m = j * 16 + fr;
+    const int img = m / (R * OW), rem = m - img * (R * OW);
+    const int r = rem / OW, col = rem - r * OW;
+    hb[j] = img * segpix + (r + 1) * HW + col + 1;
+  }
+
+  v4f acc[2][8];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int nch = a.Kc / 64, nst = nch * 9;
+  auto issue_w = [&](int s) {
+    const int c = s / 9, t = s - c * 9;
+    const unsigned koff = (unsigned)(t * a.Kc + c * 64) * 2u;
+    dma_pieces<4>(a.w, a.w_bytes, wring + (s % WS) * WB + wave * 4 * 1024, ob, koff, 0, 4);
+  };
+  v4f pst[4];
+  for (int s = 0; s < nst; ++s) {
+    const int c = s / 9, t = s - c * 9;
+    if (t == 0) {
+      // chunk c's halo into the single buffer: every wave is done with chunk c-1's taps
+      if (c > 0) __syncthreads();
+      if (PRO) halo_pro_load(a, n_first, c * 64, pst);
+      halo_issue<HP>(a, lds, c * 64, wave, 0, HP, h1, h2);
+      if (c == 0)
+        for (int q = 0; q < WS - 1 && q < nst; ++q) issue_w(q);
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+      if (PRO) halo_affine_silu<HP>(lds, wave, h1, pst);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();   // the halo is shared: every wave's pieces have landed
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("" ::: "memory");
+    } else {
+      // this wave's weight slice s has landed once at most its slices issued after it are in flight (no barrier:
+      // the slot it refills next was last read by this wave alone)
+      const int after = min(nst - 1, s + WS - 2) - s;
+      wait_vm_dyn(4 * (after > 0 ? after : 0));
+      asm volatile("" ::: "memory");
+    }
+    if (s + WS - 1 < nst) issue_w(s + WS - 1);
+    const char* Bw = wring + (s % WS) * WB;
+    const int ty = t / 3, tx = t - ty * 3;
+    const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
+    // both k-steps' fragments read up front into distinct registers; the schedule below issues the second
+    // k-step's reads between the first k-step's MFMAs (left alone, hipcc re-reads fragments into the same
+    // registers and waits for each read right before its MFMA)
+    v4i fa[2][2], fb[2][8];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = ks * 4 + fh;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = wave * 32 + i * 16 + fr;
+        fa[ks][i] = *(const v4i*)(Bw + r * 128 + ((chunk ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int h = hb[j] + delta;
+        fb[ks][j] = *(const v4i*)(lds + h * 128 + ((chunk ^ (h & 7)) << 4));
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[i][j] = mma16<T>(acc[i][j], fa[ks][i], fb[ks][j]);
+    __builtin_amdgcn_sched_group_barrier(0x100, 10, 0);    // k-step 0 reads
+#pragma unroll
+    for (int g = 0; g < 10; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // k-step 0 MFMAs ...
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // ... with the k-step 1 reads between them
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 22, 0);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      *(v4f*)(lds + (j * 16 + fr) * EP + (wave * 32 + i * 16 + fh * 4) * 4) = acc[i][j];
+  __syncthreads();
+  tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Register-weight variant of conv3x3_halo_kernel (same tile, halo image and fragment reads). Each wave
 // loads its own 64x64 weight fragments of tap stage s+1 straight into VGPRs while stage s computes (the
@@ -2642,6 +2783,12 @@ template <bool PRO>
 void launch_halo2(const ConvK& k, int hp, int R, int nimg, hipStream_t s) {
   const dim3 g = dmc::opt(dmc::OPT_NO_XCD) ? dim3(k.M / 128, dmc::cdiv(k.Cout, 128))
                                           : dim3(k.M / 128 * dmc::cdiv(k.Cout, 128));
+  if (dmc::opt(dmc::OPT_HALO_PRIV)) {   // wave-private weight rows, no per-tap barrier
+    if (hp == 6) conv3x3_halo3_kernel<6, 3, PRO><<<g, 256, 0, s>>>(k, R, nimg);
+    else if (hp == 7) conv3x3_halo3_kernel<7, 3, PRO><<<g, 256, 0, s>>>(k, R, nimg);
+    else conv3x3_halo3_kernel<9, 2, PRO><<<g, 256, 0, s>>>(k, R, nimg);
+    return;
+  }
   if (dmc::opt(dmc::OPT_HALO_NOSCHED)) {   // A/B: the compiler's own fragment-read schedule
     if (hp == 6) conv3x3_halo2_kernel<6, 3, PRO, false><<<g, 256, 0, s>>>(k, R, nimg);
     else if (hp == 7) conv3x3_halo2_kernel<7, 3, PRO, false><<<g, 256, 0, s>>>(k, R, nimg);

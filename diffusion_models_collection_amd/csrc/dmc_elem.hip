@@ -41,7 +41,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"DMC_NO_XCD", 0}, {"DMC_NO_EPI_STATS", 0}, {"DMC_HALO_NOSCHED", 0}, {"DMC_GLDS_2B", 1}, {"DMC_WG_MINPIX", 0},
     {"DMC_WG_1X1", 1}, {"DMC_WG_HALO_VER", 2}, {"DMC_GN_BWD_SLICES", 2},
     {"DMC_WG_TAPS", 0}, {"DMC_NO_SKGN", 0},
-    {"DMC_WG_HALO_TARGET", 256},
+    {"DMC_WG_HALO_TARGET", 256}, {"DMC_HALO_PRIV", 0},
 };
 struct OptTable {
   long v[OPT_COUNT];
