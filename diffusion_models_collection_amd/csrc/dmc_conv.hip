@@ -30,6 +30,7 @@ struct ConvK {
   dmc_gn_bwd_epi gb;
   float* wgb;  // wgrad: per-split bias partials [split][Cpad] = sum over the split's pixels of dy (nullptr: off)
   float* gsk;  // split-K launches: GroupNorm partials written by the split-K epilogue (nullptr: off)
+  unsigned long long* stamp;  // DMC_STAMP measurement builds only: per-wave phase clocks of the halo conv
   int* gsk_done;  // host flag: set when the launch path emitted gsk
   int M;      // N*OH*OW output pixels
   int OHW;    // OH*OW
@@ -1209,6 +1210,14 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
     dma_pieces<4>(a.w, a.w_bytes, wring + (s % WS) * WB + wave * 4 * 1024, ob, koff, 0, 4);
   };
   v4f pst[4];
+#ifdef DMC_STAMP
+  // measurement build only (never in libdmc.so): clocks of the tap loop's phases, summed per wave
+  unsigned long long ph[5] = {0, 0, 0, 0, 0}, tq = __builtin_amdgcn_s_memtime();
+  const unsigned long long t_start = tq;
+#define DMC_PH(i) do { const unsigned long long tn_ = __builtin_amdgcn_s_memtime(); ph[i] += tn_ - tq; tq = tn_; } while (0)
+#else
+#define DMC_PH(i) do { } while (0)
+#endif
   for (int s = 0; s < nst; ++s) {
     const int c = s / 9, t = s - c * 9;
     if (t == 0) {
@@ -1225,12 +1234,15 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
       const int after = min(nst - 1, s + WS - 2) - s;
       wait_vm_dyn(4 * (after > 0 ? after : 0));
     }
+    DMC_PH(0);   // chunk halo / weight-slice wait
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
+    DMC_PH(1);   // block barrier
     if (s + WS - 1 < nst) issue_w(s + WS - 1);
+    DMC_PH(2);   // LDS-DMA issue of a later slice
     const char* Bw = wring + (s % WS) * WB;
     const int ty = t / 3, tx = t - ty * 3;
     const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
@@ -1267,8 +1279,23 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);   // k-step 1 MFMAs
     }
+#ifdef DMC_STAMP
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    DMC_PH(3);   // fragment reads + MFMA issue
   }
   __syncthreads();
+  DMC_PH(4);     // the MFMA tail + the epilogue barrier
+#ifdef DMC_STAMP
+  if (a.stamp && (threadIdx.x & 63) == 0) {
+    unsigned long long* o = a.stamp + ((size_t)blockIdx.x * NW + wave) * 8;
+    for (int q = 0; q < 5; ++q) o[q] = ph[q];
+    o[5] = t_start;
+    o[6] = __builtin_amdgcn_s_memtime();
+    o[7] = (unsigned long long)nst;
+  }
+#endif
+#undef DMC_PH
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -2676,6 +2703,7 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
   k.gb_on = 0;       // likewise for the GroupNorm-backward partials
   k.wgb = nullptr;   // set by dmc_conv2d_wgrad when the bias gradient is requested
   k.gsk = nullptr; k.gsk_done = nullptr;
+  k.stamp = (unsigned long long*)dmc::opt(dmc::OPT_STAMP_PTR);   // 0 unless a DMC_STAMP probe sets it
   k.M = d->N * d->OH * d->OW; k.OHW = d->OH * d->OW;
   k.sk = nullptr; k.sk_per = 0;
   {
