@@ -1140,7 +1140,7 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
 // and a WS-slot weight ring: <= 78 KB, two blocks per CU, so one block's prologue / chunk reload / epilogue
 // overlaps the other's tap loop. At a chunk switch the block waits for its own next-chunk halo (the other block
 // keeps the CU busy). Tile geometry: R = 128 / OW rows of one image, or 128 / (OH*OW) whole images.
-template <int HP, int WS, bool PRO = false, bool SCHED = true>
+template <int HP, int WS, bool PRO = false, bool SCHED = true, bool LATE = false>
 __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int nimg) {
   using T = bf16_t;
   constexpr int NW = 4, WM = 2, BM = 128, BN = 128;
@@ -1241,7 +1241,8 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
     DMC_PH(1);   // block barrier
-    if (s + WS - 1 < nst) issue_w(s + WS - 1);
+    // LATE: the later slice's LDS-DMA is issued after this tap's MFMAs (its issue then overlaps their execution)
+    if (!LATE && s + WS - 1 < nst) issue_w(s + WS - 1);
     DMC_PH(2);   // LDS-DMA issue of a later slice
     const char* Bw = wring + (s % WS) * WB;
     const int ty = t / 3, tx = t - ty * 3;
@@ -1278,6 +1279,10 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one k-step-1 read
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);   // k-step 1 MFMAs
+    }
+    if (LATE) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + WS - 1 < nst) issue_w(s + WS - 1);
     }
 #ifdef DMC_STAMP
     __builtin_amdgcn_sched_barrier(0);
@@ -2811,6 +2816,12 @@ template <bool PRO>
 void launch_halo2(const ConvK& k, int hp, int R, int nimg, hipStream_t s) {
   const dim3 g = dmc::opt(dmc::OPT_NO_XCD) ? dim3(k.M / 128, dmc::cdiv(k.Cout, 128))
                                           : dim3(k.M / 128 * dmc::cdiv(k.Cout, 128));
+  if (dmc::opt(dmc::OPT_HALO_LATE)) {   // A/B: the later weight slice issued after the tap's MFMAs
+    if (hp == 6) conv3x3_halo2_kernel<6, 3, PRO, true, true><<<g, 256, 0, s>>>(k, R, nimg);
+    else if (hp == 7) conv3x3_halo2_kernel<7, 3, PRO, true, true><<<g, 256, 0, s>>>(k, R, nimg);
+    else conv3x3_halo2_kernel<9, 2, PRO, true, true><<<g, 256, 0, s>>>(k, R, nimg);
+    return;
+  }
   if (dmc::opt(dmc::OPT_HALO_PRIV)) {   // wave-private weight rows, no per-tap barrier
     if (hp == 6) conv3x3_halo3_kernel<6, 3, PRO><<<g, 256, 0, s>>>(k, R, nimg);
     else if (hp == 7) conv3x3_halo3_kernel<7, 3, PRO><<<g, 256, 0, s>>>(k, R, nimg);

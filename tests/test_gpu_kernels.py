@@ -229,7 +229,7 @@ def test_conv_dgrad_wgrad(dt, case):
     assert rel_err(db.cpu(), g.sum((0, 2, 3))) < 1e-5
 
 
-@pytest.mark.parametrize("variant", ["ring3", "ring4", "regw", "halo2", "halo3"])
+@pytest.mark.parametrize("variant", ["ring3", "ring4", "regw", "halo2", "halo3", "halo2_late"])
 @pytest.mark.parametrize("case", ["fwd32_concat", "fwd16_ragged_cout", "dgrad32", "fwd8_multi_image", "fallback_4x4",
                                   "fwd8_concat_b128", "fwd64_rows"])
 def test_conv3x3_halo_kernel(case, variant, monkeypatch, dmc_opt):
@@ -238,7 +238,8 @@ def test_conv3x3_halo_kernel(case, variant, monkeypatch, dmc_opt):
     (DMC_HALO_WS4), register-staged weights (DMC_HALO_RW), the two-blocks-per-CU 128-pixel kernel
     (DMC_HALO_VER=2)."""
     L, K = _lib()
-    dmc_opt("DMC_HALO_VER", 2 if variant in ("halo2", "halo3") else 1)
+    dmc_opt("DMC_HALO_VER", 2 if variant in ("halo2", "halo3", "halo2_late") else 1)
+    dmc_opt("DMC_HALO_LATE", 1 if variant == "halo2_late" else 0)
     dmc_opt("DMC_HALO_PRIV", 1 if variant == "halo3" else 0)   # wave-private weight rows, no per-tap barrier
     dmc_opt("DMC_HALO_WS4", 1 if variant == "ring4" else 0)
     dmc_opt("DMC_HALO_RW", 1 if variant == "regw" else 0)
