@@ -611,9 +611,11 @@ DMC_DEV void tile_epilogue(const ConvK& a, const char* lds, int EP, int m0, int 
     for (int pl = r0; pl < BM; pl += RS) conv_store_tile<T>(a, *(const v4f*)(lds + pl * EP + cg * 16), m0 + pl, co);
     return;
   }
-  if (sizeof(T) == 2 && !a.out_f32 && !((a.Cout | a.Csplit | a.ldy1 | a.ldy2 | a.ld_res) & 7)) {
-    tile_epilogue8<BM, BN, NT>(a, lds, EP, m0, n0);   // 16-byte stores: half the store instructions
-    return;
+  if constexpr (BN == 128) {
+    if (sizeof(T) == 2 && !a.out_f32 && !((a.Cout | a.Csplit | a.ldy1 | a.ldy2 | a.ld_res) & 7)) {
+      tile_epilogue8<BM, BN, NT>(a, lds, EP, m0, n0);   // 16-byte stores: half the store instructions
+      return;
+    }
   }
   if (co >= a.Cout) return;
   const bool of32 = a.out_f32 != 0;
@@ -1128,6 +1130,119 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       *(v4f*)(lds + (wm * 64 + j * 16 + fr) * EP + (wn * 64 + i * 16 + fh * 4) * 4) = acc[i][j];
+  __syncthreads();
+  tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
+}
+
+// A/B (DMC_HALO_CHUNK=1): the 3x3 conv with a whole chunk's weights resident. The phase clocks of the halo
+// kernels (profiles/r2_halo2_phase_clocks.txt) put 44 % of their tap loop in the per-tap weight-slice stream;
+// here a block (256 pixels x 64 output channels, 8 waves) loads chunk c's halo AND its nine tap slices
+// (9 x 64 rows x 128 B = 72 KB) with one wait and one barrier, then runs all 9 taps from LDS with no further
+// synchronisation. Twice the weight reuse per byte streamed (64 co x 256 px per slice), no overlap of the
+// load with the MFMAs (one block per CU). Plain operands only (no prologue, no fused GroupNorm statistics).
+template <int HP>
+__global__ __launch_bounds__(512) void conv3x3_chunk_kernel(ConvK a, int R, int nimg) {
+  using T = bf16_t;
+  constexpr int NW = 8, BM = 256, BN = 64;
+  constexpr int HB = HP * NW * 1024;        // halo bytes
+  constexpr int WB = BN * 128;              // one tap slice: 64 rows x 64 k
+  constexpr int EP = BN * 4 + 16;
+  constexpr int LDS_BYTES = (HB + 9 * WB) > BM * EP ? (HB + 9 * WB) : BM * EP;
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  char* const wbuf = lds + HB;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int mb = blockIdx.x, nb = 0;
+  xcd_tile((a.Cout + BN - 1) / BN, mb, nb);
+  const int m0 = mb * BM, n0 = nb * BN;
+  const int lrow = lane >> 3;
+  const int lc = (lane & 7) ^ lrow;
+  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
+  const int n_first = m0 / a.OHW;
+  const int r0 = (m0 - n_first * a.OHW) / OW;
+
+  unsigned h1[HP], h2[HP];
+#pragma unroll
+  for (int p = 0; p < HP; ++p) {
+    const int h = (wave * HP + p) * 8 + lrow;
+    h1[p] = kOOB; h2[p] = kOOB;
+    if (h < npix) {
+      const int img = h / segpix, rem = h - img * segpix;
+      const int hr = rem / HW, hc = rem - hr * HW;
+      const int iy = r0 + hr - 1, ix = hc - 1;
+      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
+        const unsigned sp = (unsigned)(((n_first + img) * a.H + iy) * a.W + ix);
+        h1[p] = (sp * a.ld1 + lc * 8) * 2u;
+        h2[p] = (sp * a.ld2 + lc * 8) * 2u;
+      }
+    }
+  }
+  // weight pieces: 72 per chunk (9 slices x 8 row groups), 9 per wave; piece q = slice q/8, rows (q%8)*8..+8
+  const unsigned wrow = (unsigned)(a.ntaps * a.Kc);
+  unsigned ow[9];
+#pragma unroll
+  for (int p = 0; p < 9; ++p) {
+    const int q = wave * 9 + p, t = q >> 3, co = n0 + (q & 7) * 8 + lrow;
+    ow[p] = co < a.Cout ? ((unsigned)co * wrow + (unsigned)(t * a.Kc) + lc * 8) * 2u : kOOB;
+  }
+  const int fr = lane & 15, fh = lane >> 4;
+  int hb[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int m = wave * 32 + j * 16 + fr;
+    const int img = m / (R * OW), rem = m - img * (R * OW);
+    const int r = rem / OW, col = rem - r * OW;
+    hb[j] = img * segpix + (r + 1) * HW + col + 1;
+  }
+
+  v4f acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int nch = a.Kc / 64;
+  for (int c = 0; c < nch; ++c) {
+    if (c > 0) __syncthreads();   // every wave is done with chunk c-1's halo and slices
+    halo_issue<HP>(a, lds, c * 64, wave, 0, HP, h1, h2);
+    dma_pieces<9>(a.w, a.w_bytes, wbuf + wave * 9 * 1024, ow, (unsigned)(c * 64) * 2u, 0, 9);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    asm volatile("" ::: "memory");
+    __syncthreads();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const char* Bw = wbuf + t * WB;
+      const int ty = t / 3, tx = t - ty * 3;
+      const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int chunk = ks * 4 + fh;
+        v4i fa[4], fb[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = i * 16 + fr;
+          fa[i] = *(const v4i*)(Bw + r * 128 + ((chunk ^ (r & 7)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int h = hb[j] + delta;
+          fb[j] = *(const v4i*)(lds + h * 128 + ((chunk ^ (h & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *(v4f*)(lds + (wave * 32 + j * 16 + fr) * EP + (i * 16 + fh * 4) * 4) = acc[i][j];
   __syncthreads();
   tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
 }
@@ -2936,6 +3051,7 @@ __global__ __launch_bounds__(256) void gn_bwd_part_kernel(const char* gy, int ld
 // Whether dmc_conv2d's chosen kernel emits the GroupNorm partials in its epilogue (tile_epilogue8: the round-1
 // halo kernel and the non-split LDS-DMA kernel, bf16, one NHWC output, whole 256-pixel tiles, 128-channel tiles).
 bool epi_stats_ok(const ConvK& k, const void* ws, size_t ws_bytes) {
+  if (dmc::opt(dmc::OPT_HALO_CHUNK)) return false;   // its 64-channel epilogue emits no partials
   if (k.dtype_bytes != 2 || k.out_f32 || k.out_nchw || k.silu_pre || k.Csplit != k.Cout || k.Cout % 128 ||
       k.M % 256 || k.OHW % 64 || ((k.Cout | k.ldy1 | k.ld_res) & 7))
     return false;
@@ -3004,9 +3120,14 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     const dim3 hgx = dmc::opt(dmc::OPT_NO_XCD) ? hg : dim3(hg.x * hg.y);   // 1-D: XCD-aware tile order
     const long hver = dmc::opt(dmc::OPT_HALO_VER);   // 1: the 8-wave kernel, 2: two blocks per CU
     int R2, nimg2;
-    const int hp2 = (buf && p.splits == 1 && !dmc::opt(dmc::OPT_NO_HALO) && hver == 2) ? halo2_plan(k, &R2, &nimg2) : 0;
+    const int hp2 = (buf && p.splits == 1 && !dmc::opt(dmc::OPT_NO_HALO) && hver == 2 && !(hp && dmc::opt(dmc::OPT_HALO_CHUNK)))
+                        ? halo2_plan(k, &R2, &nimg2) : 0;
     if (hp2) { launch_halo2<false>(k, hp2, R2, nimg2, s); return dmc::check_launch("dmc_conv2d"); }
-    if (hp && dmc::opt(dmc::OPT_HALO_RW)) {
+    if (hp && dmc::opt(dmc::OPT_HALO_CHUNK)) {   // A/B: a chunk's nine weight slices resident
+      const dim3 cg(k.M / 256 * dmc::cdiv(k.Cout, 64));
+      if (hp == 6) conv3x3_chunk_kernel<6><<<cg, 512, 0, s>>>(k, R, nimg);
+      else conv3x3_chunk_kernel<7><<<cg, 512, 0, s>>>(k, R, nimg);
+    } else if (hp && dmc::opt(dmc::OPT_HALO_RW)) {
       if (hp == 6) conv3x3_halo_rw_kernel<6><<<hg, 512, 0, s>>>(k, R, nimg);
       else conv3x3_halo_rw_kernel<7><<<hg, 512, 0, s>>>(k, R, nimg);
     } else if (hp == 6 && dmc::opt(dmc::OPT_HALO_WS4))
