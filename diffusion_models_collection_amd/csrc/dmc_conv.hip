@@ -1134,13 +1134,23 @@ __global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int n
   tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
 }
 
+// one 1-KB piece of each of a chunk's nine tap slices, in tap order (slice p at dst + p * 8 KB)
+DMC_DEV void chunk_slices(const ConvK& a, char* dst, const unsigned* off, unsigned add) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.w_bytes, 0x00020000);
+#pragma unroll
+  for (int p = 0; p < 9; ++p)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(dst + p * 8192), 16, off[p] + add, 0, 0, 0);
+}
+
 // A/B (DMC_HALO_CHUNK=1): the 3x3 conv with a whole chunk's weights resident. The phase clocks of the halo
 // kernels (profiles/r2_halo2_phase_clocks.txt) put 44 % of their tap loop in the per-tap weight-slice stream;
 // here a block (256 pixels x 64 output channels, 8 waves) loads chunk c's halo AND its nine tap slices
 // (9 x 64 rows x 128 B = 72 KB) with one wait and one barrier, then runs all 9 taps from LDS with no further
 // synchronisation. Twice the weight reuse per byte streamed (64 co x 256 px per slice), no overlap of the
 // load with the MFMAs (one block per CU). Plain operands only (no prologue, no fused GroupNorm statistics).
-template <int HP>
+// PROG (DMC_HALO_CHUNK=2): wave w loads rows 8w..8w+7 of every slice, in tap order, and tap t waits only for
+// slices <= t (one barrier per tap), so slices 1..8 land under the earlier taps' MFMAs.
+template <int HP, bool PROG = false>
 __global__ __launch_bounds__(512) void conv3x3_chunk_kernel(ConvK a, int R, int nimg) {
   using T = bf16_t;
   constexpr int NW = 8, BM = 256, BN = 64;
@@ -1183,7 +1193,7 @@ __global__ __launch_bounds__(512) void conv3x3_chunk_kernel(ConvK a, int R, int 
   unsigned ow[9];
 #pragma unroll
   for (int p = 0; p < 9; ++p) {
-    const int q = wave * 9 + p, t = q >> 3, co = n0 + (q & 7) * 8 + lrow;
+    const int q = PROG ? p * 8 + wave : wave * 9 + p, t = q >> 3, co = n0 + (q & 7) * 8 + lrow;
     ow[p] = co < a.Cout ? ((unsigned)co * wrow + (unsigned)(t * a.Kc) + lc * 8) * 2u : kOOB;
   }
   const int fr = lane & 15, fh = lane >> 4;
@@ -1206,13 +1216,25 @@ __global__ __launch_bounds__(512) void conv3x3_chunk_kernel(ConvK a, int R, int 
   for (int c = 0; c < nch; ++c) {
     if (c > 0) __syncthreads();   // every wave is done with chunk c-1's halo and slices
     halo_issue<HP>(a, lds, c * 64, wave, 0, HP, h1, h2);
-    dma_pieces<9>(a.w, a.w_bytes, wbuf + wave * 9 * 1024, ow, (unsigned)(c * 64) * 2u, 0, 9);
-    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-    asm volatile("" ::: "memory");
-    __syncthreads();
-    asm volatile("" ::: "memory");
+    if constexpr (PROG) {
+      chunk_slices(a, wbuf + wave * 1024, ow, (unsigned)(c * 64) * 2u);
+    } else {
+      dma_pieces<9>(a.w, a.w_bytes, wbuf + wave * 9 * 1024, ow, (unsigned)(c * 64) * 2u, 0, 9);
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+      asm volatile("" ::: "memory");
+      __syncthreads();
+      asm volatile("" ::: "memory");
+    }
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
+      if constexpr (PROG) {   // this wave's slices > t may still be in flight; the barrier publishes everyone's
+        wait_vm_dyn(8 - t);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" ::: "memory");
+      }
       const char* Bw = wbuf + t * WB;
       const int ty = t / 3, tx = t - ty * 3;
       const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
@@ -3125,7 +3147,10 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     if (hp2) { launch_halo2<false>(k, hp2, R2, nimg2, s); return dmc::check_launch("dmc_conv2d"); }
     if (hp && dmc::opt(dmc::OPT_HALO_CHUNK)) {   // A/B: a chunk's nine weight slices resident
       const dim3 cg(k.M / 256 * dmc::cdiv(k.Cout, 64));
-      if (hp == 6) conv3x3_chunk_kernel<6><<<cg, 512, 0, s>>>(k, R, nimg);
+      const bool prog = dmc::opt(dmc::OPT_HALO_CHUNK) == 2;
+      if (hp == 6 && prog) conv3x3_chunk_kernel<6, true><<<cg, 512, 0, s>>>(k, R, nimg);
+      else if (prog) conv3x3_chunk_kernel<7, true><<<cg, 512, 0, s>>>(k, R, nimg);
+      else if (hp == 6) conv3x3_chunk_kernel<6><<<cg, 512, 0, s>>>(k, R, nimg);
       else conv3x3_chunk_kernel<7><<<cg, 512, 0, s>>>(k, R, nimg);
     } else if (hp && dmc::opt(dmc::OPT_HALO_RW)) {
       if (hp == 6) conv3x3_halo_rw_kernel<6><<<hg, 512, 0, s>>>(k, R, nimg);

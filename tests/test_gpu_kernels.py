@@ -229,7 +229,7 @@ def test_conv_dgrad_wgrad(dt, case):
     assert rel_err(db.cpu(), g.sum((0, 2, 3))) < 1e-5
 
 
-@pytest.mark.parametrize("variant", ["ring3", "ring4", "regw", "halo2", "halo3", "halo2_late", "chunk"])
+@pytest.mark.parametrize("variant", ["ring3", "ring4", "regw", "halo2", "halo3", "halo2_late", "chunk", "chunk_prog"])
 @pytest.mark.parametrize("case", ["fwd32_concat", "fwd16_ragged_cout", "dgrad32", "fwd8_multi_image", "fallback_4x4",
                                   "fwd8_concat_b128", "fwd64_rows"])
 def test_conv3x3_halo_kernel(case, variant, monkeypatch, dmc_opt):
@@ -243,7 +243,7 @@ def test_conv3x3_halo_kernel(case, variant, monkeypatch, dmc_opt):
     dmc_opt("DMC_HALO_PRIV", 1 if variant == "halo3" else 0)   # wave-private weight rows, no per-tap barrier
     dmc_opt("DMC_HALO_WS4", 1 if variant == "ring4" else 0)
     dmc_opt("DMC_HALO_RW", 1 if variant == "regw" else 0)
-    dmc_opt("DMC_HALO_CHUNK", 1 if variant == "chunk" else 0)   # a chunk's nine weight slices resident
+    dmc_opt("DMC_HALO_CHUNK", {"chunk": 1, "chunk_prog": 2}.get(variant, 0))   # a chunk's nine weight slices resident
     # at these small M the planner would split K over the LDS-DMA kernel instead; the halo kernel is what the
     # B=128 model runs, so keep split-K off here to exercise it
     dmc_opt("DMC_NO_SPLITK", 1)
