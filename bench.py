@@ -45,7 +45,9 @@ CIFAR = dict(image_size=(32, 32), in_channels=3, model_channels=128, out_channel
              attention_resolutions=(16, 8), dropout=0.1, channel_mult=(1, 2, 2, 2), use_attention=True)
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense, MI355X_MICROARCH.md
 TRAIN_GFLOP_PER_IMG = 37.890     # fwd + bwd, = 3 x 12.632 forward
-PMC_FILE = "r2_pmc_roofline_conv.json"
+PMC_FILE = "r2_pmc_roofline_conv.json"          # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of the roofline conv
+ROOFLINE_CSV = "r2_roofline_kernel_stats.csv"   # rocprofv3 --kernel-trace --stats of `bench.py --roofline-only`
+DIT_PMC_FILE = "r3_pmc_dit_loop.json"           # rocprofv3 --pmc over `bench.py --dit-only --no-train`
 
 
 def log(*a):
@@ -94,14 +96,48 @@ def conv_roofline(dtype, B=128):
     # rocprofv3 kernel-trace average of the same command within ~1 % (profiles/r2_roofline_*), whereas an event
     # pair around every launch adds its own ~4 us
     achieved = flops / (b2b_ms * 1e-3) / 1e12
-    ver = L.get_option("DMC_HALO_VER")
-    kname = "conv3x3_halo2_kernel" if ver == 2 else "conv3x3_halo_kernel"
+    kname = "conv3x3_halo2_kernel"
     return {"kernel": f"{kname} bf16 implicit GEMM (ResBlock 3x3 128->128 @32x32, B=128, "
                       "bias+temb epilogue)" if dtype == torch.bfloat16 else "conv_fwd_kernel<f32,128,128>",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic(),
             "flops_per_launch": flops, "avg_launch_ms": round(b2b_ms, 4), "per_launch_events_ms": round(avg_ms, 4),
-            "algorithmic_bytes_per_launch": 2 * (2 * B * H * W * C) + 2 * C * 9 * C}
+            "algorithmic_bytes_per_launch": 2 * (2 * B * H * W * C) + 2 * C * 9 * C,
+            "rocprof_committed": rocprof_committed(kname, flops) if dtype == torch.bfloat16 else None}
+
+
+def rocprof_committed(kernel="conv3x3_halo2_kernel", flops=None):
+    """The roofline conv's average duration in the rocprofv3 kernel-stats CSV committed under profiles/ for this
+    tree (the same `bench.py --roofline-only` command under the profiler), and the frac it gives: the figure a
+    reader can recompute from profiles/ (the live `achieved` above is this run's own box)."""
+    import csv
+    f = os.path.join(ROOT, "profiles", ROOFLINE_CSV)
+    if not os.path.exists(f):
+        return None
+    for r in csv.DictReader(open(f)):
+        if kernel in r["Name"]:
+            us = float(r["AverageNs"]) / 1e3
+            out = {"file": f"profiles/{ROOFLINE_CSV}", "calls": int(r["Calls"]), "avg_us": round(us, 3)}
+            if flops:
+                tf = flops / (us * 1e-6) / 1e12
+                out.update(achieved=round(tf, 2), frac=round(tf / MFMA_BF16_PEAK_TFLOPS, 4))
+            return out
+    return None
+
+
+def loop_roofline(flops, seconds, scope, traffic=None):
+    """Whole-loop MFMA roofline: algorithmic FLOPs of the loop (model forward FLOPs x rows x steps) / wall."""
+    tf = flops / seconds / 1e12
+    return {"bound": "mfma", "achieved": round(tf, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic, "scope": scope}
+
+
+def dit_pmc_traffic():
+    f = os.path.join(ROOT, "profiles", DIT_PMC_FILE)
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        return json.load(fh).get("hbm_bytes_per_loop")
 
 
 def pmc_traffic():
@@ -200,13 +236,18 @@ def train_rate(trainer, pool, steps, warmup, world):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    g = getattr(trainer, "_graph", None)
+    w0 = g.ring_wait_s if g is not None else 0.0
     t0 = time.perf_counter()
     for i in range(steps):
         trainer.train_step(pool[i % len(pool)], 0)
-    host_el = time.perf_counter() - t0      # host enqueue time (the GPU may still be running)
+    host_el = time.perf_counter() - t0      # until the last train_step returned (the GPU may still be running)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    return max_over_ranks(el, world), host_el
+    # host enqueue = that time minus the waits on the graphed step's pinned-argument ring (which blocks the host
+    # until step k-4 has run, i.e. paces the host to the GPU)
+    ring = (g.ring_wait_s - w0) if g is not None else 0.0
+    return max_over_ranks(el, world), (host_el - ring, ring)
 
 
 def max_over_ranks(v, world):
@@ -294,6 +335,30 @@ def data_line(trainer, dev, B, steps):
                                        "(one reference DataLoader worker's transform work; the reference runs 4)"}}
 
 
+def rccl_one_rank_line(mp, dtype, dev, pool, steps, base_ms):
+    """The data-parallel step (GradSync + the segmented HIP-graph step: graphs cut at the gradient all-reduce
+    points, RCCL all-reduce(AVG) of each 25 MB bucket issued between the replays) on a world_size-1 'nccl' (RCCL)
+    process group, timed like the headline beside it: what the distributed plumbing costs per step on one GPU
+    (segment launches + collective calls + the stream waits), with no inter-GPU traffic."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    try:
+        model, tr = make_trainer(mp, dtype, dev, 0, 1)
+        tr.enable_grad_sync()
+        model.train()
+        el, _ = train_rate(tr, pool, steps, 5, 1)
+        segs = len(tr._graph.segs) if tr._graph is not None and tr._graph.segs else 0
+    finally:
+        dist.destroy_process_group()
+    ms = el / steps * 1e3
+    return {"train_img_s": round(pool[0].shape[0] * steps / el, 2), "ms_per_step": round(ms, 3),
+            "overhead_ms_per_step": round(ms - base_ms, 3), "graph_segments": segs, "steps": steps,
+            "note": "world_size-1 RCCL group: GradSync buckets + segmented graph replay vs the single-graph headline"}
+
+
 DIT_S2 = dict(img_size=(32, 32), patch_size=2, in_channels=3, hidden_size=384, depth=12, num_heads=6, mlp_ratio=4.0)
 
 
@@ -319,7 +384,9 @@ def dit_lines(args, dev, rank, world, B):
            "model": "DiT-S/2 (hidden 384, depth 12, 6 heads, patch 2, 256 tokens), 10 classes",
            "gflop_per_forward_img": round(gf, 3),
            "roofline": {"bound": "mfma", "achieved": round(tfs, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                        "frac": round(tfs / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+                        "frac": round(tfs / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": dit_pmc_traffic(),
+                        "traffic_unit": "HBM bytes per 50-step loop (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE over all "
+                                        f"dispatches, profiles/{DIT_PMC_FILE})",
                         "scope": "whole DDIM-50 CFG loop per GPU"}}
     if not args.no_train:
         mt = DiT(**DIT_S2, num_classes=10, dropout=0.1, compute_dtype=args.dtype).to(dev)
@@ -389,6 +456,7 @@ def main():
             dist.init_process_group("gloo", rank=rank, world_size=world)
 
     from diffusion_models_collection_amd.models import UNet
+    from diffusion_models_collection_amd.models.unet import unet_flops_per_image
     from diffusion_models_collection_amd.diffusion import DDIM
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
@@ -402,9 +470,9 @@ def main():
     model.train()
     if args.no_train:
         args.warmup, args.steps = 0, 1
-        el, host_el = 1.0, 0.0
+        el, (host_el, ring_el) = 1.0, (0.0, 0.0)
     else:
-        el, host_el = train_rate(trainer, pool, args.steps, args.warmup, world)
+        el, (host_el, ring_el) = train_rate(trainer, pool, args.steps, args.warmup, world)
     ms = el / args.steps * 1e3
     value = world * B * args.steps / el
     log(f"[bench] rank {rank}: {ms:.2f} ms/step, {value:.1f} img/s aggregate")
@@ -421,19 +489,27 @@ def main():
                       "parallelism": f"dp{world}"},
            "per_gpu_imgs_per_sec": round(value / world, 2),
            "host_enqueue_ms_per_step": round(host_el / max(args.steps, 1) * 1e3, 3),
+           "host_ring_wait_ms_per_step": round(ring_el / max(args.steps, 1) * 1e3, 3),
            "train_tflops_per_gpu": round(value / world * gflop / 1e3, 2)}
     if args.no_train:
         out["value"] = None
     if args.extra and S == 32 and not args.no_train and world == 1:
         out["data_loader"] = data_line(trainer, dev, B, args.steps)
+        try:
+            out["dp1_rccl"] = rccl_one_rank_line(mp, args.dtype, dev, pool, args.steps, ms)
+        except Exception as e:  # noqa: BLE001 -- a side line must never hide the headline
+            out["dp1_rccl"] = {"error": repr(e)}
 
     if not args.no_sample:
         model.eval()
         ddim = DDIM(1000, args.sample_steps, device=dev)
         sel = sample_rate(lambda: ddim.sample(model, (B, 3, S, S)), world)
-        out[f"ddim{args.sample_steps}"] = {"value": round(world * B / sel, 2), "unit": "img/s", "batch_per_gpu": B,
-                                           "steps": args.sample_steps, "seconds": round(sel, 3),
-                                           "scaling": "replicas"}
+        fwd_gf = unet_flops_per_image(model) / 1e9
+        out[f"ddim{args.sample_steps}"] = {
+            "value": round(world * B / sel, 2), "unit": "img/s", "batch_per_gpu": B, "steps": args.sample_steps,
+            "seconds": round(sel, 3), "scaling": "replicas", "gflop_per_forward_img": round(fwd_gf, 3),
+            "roofline": loop_roofline(B * args.sample_steps * fwd_gf * 1e9, sel,
+                                      f"whole DDIM-{args.sample_steps} loop per GPU: UNet forward FLOPs x B x steps")}
         if not args.no_cfg:
             # conditional UNet (10 classes), DDIM + classifier-free guidance 3.0 + dynamic thresholding
             # (diffusion/ddim.py:251-346): cond and null-label rows as ONE 2B forward per step
@@ -441,10 +517,13 @@ def main():
             cmodel = UNet(**mp, num_classes=10, compute_dtype=args.dtype).to(dev).eval()
             yl = torch.arange(B, device=dev) % 10
             cel = sample_rate(lambda: ddim.sample_with_cfg(cmodel, (B, 3, S, S), yl, cfg_scale=3.0), world)
-            out[f"ddim{args.sample_steps}_cfg"] = {"value": round(world * B / cel, 2), "unit": "img/s",
-                                                   "batch_per_gpu": B, "steps": args.sample_steps, "cfg_scale": 3.0,
-                                                   "p_threshold": 0.995, "forward_batch": 2 * B,
-                                                   "seconds": round(cel, 3), "scaling": "replicas"}
+            out[f"ddim{args.sample_steps}_cfg"] = {
+                "value": round(world * B / cel, 2), "unit": "img/s", "batch_per_gpu": B, "steps": args.sample_steps,
+                "cfg_scale": 3.0, "p_threshold": 0.995, "forward_batch": 2 * B, "seconds": round(cel, 3),
+                "scaling": "replicas",
+                "roofline": loop_roofline(2 * B * args.sample_steps * fwd_gf * 1e9, cel,
+                                          f"whole DDIM-{args.sample_steps} CFG loop per GPU: forward FLOPs x 2B x "
+                                          "steps")}
             del cmodel
     if args.dit and S == 32:
         model = trainer = None          # free the UNet's HBM before the DiT runs
@@ -460,10 +539,15 @@ def main():
         m64.eval()
         d100 = DDIM(1000, 100, device=dev)
         s64 = sample_rate(lambda: d100.sample(m64, (B, 3, 64, 64)), world)
+        gf64 = unet_flops_per_image(m64) / 1e9
         out["celeba64"] = {"train_img_s": round(world * B * 5 / e64, 2), "train_ms_per_step": round(e64 / 5 * 1e3, 3),
                            "ddim100_img_s": round(world * B / s64, 2), "ddim100_seconds": round(s64, 3),
                            "batch_per_gpu": B, "dtype": args.dtype, "steps_timed": 5,
-                           "train_tflops_per_gpu": round(B * 5 / e64 * TRAIN_GFLOP_PER_IMG * 4 / 1e3, 2)}
+                           "gflop_per_forward_img": round(gf64, 3),
+                           "train_tflops_per_gpu": round(B * 5 / e64 * 3 * gf64 / 1e3, 2),
+                           "roofline": loop_roofline(B * 5 * 3 * gf64 * 1e9, e64, "64x64 train step (fwd + bwd = 3x "
+                                                     "forward FLOPs) per GPU"),
+                           "ddim100_roofline": loop_roofline(B * 100 * gf64 * 1e9, s64, "whole DDIM-100 loop per GPU")}
         del m64, tr64
         if args.dtype == "bf16":
             # the reference's own arithmetic (fp32) on the same step, for comparison with the bf16 headline

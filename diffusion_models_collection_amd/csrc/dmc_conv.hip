@@ -979,296 +979,6 @@ DMC_DEV void halo_affine_silu(char* buf, int wave, const unsigned* h1, const v4f
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
-template <int HP, int WS, bool PRO = false>
-__global__ __launch_bounds__(512) void conv3x3_halo_kernel(ConvK a, int R, int nimg) {
-  using T = bf16_t;
-  constexpr int NW = 8, WM = 4, BM = 256, BN = 128;
-  constexpr int HB = HP * NW * 1024;             // bytes per halo buffer
-  constexpr int WB = BN * 128;                   // bytes per weight slot (WS slots)
-  constexpr int EP = BN * 4 + 16;                // epilogue row pitch (fp32)
-  constexpr int LDS_BYTES = (2 * HB + WS * WB) > BM * EP ? (2 * HB + WS * WB) : BM * EP;
-  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
-  char* const wring = lds + 2 * HB;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave % WM, wn = wave / WM;
-  int mb = blockIdx.x, nb = blockIdx.y;
-  if (gridDim.y == 1) xcd_tile((a.Cout + BN - 1) / BN, mb, nb);   // 1-D launch: XCD-aware tile order
-  const int m0 = mb * BM, n0 = nb * BN;
-  const int lrow = lane >> 3;
-  const int lc = (lane & 7) ^ lrow;
-  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
-  const int n_first = m0 / a.OHW;
-  const int r0 = (m0 - n_first * a.OHW) / OW;
-
-  // halo DMA source offsets per piece (chunk-independent; kOOB = zero padding / past the halo)
-  unsigned h1[HP], h2[HP];
-#pragma unroll
-  for (int p = 0; p < HP; ++p) {
-    const int h = (wave * HP + p) * 8 + lrow;
-    h1[p] = kOOB; h2[p] = kOOB;
-    if (h < npix) {
-      const int img = h / segpix, rem = h - img * segpix;
-      const int hr = rem / HW, hc = rem - hr * HW;
-      const int iy = r0 + hr - 1, ix = hc - 1;
-      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
-        const unsigned sp = (unsigned)(((n_first + img) * a.H + iy) * a.W + ix);
-        h1[p] = (sp * a.ld1 + lc * 8) * 2u;
-        h2[p] = (sp * a.ld2 + lc * 8) * 2u;
-      }
-    }
-  }
-  // weight slice offsets: 2 pieces per wave per stage
-  const unsigned wrow = (unsigned)(a.ntaps * a.Kc);
-  unsigned ob[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int co = n0 + (wave * 2 + j) * 8 + lrow;
-    ob[j] = co < a.Cout ? ((unsigned)co * wrow + lc * 8) * 2u : kOOB;
-  }
-  // halo index of each fragment row for tap (0,0)
-  const int fr = lane & 15, fh = lane >> 4;
-  int hb[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int m = wm * 64 + j * 16 + fr;
-    const int img = m / (R * OW), rem = m - img * (R * OW);
-    const int r = rem / OW, col = rem - r * OW;
-    hb[j] = img * segpix + (r + 1) * HW + col + 1;
-  }
-
-  v4f acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-  const int nch = a.Kc / 64, nst = nch * 9;
-  auto issue_w = [&](int s) {
-    const int c = s / 9, t = s - c * 9;
-    const unsigned koff = (unsigned)(t * a.Kc + c * 64) * 2u;
-    dma_pieces<2>(a.w, a.w_bytes, wring + (s % WS) * WB + wave * 2 * 1024, ob, koff, 0, 2);
-  };
-  auto part_b = [](int k) { return k * HP / 3; };
-  // halo pieces a wave issues in slot t (after the barrier of stage t): chunk c+1's halo, in three parts
-  auto halo_count = [&](int t) {
-    const int c = t / 9, k = t - c * 9;
-    return (k < 3 && c + 1 < nch) ? part_b(k + 1) - part_b(k) : 0;
-  };
-  // vector-memory instructions a wave issues in slot t: weight slice t+WS-1, then the halo part
-  auto slot_count = [&](int t) { return (t + WS - 1 < nst ? 2 : 0) + halo_count(t); };
-  // what may stay in flight when stage s starts: everything the wave issued after weight slice s (slot
-  // s-WS+1, or the prologue); the halo part issued beside that slice belongs to the next chunk
-  auto after_w = [&](int s) {
-    const int ts = s - (WS - 1);
-    int n = 0;
-    if (ts < 0) {
-      for (int q = s + 1; q < WS - 1 && q < nst; ++q) n += 2;
-      for (int t = 0; t < s; ++t) n += slot_count(t);
-    } else {
-      n = halo_count(ts);
-      for (int t = ts + 1; t < s; ++t) n += slot_count(t);
-    }
-    return n;
-  };
-
-  // GN+SiLU prologue on the halo (one image per tile): this lane's scale/shift of chunk 0
-  constexpr bool pro = PRO;   // separate instantiation: the plain kernel's code is unchanged
-  v4f pst[4];
-  if (pro) halo_pro_load(a, n_first, 0, pst);
-  halo_issue<HP>(a, lds, 0, wave, 0, HP, h1, h2);
-  for (int q = 0; q < WS - 1 && q < nst; ++q) issue_w(q);
-  if (pro) {   // this wave's own chunk-0 pieces (the stage-0 barrier publishes them)
-    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-    halo_affine_silu<HP>(lds, wave, h1, pst);
-    if (nch > 1) halo_pro_load(a, n_first, 64, pst);
-  }
-  for (int s = 0; s < nst; ++s) {
-    wait_vm_dyn(after_w(s));
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("" ::: "memory");
-    const int c = s / 9, t = s - c * 9;
-    if (s + WS - 1 < nst) issue_w(s + WS - 1);
-    if (t < 3 && c + 1 < nch) halo_issue<HP>(a, lds + ((c + 1) & 1) * HB, (c + 1) * 64, wave, part_b(t), part_b(t + 1), h1, h2);
-    const char* A = lds + (c & 1) * HB;
-    const char* Bw = wring + (s % WS) * WB;
-    const int ty = t / 3, tx = t - ty * 3;
-    const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int chunk = ks * 4 + fh;
-      v4i fa[4], fb[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = wn * 64 + i * 16 + fr;
-        fa[i] = *(const v4i*)(Bw + r * 128 + ((chunk ^ (r & 7)) << 4));
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int h = hb[j] + delta;
-        fb[j] = *(const v4i*)(A + h * 128 + ((chunk ^ (h & 7)) << 4));
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
-    }
-    if (pro && t == 8 && c + 1 < nch) {
-      // this wave's own pieces of chunk c+1 (issued in slots 9c..9c+2, landed: the stage's wait covered later
-      // weight slices); nobody reads that buffer before stage 9(c+1)'s barrier, which publishes the rewrite
-      halo_affine_silu<HP>(lds + ((c + 1) & 1) * HB, wave, h1, pst);
-      if (c + 2 < nch) halo_pro_load(a, n_first, (c + 2) * 64, pst);
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *(v4f*)(lds + (wm * 64 + j * 16 + fr) * EP + (wn * 64 + i * 16 + fh * 4) * 4) = acc[i][j];
-  __syncthreads();
-  tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
-}
-
-// one 1-KB piece of each of a chunk's nine tap slices, in tap order (slice p at dst + p * 8 KB)
-DMC_DEV void chunk_slices(const ConvK& a, char* dst, const unsigned* off, unsigned add) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.w_bytes, 0x00020000);
-#pragma unroll
-  for (int p = 0; p < 9; ++p)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(dst + p * 8192), 16, off[p] + add, 0, 0, 0);
-}
-
-// A/B (DMC_HALO_CHUNK=1): the 3x3 conv with a whole chunk's weights resident. The phase clocks of the halo
-// kernels (profiles/r2_halo2_phase_clocks.txt) put 44 % of their tap loop in the per-tap weight-slice stream;
-// here a block (256 pixels x 64 output channels, 8 waves) loads chunk c's halo AND its nine tap slices
-// (9 x 64 rows x 128 B = 72 KB) with one wait and one barrier, then runs all 9 taps from LDS with no further
-// synchronisation. Twice the weight reuse per byte streamed (64 co x 256 px per slice), no overlap of the
-// load with the MFMAs (one block per CU). Plain operands only (no prologue, no fused GroupNorm statistics).
-// PROG (DMC_HALO_CHUNK=2): wave w loads rows 8w..8w+7 of every slice, in tap order, and tap t waits only for
-// slices <= t (one barrier per tap), so slices 1..8 land under the earlier taps' MFMAs.
-template <int HP, bool PROG = false>
-__global__ __launch_bounds__(512) void conv3x3_chunk_kernel(ConvK a, int R, int nimg) {
-  using T = bf16_t;
-  constexpr int NW = 8, BM = 256, BN = 64;
-  constexpr int HB = HP * NW * 1024;        // halo bytes
-  constexpr int WB = BN * 128;              // one tap slice: 64 rows x 64 k
-  constexpr int EP = BN * 4 + 16;
-  constexpr int LDS_BYTES = (HB + 9 * WB) > BM * EP ? (HB + 9 * WB) : BM * EP;
-  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
-  char* const wbuf = lds + HB;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int mb = blockIdx.x, nb = 0;
-  xcd_tile((a.Cout + BN - 1) / BN, mb, nb);
-  const int m0 = mb * BM, n0 = nb * BN;
-  const int lrow = lane >> 3;
-  const int lc = (lane & 7) ^ lrow;
-  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
-  const int n_first = m0 / a.OHW;
-  const int r0 = (m0 - n_first * a.OHW) / OW;
-
-  unsigned h1[HP], h2[HP];
-#pragma unroll
-  for (int p = 0; p < HP; ++p) {
-    const int h = (wave * HP + p) * 8 + lrow;
-    h1[p] = kOOB; h2[p] = kOOB;
-    if (h < npix) {
-      const int img = h / segpix, rem = h - img * segpix;
-      const int hr = rem / HW, hc = rem - hr * HW;
-      const int iy = r0 + hr - 1, ix = hc - 1;
-      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
-        const unsigned sp = (unsigned)(((n_first + img) * a.H + iy) * a.W + ix);
-        h1[p] = (sp * a.ld1 + lc * 8) * 2u;
-        h2[p] = (sp * a.ld2 + lc * 8) * 2u;
-      }
-    }
-  }
-  // weight pieces: 72 per chunk (9 slices x 8 row groups), 9 per wave; piece q = slice q/8, rows (q%8)*8..+8
-  const unsigned wrow = (unsigned)(a.ntaps * a.Kc);
-  unsigned ow[9];
-#pragma unroll
-  for (int p = 0; p < 9; ++p) {
-    const int q = PROG ? p * 8 + wave : wave * 9 + p, t = q >> 3, co = n0 + (q & 7) * 8 + lrow;
-    ow[p] = co < a.Cout ? ((unsigned)co * wrow + (unsigned)(t * a.Kc) + lc * 8) * 2u : kOOB;
-  }
-  const int fr = lane & 15, fh = lane >> 4;
-  int hb[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int m = wave * 32 + j * 16 + fr;
-    const int img = m / (R * OW), rem = m - img * (R * OW);
-    const int r = rem / OW, col = rem - r * OW;
-    hb[j] = img * segpix + (r + 1) * HW + col + 1;
-  }
-
-  v4f acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-  const int nch = a.Kc / 64;
-  for (int c = 0; c < nch; ++c) {
-    if (c > 0) __syncthreads();   // every wave is done with chunk c-1's halo and slices
-    halo_issue<HP>(a, lds, c * 64, wave, 0, HP, h1, h2);
-    if constexpr (PROG) {
-      chunk_slices(a, wbuf + wave * 1024, ow, (unsigned)(c * 64) * 2u);
-    } else {
-      dma_pieces<9>(a.w, a.w_bytes, wbuf + wave * 9 * 1024, ow, (unsigned)(c * 64) * 2u, 0, 9);
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-      asm volatile("" ::: "memory");
-      __syncthreads();
-      asm volatile("" ::: "memory");
-    }
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      if constexpr (PROG) {   // this wave's slices > t may still be in flight; the barrier publishes everyone's
-        wait_vm_dyn(8 - t);
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("" ::: "memory");
-      }
-      const char* Bw = wbuf + t * WB;
-      const int ty = t / 3, tx = t - ty * 3;
-      const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int chunk = ks * 4 + fh;
-        v4i fa[4], fb[2];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = i * 16 + fr;
-          fa[i] = *(const v4i*)(Bw + r * 128 + ((chunk ^ (r & 7)) << 4));
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int h = hb[j] + delta;
-          fb[j] = *(const v4i*)(lds + h * 128 + ((chunk ^ (h & 7)) << 4));
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
-      }
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *(v4f*)(lds + (wave * 32 + j * 16 + fr) * EP + (i * 16 + fh * 4) * 4) = acc[i][j];
-  __syncthreads();
-  tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
-}
-
 // ---------------------------------------------------------------------------------------------
 // Two-blocks-per-CU halo conv. The 8-wave kernel above holds 144 KB of LDS (double-buffered 64-channel halo +
 // 3-slot weight ring) for a 256-pixel tile, so one block owns a CU: every tile's prologue (halo + first weight
@@ -1277,7 +987,7 @@ __global__ __launch_bounds__(512) void conv3x3_chunk_kernel(ConvK a, int R, int 
 // and a WS-slot weight ring: <= 78 KB, two blocks per CU, so one block's prologue / chunk reload / epilogue
 // overlaps the other's tap loop. At a chunk switch the block waits for its own next-chunk halo (the other block
 // keeps the CU busy). Tile geometry: R = 128 / OW rows of one image, or 128 / (OH*OW) whole images.
-template <int HP, int WS, bool PRO = false, bool SCHED = true, bool LATE = false>
+template <int HP, int WS, bool PRO = false, bool SCHED = true>
 __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int nimg) {
   using T = bf16_t;
   constexpr int NW = 4, WM = 2, BM = 128, BN = 128;
@@ -1378,8 +1088,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
     DMC_PH(1);   // block barrier
-    // LATE: the later slice's LDS-DMA is issued after this tap's MFMAs (its issue then overlaps their execution)
-    if (!LATE && s + WS - 1 < nst) issue_w(s + WS - 1);
+    if (s + WS - 1 < nst) issue_w(s + WS - 1);
     DMC_PH(2);   // LDS-DMA issue of a later slice
     const char* Bw = wring + (s % WS) * WB;
     const int ty = t / 3, tx = t - ty * 3;
@@ -1417,10 +1126,6 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);   // k-step 1 MFMAs
     }
-    if (LATE) {
-      __builtin_amdgcn_sched_barrier(0);
-      if (s + WS - 1 < nst) issue_w(s + WS - 1);
-    }
 #ifdef DMC_STAMP
     __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -1438,292 +1143,6 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
   }
 #endif
 #undef DMC_PH
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *(v4f*)(lds + (wm * 64 + j * 16 + fr) * EP + (wn * 64 + i * 16 + fh * 4) * 4) = acc[i][j];
-  __syncthreads();
-  tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
-}
-
-template <int HP, int WS, bool PRO = false>
-__global__ __launch_bounds__(256, 2) void conv3x3_halo3_kernel(ConvK a, int R, int nimg) {
-  using T = bf16_t;
-  constexpr int NW = 4, BM = 128, BN = 128;
-  constexpr int HB = HP * NW * 1024;             // bytes of the halo buffer
-  constexpr int WB = BN * 128;                   // bytes per weight slot
-  constexpr int EP = BN * 4 + 16;                // epilogue row pitch (fp32)
-  constexpr int STATS = NW * (BM / 64) * 16 * 64; // GroupNorm (backward) partial scratch past the epilogue tile
-  constexpr int LDS_BYTES = (HB + WS * WB) > BM * EP + STATS ? (HB + WS * WB) : BM * EP + STATS;
-  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
-  char* const wring = lds + HB;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // wave-private weights: wave w computes all 128 pixels x output channels [32w, 32w+32) -- exactly the weight rows
-  // its own DMA pieces bring in, so within a chunk no wave reads another wave's slice and the per-tap block barrier
-  // of conv3x3_halo2_kernel is gone (one barrier per 64-channel chunk, for the shared halo)
-  int mb = blockIdx.x, nb = blockIdx.y;
-  if (gridDim.y == 1) xcd_tile((a.Cout + BN - 1) / BN, mb, nb);
-  const int m0 = mb * BM, n0 = nb * BN;
-  const int lrow = lane >> 3;
-  const int lc = (lane & 7) ^ lrow;
-  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
-  const int n_first = m0 / a.OHW;
-  const int r0 = (m0 - n_first * a.OHW) / OW;
-
-  unsigned h1[HP], h2[HP];
-#pragma unroll
-  for (int p = 0; p < HP; ++p) {
-    const int h = (wave * HP + p) * 8 + lrow;
-    h1[p] = kOOB; h2[p] = kOOB;
-    if (h < npix) {
-      const int img = h / segpix, rem = h - img * segpix;
-      const int hr = rem / HW, hc = rem - hr * HW;
-      const int iy = r0 + hr - 1, ix = hc - 1;
-      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
-        const unsigned sp = (unsigned)(((n_first + img) * a.H + iy) * a.W + ix);
-        h1[p] = (sp * a.ld1 + lc * 8) * 2u;
-        h2[p] = (sp * a.ld2 + lc * 8) * 2u;
-      }
-    }
-  }
-  const unsigned wrow = (unsigned)(a.ntaps * a.Kc);
-  unsigned ob[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int co = n0 + (wave * 4 + j) * 8 + lrow;
-    ob[j] = co < a.Cout ? ((unsigned)co * wrow + lc * 8) * 2u : kOOB;
-  }
-  const int fr = lane & 15, fh = lane >> 4;
-  int hb[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int m = j * 16 + fr;
-    const int img = m / (R * OW), rem = m - img * (R * OW);
-    const int r = rem / OW, col = rem - r * OW;
-    hb[j] = img * segpix + (r + 1) * HW + col + 1;
-  }
-
-  v4f acc[2][8];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-  const int nch = a.Kc / 64, nst = nch * 9;
-  auto issue_w = [&](int s) {
-    const int c = s / 9, t = s - c * 9;
-    const unsigned koff = (unsigned)(t * a.Kc + c * 64) * 2u;
-    dma_pieces<4>(a.w, a.w_bytes, wring + (s % WS) * WB + wave * 4 * 1024, ob, koff, 0, 4);
-  };
-  v4f pst[4];
-  for (int s = 0; s < nst; ++s) {
-    const int c = s / 9, t = s - c * 9;
-    if (t == 0) {
-      // chunk c's halo into the single buffer: every wave is done with chunk c-1's taps
-      if (c > 0) __syncthreads();
-      if (PRO) halo_pro_load(a, n_first, c * 64, pst);
-      halo_issue<HP>(a, lds, c * 64, wave, 0, HP, h1, h2);
-      if (c == 0)
-        for (int q = 0; q < WS - 1 && q < nst; ++q) issue_w(q);
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-      if (PRO) halo_affine_silu<HP>(lds, wave, h1, pst);
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();   // the halo is shared: every wave's pieces have landed
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("" ::: "memory");
-    } else {
-      // this wave's weight slice s has landed once at most its slices issued after it are in flight (no barrier:
-      // the slot it refills next was last read by this wave alone)
-      const int after = min(nst - 1, s + WS - 2) - s;
-      wait_vm_dyn(4 * (after > 0 ? after : 0));
-      asm volatile("" ::: "memory");
-    }
-    if (s + WS - 1 < nst) issue_w(s + WS - 1);
-    const char* Bw = wring + (s % WS) * WB;
-    const int ty = t / 3, tx = t - ty * 3;
-    const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
-    // both k-steps' fragments read up front into distinct registers; the schedule below issues the second
-    // k-step's reads between the first k-step's MFMAs (left alone, hipcc re-reads fragments into the same
-    // registers and waits for each read right before its MFMA)
-    v4i fa[2][2], fb[2][8];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int chunk = ks * 4 + fh;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int r = wave * 32 + i * 16 + fr;
-        fa[ks][i] = *(const v4i*)(Bw + r * 128 + ((chunk ^ (r & 7)) << 4));
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int h = hb[j] + delta;
-        fb[ks][j] = *(const v4i*)(lds + h * 128 + ((chunk ^ (h & 7)) << 4));
-      }
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) acc[i][j] = mma16<T>(acc[i][j], fa[ks][i], fb[ks][j]);
-    __builtin_amdgcn_sched_group_barrier(0x100, 10, 0);    // k-step 0 reads
-#pragma unroll
-    for (int g = 0; g < 10; ++g) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // k-step 0 MFMAs ...
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // ... with the k-step 1 reads between them
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, 22, 0);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      *(v4f*)(lds + (j * 16 + fr) * EP + (wave * 32 + i * 16 + fh * 4) * 4) = acc[i][j];
-  __syncthreads();
-  tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Register-weight variant of conv3x3_halo_kernel (same tile, halo image and fragment reads). Each wave
-// loads its own 64x64 weight fragments of tap stage s+1 straight into VGPRs while stage s computes (the
-// four waves sharing a slice hit the same L1 lines), and the next chunk's halo is staged through VGPRs
-// too (loaded at the chunk's first tap, written to the other LDS buffer at its last). No weight LDS
-// traffic, no LDS-DMA issue per tap, and ONE barrier per 64-channel chunk instead of one per tap; all
-// loads are ordinary VGPR loads, so the compiler's counted waits cover them.
-
-// 16-byte loads at byte offsets off[p] + add from base; kOOB offsets read zero (the load goes to base
-// and its value is dropped: no branch around the load)
-template <int N>
-DMC_DEV void reg_load16(const char* base, const unsigned* off, unsigned add, v4i* out) {
-#pragma unroll
-  for (int p = 0; p < N; ++p) {
-    const bool ok = off[p] != kOOB;
-    v4i v = *(const v4i*)(base + (ok ? off[p] + add : 0u));
-    if (!ok) v = v4i{0, 0, 0, 0};
-    out[p] = v;
-  }
-}
-
-template <int HP>
-__global__ __launch_bounds__(512) void conv3x3_halo_rw_kernel(ConvK a, int R, int nimg) {
-  using T = bf16_t;
-  constexpr int NW = 8, WM = 4, BM = 256, BN = 128;
-  constexpr int HB = HP * NW * 1024;             // bytes per halo buffer
-  constexpr int EP = BN * 4 + 16;                // epilogue row pitch (fp32)
-  constexpr int LDS_BYTES = 2 * HB > BM * EP ? 2 * HB : BM * EP;
-  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave % WM, wn = wave / WM;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int lrow = lane >> 3;
-  const int lc = (lane & 7) ^ lrow;
-  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
-  const int n_first = m0 / a.OHW;
-  const int r0 = (m0 - n_first * a.OHW) / OW;
-
-  // halo source offsets per piece, as in conv3x3_halo_kernel (kOOB = zero padding / past the halo)
-  unsigned h1[HP], h2[HP];
-#pragma unroll
-  for (int p = 0; p < HP; ++p) {
-    const int h = (wave * HP + p) * 8 + lrow;
-    h1[p] = kOOB; h2[p] = kOOB;
-    if (h < npix) {
-      const int img = h / segpix, rem = h - img * segpix;
-      const int hy = rem / HW, hx = rem - hy * HW;
-      const int iy = r0 + hy - 1, ix = hx - 1;
-      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
-        const unsigned sp = (unsigned)(((n_first + img) * a.H + iy) * a.W + ix);
-        h1[p] = (sp * a.ld1 + lc * 8) * 2u;
-        h2[p] = (sp * a.ld2 + lc * 8) * 2u;
-      }
-    }
-  }
-  // weight fragments of this lane: rows co = n0 + wn*64 + 16i + fr, 16-byte chunk fh (ks 0) / fh+4 (ks 1)
-  const int fr = lane & 15, fh = lane >> 4;
-  const unsigned wrow = (unsigned)(a.ntaps * a.Kc);
-  unsigned wo[8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int co = n0 + wn * 64 + i * 16 + fr;
-    const unsigned o = ((unsigned)co * wrow + fh * 8) * 2u;
-    wo[i] = co < a.Cout ? o : kOOB;
-    wo[4 + i] = co < a.Cout ? o + 64u : kOOB;
-  }
-  int hb[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int m = wm * 64 + j * 16 + fr;
-    const int img = m / (R * OW), rem = m - img * (R * OW);
-    const int r = rem / OW, col = rem - r * OW;
-    hb[j] = img * segpix + (r + 1) * HW + col + 1;
-  }
-
-  v4f acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-  const int nch = a.Kc / 64, nst = nch * 9;
-  v4i hv[HP];
-  auto halo_load = [&](int c0) __attribute__((always_inline)) {
-    if (c0 < a.C1) reg_load16<HP>(a.x1, h1, (unsigned)c0 * 2u, hv);
-    else reg_load16<HP>(a.x2, h2, (unsigned)(c0 - a.C1) * 2u, hv);
-  };
-  auto halo_store = [&](int buf) __attribute__((always_inline)) {
-    char* dst = lds + buf * HB + wave * HP * 1024 + lane * 16;
-#pragma unroll
-    for (int p = 0; p < HP; ++p) *(v4i*)(dst + p * 1024) = hv[p];
-  };
-  auto load_w = [&](int s, v4i* f) __attribute__((always_inline)) {
-    const int c = s / 9, t = s - c * 9;
-    reg_load16<8>(a.w, wo, (unsigned)(t * a.Kc + c * 64) * 2u, f);
-  };
-  auto stage = [&](int s, const v4i* cur, v4i* nxt) __attribute__((always_inline)) {
-    const int c = s / 9, t = s - c * 9;
-    load_w(s + 1 < nst ? s + 1 : s, nxt);   // always issued: no branch around the loads
-    if (t == 0 && c + 1 < nch) halo_load((c + 1) * 64);
-    const char* A = lds + (c & 1) * HB;
-    const int ty = t / 3, tx = t - ty * 3;
-    const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int chunk = ks * 4 + fh;
-      v4i fb[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int h = hb[j] + delta;
-        fb[j] = *(const v4i*)(A + h * 128 + ((chunk ^ (h & 7)) << 4));
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], cur[ks * 4 + i], fb[j]);
-    }
-    if (t == 8 && c + 1 < nch) {
-      // buffer (c+1)&1 was last read in chunk c-1, which every wave finished before the previous barrier
-      halo_store((c + 1) & 1);
-      __syncthreads();
-    }
-  };
-
-  halo_load(0);
-  v4i wa[8], wb[8];
-  load_w(0, wa);
-  halo_store(0);
-  __syncthreads();
-  for (int s = 0; s < nst; s += 2) {
-    stage(s, wa, wb);
-    if (s + 1 < nst) stage(s + 1, wb, wa);
-  }
-  __syncthreads();
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -2113,7 +1532,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvK a, const char* dy
 
 // ---------------------------------------------------------------------------------------------
 // Weight gradient of a 3x3 stride-1 conv with the activation HALO resident in LDS (the wgrad twin of
-// conv3x3_halo_kernel): dW[co][t][c] = sum_p dy[p][co] * x[p + shift(t)][c].
+// 3x3 halo conv): dW[co][t][c] = sum_p dy[p][co] * x[p + shift(t)][c].
 // Block = (64-channel chunk of x, 128 output channels, a range of 256-pixel tiles). Per tile the x halo
 // is DMA'd once and serves all 9 taps; dy streams in 64-pixel stages. 8 waves: 2 (co halves of 64) x 4
 // (quarters of the 9 taps x 4 column tiles = 36 16-wide n tiles, 9 per wave) -> 36 MFMA accumulators
@@ -2141,178 +1560,6 @@ DMC_DEV v4i tr_frag(const char* img, int row0, int seg) {
     out[2 * half + 1] = ii[1];
   }
   return out;
-}
-
-template <int HP>
-__global__ __launch_bounds__(512) void wgrad3x3_halo_kernel(ConvK a, const char* dy, int ld_dy, int dy_bytes,
-                                                            float* slab, int R, int nimg, int tiles_per_split) {
-  using T = bf16_t;
-  constexpr int HB = HP * 8 * 1024;      // halo buffer bytes
-  constexpr int DB = 64 * 256;           // dy stage: 64 pixels x 128 co
-  __shared__ __attribute__((aligned(16))) char lds[2 * HB + 3 * DB];
-  char* const dring = lds + 2 * HB;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave & 1, wq = wave >> 1;              // co half, n quarter
-  const int c0 = blockIdx.x * 64, co0 = blockIdx.y * 128;
-  const int ntiles = a.M / 256;
-  const int t_begin = blockIdx.z * tiles_per_split, t_end = min(ntiles, t_begin + tiles_per_split);
-  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
-  const bool first = c0 < a.C1;
-  const int cs = first ? c0 : c0 - a.C1;                // channel offset inside its source
-  const int lds_x = first ? a.ld1 : a.ld2;
-
-  // dy DMA: 2 pieces per wave per stage, piece = 4 pixel rows x 256 B; chunk-level source swizzle
-  unsigned od[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = (wave * 2 + j) * 4 + (lane >> 4);
-    const int pc = lane & 15;
-    const int lseg = (pc >> 1) ^ swz_dy(row);
-    const int co = co0 + lseg * 16 + (pc & 1) * 8;
-    od[j] = co < a.Cout ? ((unsigned)row * ld_dy + co) * 2u : kOOB;
-  }
-  // x halo DMA: lane -> (halo row, physical chunk), logical chunk from the segment swizzle of that row
-  unsigned hx[HP];
-  auto halo_offsets = [&](int tile) {
-    const int m0 = tile * 256;
-    const int n_first = m0 / a.OHW;
-    const int r0 = (m0 - n_first * a.OHW) / OW;
-#pragma unroll
-    for (int p = 0; p < HP; ++p) {
-      const int h = (wave * HP + p) * 8 + (lane >> 3);
-      hx[p] = kOOB;
-      if (h < npix) {
-        const int img = h / segpix, rem = h - img * segpix;
-        const int hr = rem / HW, hc = rem - hr * HW;
-        const int iy = r0 + hr - 1, ix = hc - 1;
-        const int lc = ((((lane & 7) >> 1) ^ swz_x(h)) << 1) | (lane & 1);
-        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-          hx[p] = ((unsigned)(((n_first + img) * a.H + iy) * a.W + ix) * lds_x + cs + lc * 8) * 2u;
-      }
-    }
-  };
-  auto halo_issue_w = [&](int buf, int pb, int pe) {
-    dma_pieces<HP>(first ? (const void*)a.x1 : (const void*)a.x2, first ? a.x1_bytes : a.x2_bytes,
-                   lds + buf * HB + wave * HP * 1024, hx, 0u, pb, pe);
-  };
-  auto dy_issue = [&](int st) {  // global stage index -> pixels [st*64, st*64+64) of the block's tile range
-    const int tile = t_begin + (st >> 2);
-    const unsigned base = (unsigned)(tile * 256 + (st & 3) * 64) * (unsigned)ld_dy * 2u;
-    dma_pieces<2>(dy, dy_bytes, dring + (st % 3) * DB + wave * 2 * 1024, od, base, 0, 2);
-  };
-
-  // halo row of tile-local output pixel pl for tap (0,0). The lane's 8-pixel group of k-step j is
-  // pl = 32j + 8h; since 32j moves by whole rows / images, hrow(32j + 8h) = hrow(8h) + hrow(32j) - hrow(0)
-  // (a wave-uniform shift).
-  const int fh = lane >> 4;
-  auto hrow = [&](int pl) {
-    const int img = pl / (R * OW), rem = pl - img * (R * OW);
-    const int r = rem / OW, col = rem - r * OW;
-    return img * segpix + (r + 1) * HW + col + 1;
-  };
-  const int hb0 = hrow(8 * fh), hz = hrow(0);
-  // this wave's 9 n tiles: u -> (tap, 16-channel column tile)
-  int dl[9];
-#pragma unroll
-  for (int u = 0; u < 9; ++u) {
-    const int nt = wq * 9 + u, t = nt >> 2;
-    const int ty = t / 3, tx = t - ty * 3;
-    dl[u] = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
-  }
-
-  v4f acc[4][9];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int u = 0; u < 9; ++u) acc[i][u] = v4f{0.f, 0.f, 0.f, 0.f};
-  // bias gradient (a.wgb, the first channel chunk's blocks): dy fragment i = wq times an all-ones B fragment, one
-  // extra MFMA per k-step per wave; every column of the 16x16 result is the pixel sum of its co row
-  const bool bias_on = a.wgb != nullptr && blockIdx.x == 0;
-  const v4i ones = {0x3F803F80, 0x3F803F80, 0x3F803F80, 0x3F803F80};   // bf16 1.0 pairs
-  v4f accb = {0.f, 0.f, 0.f, 0.f};
-
-  const int nt_blk = t_end - t_begin, nst = nt_blk * 4;
-  // the next tile's halo goes out in three parts (slots k = 0, 1, 2 of a tile): pieces [part_b(k), part_b(k+1))
-  // -- all HP of them (HP = 7 included: 2 + 2 + 3)
-  auto part_b = [](int k) { return k * HP / 3; };
-  auto slot_count = [&](int st) {   // vector-memory instructions issued in slot st
-    const int k = st & 3;
-    return (st + 2 < nst ? 2 : 0) + ((k < 3 && (st >> 2) + 1 < nt_blk) ? part_b(k + 1) - part_b(k) : 0);
-  };
-  if (nst > 0) {
-    halo_offsets(t_begin);
-    halo_issue_w(0, 0, HP);
-    if (nt_blk > 1) halo_offsets(t_begin + 1);
-    dy_issue(0);
-    if (nst > 1) dy_issue(1);
-  }
-  for (int st = 0; st < nst; ++st) {
-    wait_vm_dyn(st == 0 ? (nst > 1 ? 2 : 0) : slot_count(st - 1));
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("" ::: "memory");
-    const int tl = st >> 2, k = st & 3;
-    if (st + 2 < nst) dy_issue(st + 2);
-    if (k < 3 && tl + 1 < nt_blk) {
-      halo_issue_w((tl + 1) & 1, part_b(k), part_b(k + 1));
-      if (k == 2 && tl + 2 < nt_blk) halo_offsets(t_begin + tl + 2);
-    }
-    const char* X = lds + (tl & 1) * HB;
-    const char* D = dring + (st % 3) * DB;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int j = k * 2 + ks;                          // 32-pixel group inside the tile
-      const int hj = __builtin_amdgcn_readfirstlane(hrow(32 * j) - hz);
-      v4i fa[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = tr_frag<256, true>(D, ks * 32 + 8 * fh, wm * 4 + i);
-      // x fragments one n tile ahead: tile u+1's two transposed reads are in flight while tile u's four MFMAs
-      // run (left alone, hipcc waits for each fragment right before its MFMAs: lgkmcnt(0) every 4 MFMAs)
-      v4i fb = tr_frag<128, false>(X, hb0 + hj + dl[0], (wq * 9) & 3);
-#pragma unroll
-      for (int u = 0; u < 9; ++u) {
-        v4i fn = fb;
-        if (u + 1 < 9) fn = tr_frag<128, false>(X, hb0 + hj + dl[u + 1], (wq * 9 + u + 1) & 3);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][u] = mma16<T>(acc[i][u], fa[i], fb);
-        if (u + 1 < 9) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the next tile's reads
-          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // this tile's MFMAs
-        }
-        fb = fn;
-      }
-      if (bias_on) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (i == wq) accb = mma16<T>(accb, fa[i], ones);
-      }
-    }
-  }
-  if (bias_on && (lane & 15) == 0) {   // column 0: rows co = 4 fh + e of dy fragment wq
-    const int co = co0 + wm * 64 + wq * 16 + fh * 4;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) a.wgb[(size_t)blockIdx.z * (gridDim.y * 128) + co + e] = accb[e];
-  }
-  // partial dW -> slab [z][Cpad][9*Kc]: C[co = 4h+e][n = r]
-  const int Cpad = gridDim.y * 128;
-  const int KK = 9 * a.Kc;
-  float* out = slab + (size_t)blockIdx.z * Cpad * KK;
-  const int fr = lane & 15;
-#pragma unroll
-  for (int u = 0; u < 9; ++u) {
-    const int nt = wq * 9 + u, t = nt >> 2;
-    const int kk = t * a.Kc + c0 + (nt & 3) * 16 + fr;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int co = co0 + wm * 64 + i * 16 + fh * 4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) out[(size_t)(co + e) * KK + kk] = acc[i][u][e];
-    }
-  }
 }
 
 // Two-blocks-per-CU twin of wgrad3x3_halo_kernel (the step conv3x3_halo2_kernel made for the forward): block =
@@ -2920,8 +2167,8 @@ RegPlan plan_reg(const ConvK& k) {
 }
 
 // Halo kernel with the GN-affine+SiLU prologue applied to the resident halo (inference: no dropout, the
-// normalised activation is not needed for a weight gradient). Returns the DMA pieces (6/7) or 0.
-int halo_pro_plan(const ConvK& k, int* R, int* nimg) {
+// normalised activation is not needed for a weight gradient). Returns the DMA pieces (6/7/9) or 0.
+int halo2_pro_plan(const ConvK& k, int* R, int* nimg) {
   if (k.dtype_bytes != 2 || k.prologue != DMC_PRO_AFFINE_SILU || k.dthresh != 0 || k.ldp < k.C1 + k.C2) return 0;
   // default since round 2 (DMC_HALO_PRO=0 turns it off): with the GroupNorm statistics taken from the producing
   // conv's epilogue the activation is not read at all before this conv; DDIM-50 645 -> 658 img/s, CFG 379 -> 389
@@ -2931,40 +2178,16 @@ int halo_pro_plan(const ConvK& k, int* R, int* nimg) {
     return 0;
   const bool buf = k.C1 % 64 == 0 && k.C2 % 64 == 0 && k.Kc == k.C1 + k.C2 && k.x1_bytes > 0 &&
                    (k.C2 == 0 || k.x2_bytes > 0) && k.w_bytes > 0;
+  // small problems keep the split-K GEMM (fed by a materialised GroupNorm output)
   if (!buf || (plan_glds(k).splits != 1 && !dmc::opt(dmc::OPT_NO_SPLITK))) return 0;
-  const int hp = halo_plan(k, R, nimg);
-  return *nimg == 1 ? hp : 0;   // one image per tile: a lane's scale/shift row is the same in every piece
-}
-
-// halo_pro_plan for the two-blocks-per-CU kernel (DMC_HALO_VER=2)
-int halo2_pro_plan(const ConvK& k, int* R, int* nimg) {
-  if (k.dtype_bytes != 2 || k.prologue != DMC_PRO_AFFINE_SILU || k.dthresh != 0 || k.ldp < k.C1 + k.C2) return 0;
-  if (!dmc::opt(dmc::OPT_HALO_PRO) || dmc::opt(dmc::OPT_NO_HALO) || dmc::opt(dmc::OPT_NO_GLDS) ||
-      dmc::opt(dmc::OPT_NO_BUFLDS) || dmc::opt(dmc::OPT_HALO_VER) != 2)
-    return 0;
-  const bool buf = k.C1 % 64 == 0 && k.C2 % 64 == 0 && k.Kc == k.C1 + k.C2 && k.x1_bytes > 0 &&
-                   (k.C2 == 0 || k.x2_bytes > 0) && k.w_bytes > 0;
-  if (!buf) return 0;
   const int hp = halo2_plan(k, R, nimg);
-  return *nimg == 1 ? hp : 0;
+  return *nimg == 1 ? hp : 0;   // one image per tile: a lane's scale/shift row is the same in every piece
 }
 
 template <bool PRO>
 void launch_halo2(const ConvK& k, int hp, int R, int nimg, hipStream_t s) {
   const dim3 g = dmc::opt(dmc::OPT_NO_XCD) ? dim3(k.M / 128, dmc::cdiv(k.Cout, 128))
                                           : dim3(k.M / 128 * dmc::cdiv(k.Cout, 128));
-  if (dmc::opt(dmc::OPT_HALO_LATE)) {   // A/B: the later weight slice issued after the tap's MFMAs
-    if (hp == 6) conv3x3_halo2_kernel<6, 3, PRO, true, true><<<g, 256, 0, s>>>(k, R, nimg);
-    else if (hp == 7) conv3x3_halo2_kernel<7, 3, PRO, true, true><<<g, 256, 0, s>>>(k, R, nimg);
-    else conv3x3_halo2_kernel<9, 2, PRO, true, true><<<g, 256, 0, s>>>(k, R, nimg);
-    return;
-  }
-  if (dmc::opt(dmc::OPT_HALO_PRIV)) {   // wave-private weight rows, no per-tap barrier
-    if (hp == 6) conv3x3_halo3_kernel<6, 3, PRO><<<g, 256, 0, s>>>(k, R, nimg);
-    else if (hp == 7) conv3x3_halo3_kernel<7, 3, PRO><<<g, 256, 0, s>>>(k, R, nimg);
-    else conv3x3_halo3_kernel<9, 2, PRO><<<g, 256, 0, s>>>(k, R, nimg);
-    return;
-  }
   if (dmc::opt(dmc::OPT_HALO_NOSCHED)) {   // A/B: the compiler's own fragment-read schedule
     if (hp == 6) conv3x3_halo2_kernel<6, 3, PRO, false><<<g, 256, 0, s>>>(k, R, nimg);
     else if (hp == 7) conv3x3_halo2_kernel<7, 3, PRO, false><<<g, 256, 0, s>>>(k, R, nimg);
@@ -3073,18 +2296,15 @@ __global__ __launch_bounds__(256) void gn_bwd_part_kernel(const char* gy, int ld
 // Whether dmc_conv2d's chosen kernel emits the GroupNorm partials in its epilogue (tile_epilogue8: the round-1
 // halo kernel and the non-split LDS-DMA kernel, bf16, one NHWC output, whole 256-pixel tiles, 128-channel tiles).
 bool epi_stats_ok(const ConvK& k, const void* ws, size_t ws_bytes) {
-  if (dmc::opt(dmc::OPT_HALO_CHUNK)) return false;   // its 64-channel epilogue emits no partials
   if (k.dtype_bytes != 2 || k.out_f32 || k.out_nchw || k.silu_pre || k.Csplit != k.Cout || k.Cout % 128 ||
       k.M % 256 || k.OHW % 64 || ((k.Cout | k.ldy1 | k.ld_res) & 7))
     return false;
   if (!dmc::opt(dmc::OPT_NO_NARROW) && ((k.C2 == 0 && k.C1 <= 8 && k.Cout >= 16) || k.Cout <= 8)) return false;
-  if (dmc::opt(dmc::OPT_NO_GLDS) || (dmc::opt(dmc::OPT_HALO_VER) != 1 && dmc::opt(dmc::OPT_HALO_VER) != 2) ||
-      dmc::opt(dmc::OPT_HALO_RW) ||
-      dmc::opt(dmc::OPT_NO_EPI_STATS))
+  if (dmc::opt(dmc::OPT_NO_GLDS) || dmc::opt(dmc::OPT_NO_EPI_STATS))
     return false;
   if (k.prologue == DMC_PRO_AFFINE_SILU) {
     int R, nimg;
-    return halo2_pro_plan(k, &R, &nimg) != 0 || halo_pro_plan(k, &R, &nimg) != 0;
+    return halo2_pro_plan(k, &R, &nimg) != 0;
   }
   if (k.prologue != DMC_PRO_NONE) return false;
   const FwdPlan p = plan_glds(k);
@@ -3101,8 +2321,7 @@ bool epi_gnb_ok(const ConvK& k, const void* ws, size_t ws_bytes) {
   const bool split = p.splits > 1 && !(ws == nullptr || ws_bytes < p.ws || dmc::opt(dmc::OPT_NO_SPLITK));
   if (split) return false;
   int R, nimg;
-  if (buf && !dmc::opt(dmc::OPT_NO_HALO) && dmc::opt(dmc::OPT_HALO_VER) == 2 && halo2_plan(k, &R, &nimg)) return true;
-  if (buf && !dmc::opt(dmc::OPT_NO_HALO) && halo_plan(k, &R, &nimg)) return false;   // the 8-wave halo kernel
+  if (buf && !dmc::opt(dmc::OPT_NO_HALO) && halo2_plan(k, &R, &nimg)) return true;
   return p.splits > 1 || p.cfg != 0 || dmc::opt(dmc::OPT_GLDS_2B);
 }
 
@@ -3123,11 +2342,6 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     int R, nimg;
     const int hp2 = halo2_pro_plan(k, &R, &nimg);
     if (hp2) { launch_halo2<true>(k, hp2, R, nimg, s); return dmc::check_launch("dmc_conv2d"); }
-    const int hp = halo_pro_plan(k, &R, &nimg);
-    const dim3 hg1 = dmc::opt(dmc::OPT_NO_XCD) ? dim3(k.M / 256, dmc::cdiv(k.Cout, 128))
-                                               : dim3(k.M / 256 * dmc::cdiv(k.Cout, 128));   // 1-D: XCD-aware
-    if (hp == 6) { conv3x3_halo_kernel<6, 3, true><<<hg1, 512, 0, s>>>(k, R, nimg); return dmc::check_launch("dmc_conv2d"); }
-    if (hp == 7) { conv3x3_halo_kernel<7, 3, true><<<hg1, 512, 0, s>>>(k, R, nimg); return dmc::check_launch("dmc_conv2d"); }
   }
   if (sizeof(T) == 2 && k.prologue == DMC_PRO_NONE && !dmc::opt(dmc::OPT_NO_GLDS)) {
     // bf16, plain operands: LDS-DMA pipelined kernel
@@ -3136,31 +2350,9 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     if (p.splits > 1) { k.sk = (float*)ws; k.sk_per = p.per; }
     const bool buf = k.C1 % 64 == 0 && k.C2 % 64 == 0 && k.Kc == k.C1 + k.C2 && k.x1_bytes > 0 &&
                      (k.C2 == 0 || k.x2_bytes > 0) && k.w_bytes > 0 && !dmc::opt(dmc::OPT_NO_BUFLDS);
-    int R, nimg;
-    const int hp = (buf && p.splits == 1 && !dmc::opt(dmc::OPT_NO_HALO)) ? halo_plan(k, &R, &nimg) : 0;
-    const dim3 hg(k.M / 256, dmc::cdiv(k.Cout, 128));
-    const dim3 hgx = dmc::opt(dmc::OPT_NO_XCD) ? hg : dim3(hg.x * hg.y);   // 1-D: XCD-aware tile order
-    const long hver = dmc::opt(dmc::OPT_HALO_VER);   // 1: the 8-wave kernel, 2: two blocks per CU
     int R2, nimg2;
-    const int hp2 = (buf && p.splits == 1 && !dmc::opt(dmc::OPT_NO_HALO) && hver == 2 && !(hp && dmc::opt(dmc::OPT_HALO_CHUNK)))
-                        ? halo2_plan(k, &R2, &nimg2) : 0;
-    if (hp2) { launch_halo2<false>(k, hp2, R2, nimg2, s); return dmc::check_launch("dmc_conv2d"); }
-    if (hp && dmc::opt(dmc::OPT_HALO_CHUNK)) {   // A/B: a chunk's nine weight slices resident
-      const dim3 cg(k.M / 256 * dmc::cdiv(k.Cout, 64));
-      const bool prog = dmc::opt(dmc::OPT_HALO_CHUNK) == 2;
-      if (hp == 6 && prog) conv3x3_chunk_kernel<6, true><<<cg, 512, 0, s>>>(k, R, nimg);
-      else if (prog) conv3x3_chunk_kernel<7, true><<<cg, 512, 0, s>>>(k, R, nimg);
-      else if (hp == 6) conv3x3_chunk_kernel<6><<<cg, 512, 0, s>>>(k, R, nimg);
-      else conv3x3_chunk_kernel<7><<<cg, 512, 0, s>>>(k, R, nimg);
-    } else if (hp && dmc::opt(dmc::OPT_HALO_RW)) {
-      if (hp == 6) conv3x3_halo_rw_kernel<6><<<hg, 512, 0, s>>>(k, R, nimg);
-      else conv3x3_halo_rw_kernel<7><<<hg, 512, 0, s>>>(k, R, nimg);
-    } else if (hp == 6 && dmc::opt(dmc::OPT_HALO_WS4))
-      conv3x3_halo_kernel<6, 4><<<hgx, 512, 0, s>>>(k, R, nimg);
-    else if (hp == 6)
-      conv3x3_halo_kernel<6, 3><<<hgx, 512, 0, s>>>(k, R, nimg);
-    else if (hp == 7)
-      conv3x3_halo_kernel<7, 3><<<hgx, 512, 0, s>>>(k, R, nimg);
+    const int hp2 = (buf && p.splits == 1 && !dmc::opt(dmc::OPT_NO_HALO)) ? halo2_plan(k, &R2, &nimg2) : 0;
+    if (hp2) launch_halo2<false>(k, hp2, R2, nimg2, s);
     else if (buf) launch_glds<true>(k, p, s);
     else launch_glds<false>(k, p, s);
     return dmc::check_launch("dmc_conv2d");
@@ -3347,7 +2539,7 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   // bias partials after the weight slab (dmc_conv2d_wgrad_workspace sized for the larger split count)
   float* const bslab = d->wg_bias ? (float*)workspace + (size_t)splits * KK * Cpad : nullptr;
   k.wgb = bslab;
-  if (halo && dmc::opt(dmc::OPT_WG_HALO_VER) == 2) {
+  if (halo) {
     // two blocks per CU: 64-co blocks, the same split count (twice the co tiles, half the block target's share)
     g = dim3(d->Kc / 64, dmc::cdiv(d->Cout, 64), splits);
     if (hp.hp == 6)
@@ -3355,12 +2547,6 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
     else
       wgrad3x3_halo2_kernel<7><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
     g.y = dmc::cdiv(d->Cout, 128);   // the reduce's slab pitch: Cout rounded to 128
-  } else if (halo) {
-    g = dim3(d->Kc / 64, dmc::cdiv(d->Cout, 128), splits);
-    if (hp.hp == 6)
-      wgrad3x3_halo_kernel<6><<<g, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
-    else
-      wgrad3x3_halo_kernel<7><<<g, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
   } else if (w1x1) {
     g.z = splits;
     const dim3 g1(g.x * g.y * g.z);
@@ -3414,7 +2600,7 @@ extern "C" int dmc_conv_halo_prologue(const dmc_conv_desc* d) {
   ConvK k;
   if (fill_convk(d, nullptr, nullptr, nullptr, nullptr, nullptr, k) != 0) return 0;
   int R, nimg;
-  return halo_pro_plan(k, &R, &nimg) ? 1 : 0;
+  return halo2_pro_plan(k, &R, &nimg) ? 1 : 0;
 }
 
 extern "C" int dmc_pack_tiles(const dmc_pack_job* j, int job_index, int* tiles, int cap) {

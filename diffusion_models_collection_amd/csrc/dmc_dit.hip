@@ -188,31 +188,36 @@ __global__ __launch_bounds__(256) void ln_mod_bwd_kernel(const void* dh, int ld_
       }
     }
   }
-  // cross-wave reduction of the per-channel sums, fixed order (wave 0 + 1 + 2 + 3)
+  // cross-wave reduction of the per-channel sums, fixed order (wave 0 + 1 + 2 + 3), over 512-channel slices
+  // (hidden sizes up to the forward's 2048 with a 16 KB LDS scratch)
   float* rs_ = &red[0][0][0];
   const int stride = 2 * 512;
+  for (int cb = 0; cb < C; cb += 512) {
+    if (cb > 0) __syncthreads();   // the previous slice's reads are done
 #pragma unroll
-  for (int k = 0; k < kMaxV; ++k) {
-    const int c = (lane + 64 * k) * 4;
-    if (c < C) {
+    for (int k = 0; k < kMaxV; ++k) {
+      const int c = (lane + 64 * k) * 4;
+      if (c >= cb && c < cb + 512 && c < C) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        rs_[wave * stride + (c + e)] = as[k][e];
-        rs_[wave * stride + 512 + (c + e)] = ah[k][e];
+        for (int e = 0; e < 4; ++e) {
+          rs_[wave * stride + (c - cb + e)] = as[k][e];
+          rs_[wave * stride + 512 + (c - cb + e)] = ah[k][e];
+        }
       }
     }
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float s = 0.f, t = 0.f;
+    __syncthreads();
+    for (int cl = threadIdx.x; cl < 512 && cb + cl < C; cl += 256) {
+      const int c = cb + cl;
+      float s = 0.f, t = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) { s += rs_[w * stride + c]; t += rs_[w * stride + 512 + c]; }
-    if (S == 1) {
-      dscale[(size_t)b * ld_mod + c] = s;
-      dshift[(size_t)b * ld_mod + c] = t;
-    } else {
-      ws[((size_t)(b * S + sp) * 2) * C + c] = s;
-      ws[((size_t)(b * S + sp) * 2 + 1) * C + c] = t;
+      for (int w = 0; w < 4; ++w) { s += rs_[w * stride + cl]; t += rs_[w * stride + 512 + cl]; }
+      if (S == 1) {
+        dscale[(size_t)b * ld_mod + c] = s;
+        dshift[(size_t)b * ld_mod + c] = t;
+      } else {
+        ws[((size_t)(b * S + sp) * 2) * C + c] = s;
+        ws[((size_t)(b * S + sp) * 2 + 1) * C + c] = t;
+      }
     }
   }
 }
@@ -272,19 +277,23 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(const float* dy, const vo
       }
     }
   }
+  for (int cb = 0; cb < C; cb += 512) {   // 512-channel slices of the 8 KB LDS scratch (C up to 2048)
+    if (cb > 0) __syncthreads();
 #pragma unroll
-  for (int k = 0; k < kMaxV; ++k) {
-    const int c = (lane + 64 * k) * 4;
-    if (c < C) {
+    for (int k = 0; k < kMaxV; ++k) {
+      const int c = (lane + 64 * k) * 4;
+      if (c >= cb && c < cb + 512 && c < C) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) red[wave][c + e] = acc[k][e];
+        for (int e = 0; e < 4; ++e) red[wave][c - cb + e] = acc[k][e];
+      }
     }
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    const float v = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
-    if (S == 1) dgate[(size_t)b * ld_mod + c] = v;
-    else ws[(size_t)(b * S + sp) * C + c] = v;
+    __syncthreads();
+    for (int cl = threadIdx.x; cl < 512 && cb + cl < C; cl += 256) {
+      const int c = cb + cl;
+      const float v = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+      if (S == 1) dgate[(size_t)b * ld_mod + c] = v;
+      else ws[(size_t)(b * S + sp) * C + c] = v;
+    }
   }
 }
 
@@ -458,7 +467,8 @@ extern "C" size_t dmc_dit_rowsum_workspace(int B, int C, int L) {
 extern "C" int dmc_ln_mod_bwd(int dtype, const void* dh, int ld_dh, const float* x, const float* mean,
                               const float* rstd, const float* scale, int ld_mod, int T, int C, int L, float* dx,
                               float* dscale, float* dshift, void* workspace, void* stream) {
-  DMC_REQUIRE(C % 4 == 0 && C <= 512 && T % L == 0 && L > 0, "ln_mod_bwd: C %d (<= 512) T %d L %d", C, T, L);
+  DMC_REQUIRE(C % 4 == 0 && C <= 64 * 4 * kMaxV && T % L == 0 && L > 0, "ln_mod_bwd: C %d (<= %d) T %d L %d", C,
+              64 * 4 * kMaxV, T, L);
   hipStream_t s = dmc::as_stream(stream);
   const int B = T / L;
   const int S = workspace ? row_splits(B, L) : 1;
@@ -475,7 +485,8 @@ extern "C" int dmc_ln_mod_bwd(int dtype, const void* dh, int ld_dh, const float*
 extern "C" int dmc_gate_bwd(int dtype, const float* dy, const void* br, int ld_br, const float* gate, int ld_mod, int T,
                             int C, int L, uint32_t drop_seed, const uint32_t* drop_seed_base, uint32_t drop_thresh,
                             float drop_scale, void* dbr, int ld_dbr, float* dgate, void* workspace, void* stream) {
-  DMC_REQUIRE(C % 4 == 0 && C <= 512 && T % L == 0 && L > 0, "gate_bwd: C %d (<= 512) T %d L %d", C, T, L);
+  DMC_REQUIRE(C % 4 == 0 && C <= 64 * 4 * kMaxV && T % L == 0 && L > 0, "gate_bwd: C %d (<= %d) T %d L %d", C,
+              64 * 4 * kMaxV, T, L);
   const Drop d = make_drop(drop_seed, drop_seed_base, drop_thresh, drop_scale);
   hipStream_t s = dmc::as_stream(stream);
   const int B = T / L;

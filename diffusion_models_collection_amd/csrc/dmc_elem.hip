@@ -35,14 +35,14 @@ struct OptDef {
 // name (= environment variable), default
 constexpr OptDef kOpts[OPT_COUNT] = {
     {"DMC_NO_NARROW", 0},  {"DMC_NO_GLDS", 0},        {"DMC_NO_SPLITK", 0},          {"DMC_NO_BUFLDS", 0},
-    {"DMC_NO_HALO", 0},    {"DMC_HALO_PRO", 1},       {"DMC_HALO_RW", 0},            {"DMC_HALO_WS4", 0},
+    {"DMC_NO_HALO", 0},    {"DMC_HALO_PRO", 1},
     {"DMC_GN_STATS_SPLIT", 0}, {"DMC_GN_BWD_SPLIT", 0}, {"DMC_ATTN_STAGED", 0},    {"DMC_ATTN_HG", 0},
-    {"DMC_WG_BLOCKS", 512}, {"DMC_GN_STATS_ONE_MAX", 1l << 20}, {"DMC_GN_BWD_ONE_MAX", 65536}, {"DMC_HALO_VER", 2},
+    {"DMC_WG_BLOCKS", 512}, {"DMC_GN_STATS_ONE_MAX", 1l << 20}, {"DMC_GN_BWD_ONE_MAX", 65536},
     {"DMC_NO_XCD", 0}, {"DMC_NO_EPI_STATS", 0}, {"DMC_HALO_NOSCHED", 0}, {"DMC_GLDS_2B", 1}, {"DMC_WG_MINPIX", 0},
-    {"DMC_WG_1X1", 1}, {"DMC_WG_HALO_VER", 2}, {"DMC_GN_BWD_SLICES", 2},
+    {"DMC_WG_1X1", 1}, {"DMC_GN_BWD_SLICES", 2},
     {"DMC_WG_TAPS", 0}, {"DMC_NO_SKGN", 0},
-    {"DMC_WG_HALO_TARGET", 256}, {"DMC_HALO_PRIV", 0},
-    {"DMC_STAMP_PTR", 0}, {"DMC_HALO_LATE", 0}, {"DMC_HALO_CHUNK", 0},
+    {"DMC_WG_HALO_TARGET", 256},
+    {"DMC_STAMP_PTR", 0},
 };
 struct OptTable {
   long v[OPT_COUNT];

@@ -121,6 +121,11 @@ class DeviceLoader:
         batches = self.epoch_indices()
         if isinstance(self.sampler, DistributedSampler):
             self.epoch = self.sampler.epoch
+        ep = self.epoch
+        if self.sampler is None:
+            # advance when the epoch STARTS: an iteration cut short (early break, an exception) must not make the
+            # next epoch reuse this epoch's flips
+            self.epoch += 1
         if not batches:
             return
         flat = torch.cat(batches)
@@ -128,7 +133,7 @@ class DeviceLoader:
         if flat.numel() and (int(flat.min()) < 0 or int(flat.max()) >= n):
             raise IndexError("sampler produced an index outside the dataset")
         idx = flat.to(torch.int32).to(self.device, non_blocking=True)
-        fseed = epoch_seed(self.seed, self.epoch)
+        fseed = epoch_seed(self.seed, ep)
         # flip-hash positions: the rank's slice of the epoch (distributed) so ranks draw independent flips
         pos = self.sampler.rank * self.sampler.num_samples if isinstance(self.sampler, DistributedSampler) else 0
         pos_base = pos
@@ -140,8 +145,6 @@ class DeviceLoader:
                            labels=self.labels if self.conditional else None, labels_out=y)
             pos += B
             yield (x, y) if self.conditional else x
-        if self.sampler is None:
-            self.epoch += 1
 
 
 def get_dataloader(config, dataset, rank=0, world_size=1, train=True, device=None):

@@ -17,9 +17,16 @@ arithmetic, and that is what made the round-1 tables host-dependent:
 
 Everything else (+, -, *, /, clamp, pad) is IEEE fp32 in both. The op ORDER is the reference's, operation
 for operation, so `build_tables(prims=TorchPrims)` on the fixture host reproduces every one of the 36
-fixture tables bit for bit (tests/test_abi_api.py), and the product tables (`IEEE`) are identical on every
-host and equal the fixture everywhere except at the entries where the fixture host's MKL sqrt/cos was
-itself not correctly rounded (each such entry is checked to be exactly that case, <= 1 ulp at the sqrt).
+fixture tables bit for bit (tests/test_abi_api.py), and the product tables (`IEEE`) equal the fixture
+everywhere except at the entries where the fixture host's MKL sqrt/cos was itself not correctly rounded (each
+such entry is checked to be exactly that case, <= 1 ulp at the sqrt).
+
+Host independence, precisely: sqrt is IEEE (correctly rounded) everywhere. log and cos are evaluated in double by
+the host libm and rounded once to fp32; that equals the correctly rounded fp32 result unless the double value
+falls within libm's error of an fp32 rounding boundary. tests/test_abi_api.py
+(test_schedule_log_cos_rounding_margin) checks, for every log / cos argument the three schedules use, that the
+double value is more than 64 double ulps from the nearest fp32 rounding boundary, so any libm accurate to 64 ulps
+gives the same fp32 bits.
 """
 import math
 

@@ -10,7 +10,8 @@ Arithmetic runs in fused HIP kernels (libdmc.so):
 The cond/uncond forwards of CFG are batched into ONE 2B forward.
 
 Schedule tables are built on the host by _schedule.py: the reference's op sequence as explicit IEEE fp32
-numpy arithmetic (identical bits on every host), then uploaded once.
+numpy arithmetic (the same bits on any host whose libm log/cos are accurate to 64 double ulps: _schedule.py),
+then uploaded once.
 
 Extra optional keyword arguments (not in the reference, all default to the reference behaviour):
 p_sample(noise=...), sample(x_T=...), sample_with_cfg(x_T=...) inject the Gaussian draws for parity tests.

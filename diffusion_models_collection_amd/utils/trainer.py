@@ -246,6 +246,7 @@ class GraphedTrainStep:
     def __init__(self, trainer):
         self.tr = trainer
         self.calls = 0
+        self.ring_wait_s = 0.0       # host seconds spent waiting for a pinned ring slot (paces the host to the GPU)
         self.graph = None
         self.failed = False
         self.key = None
@@ -337,7 +338,9 @@ class GraphedTrainStep:
                 state["done"] = hi
                 begin()
 
-        hook.wants = lambda hi, final: True
+        # the executor joins its weight-gradient side stream only where a segment ends (True here
+        # serialised the side stream after every record of every captured segment)
+        hook.wants = lambda hi, final: final or gs.cut(hi, state["done"], ex.gtotal, final)
         self.one = torch.ones((), dtype=torch.float32, device=dev)
         old_hook = ex.grad_hook
         ex.grad_hook = hook
@@ -426,7 +429,9 @@ class GraphedTrainStep:
         k = self.slot % self.RING
         self.slot += 1
         if self.ring_ev[k] is not None:
+            t0 = time.perf_counter()
             self.ring_ev[k].synchronize()      # the pinned slot's previous copy has been consumed
+            self.ring_wait_s += time.perf_counter() - t0
         self.ring[k].copy_(h)
         self.h_dev.copy_(self.ring[k], non_blocking=True)
         ev = torch.cuda.Event()
@@ -457,9 +462,7 @@ class DiffusionTrainer:
                 with torch.no_grad():
                     for t in list(self.model.parameters()) + list(self.model.buffers()):
                         dist.broadcast(t, src=0)
-                # bucket size: the reference's DDP default (25 MB); 'ddp_bucket_mb' (not a reference key) overrides
-                bmb = float((config or {}).get('ddp_bucket_mb', 25))
-                self.grad_sync = GradSync(self.model.executor, bucket_bytes=int(bmb * 1024 * 1024))
+                self.grad_sync = self._make_grad_sync(config)
             else:
                 self.model = DDP(model)
 
@@ -518,6 +521,21 @@ class DiffusionTrainer:
                          experiment_name=self.config.get('experiment_name', 'experiment'), config=self.config)
 
     # ------------------------------------------------------------------------------------------
+    def _make_grad_sync(self, config, process_group=None):
+        # bucket size: the reference's DDP default (25 MB); 'ddp_bucket_mb' (not a reference key) overrides
+        bmb = float((config or {}).get('ddp_bucket_mb', 25))
+        return GradSync(self.model.executor, process_group=process_group, bucket_bytes=int(bmb * 1024 * 1024))
+
+    def enable_grad_sync(self, process_group=None):
+        """Average gradients over `process_group` (default: the initialised default group) from inside the HIP
+        backward even when this trainer was built with world_size 1 -- the data-parallel step (GradSync + the
+        segmented graph) on a one-rank group, used to exercise and time the RCCL path on a single GPU."""
+        if not dist.is_initialized() or not _is_dmc_model(self._raw_model):
+            raise RuntimeError("enable_grad_sync needs an initialised process group and a dmc backbone")
+        self.grad_sync = self._make_grad_sync(self.config, process_group)
+        self._graph = GraphedTrainStep(self) if GraphedTrainStep.supported(self) else None
+        return self.grad_sync
+
     @property
     def _module(self):
         return self.model.module if isinstance(self.model, DDP) else self.model
@@ -624,6 +642,8 @@ class DiffusionTrainer:
         if self.is_distributed and hasattr(self.train_loader, "sampler") and hasattr(self.train_loader.sampler,
                                                                                      "set_epoch"):
             self.train_loader.sampler.set_epoch(epoch)
+        elif hasattr(self.train_loader, "set_epoch"):
+            self.train_loader.set_epoch(epoch)      # the device loader's flip hash is keyed by the epoch
         progress_bar = tqdm(self.train_loader, desc=f"Epoch {epoch}/{self.epochs}", disable=not self.is_main_process)
         self.optimizer.zero_grad()
         for i, batch in enumerate(progress_bar):

@@ -35,6 +35,10 @@ Fixture list (every array is float32 / int64 data, loaded with numpy.load(allow_
                      gradients of sum(out * cot) w.r.t. every parameter and x
   dit_s2.npz         DiT-S/2 at 32x32 (BASELINE config #4): weights NOT stored (seed + perturbation are
                      reproduced, per-tensor checksums pin them), output, grad_x, gradient summaries
+  trainer_1k.npz     north_star "p_losses ... over 1k steps": the reference DiffusionTrainer for 1000 steps on the
+                     tiny unconditional UNet (dropout 0; inputs = numpy PCG64 draws from stored seeds), every
+                     step's loss, theta_k at k = 0/250/500/750 with the step-k gradient summaries, AdamW moments
+                     at k = 500, final parameter / EMA sums, and the same run on one host thread (losses_alt)
 """
 import os
 import sys
@@ -464,11 +468,110 @@ def gen_dit_s2(B=2):
     npz(OUT / "dit_s2.npz", **arrs)
 
 
+K1_STEPS, K1_B = 1000, 4
+K1_SNAP = (0, 250, 500, 750)      # theta_k stored (weights BEFORE step k, i.e. the ones step k's loss sees)
+K1_OPT = 500                      # AdamW exp_avg / exp_avg_sq stored here too (teacher-forced window restart)
+K1_SEEDS = (41, 42, 43)           # numpy PCG64 seeds of x0 / t / noise; the tests regenerate the draws
+
+
+def k1_inputs():
+    """The 1000 steps' inputs, host-independent: numpy PCG64 draws in step order (x0 ~ U(-1,1), t ~ U{0..999},
+    noise ~ N(0,1), float32)."""
+    rx, rt, rn = (np.random.default_rng(s) for s in K1_SEEDS)
+    shape = (K1_B, 3, 16, 16)
+    xs, ts, ns = [], [], []
+    for _ in range(K1_STEPS):
+        xs.append(torch.from_numpy(rx.random(shape, dtype=np.float32) * np.float32(2) - np.float32(1)))
+        ts.append(torch.from_numpy(rt.integers(0, 1000, (K1_B,), dtype=np.int64)))
+        ns.append(torch.from_numpy(rn.standard_normal(shape, dtype=np.float32)))
+    return xs, ts, ns
+
+
+def _run_ref_1k(threads, capture):
+    """The reference DiffusionTrainer (utils/trainer.py:221-273) for 1000 steps on the tiny unconditional UNet
+    (dropout 0, l2, clip 1.0, AdamW lr 2e-4 wd 1e-4, EMA 0.9999), t and noise injected per step."""
+    from utils import trainer as trainer_mod
+    torch.set_num_threads(threads)
+    cfg = dict(TINY_CFGS["unet_tiny_uncond"])
+    torch.manual_seed(1234)
+    m = UNet(**cfg).float()
+    xs, ts, ns = k1_inputs()
+    ddpm = DDPM(1000, 1e-4, 0.02, "linear", device="cpu")
+    opt = torch.optim.AdamW(m.parameters(), lr=2e-4, weight_decay=1e-4)
+    config = {"epochs": 1, "save_dir": "/tmp/gg_ckpt1k", "sample_dir": "/tmp/gg_smp1k", "loss_type": "l2",
+              "use_ema": True, "ema_decay": 0.9999, "model_type": "unet",
+              "model_params": {k: v for k, v in cfg.items() if k != "num_classes"}}
+    tr = trainer_mod.DiffusionTrainer(m, ddpm, xs, opt, None, device="cpu", config=config)
+    t_it, n_it = iter(ts), iter(ns)
+    losses = []
+    snaps = {}
+    step = [0]
+    orig_pl, orig_clip = ddpm.p_losses, torch.nn.utils.clip_grad_norm_
+    orig_randint, orig_randn_like = torch.randint, torch.randn_like
+
+    def p_losses(model, x, t, y=None, noise=None, loss_type="l2"):
+        k = step[0]
+        if capture and k in K1_SNAP:
+            snaps[f"theta/{k}"] = {n: v.detach().clone() for n, v in m.state_dict().items()}
+            if k == K1_OPT:
+                snaps["m"] = {n: opt.state[p]["exp_avg"].clone() for n, p in m.named_parameters()}
+                snaps["v"] = {n: opt.state[p]["exp_avg_sq"].clone() for n, p in m.named_parameters()}
+        loss = orig_pl(model, x, t, y, noise=noise, loss_type=loss_type)
+        losses.append(loss.item())
+        return loss
+
+    def clip(params, max_norm, *a, **kw):
+        k = step[0]
+        if capture and k in K1_SNAP:
+            snaps[f"grad/{k}"] = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+        step[0] += 1
+        return orig_clip(params, max_norm, *a, **kw)
+
+    ddpm.p_losses = p_losses
+    torch.nn.utils.clip_grad_norm_ = clip
+    torch.randint = lambda *a, **kw: next(t_it)
+    torch.randn_like = lambda a, *k, **kw: next(n_it).clone()
+    try:
+        tr.train_epoch(1)
+    finally:
+        torch.randint, torch.randn_like = orig_randint, orig_randn_like
+        torch.nn.utils.clip_grad_norm_ = orig_clip
+        ddpm.p_losses = orig_pl
+        torch.set_num_threads(8)
+    assert len(losses) == K1_STEPS
+    return losses, snaps, m, tr
+
+
+def gen_trainer_1k():
+    """north_star "p_losses matching reference to 1e-4 over 1k steps" (SURVEY §7 protocol (ii)): the reference's
+    1000-step training run with every step's loss, the weights theta_k at K1_SNAP (with the step-k gradient as a
+    per-tensor summary), AdamW state at K1_OPT, and the same run on ONE host thread (`losses_alt`: the spread a
+    mere change of summation order produces, which calibrates the free-running band of the GPU test)."""
+    losses, snaps, m, tr = _run_ref_1k(8, True)
+    alt, _, _, _ = _run_ref_1k(1, False)
+    arrs = {"losses": np.array(losses, dtype=np.float64), "losses_alt": np.array(alt, dtype=np.float64),
+            "snap_steps": np.array(K1_SNAP), "opt_step": np.array([K1_OPT]), "seeds": np.array(K1_SEEDS),
+            "batch": np.array([K1_B])}
+    for k in K1_SNAP:
+        for n, v in snaps[f"theta/{k}"].items():
+            arrs[f"theta/{k}/{n}"] = v
+        for n, v in snaps[f"grad/{k}"].items():
+            grad_summary(n, v, arrs, f"g{k}/")
+    for n in snaps["m"]:
+        arrs[f"exp_avg/{n}"] = snaps["m"][n]
+        arrs[f"exp_avg_sq/{n}"] = snaps["v"][n]
+    for n, v in m.state_dict().items():
+        arrs[f"psum_final/{n}"] = v.double().sum().reshape(1)
+    for n, v in tr.ema_model.state_dict().items():
+        arrs[f"esum_final/{n}"] = v.double().sum().reshape(1)
+    npz(OUT / "trainer_1k.npz", **arrs)
+
+
 GENERATORS = {"schedules": gen_schedules, "tiny": lambda: [gen_unet(n, c) for n, c in TINY_CFGS.items()],
               "diffusion_ops": gen_diffusion_ops, "trainer_traj": gen_trainer_traj,
               "ddpm_sample": gen_ddpm_sample, "big": lambda: [gen_big_unet(n, c) for n, c in BIG_CFGS.items()],
               "checkpoint": gen_checkpoint, "dit": lambda: [gen_dit(n, c) for n, c in DIT_CFGS.items()],
-              "dit_s2": gen_dit_s2}
+              "dit_s2": gen_dit_s2, "trainer_1k": gen_trainer_1k}
 
 
 if __name__ == "__main__":

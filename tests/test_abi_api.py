@@ -61,6 +61,45 @@ def test_schedule_op_sequence_reproduces_fixture():
                 assert np.array_equal(v.view(np.int32), g[f"{kind}/{name}"].numpy().view(np.int32)), (kind, name)
 
 
+def test_schedule_log_cos_rounding_margin():
+    """log / cos go through the host libm in double and are rounded once to fp32. For every argument
+    the three schedules pass to them, the double result lies more than 64 double ulps away from the nearest fp32
+    rounding boundary (midpoint between adjacent fp32 values), so any libm accurate to 64 ulps produces the same
+    fp32 table bits: the tables are host-independent under that (weak) accuracy assumption."""
+    import math
+    import numpy as np
+    from diffusion_models_collection_amd.diffusion import _schedule as S
+    args = {"log": [], "cos": []}
+
+    class Rec(S.IEEE):
+        @staticmethod
+        def log(x):
+            args["log"].extend(np.asarray(x, np.float32).ravel().tolist())
+            return S.IEEE.log(x)
+
+        @staticmethod
+        def cos(x):
+            args["cos"].extend(np.asarray(x, np.float32).ravel().tolist())
+            return S.IEEE.cos(x)
+
+    for kind in ("linear", "cosine", "quadratic"):
+        S.build_tables(1000, 1e-4, 0.02, kind, prims=Rec)
+    assert args["log"] and args["cos"]
+    worst = math.inf
+    for name, fn in (("log", math.log), ("cos", math.cos)):
+        for v in args[name]:
+            d = fn(float(v))
+            f = np.float32(d)
+            if float(f) == d or d == 0.0:
+                continue
+            other = np.nextafter(f, np.float32(np.inf) if d > float(f) else np.float32(-np.inf))
+            mid = (float(f) + float(other)) / 2.0
+            margin = abs(d - mid) / math.ulp(d)
+            worst = min(worst, margin)
+            assert margin > 64, (name, v, d, margin)
+    print(f"worst log/cos margin to an fp32 rounding boundary: {worst:.3g} double ulps")
+
+
 def test_schedule_tables_host_independent_and_pinned():
     """Product tables: IEEE op sequence (identical on every host), pinned against the fixture per
     conftest.check_schedule_vs_fixture; DDIM timesteps bit-exact for every fixture (T, S)."""

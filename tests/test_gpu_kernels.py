@@ -123,16 +123,14 @@ def test_upsample2x_nhwc_bitwise(dt):
     assert torch.equal(y.permute(0, 3, 1, 2).float(), ref)
 
 
-@pytest.mark.parametrize("ver", [1, 2])
 @pytest.mark.parametrize("case", ["c32_two_sources", "c16_wide", "c32_384", "c8_multi_image"])
-def test_conv3x3_halo_gn_silu_prologue(case, ver, monkeypatch, dmc_opt):
+def test_conv3x3_halo_gn_silu_prologue(case, monkeypatch, dmc_opt):
     """Inference prologue on the halo kernel: conv(SiLU(x*scale+shift)) with the GroupNorm affine + SiLU
     applied to the LDS-resident halo equals, BITWISE, dmc_gn_apply materialisation followed by the plain halo
     conv (same op sequence and bf16 rounding), and the fp32 torch reference within bf16 tolerance."""
     L, K = _lib()
     dmc_opt("DMC_NO_SPLITK", 1)   # small N: keep the planner on the halo kernel
     dmc_opt("DMC_HALO_PRO", 1)    # the halo prologue path (default on)
-    dmc_opt("DMC_HALO_VER", ver)  # 1: 256-pixel 8-wave kernel, 2: 128-pixel two-blocks-per-CU kernel
     dt = torch.bfloat16
     torch.manual_seed(11)
     N, H, C1, C2, Cout = {"c32_two_sources": (2, 32, 128, 64, 128), "c16_wide": (3, 16, 256, 0, 256),
@@ -229,21 +227,16 @@ def test_conv_dgrad_wgrad(dt, case):
     assert rel_err(db.cpu(), g.sum((0, 2, 3))) < 1e-5
 
 
-@pytest.mark.parametrize("variant", ["ring3", "ring4", "regw", "halo2", "halo3", "halo2_late", "chunk", "chunk_prog"])
+@pytest.mark.parametrize("variant", ["halo2", "halo2_nosched"])
 @pytest.mark.parametrize("case", ["fwd32_concat", "fwd16_ragged_cout", "dgrad32", "fwd8_multi_image", "fallback_4x4",
                                   "fwd8_concat_b128", "fwd64_rows"])
 def test_conv3x3_halo_kernel(case, variant, monkeypatch, dmc_opt):
-    """bf16 3x3 stride-1 convs on the LDS-halo kernel (whole-row 256-pixel tiles) vs an fp32 reference and
-    vs the per-tap kernel (DMC_NO_HALO) on the same inputs. Variants: 3- or 4-slot LDS-DMA weight ring
-    (DMC_HALO_WS4), register-staged weights (DMC_HALO_RW), the two-blocks-per-CU 128-pixel kernel
-    (DMC_HALO_VER=2)."""
+    """bf16 3x3 stride-1 convs on the LDS-halo kernel (conv3x3_halo2_kernel: 128-pixel tiles of whole rows or
+    whole images, two blocks per CU) vs an fp32 reference and vs the per-tap kernel (DMC_NO_HALO) on the same
+    inputs; its weight-gradient twin (wgrad3x3_halo2_kernel) likewise. Variants: the scheduled fragment reads
+    (default) and the compiler's own schedule (DMC_HALO_NOSCHED)."""
     L, K = _lib()
-    dmc_opt("DMC_HALO_VER", 2 if variant in ("halo2", "halo3", "halo2_late") else 1)
-    dmc_opt("DMC_HALO_LATE", 1 if variant == "halo2_late" else 0)
-    dmc_opt("DMC_HALO_PRIV", 1 if variant == "halo3" else 0)   # wave-private weight rows, no per-tap barrier
-    dmc_opt("DMC_HALO_WS4", 1 if variant == "ring4" else 0)
-    dmc_opt("DMC_HALO_RW", 1 if variant == "regw" else 0)
-    dmc_opt("DMC_HALO_CHUNK", {"chunk": 1, "chunk_prog": 2}.get(variant, 0))   # a chunk's nine weight slices resident
+    dmc_opt("DMC_HALO_NOSCHED", 1 if variant == "halo2_nosched" else 0)
     # at these small M the planner would split K over the LDS-DMA kernel instead; the halo kernel is what the
     # B=128 model runs, so keep split-K off here to exercise it
     dmc_opt("DMC_NO_SPLITK", 1)
@@ -681,7 +674,7 @@ def test_conv_fp32_gemm_splitk_silu_pre(Cin, Cout):
     assert rel_err(y.view(N, Cout).cpu(), ref) < 1e-5
 
 
-@pytest.mark.parametrize("case", ["halo3x3", "halo2_3x3", "glds1x1", "splitk_small", "fp32_reg", "concat_two"])
+@pytest.mark.parametrize("case", ["halo2_3x3", "glds1x1", "splitk_small", "fp32_reg", "concat_two"])
 def test_conv_epilogue_groupnorm_partials(case, dmc_opt):
     """dmc_conv_desc.gn_part + dmc_gn_finalize (the conv epilogue's GroupNorm partials: in-kernel on the halo and
     LDS-DMA paths, one pass over the output elsewhere) give the statistics dmc_gn_stats computes over the stored
@@ -689,9 +682,8 @@ def test_conv_epilogue_groupnorm_partials(case, dmc_opt):
     from diffusion_models_collection_amd import _lib as L, kernels as K
     gen = torch.Generator().manual_seed(11)
     dt = torch.float32 if case == "fp32_reg" else torch.bfloat16
-    dmc_opt("DMC_HALO_VER", 2 if case == "halo2_3x3" else 1)
     # (the halo cases need >= 240 256x128 tiles: fewer take the split-K path, whose partials come from one pass)
-    N, H, W, Cin, Cout, taps = {"halo3x3": (32, 32, 32, 128, 256, K.TAPS3), "glds1x1": (8, 16, 16, 256, 256, K.TAPS1),
+    N, H, W, Cin, Cout, taps = {"glds1x1": (8, 16, 16, 256, 256, K.TAPS1),
                                 "halo2_3x3": (32, 32, 32, 128, 256, K.TAPS3),
                                 "splitk_small": (2, 8, 8, 256, 256, K.TAPS3), "fp32_reg": (2, 16, 16, 64, 128, K.TAPS3),
                                 "concat_two": (4, 16, 16, 128, 128, K.TAPS3)}[case]
@@ -719,7 +711,7 @@ def test_conv_epilogue_groupnorm_partials(case, dmc_opt):
         dmc_opt("DMC_NO_SKGN", 0)
         torch.cuda.synchronize()
         assert torch.equal(y1, y1s) and torch.equal(p1, p1s)
-    if case in ("halo3x3", "halo2_3x3"):
+    if case == "halo2_3x3":
         d = K.make_desc(dt, N, H, W, Cin, 0, Cin, 0, L.kc_for(Cin, dt), H, W, Cout, taps)
         K.set_epilogue(d, ldy1=Cout)
         assert K.conv_fused(d) & L.FUSED_GN_STATS, case
@@ -736,8 +728,8 @@ def test_conv_epilogue_groupnorm_partials(case, dmc_opt):
         assert rel_err(got, ref) < 2e-5, (case, rel_err(got, ref))
 
 
-@pytest.mark.parametrize("case", ["halo2_3x3", "glds1x1_2b", "glds1x1_8wave", "halo1_3x3", "splitk_small",
-                                  "concat_two", "cfg2_small"])
+@pytest.mark.parametrize("case", ["halo2_3x3", "glds1x1_2b", "glds1x1_8wave", "splitk_small", "concat_two",
+                                  "cfg2_small"])
 @pytest.mark.parametrize("silu,dropout", [(True, False), (True, True), (False, False)])
 def test_conv_epilogue_groupnorm_backward_partials(case, silu, dropout, dmc_opt):
     """dmc_conv_desc.gnb: the conv that produces the gradient g of dropout(SiLU(GroupNorm(x))) also writes the
@@ -747,11 +739,10 @@ def test_conv_epilogue_groupnorm_backward_partials(case, silu, dropout, dmc_opt)
     reduction (summation order only)."""
     import numpy as np
     from diffusion_models_collection_amd import _lib as L, kernels as K
-    dmc_opt("DMC_HALO_VER", 1 if case == "halo1_3x3" else 2)
     dmc_opt("DMC_GLDS_2B", 0 if case == "glds1x1_8wave" else 1)
     N, H, W, Cin, C1, C2, taps = {
         "halo2_3x3": (32, 32, 32, 128, 256, 0, K.TAPS3), "glds1x1_2b": (128, 16, 16, 256, 256, 0, K.TAPS1),
-        "glds1x1_8wave": (128, 16, 16, 256, 256, 0, K.TAPS1), "halo1_3x3": (32, 32, 32, 128, 256, 0, K.TAPS3),
+        "glds1x1_8wave": (128, 16, 16, 256, 256, 0, K.TAPS1),
         "splitk_small": (2, 8, 8, 256, 256, 0, K.TAPS3), "concat_two": (64, 16, 16, 128, 128, 128, K.TAPS3),
         "cfg2_small": (2, 16, 16, 128, 128, 0, K.TAPS1)}[case]
     C, G, dt, HW = C1 + C2, 8, torch.bfloat16, H * W

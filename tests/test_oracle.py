@@ -303,3 +303,27 @@ def test_oracle_dit_s2():
     torch.testing.assert_close(x.grad, g["grad_x"], rtol=1e-3, atol=1e-4)
     for k, p in sd.items():
         check_grad_summary(k, p.grad, g, 1e-3)
+
+
+def test_oracle_trainer_1k_snapshots():
+    """The 1000-step fixture (tests/golden/trainer_1k.npz, the reference's own DiffusionTrainer run): at every stored
+    theta_k the oracle's step-k loss equals the reference's within 1e-6 and its gradient matches the stored
+    summaries within 1e-4 of each tensor's absmax; the inputs are regenerated from the fixture's seeds (numpy PCG64,
+    host-independent); and the reference's two runs (8 vs 1 host threads) agree to 1e-5 per step."""
+    import numpy as np
+    from test_gpu_protocol import k1_inputs
+    g = load_golden("trainer_1k")
+    xs, ts, ns = k1_inputs(g)
+    assert len(xs) == 1000 and tuple(xs[0].shape) == (4, 3, 16, 16)
+    tab = DO.schedule()
+    for k in (int(s) for s in g["snap_steps"]):
+        orc, sd = make_oracle(split_params(g, f"theta/{k}/"), TINY["unet_tiny_uncond"], requires_grad=True)
+        loss = DO.loss("l2", ns[k], orc.forward(DO.q_sample(tab, xs[k], ts[k], ns[k]), ts[k], None, training=True))
+        loss.backward()
+        assert abs(loss.item() - float(g["losses"][k])) < 1e-6, (k, loss.item(), float(g["losses"][k]))
+        pre = f"g{k}/"
+        summ = {"g" + key[len(pre):]: v for key, v in g.items() if key.startswith(pre)}
+        for name, p in sd.items():
+            if p.grad is not None:
+                check_grad_summary(name, p.grad, summ, 1e-4)
+    assert np.abs(g["losses"].numpy() - g["losses_alt"].numpy()).max() < 1e-5
