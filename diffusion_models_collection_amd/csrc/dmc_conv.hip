@@ -38,6 +38,7 @@ struct ConvK {
   int sk_per; // K stages per split
   int x1_bytes, x2_bytes, w_bytes;  // operand extents for buffer resources (0: too large / absent)
   int dtype_bytes;  // 4 (fp32) or 2 (bf16) storage
+  GnPart gq;        // halo GN+SiLU prologue: statistics from conv-epilogue partials (gq.p1 == nullptr: psc / psh)
 };
 
 // Source pixel of output pixel (n,oy,ox) under tap; returns -1 if it falls in the zero padding.
@@ -943,8 +944,20 @@ DMC_DEV void halo_issue(const ConvK& a, char* buf, int c0, int wave, int pb, int
 // rounding of gn_apply_kernel, so the conv sees bitwise the operand a materialised GN-apply pass would have
 // written. Zero-padding rows (kOOB) stay zero: the reference pads the normalised activation. A lane's 8
 // channels are the same in every piece, so its scale/shift (ss/tt) are loaded once per chunk, a chunk ahead.
-DMC_DEV void halo_pro_load(const ConvK& a, int n, int c0, v4f* st) {
+DMC_DEV void halo_pro_load(const ConvK& a, int n, int c0, v4f* st, const float (*gst)[2]) {
   const int lane = threadIdx.x & 63, lrow = lane >> 3, lc = (lane & 7) ^ lrow;
+  if (a.gq.p1) {
+    // statistics combined in-block from the partials (gst); the affine folded here exactly as dmc_gn_finalize
+    const int c = c0 + lc * 8, g = c / ((a.C1 + a.C2) / a.gq.G);   // a lane's 8 channels lie in one group
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float sc, sh;
+      gn_fold(gst[g][0], gst[g][1], a.gq.gamma ? a.gq.gamma[c + e] : 1.f, a.gq.beta ? a.gq.beta[c + e] : 0.f, sc, sh);
+      st[e >> 2][e & 3] = sc;
+      st[2 + (e >> 2)][e & 3] = sh;
+    }
+    return;
+  }
   const float* sc = a.psc + (size_t)n * a.ldp + c0 + lc * 8;
   const float* sh = a.psh + (size_t)n * a.ldp + c0 + lc * 8;
   st[0] = *(const v4f*)sc; st[1] = *(const v4f*)(sc + 4);
@@ -1057,6 +1070,17 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
     dma_pieces<4>(a.w, a.w_bytes, wring + (s % WS) * WB + wave * 4 * 1024, ob, koff, 0, 4);
   };
   v4f pst[4];
+  // GN+SiLU prologue from conv-epilogue partials: the image's group statistics, one wave per group (the code and
+  // bits of dmc_gn_finalize), before the first chunk -- the finalize launch between the two convs is gone
+  __shared__ float gst[PRO ? 64 : 1][2];
+  if (PRO && a.gq.p1) {
+    for (int g = wave; g < a.gq.G; g += NW) {
+      float mu, rs;
+      gn_part_group(a.gq, n_first, g, mu, rs);
+      if (lane == 0) { gst[g][0] = mu; gst[g][1] = rs; }
+    }
+    __syncthreads();
+  }
 #ifdef DMC_STAMP
   // measurement build only (never in libdmc.so): clocks of the tap loop's phases, summed per wave
   unsigned long long ph[5] = {0, 0, 0, 0, 0}, tq = __builtin_amdgcn_s_memtime();
@@ -1070,7 +1094,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
     if (t == 0) {
       // chunk c's halo into the single buffer: every wave is done with chunk c-1's taps
       if (c > 0) __syncthreads();
-      if (PRO) halo_pro_load(a, n_first, c * 64, pst);
+      if (PRO) halo_pro_load(a, n_first, c * 64, pst, gst);
       halo_issue<HP>(a, lds, c * 64, wave, 0, HP, h1, h2);
       if (c == 0)
         for (int q = 0; q < WS - 1 && q < nst; ++q) issue_w(q);
@@ -2075,6 +2099,17 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
     DMC_REQUIRE(ok, "conv: taps must form a regular grid");
   }
   k.prologue = d->prologue; k.psc = d->pro_scale; k.psh = d->pro_shift; k.ldp = d->ld_pro;
+  k.gq = GnPart{nullptr, nullptr, 0, 0, 0, 0, 0.f, nullptr, nullptr};
+  if (d->pro_gn) {
+    const dmc_gn_part_src* q = d->pro_gn;
+    const int C = d->C1 + d->C2;
+    DMC_REQUIRE(d->prologue == DMC_PRO_AFFINE_SILU && q->part1 && q->C1 == d->C1 && q->C2 == d->C2 &&
+                    q->HW == d->H * d->W && q->HW % 64 == 0 && q->G > 0 && q->G <= 64 && C % q->G == 0 &&
+                    (C / q->G) % 8 == 0 && (q->C2 == 0 || q->part2),
+                "conv: pro_gn partials (GN+SiLU prologue, 64-pixel segments, 8-channel chunks in <= 64 groups)");
+    k.gq = GnPart{q->part1, q->part2, q->C1 / 8, q->C2 / 8, q->HW / 64, q->G, q->eps, q->gamma, q->beta};
+    k.ldp = C;     // the halo prologue planner's "scale / shift cover every channel" condition
+  }
   k.dseed = d->drop_seed; k.dthresh = d->drop_thresh; k.dscale = d->drop_scale; k.dld = d->drop_ld;
   k.dseed_base = d->drop_seed_base;
   k.bias = d->bias; k.addvec = d->addvec; k.ld_add = d->ld_add; k.resid = (const char*)d->resid; k.ld_res = d->ld_res;
@@ -2343,6 +2378,8 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     const int hp2 = halo2_pro_plan(k, &R, &nimg);
     if (hp2) { launch_halo2<true>(k, hp2, R, nimg, s); return dmc::check_launch("dmc_conv2d"); }
   }
+  DMC_REQUIRE(k.gq.p1 == nullptr, "conv: pro_gn (statistics from partials) needs the halo GN+SiLU prologue kernel "
+                                  "(dmc_conv_halo_prologue)");
   if (sizeof(T) == 2 && k.prologue == DMC_PRO_NONE && !dmc::opt(dmc::OPT_NO_GLDS)) {
     // bf16, plain operands: LDS-DMA pipelined kernel
     FwdPlan p = plan_glds(k);

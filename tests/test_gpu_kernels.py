@@ -866,3 +866,63 @@ def test_wgrad_glds_taps(case, on, dmc_opt):
     torch.cuda.synchronize()
     assert rel_err(dw.cpu(), w.grad) < 1e-5
     assert rel_err(db.cpu(), g.float().sum((0, 2, 3))) < 1e-5
+
+
+@pytest.mark.parametrize("case", ["c32_one_source", "c16_concat_straddle", "c8_attention_nosilu"])
+def test_gn_from_partials_in_consumer_bitwise(case, dmc_opt):
+    """The finalize launch folded into the GroupNorm consumers (dmc_gn_part_src): dmc_gn_apply_part (train and
+    inference) equals dmc_gn_finalize + dmc_gn_apply BITWISE, including the mean / rstd it stores for the backward
+    (with and without dropout); and where the halo GN+SiLU prologue applies (32x32 / 16x16, one image per tile), the
+    conv with pro_gn equals the conv fed the finalize's scale / shift bitwise. Group 5 of the 384-channel concat
+    straddles the two sources (models/unet.py:284)."""
+    from diffusion_models_collection_amd import _lib as L, kernels as K
+    dt = torch.bfloat16
+    gen = torch.Generator().manual_seed(13)
+    N, H, C1, C2, silu = {"c32_one_source": (8, 32, 128, 0, True), "c16_concat_straddle": (4, 16, 256, 128, True),
+                          "c8_attention_nosilu": (16, 8, 256, 0, False)}[case]
+    W, C, G = H, C1 + C2, 8
+    HW = H * W
+
+    def producer(cout, seed):
+        g = torch.Generator().manual_seed(seed)
+        x = (torch.randn(N, H, W, 64, generator=g) + 0.3).to(DEV).to(dt)
+        w = (torch.randn(cout, 64, 1, 1, generator=g) * 0.2).to(DEV)
+        b = (torch.randn(cout, generator=g) + 1.0).to(DEV)
+        y = torch.empty(N, H, W, cout, dtype=dt, device=DEV)
+        part = torch.empty(N * HW // 64 * (cout // 8) * 2, device=DEV)
+        d = K.make_desc(dt, N, H, W, 64, 0, 64, 0, L.kc_for(64, dt), H, W, cout, K.TAPS1)
+        K.set_epilogue(d, bias=b, ldy1=cout, gn_part=part)
+        K.conv(d, x, None, K.pack_weight(L.PACK_FWD, dt, w, L.kc_for(64, dt)), y)
+        return y, part
+
+    y1, p1 = producer(C1, 1)
+    y2, p2 = producer(C2, 2) if C2 else (None, None)
+    gamma = (torch.rand(C, generator=gen) + 0.5).to(DEV)
+    beta = torch.randn(C, generator=gen).to(DEV)
+    sc, sh, mr = K.gn_finalize(p1, C1, p2, C2, N, HW, G, 1e-5, gamma, beta)
+    lazy = K.GnLazy(p1, C1, p2, C2, N, HW, G, 1e-5, gamma, beta)
+    for drop in (None, (99, 1 << 30, 4.0 / 3.0)):
+        a_ref = K.gn_apply(dt, y1, y2, N, HW, C1, C2, C1, C2, sc, sh, silu=silu, drop=drop)
+        a_new = K.gn_apply_part(dt, y1, y2, N, HW, C1, C2, C1, C2, lazy, silu=silu, drop=drop)
+        torch.cuda.synchronize()
+        assert torch.equal(a_ref, a_new), drop
+        assert torch.equal(lazy.mr, mr)
+    if silu and H >= 16:
+        w = (torch.randn(128, C, 3, 3, generator=gen) * 0.03).to(DEV)
+        Kc = L.kc_for(C, dt)
+        wp = K.pack_weight(L.PACK_FWD, dt, w, Kc)
+        outs = []
+        for use_lazy in (False, True):
+            d = K.make_desc(dt, N, H, W, C1, C2, C1, C2, Kc, H, W, 128, K.TAPS3)
+            if use_lazy:
+                K.set_prologue(d, L.PRO_AFFINE_SILU, ld=C, gn=lazy)
+            else:
+                K.set_prologue(d, L.PRO_AFFINE_SILU, sc, sh, C)
+            dmc_opt("DMC_NO_SPLITK", 1)   # small N: keep the planner on the halo kernel
+            assert K.conv_halo_prologue(d), case
+            K.set_epilogue(d, ldy1=128)
+            y = torch.empty(N, H, W, 128, dtype=dt, device=DEV)
+            K.conv(d, y1, y2, wp, y)
+            outs.append(y)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1])
