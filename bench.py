@@ -430,6 +430,8 @@ def main():
                     help="skip the 64x64 (config #5) and fp32 side lines")
     ap.add_argument("--no-dit", dest="dit", action="store_false", help="skip the DiT-S/2 (config #4) line")
     ap.add_argument("--dit-only", action="store_true", help="only the DiT-S/2 line (profiling)")
+    ap.add_argument("--dist-one-rank", action="store_true",
+                    help="profiling: the headline step through GradSync + the segmented graph on a 1-rank RCCL group")
     args = ap.parse_args()
     if args.dit_only:
         torch.cuda.set_device(0)
@@ -463,6 +465,13 @@ def main():
     S = args.image_size
     mp = dict(CIFAR, image_size=(S, S))
     model, trainer = make_trainer(mp, args.dtype, dev, rank, world)
+    if args.dist_one_rank and world == 1:
+        import socket
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+        trainer.enable_grad_sync()
     B = args.batch
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = [torch.rand(B, 3, S, S, device=dev, generator=gen) * 2 - 1 for _ in range(4)]
@@ -568,7 +577,7 @@ def main():
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

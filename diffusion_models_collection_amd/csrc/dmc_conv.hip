@@ -1000,7 +1000,11 @@ DMC_DEV void halo_affine_silu(char* buf, int wave, const unsigned* h1, const v4f
 // and a WS-slot weight ring: <= 78 KB, two blocks per CU, so one block's prologue / chunk reload / epilogue
 // overlaps the other's tap loop. At a chunk switch the block waits for its own next-chunk halo (the other block
 // keeps the CU busy). Tile geometry: R = 128 / OW rows of one image, or 128 / (OH*OW) whole images.
-template <int HP, int WS, bool PRO = false, bool SCHED = true>
+// DPOS (DMC_HALO_DPOS, A/B): where a stage issues the later weight slice's LDS-DMA. 0: right after the block barrier
+// (its ~400-cycle issue then sits in front of the fragment reads); 1: after the first k-step's fragment reads, so the
+// issue overlaps their LDS latency; 2: half there, half after the second k-step's reads. With DPOS != 0 the issue is
+// unconditional (the tail re-loads the last slice into the free slot) so it stays in the reads' scheduling region.
+template <int HP, int WS, bool PRO = false, bool SCHED = true, int DPOS = 0>
 __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int nimg) {
   using T = bf16_t;
   constexpr int NW = 4, WM = 2, BM = 128, BN = 128;
@@ -1069,6 +1073,13 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
     const unsigned koff = (unsigned)(t * a.Kc + c * 64) * 2u;
     dma_pieces<4>(a.w, a.w_bytes, wring + (s % WS) * WB + wave * 4 * 1024, ob, koff, 0, 4);
   };
+  // DPOS != 0: slot (s + WS - 1) % WS gets slice min(s + WS - 1, nst - 1) (branch-free), pieces [pb, pe)
+  auto issue_w_part = [&](int s, int pb, int pe) {
+    const int sl = min(s + WS - 1, nst - 1);
+    const int c = sl / 9, t = sl - c * 9;
+    const unsigned koff = (unsigned)(t * a.Kc + c * 64) * 2u;
+    dma_pieces<4>(a.w, a.w_bytes, wring + ((s + WS - 1) % WS) * WB + wave * 4 * 1024, ob, koff, pb, pe);
+  };
   v4f pst[4];
   // GN+SiLU prologue from conv-epilogue partials: the image's group statistics, one wave per group (the code and
   // bits of dmc_gn_finalize), before the first chunk -- the finalize launch between the two convs is gone
@@ -1100,10 +1111,12 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
         for (int q = 0; q < WS - 1 && q < nst; ++q) issue_w(q);
       __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
       if (PRO) halo_affine_silu<HP>(lds, wave, h1, pst);
-    } else {
+    } else if (DPOS == 0) {
       // weight slice s has landed once at most the slices issued after it are in flight
       const int after = min(nst - 1, s + WS - 2) - s;
       wait_vm_dyn(4 * (after > 0 ? after : 0));
+    } else {
+      wait_vm_dyn(4 * (WS - 2));   // every stage issued one slice: WS - 2 slices are younger than slice s
     }
     DMC_PH(0);   // chunk halo / weight-slice wait
     asm volatile("" ::: "memory");
@@ -1112,7 +1125,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
     DMC_PH(1);   // block barrier
-    if (s + WS - 1 < nst) issue_w(s + WS - 1);
+    if (DPOS == 0 && s + WS - 1 < nst) issue_w(s + WS - 1);
     DMC_PH(2);   // LDS-DMA issue of a later slice
     const char* Bw = wring + (s % WS) * WB;
     const int ty = t / 3, tx = t - ty * 3;
@@ -1134,6 +1147,17 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
         const int h = hb[j] + delta;
         fb[ks][j] = *(const v4i*)(lds + h * 128 + ((chunk ^ (h & 7)) << 4));
       }
+      if (DPOS != 0 && ks == 0) {
+        // the k-step-0 reads are issued; the DMA issue (M0 writes) runs while they are in flight
+        __builtin_amdgcn_sched_barrier(0);
+        issue_w_part(s, 0, DPOS == 1 ? 4 : 2);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (DPOS == 2) {
+      __builtin_amdgcn_sched_barrier(0);
+      issue_w_part(s, 2, 4);
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -1141,7 +1165,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[ks][i], fb[ks][j]);
-    if (SCHED) {
+    if (SCHED && DPOS == 0) {
       __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);    // k-step 0 reads
 #pragma unroll
       for (int g = 0; g < 8; ++g) {
@@ -1149,6 +1173,14 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one k-step-1 read
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);   // k-step 1 MFMAs
+    }
+    if (SCHED && DPOS == 1) {   // after the DMA fence: k-step-1 reads between the k-step-0 MFMAs
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
     }
 #ifdef DMC_STAMP
     __builtin_amdgcn_sched_barrier(0);
@@ -1167,6 +1199,10 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
   }
 #endif
 #undef DMC_PH
+  if (DPOS != 0) {   // the tail's slot re-loads may still be landing in the ring the epilogue reuses
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    __syncthreads();
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -2223,6 +2259,18 @@ template <bool PRO>
 void launch_halo2(const ConvK& k, int hp, int R, int nimg, hipStream_t s) {
   const dim3 g = dmc::opt(dmc::OPT_NO_XCD) ? dim3(k.M / 128, dmc::cdiv(k.Cout, 128))
                                           : dim3(k.M / 128 * dmc::cdiv(k.Cout, 128));
+  if (dmc::opt(dmc::OPT_HALO_DPOS) == 1) {   // A/B: the later slice's DMA issued after the k-step-0 reads
+    if (hp == 6) conv3x3_halo2_kernel<6, 3, PRO, true, 1><<<g, 256, 0, s>>>(k, R, nimg);
+    else if (hp == 7) conv3x3_halo2_kernel<7, 3, PRO, true, 1><<<g, 256, 0, s>>>(k, R, nimg);
+    else conv3x3_halo2_kernel<9, 2, PRO, true, 1><<<g, 256, 0, s>>>(k, R, nimg);
+    return;
+  }
+  if (dmc::opt(dmc::OPT_HALO_DPOS) == 2) {   // A/B: half after the k-step-0 reads, half after the k-step-1 reads
+    if (hp == 6) conv3x3_halo2_kernel<6, 3, PRO, true, 2><<<g, 256, 0, s>>>(k, R, nimg);
+    else if (hp == 7) conv3x3_halo2_kernel<7, 3, PRO, true, 2><<<g, 256, 0, s>>>(k, R, nimg);
+    else conv3x3_halo2_kernel<9, 2, PRO, true, 2><<<g, 256, 0, s>>>(k, R, nimg);
+    return;
+  }
   if (dmc::opt(dmc::OPT_HALO_NOSCHED)) {   // A/B: the compiler's own fragment-read schedule
     if (hp == 6) conv3x3_halo2_kernel<6, 3, PRO, false><<<g, 256, 0, s>>>(k, R, nimg);
     else if (hp == 7) conv3x3_halo2_kernel<7, 3, PRO, false><<<g, 256, 0, s>>>(k, R, nimg);

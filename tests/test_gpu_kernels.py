@@ -123,14 +123,16 @@ def test_upsample2x_nhwc_bitwise(dt):
     assert torch.equal(y.permute(0, 3, 1, 2).float(), ref)
 
 
+@pytest.mark.parametrize("dpos", [0, 1])
 @pytest.mark.parametrize("case", ["c32_two_sources", "c16_wide", "c32_384", "c8_multi_image"])
-def test_conv3x3_halo_gn_silu_prologue(case, monkeypatch, dmc_opt):
+def test_conv3x3_halo_gn_silu_prologue(case, dpos, monkeypatch, dmc_opt):
     """Inference prologue on the halo kernel: conv(SiLU(x*scale+shift)) with the GroupNorm affine + SiLU
     applied to the LDS-resident halo equals, BITWISE, dmc_gn_apply materialisation followed by the plain halo
     conv (same op sequence and bf16 rounding), and the fp32 torch reference within bf16 tolerance."""
     L, K = _lib()
     dmc_opt("DMC_NO_SPLITK", 1)   # small N: keep the planner on the halo kernel
     dmc_opt("DMC_HALO_PRO", 1)    # the halo prologue path (default on)
+    dmc_opt("DMC_HALO_DPOS", dpos)
     dt = torch.bfloat16
     torch.manual_seed(11)
     N, H, C1, C2, Cout = {"c32_two_sources": (2, 32, 128, 64, 128), "c16_wide": (3, 16, 256, 0, 256),
@@ -227,16 +229,18 @@ def test_conv_dgrad_wgrad(dt, case):
     assert rel_err(db.cpu(), g.sum((0, 2, 3))) < 1e-5
 
 
-@pytest.mark.parametrize("variant", ["halo2", "halo2_nosched"])
+@pytest.mark.parametrize("variant", ["halo2", "halo2_nosched", "halo2_dpos1", "halo2_dpos2"])
 @pytest.mark.parametrize("case", ["fwd32_concat", "fwd16_ragged_cout", "dgrad32", "fwd8_multi_image", "fallback_4x4",
                                   "fwd8_concat_b128", "fwd64_rows"])
 def test_conv3x3_halo_kernel(case, variant, monkeypatch, dmc_opt):
     """bf16 3x3 stride-1 convs on the LDS-halo kernel (conv3x3_halo2_kernel: 128-pixel tiles of whole rows or
     whole images, two blocks per CU) vs an fp32 reference and vs the per-tap kernel (DMC_NO_HALO) on the same
     inputs; its weight-gradient twin (wgrad3x3_halo2_kernel) likewise. Variants: the scheduled fragment reads
-    (default) and the compiler's own schedule (DMC_HALO_NOSCHED)."""
+    (default), the compiler's own schedule (DMC_HALO_NOSCHED), and the weight slice's LDS-DMA issued after the
+    first k-step's fragment reads (DMC_HALO_DPOS=1) or split around both k-steps' reads (=2)."""
     L, K = _lib()
     dmc_opt("DMC_HALO_NOSCHED", 1 if variant == "halo2_nosched" else 0)
+    dmc_opt("DMC_HALO_DPOS", {"halo2_dpos1": 1, "halo2_dpos2": 2}.get(variant, 0))
     # at these small M the planner would split K over the LDS-DMA kernel instead; the halo kernel is what the
     # B=128 model runs, so keep split-K off here to exercise it
     dmc_opt("DMC_NO_SPLITK", 1)
