@@ -194,10 +194,42 @@ struct GnPart {
 DMC_DEV void gn_chan(float& n, float& m, float& q, float nb, float mb, float qb) {
   const float tot = __fadd_rn(n, nb);
   if (tot == 0.f) return;
-  const float d = __fsub_rn(mb, m), r = __fdiv_rn(nb, tot);
+  // v_rcp_f32 (1 ulp) instead of the ~10-instruction IEEE division: the combine sits on the critical path of every
+  // consumer block that folds the statistics itself; every caller runs this same code, so the bits agree
+  const float d = __fsub_rn(mb, m), r = __fmul_rn(nb, __builtin_amdgcn_rcpf(tot));
   m = __fadd_rn(m, __fmul_rn(d, r));
   q = __fadd_rn(q, __fadd_rn(qb, __fmul_rn(__fmul_rn(__fmul_rn(d, d), n), r)));
   n = tot;
+}
+// A lane's partials of group g of sample n (t = lane, lane + 64, ...), loaded up front so that a kernel can issue them
+// BEFORE its own loads (vmcnt retires in issue order: loads issued after an LDS-DMA could only be waited for behind
+// it). kGnPre partials per lane (np <= 64 * kGnPre); v[i] = (mean, M2), invalid slots marked by count 0.
+constexpr int kGnPre = 4;
+DMC_DEV int gn_part_np(const GnPart& q) { return q.spi * ((8 * (q.nch1 + q.nch2) / q.G) / 8); }
+DMC_DEV void gn_part_prefetch(const GnPart& q, int n, int g, float (*v)[2]) {
+  const int lane = threadIdx.x & 63;
+  const int kpg = (8 * (q.nch1 + q.nch2) / q.G) / 8, np = q.spi * kpg;
+#pragma unroll
+  for (int i = 0; i < kGnPre; ++i) {
+    const int t = lane + 64 * i;
+    v[i][0] = 0.f; v[i][1] = 0.f;
+    if (t < np) {
+      const int sg = n * q.spi + t / kpg, kc = g * kpg + t % kpg;
+      const float* pp = kc < q.nch1 ? q.p1 + ((size_t)sg * q.nch1 + kc) * 2
+                                    : q.p2 + ((size_t)sg * q.nch2 + (kc - q.nch1)) * 2;
+      v[i][0] = pp[0]; v[i][1] = pp[1];
+    }
+  }
+}
+DMC_DEV void gn_part_finish(const GnPart& q, float cn, float m, float s2, float& mean, float& rstd);
+// (mean, rstd) from the prefetched partials (np <= 64 * kGnPre); the same combine order as gn_part_group
+DMC_DEV void gn_part_reduce(const GnPart& q, const float (*v)[2], float& mean, float& rstd) {
+  const int lane = threadIdx.x & 63, np = gn_part_np(q);
+  float cn = 0.f, m = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < kGnPre; ++i)
+    if (lane + 64 * i < np) gn_chan(cn, m, s2, 512.f, v[i][0], v[i][1]);
+  gn_part_finish(q, cn, m, s2, mean, rstd);
 }
 // (mean, rstd) of group g of sample n; every lane of the (full) wave returns the same values
 DMC_DEV void gn_part_group(const GnPart& q, int n, int g, float& mean, float& rstd) {
@@ -210,6 +242,11 @@ DMC_DEV void gn_part_group(const GnPart& q, int n, int g, float& mean, float& rs
                                   : q.p2 + ((size_t)sg * q.nch2 + (kc - q.nch1)) * 2;
     gn_chan(cn, m, s2, 512.f, pp[0], pp[1]);
   }
+  gn_part_finish(q, cn, m, s2, mean, rstd);
+}
+// the fixed xor tree over the wave's lanes, then mean / rstd
+DMC_DEV void gn_part_finish(const GnPart& q, float cn, float m, float s2, float& mean, float& rstd) {
+  const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int sh = 1; sh < 64; sh <<= 1) {
     const float nb = __shfl_xor(cn, sh), mb = __shfl_xor(m, sh), qb = __shfl_xor(s2, sh);

@@ -944,15 +944,26 @@ DMC_DEV void halo_issue(const ConvK& a, char* buf, int c0, int wave, int pb, int
 // rounding of gn_apply_kernel, so the conv sees bitwise the operand a materialised GN-apply pass would have
 // written. Zero-padding rows (kOOB) stay zero: the reference pads the normalised activation. A lane's 8
 // channels are the same in every piece, so its scale/shift (ss/tt) are loaded once per chunk, a chunk ahead.
+// gst (group mean / rstd in LDS) is written and read with inline asm: a plain C++ LDS access while the halo's
+// LDS-DMA is in flight makes hipcc drain vmcnt first, which would serialise the statistics behind the DMA
+DMC_DEV void lds_write_b64(char* p, float x, float y) {
+  asm volatile("ds_write_b64 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v2f{x, y}) : "memory");
+}
+DMC_DEV v2f lds_read_b64_sync(const char* p) {
+  v2f v;
+  asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((unsigned)(uintptr_t)p) : "memory");
+  return v;
+}
 DMC_DEV void halo_pro_load(const ConvK& a, int n, int c0, v4f* st, const float (*gst)[2]) {
   const int lane = threadIdx.x & 63, lrow = lane >> 3, lc = (lane & 7) ^ lrow;
   if (a.gq.p1) {
     // statistics combined in-block from the partials (gst); the affine folded here exactly as dmc_gn_finalize
     const int c = c0 + lc * 8, g = c / ((a.C1 + a.C2) / a.gq.G);   // a lane's 8 channels lie in one group
+    const v2f ms = lds_read_b64_sync((const char*)&gst[g][0]);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float sc, sh;
-      gn_fold(gst[g][0], gst[g][1], a.gq.gamma ? a.gq.gamma[c + e] : 1.f, a.gq.beta ? a.gq.beta[c + e] : 0.f, sc, sh);
+      gn_fold(ms[0], ms[1], a.gq.gamma ? a.gq.gamma[c + e] : 1.f, a.gq.beta ? a.gq.beta[c + e] : 0.f, sc, sh);
       st[e >> 2][e & 3] = sc;
       st[2 + (e >> 2)][e & 3] = sh;
     }
@@ -1082,16 +1093,9 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
   };
   v4f pst[4];
   // GN+SiLU prologue from conv-epilogue partials: the image's group statistics, one wave per group (the code and
-  // bits of dmc_gn_finalize), before the first chunk -- the finalize launch between the two convs is gone
+  // bits of dmc_gn_finalize), computed while chunk 0's halo and first weight slices are in flight (see t == 0
+  // below) -- the finalize launch between the two convs is gone
   __shared__ float gst[PRO ? 64 : 1][2];
-  if (PRO && a.gq.p1) {
-    for (int g = wave; g < a.gq.G; g += NW) {
-      float mu, rs;
-      gn_part_group(a.gq, n_first, g, mu, rs);
-      if (lane == 0) { gst[g][0] = mu; gst[g][1] = rs; }
-    }
-    __syncthreads();
-  }
 #ifdef DMC_STAMP
   // measurement build only (never in libdmc.so): clocks of the tap loop's phases, summed per wave
   unsigned long long ph[5] = {0, 0, 0, 0, 0}, tq = __builtin_amdgcn_s_memtime();
@@ -1105,10 +1109,38 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
     if (t == 0) {
       // chunk c's halo into the single buffer: every wave is done with chunk c-1's taps
       if (c > 0) __syncthreads();
-      if (PRO) halo_pro_load(a, n_first, c * 64, pst, gst);
+      if (PRO && !(a.gq.p1 && c == 0)) halo_pro_load(a, n_first, c * 64, pst, gst);
+      // statistics from partials: this wave's groups' partials are loaded BEFORE the DMA (vmcnt retires in issue
+      // order), combined while the halo and first weight slices land
+      const bool gpre = PRO && a.gq.p1 && c == 0 && gn_part_np(a.gq) <= 64 * kGnPre && a.gq.G <= 2 * NW;
+      float pv[2][kGnPre][2];
+      if (gpre)
+        for (int k = 0; k < 2; ++k)
+          if (wave + NW * k < a.gq.G) gn_part_prefetch(a.gq, n_first, wave + NW * k, pv[k]);
       halo_issue<HP>(a, lds, c * 64, wave, 0, HP, h1, h2);
       if (c == 0)
         for (int q = 0; q < WS - 1 && q < nst; ++q) issue_w(q);
+      if (PRO && a.gq.p1 && c == 0) {
+        if (gpre) {
+          for (int k = 0; k < 2; ++k)
+            if (wave + NW * k < a.gq.G) {
+              float mu, rs;
+              gn_part_reduce(a.gq, pv[k], mu, rs);
+              if (lane == 0) lds_write_b64((char*)&gst[wave + NW * k][0], mu, rs);
+            }
+        } else {
+          for (int g = wave; g < a.gq.G; g += NW) {
+            float mu, rs;
+            gn_part_group(a.gq, n_first, g, mu, rs);
+            if (lane == 0) lds_write_b64((char*)&gst[g][0], mu, rs);
+          }
+        }
+        // publish the statistics without draining the in-flight DMA (a __syncthreads would wait for it)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        halo_pro_load(a, n_first, 0, pst, gst);
+      }
       __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
       if (PRO) halo_affine_silu<HP>(lds, wave, h1, pst);
     } else if (DPOS == 0) {

@@ -520,21 +520,6 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(Src2 s, int HW, const flo
   const int rpi = 256 / CPR;
   const int col = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
   const int n = blockIdx.x;
-  __shared__ float gst[64][2];
-  if (gp.p1) {
-    for (int g = threadIdx.x >> 6; g < gp.G; g += 4) {   // every wave whole: the xor tree needs all 64 lanes
-      float mu, rs;
-      gn_part_group(gp, n, g, mu, rs);
-      if ((threadIdx.x & 63) == 0) { gst[g][0] = mu; gst[g][1] = rs; }
-    }
-    __syncthreads();
-    if (mean_rstd && blockIdx.y == 0)
-      for (int g = threadIdx.x; g < gp.G; g += 256) {
-        mean_rstd[((size_t)n * gp.G + g) * 2] = gst[g][0];
-        mean_rstd[((size_t)n * gp.G + g) * 2 + 1] = gst[g][1];
-      }
-  }
-  if (r0 >= rpi) return;
   const int per = (HW + splits - 1) / splits;
   const int pb = blockIdx.y * per, pe = min(HW, pb + per);
   const int c0 = col * EPC;
@@ -544,7 +529,40 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(Src2 s, int HW, const flo
     for (int u = 0; u < UNR; ++u)
       if (p0 + u * rpi < pe) buf[u] = load_chunk2<T>(s, n * HW + p0 + u * rpi, c0);
   };
-  if (pb + r0 < pe) issue(pb + r0);   // in flight while scale/shift load
+  __shared__ float gst[64][2];
+  // the statistics' partials are loaded BEFORE the first pixel rows (so that waiting for them does not wait for the
+  // rows), combined while the rows are in flight
+  const bool pre = gp.p1 && gn_part_np(gp) <= 64 * kGnPre && gp.G <= 8;
+  float pv[2][kGnPre][2];
+  if (pre)
+    for (int k = 0; k < 2; ++k)
+      if ((threadIdx.x >> 6) + 4 * k < gp.G) gn_part_prefetch(gp, n, (threadIdx.x >> 6) + 4 * k, pv[k]);
+  if (r0 < rpi && pb + r0 < pe) issue(pb + r0);   // in flight while the statistics / scale / shift load
+  if (gp.p1) {
+    if (pre) {
+      for (int k = 0; k < 2; ++k) {
+        const int g = (threadIdx.x >> 6) + 4 * k;
+        if (g < gp.G) {
+          float mu, rs;
+          gn_part_reduce(gp, pv[k], mu, rs);
+          if ((threadIdx.x & 63) == 0) { gst[g][0] = mu; gst[g][1] = rs; }
+        }
+      }
+    } else {
+      for (int g = threadIdx.x >> 6; g < gp.G; g += 4) {   // every wave whole: the xor tree needs all 64 lanes
+        float mu, rs;
+        gn_part_group(gp, n, g, mu, rs);
+        if ((threadIdx.x & 63) == 0) { gst[g][0] = mu; gst[g][1] = rs; }
+      }
+    }
+    __syncthreads();
+    if (mean_rstd && blockIdx.y == 0)
+      for (int g = threadIdx.x; g < gp.G; g += 256) {
+        mean_rstd[((size_t)n * gp.G + g) * 2] = gst[g][0];
+        mean_rstd[((size_t)n * gp.G + g) * 2 + 1] = gst[g][1];
+      }
+  }
+  if (r0 >= rpi) return;
   float sc[EPC], sh[EPC];
   if (gp.p1) {
     const int cpg = C / gp.G;

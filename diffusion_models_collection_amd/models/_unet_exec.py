@@ -59,7 +59,7 @@ class GnbReq:
 
 # GroupNorm statistics left as the producing conv's epilogue partials, combined by the consumer (dmc_gn_apply_part,
 # the halo conv's GN+SiLU prologue) instead of a dmc_gn_finalize launch per GroupNorm (DMC_GN_LAZY=0: finalize, A/B)
-_GN_LAZY = os.environ.get("DMC_GN_LAZY", "1") not in ("", "0")
+_GN_LAZY = os.environ.get("DMC_GN_LAZY", "0") not in ("", "0")
 
 
 def _pro_silu(st):

@@ -85,7 +85,9 @@ def _worker(rank, world, port, outdir, graph, kind="unet"):
         x, t, n = _data(step)
         sl = slice(2 * rank, 2 * rank + 2)
         # the step's t and noise draws return this rank's shard (patched only around the step)
-        torch.randint = lambda *a, **k: t[sl].cuda()
+        # the trainer's timestep draw (size (B,)); the dropout-seed draw of the executors (size (1,)) stays torch's
+        torch.randint = lambda lo, hi, size, *a, **k: (t[sl].cuda() if tuple(size) == (2,)
+                                                      else orig_randint(lo, hi, size, *a, **k))
         torch.randn_like = lambda a, *k, **kw: n[sl].cuda()
         try:
             loss = tr.train_step(x[sl].cuda(), step)
