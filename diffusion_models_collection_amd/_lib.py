@@ -39,14 +39,8 @@ class ConvDesc(ctypes.Structure):
         ("bias", _c_p), ("addvec", _c_p), ("ld_add", _c_int), ("resid", _c_p), ("ld_res", _c_int),
         ("silu_pre", _c_p), ("ld_silu", _c_int), ("Csplit", _c_int), ("ldy1", _c_int), ("ldy2", _c_int),
         ("out_f32", _c_int), ("out_nchw", _c_int), ("act", _c_int), ("y_pre", _c_p), ("ld_pre", _c_int),
-        ("gnb", _c_p), ("gn_part", _c_p), ("wg_bias", _c_p), ("pro_gn", _c_p),
+        ("gnb", _c_p), ("gn_part", _c_p), ("wg_bias", _c_p),
     ]
-
-
-class GnPartSrc(ctypes.Structure):
-    """include/dmc.h dmc_gn_part_src: GroupNorm statistics still as conv-epilogue partials."""
-    _fields_ = [("part1", _c_p), ("part2", _c_p), ("C1", _c_int), ("C2", _c_int), ("HW", _c_int), ("G", _c_int),
-                ("eps", _c_f), ("gamma", _c_p), ("beta", _c_p)]
 
 
 class GnBwdEpi(ctypes.Structure):
@@ -96,9 +90,6 @@ def _load():
                                      _c_p, _c_p]),
         "dmc_gn_apply": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p,
                                   _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_int, _c_p]),
-        "dmc_gn_apply_part": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
-                                       ctypes.POINTER(GnPartSrc), _c_p, _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p,
-                                       _c_int, _c_p]),
         "dmc_gn_silu_bwd": (_c_int, [_c_int, _c_p, _c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int,
                                      _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_p,
                                      _c_int, _c_int, _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_p, _c_p, _c_p,

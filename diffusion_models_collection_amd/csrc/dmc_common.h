@@ -174,92 +174,3 @@ template <> DMC_DEV float ld_as_f<bf16_t>(const void* p, size_t i) { return bf2f
 template <typename T> DMC_DEV void st_from_f(void* p, size_t i, float v);
 template <> DMC_DEV void st_from_f<float>(void* p, size_t i, float v) { ((float*)p)[i] = v; }
 template <> DMC_DEV void st_from_f<bf16_t>(void* p, size_t i, float v) { ((bf16_t*)p)[i] = (bf16_t)f2bf(v); }
-
-// ---- GroupNorm statistics from conv-epilogue partials (dmc_conv_desc.gn_part) ----
-// Per (64-pixel segment, 8-channel chunk) the producing conv stored (mean, M2) of its 512 values; source 1's chunks
-// come first, then source 2's (virtual concat). One full wave combines a group's partials of one sample by Chan's
-// formula: lane l takes partials l, l+64, ... (segments outer, chunks inner), then a fixed xor tree. Every kernel that
-// needs a group's (mean, rstd) -- dmc_gn_finalize, dmc_gn_apply with partials, the halo conv's GN+SiLU prologue --
-// runs THIS code, with explicitly rounded operations (no contraction), so all of them produce the same bits.
-struct GnPart {
-  const float* p1;
-  const float* p2;
-  int nch1, nch2;      // 8-channel chunks per source
-  int spi;             // 64-pixel segments per sample
-  int G;               // groups
-  float eps;
-  const float* gamma;  // [C] or NULL (1)
-  const float* beta;   // [C] or NULL (0)
-};
-DMC_DEV void gn_chan(float& n, float& m, float& q, float nb, float mb, float qb) {
-  const float tot = __fadd_rn(n, nb);
-  if (tot == 0.f) return;
-  // v_rcp_f32 (1 ulp) instead of the ~10-instruction IEEE division: the combine sits on the critical path of every
-  // consumer block that folds the statistics itself; every caller runs this same code, so the bits agree
-  const float d = __fsub_rn(mb, m), r = __fmul_rn(nb, __builtin_amdgcn_rcpf(tot));
-  m = __fadd_rn(m, __fmul_rn(d, r));
-  q = __fadd_rn(q, __fadd_rn(qb, __fmul_rn(__fmul_rn(__fmul_rn(d, d), n), r)));
-  n = tot;
-}
-// A lane's partials of group g of sample n (t = lane, lane + 64, ...), loaded up front so that a kernel can issue them
-// BEFORE its own loads (vmcnt retires in issue order: loads issued after an LDS-DMA could only be waited for behind
-// it). kGnPre partials per lane (np <= 64 * kGnPre); v[i] = (mean, M2), invalid slots marked by count 0.
-constexpr int kGnPre = 4;
-DMC_DEV int gn_part_np(const GnPart& q) { return q.spi * ((8 * (q.nch1 + q.nch2) / q.G) / 8); }
-DMC_DEV void gn_part_prefetch(const GnPart& q, int n, int g, float (*v)[2]) {
-  const int lane = threadIdx.x & 63;
-  const int kpg = (8 * (q.nch1 + q.nch2) / q.G) / 8, np = q.spi * kpg;
-#pragma unroll
-  for (int i = 0; i < kGnPre; ++i) {
-    const int t = lane + 64 * i;
-    v[i][0] = 0.f; v[i][1] = 0.f;
-    if (t < np) {
-      const int sg = n * q.spi + t / kpg, kc = g * kpg + t % kpg;
-      const float* pp = kc < q.nch1 ? q.p1 + ((size_t)sg * q.nch1 + kc) * 2
-                                    : q.p2 + ((size_t)sg * q.nch2 + (kc - q.nch1)) * 2;
-      v[i][0] = pp[0]; v[i][1] = pp[1];
-    }
-  }
-}
-DMC_DEV void gn_part_finish(const GnPart& q, float cn, float m, float s2, float& mean, float& rstd);
-// (mean, rstd) from the prefetched partials (np <= 64 * kGnPre); the same combine order as gn_part_group
-DMC_DEV void gn_part_reduce(const GnPart& q, const float (*v)[2], float& mean, float& rstd) {
-  const int lane = threadIdx.x & 63, np = gn_part_np(q);
-  float cn = 0.f, m = 0.f, s2 = 0.f;
-#pragma unroll
-  for (int i = 0; i < kGnPre; ++i)
-    if (lane + 64 * i < np) gn_chan(cn, m, s2, 512.f, v[i][0], v[i][1]);
-  gn_part_finish(q, cn, m, s2, mean, rstd);
-}
-// (mean, rstd) of group g of sample n; every lane of the (full) wave returns the same values
-DMC_DEV void gn_part_group(const GnPart& q, int n, int g, float& mean, float& rstd) {
-  const int lane = threadIdx.x & 63;
-  const int C = 8 * (q.nch1 + q.nch2), cpg = C / q.G, kpg = cpg / 8, np = q.spi * kpg;
-  float cn = 0.f, m = 0.f, s2 = 0.f;
-  for (int t = lane; t < np; t += 64) {
-    const int sg = n * q.spi + t / kpg, kc = g * kpg + t % kpg;
-    const float* pp = kc < q.nch1 ? q.p1 + ((size_t)sg * q.nch1 + kc) * 2
-                                  : q.p2 + ((size_t)sg * q.nch2 + (kc - q.nch1)) * 2;
-    gn_chan(cn, m, s2, 512.f, pp[0], pp[1]);
-  }
-  gn_part_finish(q, cn, m, s2, mean, rstd);
-}
-// the fixed xor tree over the wave's lanes, then mean / rstd
-DMC_DEV void gn_part_finish(const GnPart& q, float cn, float m, float s2, float& mean, float& rstd) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int sh = 1; sh < 64; sh <<= 1) {
-    const float nb = __shfl_xor(cn, sh), mb = __shfl_xor(m, sh), qb = __shfl_xor(s2, sh);
-    // both lanes of a pair must end with the same value: combine in lane order (lower lane first)
-    if ((lane & sh) == 0) gn_chan(cn, m, s2, nb, mb, qb);
-    else { float n2 = nb, m2 = mb, q2 = qb; gn_chan(n2, m2, q2, cn, m, s2); cn = n2; m = m2; s2 = q2; }
-  }
-  mean = m;
-  const float var = fmaxf(__fdiv_rn(s2, cn), 0.f);
-  rstd = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(var, q.eps)));
-}
-// the folded per-channel affine of nn.GroupNorm: y = x * scale + shift
-DMC_DEV void gn_fold(float mean, float rstd, float gm, float bt, float& scale, float& shift) {
-  scale = __fmul_rn(rstd, gm);
-  shift = __fsub_rn(bt, __fmul_rn(mean, scale));
-}

@@ -38,7 +38,6 @@ struct ConvK {
   int sk_per; // K stages per split
   int x1_bytes, x2_bytes, w_bytes;  // operand extents for buffer resources (0: too large / absent)
   int dtype_bytes;  // 4 (fp32) or 2 (bf16) storage
-  GnPart gq;        // halo GN+SiLU prologue: statistics from conv-epilogue partials (gq.p1 == nullptr: psc / psh)
 };
 
 // Source pixel of output pixel (n,oy,ox) under tap; returns -1 if it falls in the zero padding.
@@ -944,31 +943,8 @@ DMC_DEV void halo_issue(const ConvK& a, char* buf, int c0, int wave, int pb, int
 // rounding of gn_apply_kernel, so the conv sees bitwise the operand a materialised GN-apply pass would have
 // written. Zero-padding rows (kOOB) stay zero: the reference pads the normalised activation. A lane's 8
 // channels are the same in every piece, so its scale/shift (ss/tt) are loaded once per chunk, a chunk ahead.
-// gst (group mean / rstd in LDS) is written and read with inline asm: a plain C++ LDS access while the halo's
-// LDS-DMA is in flight makes hipcc drain vmcnt first, which would serialise the statistics behind the DMA
-DMC_DEV void lds_write_b64(char* p, float x, float y) {
-  asm volatile("ds_write_b64 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v2f{x, y}) : "memory");
-}
-DMC_DEV v2f lds_read_b64_sync(const char* p) {
-  v2f v;
-  asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((unsigned)(uintptr_t)p) : "memory");
-  return v;
-}
-DMC_DEV void halo_pro_load(const ConvK& a, int n, int c0, v4f* st, const float (*gst)[2]) {
+DMC_DEV void halo_pro_load(const ConvK& a, int n, int c0, v4f* st) {
   const int lane = threadIdx.x & 63, lrow = lane >> 3, lc = (lane & 7) ^ lrow;
-  if (a.gq.p1) {
-    // statistics combined in-block from the partials (gst); the affine folded here exactly as dmc_gn_finalize
-    const int c = c0 + lc * 8, g = c / ((a.C1 + a.C2) / a.gq.G);   // a lane's 8 channels lie in one group
-    const v2f ms = lds_read_b64_sync((const char*)&gst[g][0]);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float sc, sh;
-      gn_fold(ms[0], ms[1], a.gq.gamma ? a.gq.gamma[c + e] : 1.f, a.gq.beta ? a.gq.beta[c + e] : 0.f, sc, sh);
-      st[e >> 2][e & 3] = sc;
-      st[2 + (e >> 2)][e & 3] = sh;
-    }
-    return;
-  }
   const float* sc = a.psc + (size_t)n * a.ldp + c0 + lc * 8;
   const float* sh = a.psh + (size_t)n * a.ldp + c0 + lc * 8;
   st[0] = *(const v4f*)sc; st[1] = *(const v4f*)(sc + 4);
@@ -1011,11 +987,7 @@ DMC_DEV void halo_affine_silu(char* buf, int wave, const unsigned* h1, const v4f
 // and a WS-slot weight ring: <= 78 KB, two blocks per CU, so one block's prologue / chunk reload / epilogue
 // overlaps the other's tap loop. At a chunk switch the block waits for its own next-chunk halo (the other block
 // keeps the CU busy). Tile geometry: R = 128 / OW rows of one image, or 128 / (OH*OW) whole images.
-// DPOS (DMC_HALO_DPOS, A/B): where a stage issues the later weight slice's LDS-DMA. 0: right after the block barrier
-// (its ~400-cycle issue then sits in front of the fragment reads); 1: after the first k-step's fragment reads, so the
-// issue overlaps their LDS latency; 2: half there, half after the second k-step's reads. With DPOS != 0 the issue is
-// unconditional (the tail re-loads the last slice into the free slot) so it stays in the reads' scheduling region.
-template <int HP, int WS, bool PRO = false, bool SCHED = true, int DPOS = 0>
+template <int HP, int WS, bool PRO = false, bool SCHED = true>
 __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int nimg) {
   using T = bf16_t;
   constexpr int NW = 4, WM = 2, BM = 128, BN = 128;
@@ -1084,18 +1056,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
     const unsigned koff = (unsigned)(t * a.Kc + c * 64) * 2u;
     dma_pieces<4>(a.w, a.w_bytes, wring + (s % WS) * WB + wave * 4 * 1024, ob, koff, 0, 4);
   };
-  // DPOS != 0: slot (s + WS - 1) % WS gets slice min(s + WS - 1, nst - 1) (branch-free), pieces [pb, pe)
-  auto issue_w_part = [&](int s, int pb, int pe) {
-    const int sl = min(s + WS - 1, nst - 1);
-    const int c = sl / 9, t = sl - c * 9;
-    const unsigned koff = (unsigned)(t * a.Kc + c * 64) * 2u;
-    dma_pieces<4>(a.w, a.w_bytes, wring + ((s + WS - 1) % WS) * WB + wave * 4 * 1024, ob, koff, pb, pe);
-  };
   v4f pst[4];
-  // GN+SiLU prologue from conv-epilogue partials: the image's group statistics, one wave per group (the code and
-  // bits of dmc_gn_finalize), computed while chunk 0's halo and first weight slices are in flight (see t == 0
-  // below) -- the finalize launch between the two convs is gone
-  __shared__ float gst[PRO ? 64 : 1][2];
 #ifdef DMC_STAMP
   // measurement build only (never in libdmc.so): clocks of the tap loop's phases, summed per wave
   unsigned long long ph[5] = {0, 0, 0, 0, 0}, tq = __builtin_amdgcn_s_memtime();
@@ -1109,46 +1070,16 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
     if (t == 0) {
       // chunk c's halo into the single buffer: every wave is done with chunk c-1's taps
       if (c > 0) __syncthreads();
-      if (PRO && !(a.gq.p1 && c == 0)) halo_pro_load(a, n_first, c * 64, pst, gst);
-      // statistics from partials: this wave's groups' partials are loaded BEFORE the DMA (vmcnt retires in issue
-      // order), combined while the halo and first weight slices land
-      const bool gpre = PRO && a.gq.p1 && c == 0 && gn_part_np(a.gq) <= 64 * kGnPre && a.gq.G <= 2 * NW;
-      float pv[2][kGnPre][2];
-      if (gpre)
-        for (int k = 0; k < 2; ++k)
-          if (wave + NW * k < a.gq.G) gn_part_prefetch(a.gq, n_first, wave + NW * k, pv[k]);
+      if (PRO) halo_pro_load(a, n_first, c * 64, pst);
       halo_issue<HP>(a, lds, c * 64, wave, 0, HP, h1, h2);
       if (c == 0)
         for (int q = 0; q < WS - 1 && q < nst; ++q) issue_w(q);
-      if (PRO && a.gq.p1 && c == 0) {
-        if (gpre) {
-          for (int k = 0; k < 2; ++k)
-            if (wave + NW * k < a.gq.G) {
-              float mu, rs;
-              gn_part_reduce(a.gq, pv[k], mu, rs);
-              if (lane == 0) lds_write_b64((char*)&gst[wave + NW * k][0], mu, rs);
-            }
-        } else {
-          for (int g = wave; g < a.gq.G; g += NW) {
-            float mu, rs;
-            gn_part_group(a.gq, n_first, g, mu, rs);
-            if (lane == 0) lds_write_b64((char*)&gst[g][0], mu, rs);
-          }
-        }
-        // publish the statistics without draining the in-flight DMA (a __syncthreads would wait for it)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        halo_pro_load(a, n_first, 0, pst, gst);
-      }
       __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
       if (PRO) halo_affine_silu<HP>(lds, wave, h1, pst);
-    } else if (DPOS == 0) {
+    } else {
       // weight slice s has landed once at most the slices issued after it are in flight
       const int after = min(nst - 1, s + WS - 2) - s;
       wait_vm_dyn(4 * (after > 0 ? after : 0));
-    } else {
-      wait_vm_dyn(4 * (WS - 2));   // every stage issued one slice: WS - 2 slices are younger than slice s
     }
     DMC_PH(0);   // chunk halo / weight-slice wait
     asm volatile("" ::: "memory");
@@ -1157,7 +1088,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
     DMC_PH(1);   // block barrier
-    if (DPOS == 0 && s + WS - 1 < nst) issue_w(s + WS - 1);
+    if (s + WS - 1 < nst) issue_w(s + WS - 1);
     DMC_PH(2);   // LDS-DMA issue of a later slice
     const char* Bw = wring + (s % WS) * WB;
     const int ty = t / 3, tx = t - ty * 3;
@@ -1179,17 +1110,6 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
         const int h = hb[j] + delta;
         fb[ks][j] = *(const v4i*)(lds + h * 128 + ((chunk ^ (h & 7)) << 4));
       }
-      if (DPOS != 0 && ks == 0) {
-        // the k-step-0 reads are issued; the DMA issue (M0 writes) runs while they are in flight
-        __builtin_amdgcn_sched_barrier(0);
-        issue_w_part(s, 0, DPOS == 1 ? 4 : 2);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    if (DPOS == 2) {
-      __builtin_amdgcn_sched_barrier(0);
-      issue_w_part(s, 2, 4);
-      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -1197,7 +1117,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[ks][i], fb[ks][j]);
-    if (SCHED && DPOS == 0) {
+    if (SCHED) {
       __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);    // k-step 0 reads
 #pragma unroll
       for (int g = 0; g < 8; ++g) {
@@ -1205,14 +1125,6 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one k-step-1 read
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);   // k-step 1 MFMAs
-    }
-    if (SCHED && DPOS == 1) {   // after the DMA fence: k-step-1 reads between the k-step-0 MFMAs
-#pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
     }
 #ifdef DMC_STAMP
     __builtin_amdgcn_sched_barrier(0);
@@ -1231,10 +1143,6 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
   }
 #endif
 #undef DMC_PH
-  if (DPOS != 0) {   // the tail's slot re-loads may still be landing in the ring the epilogue reuses
-    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-    __syncthreads();
-  }
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -2167,17 +2075,6 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
     DMC_REQUIRE(ok, "conv: taps must form a regular grid");
   }
   k.prologue = d->prologue; k.psc = d->pro_scale; k.psh = d->pro_shift; k.ldp = d->ld_pro;
-  k.gq = GnPart{nullptr, nullptr, 0, 0, 0, 0, 0.f, nullptr, nullptr};
-  if (d->pro_gn) {
-    const dmc_gn_part_src* q = d->pro_gn;
-    const int C = d->C1 + d->C2;
-    DMC_REQUIRE(d->prologue == DMC_PRO_AFFINE_SILU && q->part1 && q->C1 == d->C1 && q->C2 == d->C2 &&
-                    q->HW == d->H * d->W && q->HW % 64 == 0 && q->G > 0 && q->G <= 64 && C % q->G == 0 &&
-                    (C / q->G) % 8 == 0 && (q->C2 == 0 || q->part2),
-                "conv: pro_gn partials (GN+SiLU prologue, 64-pixel segments, 8-channel chunks in <= 64 groups)");
-    k.gq = GnPart{q->part1, q->part2, q->C1 / 8, q->C2 / 8, q->HW / 64, q->G, q->eps, q->gamma, q->beta};
-    k.ldp = C;     // the halo prologue planner's "scale / shift cover every channel" condition
-  }
   k.dseed = d->drop_seed; k.dthresh = d->drop_thresh; k.dscale = d->drop_scale; k.dld = d->drop_ld;
   k.dseed_base = d->drop_seed_base;
   k.bias = d->bias; k.addvec = d->addvec; k.ld_add = d->ld_add; k.resid = (const char*)d->resid; k.ld_res = d->ld_res;
@@ -2291,18 +2188,6 @@ template <bool PRO>
 void launch_halo2(const ConvK& k, int hp, int R, int nimg, hipStream_t s) {
   const dim3 g = dmc::opt(dmc::OPT_NO_XCD) ? dim3(k.M / 128, dmc::cdiv(k.Cout, 128))
                                           : dim3(k.M / 128 * dmc::cdiv(k.Cout, 128));
-  if (dmc::opt(dmc::OPT_HALO_DPOS) == 1) {   // A/B: the later slice's DMA issued after the k-step-0 reads
-    if (hp == 6) conv3x3_halo2_kernel<6, 3, PRO, true, 1><<<g, 256, 0, s>>>(k, R, nimg);
-    else if (hp == 7) conv3x3_halo2_kernel<7, 3, PRO, true, 1><<<g, 256, 0, s>>>(k, R, nimg);
-    else conv3x3_halo2_kernel<9, 2, PRO, true, 1><<<g, 256, 0, s>>>(k, R, nimg);
-    return;
-  }
-  if (dmc::opt(dmc::OPT_HALO_DPOS) == 2) {   // A/B: half after the k-step-0 reads, half after the k-step-1 reads
-    if (hp == 6) conv3x3_halo2_kernel<6, 3, PRO, true, 2><<<g, 256, 0, s>>>(k, R, nimg);
-    else if (hp == 7) conv3x3_halo2_kernel<7, 3, PRO, true, 2><<<g, 256, 0, s>>>(k, R, nimg);
-    else conv3x3_halo2_kernel<9, 2, PRO, true, 2><<<g, 256, 0, s>>>(k, R, nimg);
-    return;
-  }
   if (dmc::opt(dmc::OPT_HALO_NOSCHED)) {   // A/B: the compiler's own fragment-read schedule
     if (hp == 6) conv3x3_halo2_kernel<6, 3, PRO, false><<<g, 256, 0, s>>>(k, R, nimg);
     else if (hp == 7) conv3x3_halo2_kernel<7, 3, PRO, false><<<g, 256, 0, s>>>(k, R, nimg);
@@ -2458,8 +2343,6 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     const int hp2 = halo2_pro_plan(k, &R, &nimg);
     if (hp2) { launch_halo2<true>(k, hp2, R, nimg, s); return dmc::check_launch("dmc_conv2d"); }
   }
-  DMC_REQUIRE(k.gq.p1 == nullptr, "conv: pro_gn (statistics from partials) needs the halo GN+SiLU prologue kernel "
-                                  "(dmc_conv_halo_prologue)");
   if (sizeof(T) == 2 && k.prologue == DMC_PRO_NONE && !dmc::opt(dmc::OPT_NO_GLDS)) {
     // bf16, plain operands: LDS-DMA pipelined kernel
     FwdPlan p = plan_glds(k);

@@ -42,7 +42,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"DMC_WG_1X1", 1}, {"DMC_GN_BWD_SLICES", 2},
     {"DMC_WG_TAPS", 0}, {"DMC_NO_SKGN", 0},
     {"DMC_WG_HALO_TARGET", 256},
-    {"DMC_STAMP_PTR", 0}, {"DMC_HALO_DPOS", 0},
+    {"DMC_STAMP_PTR", 0},
 };
 struct OptTable {
   long v[OPT_COUNT];

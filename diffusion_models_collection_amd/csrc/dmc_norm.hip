@@ -506,19 +506,16 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float* in, int R, in
 // by the backward (weight gradients read `a` directly, dropout masks never stored).
 // Grid (N, pixel splits); a thread owns one 16-byte channel chunk column (its scale/shift stay in
 // registers) and walks pixels of one sample, so each wave streams whole contiguous rows.
-// With gp.p1 set (dmc_gn_apply_part) the block first combines sample n's GroupNorm statistics from the producing
-// convs' epilogue partials (gn_part_group: the code dmc_gn_finalize runs, so the same bits) -- no finalize launch --
-// and block (n, 0) also stores mean / rstd for the backward.
 template <typename T>
 __global__ __launch_bounds__(256) void gn_apply_kernel(Src2 s, int HW, const float* scale, const float* shift,
                                                        int silu, uint32_t seed0, const uint32_t* seed_base,
-                                                       uint32_t thresh, float dscale, char* out, int ldo, int splits,
-                                                       GnPart gp, float* mean_rstd) {
+                                                       uint32_t thresh, float dscale, char* out, int ldo, int splits) {
   const uint32_t seed = drop_seed(seed0, seed_base);
   constexpr int EPC = TT<T>::KPL;
   const int C = s.C1 + s.C2, CPR = C / EPC;
   const int rpi = 256 / CPR;
   const int col = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
+  if (r0 >= rpi) return;
   const int n = blockIdx.x;
   const int per = (HW + splits - 1) / splits;
   const int pb = blockIdx.y * per, pe = min(HW, pb + per);
@@ -529,54 +526,12 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(Src2 s, int HW, const flo
     for (int u = 0; u < UNR; ++u)
       if (p0 + u * rpi < pe) buf[u] = load_chunk2<T>(s, n * HW + p0 + u * rpi, c0);
   };
-  __shared__ float gst[64][2];
-  // the statistics' partials are loaded BEFORE the first pixel rows (so that waiting for them does not wait for the
-  // rows), combined while the rows are in flight
-  const bool pre = gp.p1 && gn_part_np(gp) <= 64 * kGnPre && gp.G <= 8;
-  float pv[2][kGnPre][2];
-  if (pre)
-    for (int k = 0; k < 2; ++k)
-      if ((threadIdx.x >> 6) + 4 * k < gp.G) gn_part_prefetch(gp, n, (threadIdx.x >> 6) + 4 * k, pv[k]);
-  if (r0 < rpi && pb + r0 < pe) issue(pb + r0);   // in flight while the statistics / scale / shift load
-  if (gp.p1) {
-    if (pre) {
-      for (int k = 0; k < 2; ++k) {
-        const int g = (threadIdx.x >> 6) + 4 * k;
-        if (g < gp.G) {
-          float mu, rs;
-          gn_part_reduce(gp, pv[k], mu, rs);
-          if ((threadIdx.x & 63) == 0) { gst[g][0] = mu; gst[g][1] = rs; }
-        }
-      }
-    } else {
-      for (int g = threadIdx.x >> 6; g < gp.G; g += 4) {   // every wave whole: the xor tree needs all 64 lanes
-        float mu, rs;
-        gn_part_group(gp, n, g, mu, rs);
-        if ((threadIdx.x & 63) == 0) { gst[g][0] = mu; gst[g][1] = rs; }
-      }
-    }
-    __syncthreads();
-    if (mean_rstd && blockIdx.y == 0)
-      for (int g = threadIdx.x; g < gp.G; g += 256) {
-        mean_rstd[((size_t)n * gp.G + g) * 2] = gst[g][0];
-        mean_rstd[((size_t)n * gp.G + g) * 2 + 1] = gst[g][1];
-      }
-  }
-  if (r0 >= rpi) return;
+  if (pb + r0 < pe) issue(pb + r0);   // in flight while scale/shift load
   float sc[EPC], sh[EPC];
-  if (gp.p1) {
-    const int cpg = C / gp.G;
 #pragma unroll
-    for (int e = 0; e < EPC; ++e) {
-      const int c = c0 + e, g = c / cpg;
-      gn_fold(gst[g][0], gst[g][1], gp.gamma ? gp.gamma[c] : 1.f, gp.beta ? gp.beta[c] : 0.f, sc[e], sh[e]);
-    }
-  } else {
-#pragma unroll
-    for (int e = 0; e < EPC; ++e) {
-      sc[e] = scale[(size_t)n * C + c0 + e];
-      sh[e] = shift[(size_t)n * C + c0 + e];
-    }
+  for (int e = 0; e < EPC; ++e) {
+    sc[e] = scale[(size_t)n * C + c0 + e];
+    sh[e] = shift[(size_t)n * C + c0 + e];
   }
   for (int p0 = pb + r0; p0 < pe; p0 += UNR * rpi) {
     if (p0 != pb + r0) issue(p0);
@@ -864,23 +819,50 @@ extern "C" int dmc_gn_stats(int dtype, const void* x1, const void* x2, int N, in
 }
 
 namespace {
-// GroupNorm statistics from the conv-epilogue partials (dmc_conv_desc.gn_part): one wave per (n, g) runs
-// gn_part_group (dmc_common.h); mean / rstd and the folded per-channel scale / shift are written as gn_stats does.
-__global__ __launch_bounds__(256) void gn_finalize_kernel(GnPart gp, int N, float* mean_rstd, float* scale,
+// GroupNorm statistics from the conv-epilogue partials (dmc_conv_desc.gn_part): one wave per (n, g). Lane l takes
+// partials l, l+64, ... of image n's 64-pixel segments x the group's 8-channel chunks (segments outer, chunks
+// inner; source 1's chunks, then source 2's), then the lanes combine by Chan's formula over a fixed xor tree
+// (deterministic); mean / rstd and the folded per-channel scale / shift are written exactly as gn_stats does.
+DMC_DEV void chan(float& n, float& m, float& q, float nb, float mb, float qb) {
+  const float tot = n + nb;
+  if (tot == 0.f) return;
+  const float d = mb - m, r = nb / tot;
+  m += d * r;
+  q += qb + d * d * n * r;
+  n = tot;
+}
+
+__global__ __launch_bounds__(256) void gn_finalize_kernel(const float* p1, int nch1, const float* p2, int nch2, int N,
+                                                          int spi, int G, float eps, const float* gamma,
+                                                          const float* beta, float* mean_rstd, float* scale,
                                                           float* shift) {
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= N * gp.G) return;
-  const int n = i / gp.G, g = i - n * gp.G;
-  const int C = 8 * (gp.nch1 + gp.nch2), cpg = C / gp.G;
-  float mean, rstd;
-  gn_part_group(gp, n, g, mean, rstd);
+  if (i >= N * G) return;
+  const int n = i / G, g = i - n * G;
+  const int C = 8 * (nch1 + nch2), cpg = C / G, kpg = cpg / 8, np = spi * kpg;
+  float cn = 0.f, m = 0.f, q = 0.f;
+  for (int t = lane; t < np; t += 64) {
+    const int sg = n * spi + t / kpg, kc = g * kpg + t % kpg;
+    const float* pp = kc < nch1 ? p1 + ((size_t)sg * nch1 + kc) * 2 : p2 + ((size_t)sg * nch2 + (kc - nch1)) * 2;
+    chan(cn, m, q, 512.f, pp[0], pp[1]);
+  }
+#pragma unroll
+  for (int sh = 1; sh < 64; sh <<= 1) {
+    const float nb = __shfl_xor(cn, sh), mb = __shfl_xor(m, sh), qb = __shfl_xor(q, sh);
+    // both lanes of a pair must end with the same value: combine in lane order (lower lane first)
+    if ((lane & sh) == 0) chan(cn, m, q, nb, mb, qb);
+    else { float n2 = nb, m2 = mb, q2 = qb; chan(n2, m2, q2, cn, m, q); cn = n2; m = m2; q = q2; }
+  }
+  const float mean = m;
+  const float var = fmaxf(q / cn, 0.f);
+  const float rstd = 1.0f / sqrtf(var + eps);
   if (lane == 0 && mean_rstd) { mean_rstd[(size_t)i * 2] = mean; mean_rstd[(size_t)i * 2 + 1] = rstd; }
   for (int c = g * cpg + lane; c < (g + 1) * cpg; c += 64) {
-    float sc, sh;
-    gn_fold(mean, rstd, gp.gamma ? gp.gamma[c] : 1.f, gp.beta ? gp.beta[c] : 0.f, sc, sh);
+    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    const float sc = rstd * gm;
     scale[(size_t)n * C + c] = sc;
-    shift[(size_t)n * C + c] = sh;
+    shift[(size_t)n * C + c] = bt - mean * sc;
   }
 }
 }  // namespace
@@ -893,8 +875,9 @@ extern "C" int dmc_gn_finalize(const float* part1, int C1, const float* part2, i
               "gn_finalize: HW %d, C1 %d, C2 %d, G %d (64-pixel segments, 8-channel chunks inside groups)", HW, C1,
               C2, G);
   const int total = N * G;
-  const GnPart gp{part1, part2, C1 / 8, C2 / 8, HW / 64, G, eps, gamma, beta};
-  gn_finalize_kernel<<<(total + 3) / 4, 256, 0, dmc::as_stream(stream)>>>(gp, N, mean_rstd, scale, shift);
+  gn_finalize_kernel<<<(total + 3) / 4, 256, 0, dmc::as_stream(stream)>>>(part1, C1 / 8, part2, C2 / 8, N, HW / 64,
+                                                                               G, eps, gamma, beta, mean_rstd, scale,
+                                                                               shift);
   return dmc::check_launch("dmc_gn_finalize");
 }
 
@@ -974,11 +957,10 @@ extern "C" int dmc_channel_sum(int dtype, const void* dy, int N, int HW, int C, 
   return dmc::check_launch("dmc_channel_sum");
 }
 
-namespace {
-int gn_apply_launch(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1, int ld2,
-                    const float* scale, const float* shift, int silu, uint32_t drop_seed,
-                    const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* out, int ld_out,
-                    const GnPart& gp, float* mean_rstd, void* stream) {
+extern "C" int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1, int ld2,
+                            const float* scale, const float* shift, int silu, uint32_t drop_seed,
+                            const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* out,
+                            int ld_out, void* stream) {
   const int epc = dtype == DMC_F32 ? 4 : 8;
   DMC_REQUIRE(C1 % epc == 0 && C2 % epc == 0 && ld_out % epc == 0 && (C1 + C2) / epc <= 256,
               "gn_apply: channel alignment");
@@ -991,33 +973,9 @@ int gn_apply_launch(int dtype, const void* x1, const void* x2, int N, int HW, in
   dim3 g(N, splits);
   if (dtype == DMC_F32)
     gn_apply_kernel<float><<<g, 256, 0, s>>>(src, HW, scale, shift, silu, drop_seed, drop_seed_base, drop_thresh, drop_scale,
-                                             (char*)out, ld_out, splits, gp, mean_rstd);
+                                             (char*)out, ld_out, splits);
   else
     gn_apply_kernel<bf16_t><<<g, 256, 0, s>>>(src, HW, scale, shift, silu, drop_seed, drop_seed_base, drop_thresh, drop_scale,
-                                              (char*)out, ld_out, splits, gp, mean_rstd);
+                                              (char*)out, ld_out, splits);
   return dmc::check_launch("dmc_gn_apply");
-}
-}  // namespace
-
-extern "C" int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1, int ld2,
-                            const float* scale, const float* shift, int silu, uint32_t drop_seed,
-                            const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* out,
-                            int ld_out, void* stream) {
-  const GnPart none{nullptr, nullptr, 0, 0, 0, 0, 0.f, nullptr, nullptr};
-  return gn_apply_launch(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, scale, shift, silu, drop_seed, drop_seed_base,
-                         drop_thresh, drop_scale, out, ld_out, none, nullptr, stream);
-}
-
-extern "C" int dmc_gn_apply_part(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1,
-                                 int ld2, const dmc_gn_part_src* gsrc, float* mean_rstd, int silu, uint32_t drop_seed,
-                                 const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* out,
-                                 int ld_out, void* stream) {
-  DMC_REQUIRE(gsrc && gsrc->part1 && gsrc->C1 == C1 && gsrc->C2 == C2 && gsrc->HW == HW && HW % 64 == 0 &&
-                  gsrc->G > 0 && gsrc->G <= 64 && (C1 + C2) % gsrc->G == 0 && ((C1 + C2) / gsrc->G) % 8 == 0 &&
-                  C1 % 8 == 0 && C2 % 8 == 0 && (C2 == 0 || gsrc->part2),
-              "gn_apply_part: partials for C1 %d C2 %d HW %d (64-pixel segments, 8-channel chunks in <= 64 groups)",
-              C1, C2, HW);
-  const GnPart gp{gsrc->part1, gsrc->part2, C1 / 8, C2 / 8, HW / 64, gsrc->G, gsrc->eps, gsrc->gamma, gsrc->beta};
-  return gn_apply_launch(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, nullptr, nullptr, silu, drop_seed, drop_seed_base,
-                         drop_thresh, drop_scale, out, ld_out, gp, mean_rstd, stream);
 }

@@ -62,14 +62,12 @@ def drop_args(drop):
     return drop[0], (drop[3] if len(drop) > 3 else None), drop[1], drop[2]
 
 
-def set_prologue(d, kind=L.PRO_NONE, scale=None, shift=None, ld=0, drop=None, drop_ld=0, gn=None):
-    """gn: a GnLazy (statistics as conv-epilogue partials) instead of scale / shift (halo GN+SiLU prologue only)."""
+def set_prologue(d, kind=L.PRO_NONE, scale=None, shift=None, ld=0, drop=None, drop_ld=0):
     d.prologue = kind
-    d._keep_pro = (scale, shift, gn)   # the descriptor holds raw pointers: keep the tensors alive with it
+    d._keep_pro = (scale, shift)   # the descriptor holds raw pointers: keep the tensors alive with it
     d.pro_scale = ptr(scale)
     d.pro_shift = ptr(shift)
     d.ld_pro = ld
-    d.pro_gn = None if gn is None else ctypes.addressof(gn.src)
     d.drop_seed, d.drop_seed_base, d.drop_thresh, d.drop_scale = drop_args(drop)
     d.drop_ld = drop_ld if drop is not None else 0
 
@@ -246,36 +244,6 @@ def gn_finalize(p1, C1, p2, C2, N, HW, G, eps, gamma, beta):
     check(LIB.dmc_gn_finalize(ptr(p1), C1, ptr(p2), C2, N, HW, G, eps, ptr(gamma), ptr(beta), ptr(mr), ptr(sc),
                               ptr(sh), L.stream()), "dmc_gn_finalize")
     return sc, sh, mr
-
-
-class GnLazy:
-    """GroupNorm statistics left as the producing convs' epilogue partials (dmc_gn_part_src): the consumer -- the
-    halo conv's GN+SiLU prologue, or dmc_gn_apply_part -- combines them itself (the code and bits of dmc_gn_finalize),
-    so no finalize launch runs between the producing conv and its GroupNorm consumer. `mr` ([N][G][2] mean / rstd)
-    is written by dmc_gn_apply_part for the backward; st[2] reads it, as for the (scale, shift, mean_rstd) tuple."""
-
-    def __init__(self, p1, C1, p2, C2, N, HW, G, eps, gamma, beta):
-        self.src = L.GnPartSrc(ptr(p1), ptr(p2), C1, C2, HW, G, float(eps), ptr(gamma), ptr(beta))
-        self._keep = (p1, p2, gamma, beta)
-        self.N, self.C, self.G = N, C1 + C2, G
-        self.mr = torch.empty(N * G * 2, dtype=torch.float32, device=p1.device)
-
-    def __getitem__(self, i):
-        if i == 2:
-            return self.mr
-        raise TypeError("GnLazy holds partials, not a folded scale / shift (use gn_apply_part / the halo prologue)")
-
-
-def gn_apply_part(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, gn, silu=True, drop=None, out=None):
-    """gn_apply with the statistics combined from conv-epilogue partials in the same launch (GnLazy)."""
-    C = C1 + C2
-    if out is None:
-        out = torch.empty(N * HW * C, dtype=dtype, device=x1.device)
-    seed, base, thresh, dscale = drop_args(drop)
-    check(LIB.dmc_gn_apply_part(L.dtype_code(dtype), ptr(x1), ptr(x2), N, HW, C1, C2, ld1, ld2, ctypes.byref(gn.src),
-                                ptr(gn.mr), int(silu), seed, base, thresh, dscale, ptr(out), C, L.stream()),
-          "dmc_gn_apply_part")
-    return out
 
 
 def gn_apply(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, scale, shift, silu=True, drop=None, out=None):

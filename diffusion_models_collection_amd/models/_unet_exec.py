@@ -57,18 +57,6 @@ class GnbReq:
         self.epi, self.part = epi, part
 
 
-# GroupNorm statistics left as the producing conv's epilogue partials, combined by the consumer (dmc_gn_apply_part,
-# the halo conv's GN+SiLU prologue) instead of a dmc_gn_finalize launch per GroupNorm (DMC_GN_LAZY=0: finalize, A/B)
-_GN_LAZY = os.environ.get("DMC_GN_LAZY", "0") not in ("", "0")
-
-
-def _pro_silu(st):
-    """The conv prologue spec of SiLU(GroupNorm(x)) for statistics `st`: (kind, GnLazy) or (kind, scale, shift)."""
-    if isinstance(st, K.GnLazy):
-        return (L.PRO_AFFINE_SILU, st)
-    return (L.PRO_AFFINE_SILU, st[0], st[1])
-
-
 def _seed_from_torch():
     # dropout seeds follow torch's CPU generator (torch.manual_seed / set_seed semantics), no device sync
     return int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
@@ -176,10 +164,7 @@ class ExecCore:
             w = self._wpack(conv, packmode, Kc, dtype)
         d = K.make_desc(dtype, N, a.H, a.W, C1, C2, ld1, ld2, Kc, OH, OW, Cout, taps, mode, stride)
         if pro is not None:
-            if isinstance(pro[1], K.GnLazy):          # (kind, GnLazy): statistics folded inside the halo kernel
-                K.set_prologue(d, pro[0], ld=C1 + C2, drop=drop, drop_ld=C1 + C2, gn=pro[1])
-            else:
-                K.set_prologue(d, pro[0], pro[1], pro[2], C1 + C2, drop, C1 + C2)
+            K.set_prologue(d, pro[0], pro[1], pro[2], C1 + C2, drop, C1 + C2)
         elif drop is not None:
             if act not in (L.ACT_GELU_DROP, L.ACT_DGELU):
                 raise ValueError("dropout needs a prologue (or the GELU-dropout epilogue)")
@@ -229,10 +214,7 @@ class ExecCore:
         d = K.make_desc(dtype, N, a.H, a.W, C1, C2, a.t.shape[-1], srcs[1].t.shape[-1] if len(srcs) > 1 else 0, Kc,
                         OH, OW, Cout, taps, mode, stride)
         if pro is not None:
-            if isinstance(pro[1], K.GnLazy):          # (kind, GnLazy): statistics folded inside the halo kernel
-                K.set_prologue(d, pro[0], ld=C1 + C2, drop=drop, drop_ld=C1 + C2, gn=pro[1])
-            else:
-                K.set_prologue(d, pro[0], pro[1], pro[2], C1 + C2, drop, C1 + C2)
+            K.set_prologue(d, pro[0], pro[1], pro[2], C1 + C2, drop, C1 + C2)
         K.wgrad(d, dy, ld_dy, a.t, srcs[1].t if len(srcs) > 1 else None, dw, self.training_grad_scale, dbias=dbias)
 
     def _new(self, N, H, W, C, dtype=None):
@@ -364,11 +346,7 @@ class UNetExecutor(ExecCore):
         C = a.C + (b.C if b else 0)
         if (all(s.part is not None for s in srcs) and (a.H * a.W) % 64 == 0 and C % gn.num_groups == 0
                 and (C // gn.num_groups) % 8 == 0):
-            # statistics from the producing convs' epilogue partials: no pass over the activation; left as partials
-            # for the consumer to combine (no finalize launch) unless DMC_GN_LAZY=0
-            if _GN_LAZY and gn.num_groups <= 64:
-                return K.GnLazy(a.part, a.C, b.part if b else None, b.C if b else 0, N, a.H * a.W, gn.num_groups,
-                                gn.eps, gn.weight, gn.bias)
+            # statistics from the producing convs' epilogue partials: no pass over the activation
             return K.gn_finalize(a.part, a.C, b.part if b else None, b.C if b else 0, N, a.H * a.W, gn.num_groups,
                                  gn.eps, gn.weight, gn.bias)
         return K.gn_stats(dtype, a.t, b.t if b else None, N, a.H * a.W, a.C, b.C if b else 0, a.t.shape[-1],
@@ -380,10 +358,6 @@ class UNetExecutor(ExecCore):
         b = srcs[1] if len(srcs) > 1 else None
         N = a.t.shape[0]
         C = a.C + (b.C if b else 0)
-        if isinstance(st, K.GnLazy):
-            out = K.gn_apply_part(self.dt, a.t, b.t if b else None, N, a.H * a.W, a.C, b.C if b else 0,
-                                  a.t.shape[-1], b.t.shape[-1] if b else 0, st, silu=silu, drop=drop)
-            return Act(out.view(N, a.H, a.W, C), a.H, a.W, C)
         out = K.gn_apply(self.dt, a.t, b.t if b else None, N, a.H * a.W, a.C, b.C if b else 0, a.t.shape[-1],
                          b.t.shape[-1] if b else 0, st[0], st[1], silu=silu, drop=drop)
         return Act(out.view(N, a.H, a.W, C), a.H, a.W, C)
@@ -397,16 +371,13 @@ class UNetExecutor(ExecCore):
         b = srcs[1] if len(srcs) > 1 else None
         N = a.t.shape[0]
         key = (N, a.H, a.W, a.C, b.C if b else 0, a.t.shape[-1], b.t.shape[-1] if b else 0, Cout,
-               isinstance(st, K.GnLazy), L.get_option("DMC_HALO_PRO"))
+               L.get_option("DMC_HALO_PRO"))
         ok = self._halo_pro_cache.get(key)
         if ok is None:
             C1, C2 = a.C, (b.C if b else 0)
             d = K.make_desc(self.dt, N, a.H, a.W, C1, C2, key[5], key[6], L.kc_for(C1 + C2, self.dt), a.H, a.W, Cout,
                             K.TAPS3)
-            if isinstance(st, K.GnLazy):
-                K.set_prologue(d, L.PRO_AFFINE_SILU, ld=C1 + C2, gn=st)
-            else:
-                K.set_prologue(d, L.PRO_AFFINE_SILU, st[0], st[1], C1 + C2)
+            K.set_prologue(d, L.PRO_AFFINE_SILU, st[0], st[1], C1 + C2)
             ok = self._halo_pro_cache[key] = K.conv_halo_prologue(d)
         return ok
 
@@ -538,13 +509,12 @@ class UNetExecutor(ExecCore):
                 srcs = [h]
         # ---- output: GN -> SiLU -> conv3x3 -> NCHW fp32 ----
         gno, convo = m.output[0], m.output[2]
-        sto = self._gn([h], gno)
-        ao = self._apply([h], sto, silu=True)
-        mr = sto[2]
+        sc, sh, mr = self._gn([h], gno)
+        ao = self._apply([h], (sc, sh, mr), silu=True)
         out = torch.empty(N, m.out_channels, H, W, dtype=f32, device=x.device)
         self._conv([ao], convo, K.TAPS3, H, W, m.out_channels, bias=convo.bias, out=out, out_f32=True, out_nchw=True)
         if keep:
-            tape.append(("out", h, (None, None, mr), ao))
+            tape.append(("out", h, (sc, sh, mr), ao))
         return out, tape
 
     def _layer(self, srcs, layer, tape):
@@ -584,7 +554,7 @@ class UNetExecutor(ExecCore):
         off = self.temb_off[id(rb)]
         if tape is None and self._halo_pro_ok(srcs, Cout, st1):
             a1 = None
-            self._conv(srcs, conv1, K.TAPS3, H, W, Cout, pro=_pro_silu(st1), bias=conv1.bias,
+            self._conv(srcs, conv1, K.TAPS3, H, W, Cout, pro=(L.PRO_AFFINE_SILU, st1[0], st1[1]), bias=conv1.bias,
                        addvec=self.addvec.view(N, -1)[:, off:], ld_add=self.temb_total, out=h1.t, stats=h1)
         else:
             a1 = self._apply(srcs, st1, silu=True)
@@ -606,7 +576,7 @@ class UNetExecutor(ExecCore):
         out = self._new(N, H, W, Cout)
         if tape is None and drop is None and self._halo_pro_ok([h1], Cout, st2):
             a2 = None
-            self._conv([h1], conv2, K.TAPS3, H, W, Cout, pro=_pro_silu(st2), bias=conv2.bias,
+            self._conv([h1], conv2, K.TAPS3, H, W, Cout, pro=(L.PRO_AFFINE_SILU, st2[0], st2[1]), bias=conv2.bias,
                        resid=resid, out=out.t, stats=out)
         else:
             a2 = self._apply([h1], st2, silu=True, drop=drop)

@@ -67,18 +67,6 @@ typedef struct dmc_gn_bwd_epi {
   float* part;               /* out: [M/64][Cout][2] */
 } dmc_gn_bwd_epi;
 
-/* GroupNorm statistics still in conv-epilogue partial form (dmc_conv_desc.gn_part of the producing conv(s)): the
- * consumer combines them itself -- the same code and bits as dmc_gn_finalize -- so no finalize launch sits between
- * the producing conv and its GroupNorm consumer (models/unet.py:34/:55/:84 GroupNorm(8, C)). */
-typedef struct dmc_gn_part_src {
-  const float* part1;        /* [N*HW/64][C1/8][2] (mean, M2) of source 1 */
-  const float* part2;        /* [N*HW/64][C2/8][2] of source 2 (virtual concat), or NULL */
-  int C1, C2, HW, G;
-  float eps;
-  const float* gamma;        /* [C1+C2] or NULL */
-  const float* beta;
-} dmc_gn_part_src;
-
 typedef struct dmc_conv_desc {
   int dtype;
   int N, H, W;               /* source batch and spatial size */
@@ -117,9 +105,6 @@ typedef struct dmc_conv_desc {
                               * OH*OW % 64 == 0, Cout % 8 == 0, one NHWC output. Finalised by dmc_gn_finalize. */
   float* wg_bias;            /* dmc_conv2d_wgrad only: if set, also the bias gradient wg_bias[co] = scale * sum over
                               * pixels of dy[pix][co] (nn.Conv2d bias), from the same pass over dy */
-  const dmc_gn_part_src* pro_gn; /* with prologue DMC_PRO_AFFINE_SILU on the halo kernel (dmc_conv_halo_prologue):
-                              * the GroupNorm scale / shift are folded from these partials inside the kernel
-                              * (pro_scale / pro_shift unused); the call fails where the halo prologue does not apply */
 } dmc_conv_desc;
 enum { DMC_ACT_NONE = 0, DMC_ACT_GELU = 1, DMC_ACT_GELU_DROP = 2, DMC_ACT_DGELU = 3 };
 /* DGELU: the backward of GELU_DROP / GELU on an input-gradient conv: out = round(acc) * mask * scale * gelu'(u) with
@@ -196,13 +181,6 @@ int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C
                  int ld2, const float* scale, const float* shift, int silu, uint32_t drop_seed,
                  const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* out, int ld_out,
                  void* stream);
-/* dmc_gn_apply with the statistics taken from conv-epilogue partials (dmc_gn_part_src) instead of a finalized
- * scale / shift: dmc_gn_finalize + dmc_gn_apply in ONE launch, bitwise the same output; mean_rstd ([N][G][2], may
- * be NULL) receives the statistics for the backward. */
-int dmc_gn_apply_part(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1, int ld2,
-                      const dmc_gn_part_src* gn, float* mean_rstd, int silu, uint32_t drop_seed,
-                      const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* out, int ld_out,
-                      void* stream);
 
 /* Backward of a = dropout(SiLU(GroupNorm(x))) (silu=1) or a = GroupNorm(x) (silu=0, AttentionBlock
  * norm :80): g = dL/da (dtype, [pix][ld_g]); writes

@@ -123,16 +123,14 @@ def test_upsample2x_nhwc_bitwise(dt):
     assert torch.equal(y.permute(0, 3, 1, 2).float(), ref)
 
 
-@pytest.mark.parametrize("dpos", [0, 1])
 @pytest.mark.parametrize("case", ["c32_two_sources", "c16_wide", "c32_384", "c8_multi_image"])
-def test_conv3x3_halo_gn_silu_prologue(case, dpos, monkeypatch, dmc_opt):
+def test_conv3x3_halo_gn_silu_prologue(case, monkeypatch, dmc_opt):
     """Inference prologue on the halo kernel: conv(SiLU(x*scale+shift)) with the GroupNorm affine + SiLU
     applied to the LDS-resident halo equals, BITWISE, dmc_gn_apply materialisation followed by the plain halo
     conv (same op sequence and bf16 rounding), and the fp32 torch reference within bf16 tolerance."""
     L, K = _lib()
     dmc_opt("DMC_NO_SPLITK", 1)   # small N: keep the planner on the halo kernel
     dmc_opt("DMC_HALO_PRO", 1)    # the halo prologue path (default on)
-    dmc_opt("DMC_HALO_DPOS", dpos)
     dt = torch.bfloat16
     torch.manual_seed(11)
     N, H, C1, C2, Cout = {"c32_two_sources": (2, 32, 128, 64, 128), "c16_wide": (3, 16, 256, 0, 256),
@@ -229,18 +227,16 @@ def test_conv_dgrad_wgrad(dt, case):
     assert rel_err(db.cpu(), g.sum((0, 2, 3))) < 1e-5
 
 
-@pytest.mark.parametrize("variant", ["halo2", "halo2_nosched", "halo2_dpos1", "halo2_dpos2"])
+@pytest.mark.parametrize("variant", ["halo2", "halo2_nosched"])
 @pytest.mark.parametrize("case", ["fwd32_concat", "fwd16_ragged_cout", "dgrad32", "fwd8_multi_image", "fallback_4x4",
                                   "fwd8_concat_b128", "fwd64_rows"])
 def test_conv3x3_halo_kernel(case, variant, monkeypatch, dmc_opt):
     """bf16 3x3 stride-1 convs on the LDS-halo kernel (conv3x3_halo2_kernel: 128-pixel tiles of whole rows or
     whole images, two blocks per CU) vs an fp32 reference and vs the per-tap kernel (DMC_NO_HALO) on the same
     inputs; its weight-gradient twin (wgrad3x3_halo2_kernel) likewise. Variants: the scheduled fragment reads
-    (default), the compiler's own schedule (DMC_HALO_NOSCHED), and the weight slice's LDS-DMA issued after the
-    first k-step's fragment reads (DMC_HALO_DPOS=1) or split around both k-steps' reads (=2)."""
+    (default) and the compiler's own schedule (DMC_HALO_NOSCHED)."""
     L, K = _lib()
     dmc_opt("DMC_HALO_NOSCHED", 1 if variant == "halo2_nosched" else 0)
-    dmc_opt("DMC_HALO_DPOS", {"halo2_dpos1": 1, "halo2_dpos2": 2}.get(variant, 0))
     # at these small M the planner would split K over the LDS-DMA kernel instead; the halo kernel is what the
     # B=128 model runs, so keep split-K off here to exercise it
     dmc_opt("DMC_NO_SPLITK", 1)
@@ -870,63 +866,3 @@ def test_wgrad_glds_taps(case, on, dmc_opt):
     torch.cuda.synchronize()
     assert rel_err(dw.cpu(), w.grad) < 1e-5
     assert rel_err(db.cpu(), g.float().sum((0, 2, 3))) < 1e-5
-
-
-@pytest.mark.parametrize("case", ["c32_one_source", "c16_concat_straddle", "c8_attention_nosilu"])
-def test_gn_from_partials_in_consumer_bitwise(case, dmc_opt):
-    """The finalize launch folded into the GroupNorm consumers (dmc_gn_part_src): dmc_gn_apply_part (train and
-    inference) equals dmc_gn_finalize + dmc_gn_apply BITWISE, including the mean / rstd it stores for the backward
-    (with and without dropout); and where the halo GN+SiLU prologue applies (32x32 / 16x16, one image per tile), the
-    conv with pro_gn equals the conv fed the finalize's scale / shift bitwise. Group 5 of the 384-channel concat
-    straddles the two sources (models/unet.py:284)."""
-    from diffusion_models_collection_amd import _lib as L, kernels as K
-    dt = torch.bfloat16
-    gen = torch.Generator().manual_seed(13)
-    N, H, C1, C2, silu = {"c32_one_source": (8, 32, 128, 0, True), "c16_concat_straddle": (4, 16, 256, 128, True),
-                          "c8_attention_nosilu": (16, 8, 256, 0, False)}[case]
-    W, C, G = H, C1 + C2, 8
-    HW = H * W
-
-    def producer(cout, seed):
-        g = torch.Generator().manual_seed(seed)
-        x = (torch.randn(N, H, W, 64, generator=g) + 0.3).to(DEV).to(dt)
-        w = (torch.randn(cout, 64, 1, 1, generator=g) * 0.2).to(DEV)
-        b = (torch.randn(cout, generator=g) + 1.0).to(DEV)
-        y = torch.empty(N, H, W, cout, dtype=dt, device=DEV)
-        part = torch.empty(N * HW // 64 * (cout // 8) * 2, device=DEV)
-        d = K.make_desc(dt, N, H, W, 64, 0, 64, 0, L.kc_for(64, dt), H, W, cout, K.TAPS1)
-        K.set_epilogue(d, bias=b, ldy1=cout, gn_part=part)
-        K.conv(d, x, None, K.pack_weight(L.PACK_FWD, dt, w, L.kc_for(64, dt)), y)
-        return y, part
-
-    y1, p1 = producer(C1, 1)
-    y2, p2 = producer(C2, 2) if C2 else (None, None)
-    gamma = (torch.rand(C, generator=gen) + 0.5).to(DEV)
-    beta = torch.randn(C, generator=gen).to(DEV)
-    sc, sh, mr = K.gn_finalize(p1, C1, p2, C2, N, HW, G, 1e-5, gamma, beta)
-    lazy = K.GnLazy(p1, C1, p2, C2, N, HW, G, 1e-5, gamma, beta)
-    for drop in (None, (99, 1 << 30, 4.0 / 3.0)):
-        a_ref = K.gn_apply(dt, y1, y2, N, HW, C1, C2, C1, C2, sc, sh, silu=silu, drop=drop)
-        a_new = K.gn_apply_part(dt, y1, y2, N, HW, C1, C2, C1, C2, lazy, silu=silu, drop=drop)
-        torch.cuda.synchronize()
-        assert torch.equal(a_ref, a_new), drop
-        assert torch.equal(lazy.mr, mr)
-    if silu and H >= 16:
-        w = (torch.randn(128, C, 3, 3, generator=gen) * 0.03).to(DEV)
-        Kc = L.kc_for(C, dt)
-        wp = K.pack_weight(L.PACK_FWD, dt, w, Kc)
-        outs = []
-        for use_lazy in (False, True):
-            d = K.make_desc(dt, N, H, W, C1, C2, C1, C2, Kc, H, W, 128, K.TAPS3)
-            if use_lazy:
-                K.set_prologue(d, L.PRO_AFFINE_SILU, ld=C, gn=lazy)
-            else:
-                K.set_prologue(d, L.PRO_AFFINE_SILU, sc, sh, C)
-            dmc_opt("DMC_NO_SPLITK", 1)   # small N: keep the planner on the halo kernel
-            assert K.conv_halo_prologue(d), case
-            K.set_epilogue(d, ldy1=128)
-            y = torch.empty(N, H, W, 128, dtype=dt, device=DEV)
-            K.conv(d, y1, y2, wp, y)
-            outs.append(y)
-        torch.cuda.synchronize()
-        assert torch.equal(outs[0], outs[1])

@@ -335,7 +335,7 @@ def test_dropout_statistics_resblock():
     m = UNet(**dict(CIFAR, dropout=p), compute_dtype="bf16").to(DEV).train()
     x = torch.randn(16, 3, 32, 32, device=DEV)
     t = torch.randint(0, 1000, (16,), device=DEV)
-    orig, orig_part = K.gn_apply, K.gn_apply_part
+    orig = K.gn_apply
     caps = []
 
     def wrapped(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, scale, shift, silu=True, drop=None, out=None):
@@ -345,15 +345,7 @@ def test_dropout_statistics_resblock():
             caps.append((r.detach().float().clone(), u.detach().float().clone()))
         return r
 
-    def wrapped_part(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, gn, silu=True, drop=None, out=None):
-        # the statistics-from-partials form of the same launch (GroupNorm inputs produced by a conv epilogue)
-        r = orig_part(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, gn, silu=silu, drop=drop, out=out)
-        if drop is not None:
-            u = orig_part(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, gn, silu=silu, drop=None)
-            caps.append((r.detach().float().clone(), u.detach().float().clone()))
-        return r
-
-    K.gn_apply, K.gn_apply_part = wrapped, wrapped_part
+    K.gn_apply = wrapped
     try:
         steps = []
         for seed in (123, 124):
@@ -364,7 +356,7 @@ def test_dropout_statistics_resblock():
             torch.cuda.synchronize()
             steps.append(list(caps))
     finally:
-        K.gn_apply, K.gn_apply_part = orig, orig_part
+        K.gn_apply = orig
     nlayers = len(steps[0])
     assert nlayers == 22, nlayers       # one dropout per ResidualBlock (22 blocks)
     for s_idx, layers in enumerate(steps):
