@@ -45,8 +45,8 @@ CIFAR = dict(image_size=(32, 32), in_channels=3, model_channels=128, out_channel
              attention_resolutions=(16, 8), dropout=0.1, channel_mult=(1, 2, 2, 2), use_attention=True)
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense, MI355X_MICROARCH.md
 TRAIN_GFLOP_PER_IMG = 37.890     # fwd + bwd, = 3 x 12.632 forward
-PMC_FILE = "r2_pmc_roofline_conv.json"          # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of the roofline conv
-ROOFLINE_CSV = "r2_roofline_kernel_stats.csv"   # rocprofv3 --kernel-trace --stats of `bench.py --roofline-only`
+PMC_FILE = "r3_pmc_roofline_conv.json"          # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of the roofline conv
+ROOFLINE_CSV = "r3_roofline_kernel_stats.csv"   # rocprofv3 --kernel-trace --stats of `bench.py --roofline-only`
 DIT_PMC_FILE = "r3_pmc_dit_loop.json"           # rocprofv3 --pmc over `bench.py --dit-only --no-train`
 
 
@@ -59,7 +59,7 @@ def conv_roofline(dtype, B=128):
     its GN+SiLU input is materialised by the GN-apply pass, as in training; the halo kernel the library picks by
     default: conv3x3_halo2_kernel, two 128-pixel blocks per CU) with HIP events on the stream it is
     launched on. `achieved` / `avg_launch_ms`: the average of 50 launches issued back to back between two events
-    (agrees with the rocprofv3 kernel-trace average, profiles/r2_roofline_kernel_stats.csv);
+    (agrees with the rocprofv3 kernel-trace average, profiles/r3_roofline_kernel_stats.csv);
     `per_launch_events_ms`: an event pair around every launch (includes the events' own overhead)."""
     from diffusion_models_collection_amd import _lib as L, kernels as K
     H = W = 32
@@ -93,7 +93,7 @@ def conv_roofline(dtype, B=128):
     b2b_ms = e0.elapsed_time(e1) / n
     flops = 2.0 * B * H * W * C * C * 9
     # the launch duration is taken from the 50 back-to-back launches between two events: it agrees with the
-    # rocprofv3 kernel-trace average of the same command within ~1 % (profiles/r2_roofline_*), whereas an event
+    # rocprofv3 kernel-trace average of the same command within ~1 % (profiles/r3_roofline_*), whereas an event
     # pair around every launch adds its own ~4 us
     achieved = flops / (b2b_ms * 1e-3) / 1e12
     kname = "conv3x3_halo2_kernel"

@@ -25,3 +25,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/profs -o profs --output
   || { tail -30 $O/profs.err; exit 1; }
 python3 scripts/trace_summary.py "$(find $O/profs -name '*kernel_trace.csv' | head -1)" --steps 100 --top 50 > $O/sample_summary.txt
 head -3 $O/sample_summary.txt
+timeout -k 10 300 rocprofv3 --kernel-trace -d $O/profd -o profd --output-format csv -- \
+  python3 bench.py --steps 10 --warmup 3 --no-cpu --no-extra --no-dit --no-sample --no-roofline --dist-one-rank > $O/profd.json 2> $O/profd.err \
+  || { tail -30 $O/profd.err; exit 1; }
+python3 scripts/trace_summary.py "$(find $O/profd -name '*kernel_trace.csv' | head -1)" --steps 9 --marker adamw_flat --top 60 > $O/train_dist1_summary.txt
+head -3 $O/train_dist1_summary.txt
