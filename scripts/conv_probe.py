@@ -17,6 +17,7 @@ from diffusion_models_collection_amd import _lib as L, kernels as K  # noqa: E40
 SHAPES = {
     "r128_32": (128, 32, 32, 128, 0, 128, "3"),      # ResBlock 128->128 @32x32 (the bench roofline kernel)
     "r384_32": (128, 32, 32, 256, 128, 128, "3"),    # decoder concat 384->128 @32x32
+    "r128_64": (128, 64, 64, 128, 0, 128, "3"),      # config #5 (64x64) ResBlock 128->128
     "r256_16": (128, 16, 16, 256, 0, 256, "3"),
     "r512_8": (128, 8, 8, 256, 256, 256, "3"),       # small M: split-K
     "r512_4": (128, 4, 4, 256, 256, 256, "3"),
