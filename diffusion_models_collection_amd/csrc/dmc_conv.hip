@@ -10,7 +10,6 @@
 //   consecutive output channels of one pixel, which is one vector store in NHWC.
 // Weight gradient: C[co][kk] = sum_pix dY[pix][co] * A[pix][kk]; both operands are staged as
 //   [pixel][channel] images and read transposed (ds_read_b64_tr_b16 for bf16).
-#include <utility>
 #include "dmc_common.h"
 #include "dmc_internal.h"
 
@@ -39,7 +38,6 @@ struct ConvK {
   int sk_per; // K stages per split
   int x1_bytes, x2_bytes, w_bytes;  // operand extents for buffer resources (0: too large / absent)
   int dtype_bytes;  // 4 (fp32) or 2 (bf16) storage
-  int trot;         // halo conv: 1 = block-rotated tap order, 2 = taps and chunks (DMC_HALO_ROT)
 };
 
 // Source pixel of output pixel (n,oy,ox) under tap; returns -1 if it falls in the zero padding.
@@ -371,7 +369,7 @@ DMC_DEV void chan_eq(float& m, float& q, float mb, float qb, float n) {
 }
 
 template <int BM, int BN, int NT>
-DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int n0, const char* scratch = nullptr) {
+DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int n0) {
   constexpr int CG = BN / 8, RS = NT / CG, IT = BM / RS;
   constexpr int SEG = 64, NSEG = BM / SEG, KPS = SEG / RS;   // GroupNorm partial segments of 64 pixels
   static_assert(CG == 16 && SEG % RS == 0 && BM % SEG == 0, "GroupNorm partial geometry");
@@ -534,7 +532,7 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
       for (int j = 0; j < NSEG; ++j)
 #pragma unroll
         for (int e = 0; e < 8; ++e) { gs1[j][e] += __shfl_xor(gs1[j][e], sh); gs2[j][e] += __shfl_xor(gs2[j][e], sh); }
-    float* red = (float*)(scratch ? scratch : lds + BM * EP);            // [NW][NSEG][CG][16]
+    float* red = (float*)(lds + BM * EP);            // [NW][NSEG][CG][16]
     if (lane < CG) {
 #pragma unroll
       for (int j = 0; j < NSEG; ++j)
@@ -572,7 +570,7 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
       }
       cnt *= 2.f;
     }
-    float* red = (float*)(scratch ? scratch : lds + BM * EP);            // [NW][NSEG][CG][2], past the epilogue tile
+    float* red = (float*)(lds + BM * EP);            // [NW][NSEG][CG][2], past the epilogue tile
     if (lane < CG) {
 #pragma unroll
       for (int j = 0; j < NSEG; ++j) {
@@ -605,7 +603,7 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
 // form costs more VALU than the tile's MFMAs leave room for). NCHW output, fused silu' and ragged channel
 // groups take conv_store_tile.
 template <typename T, int BM, int BN, int NT>
-DMC_DEV void tile_epilogue(const ConvK& a, const char* lds, int EP, int m0, int n0, const char* scratch = nullptr) {
+DMC_DEV void tile_epilogue(const ConvK& a, const char* lds, int EP, int m0, int n0) {
   constexpr int CG = BN / 4, RS = NT / CG;
   const int cg = threadIdx.x % CG, r0 = threadIdx.x / CG;
   const int co = n0 + cg * 4;
@@ -615,7 +613,7 @@ DMC_DEV void tile_epilogue(const ConvK& a, const char* lds, int EP, int m0, int 
   }
   if constexpr (BN == 128) {
     if (sizeof(T) == 2 && !a.out_f32 && !((a.Cout | a.Csplit | a.ldy1 | a.ldy2 | a.ld_res) & 7)) {
-      tile_epilogue8<BM, BN, NT>(a, lds, EP, m0, n0, scratch);   // 16-byte stores: half the store instructions
+      tile_epilogue8<BM, BN, NT>(a, lds, EP, m0, n0);   // 16-byte stores: half the store instructions
       return;
     }
   }
@@ -1053,16 +1051,9 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
     for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
   const int nch = a.Kc / 64, nst = nch * 9;
-  // Tap (and chunk) order rotated per block: the blocks resident together stream different weight slices
-  // instead of all hitting the same 16 KB of the XCD's L2 at once (9 and 8 are coprime, so blocks b, b+8, ...
-  // of one XCD start at different taps). The sum order differs per block; every block is still deterministic.
-  const int trot = a.trot ? (int)(blockIdx.x % 9) : 0;
-  const int crot = a.trot == 2 ? (int)((blockIdx.x / 9) % nch) : 0;
-  auto tap_of = [&](int t) { return t + trot >= 9 ? t + trot - 9 : t + trot; };
-  auto chunk_of = [&](int c) { return c + crot >= nch ? c + crot - nch : c + crot; };
   auto issue_w = [&](int s) {
     const int c = s / 9, t = s - c * 9;
-    const unsigned koff = (unsigned)(tap_of(t) * a.Kc + chunk_of(c) * 64) * 2u;
+    const unsigned koff = (unsigned)(t * a.Kc + c * 64) * 2u;
     dma_pieces<4>(a.w, a.w_bytes, wring + (s % WS) * WB + wave * 4 * 1024, ob, koff, 0, 4);
   };
   v4f pst[4];
@@ -1079,8 +1070,8 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
     if (t == 0) {
       // chunk c's halo into the single buffer: every wave is done with chunk c-1's taps
       if (c > 0) __syncthreads();
-      if (PRO) halo_pro_load(a, n_first, chunk_of(c) * 64, pst);
-      halo_issue<HP>(a, lds, chunk_of(c) * 64, wave, 0, HP, h1, h2);
+      if (PRO) halo_pro_load(a, n_first, c * 64, pst);
+      halo_issue<HP>(a, lds, c * 64, wave, 0, HP, h1, h2);
       if (c == 0)
         for (int q = 0; q < WS - 1 && q < nst; ++q) issue_w(q);
       __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
@@ -1100,7 +1091,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
     if (s + WS - 1 < nst) issue_w(s + WS - 1);
     DMC_PH(2);   // LDS-DMA issue of a later slice
     const char* Bw = wring + (s % WS) * WB;
-    const int tr = tap_of(t), ty = tr / 3, tx = tr - ty * 3;
+    const int ty = t / 3, tx = t - ty * 3;
     const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
     // both k-steps' fragments read up front into distinct registers; the schedule below issues the second
     // k-step's reads between the first k-step's MFMAs (left alone, hipcc re-reads fragments into the same
@@ -1159,292 +1150,6 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
       *(v4f*)(lds + (wm * 64 + j * 16 + fr) * EP + (wn * 64 + i * 16 + fh * 4) * 4) = acc[i][j];
   __syncthreads();
   tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
-}
-
-// ---------------------------------------------------------------------------------------------
-// 3x3 conv with the WEIGHT operand in registers (conv3x3_hw_kernel, DMC_HALO_VER=4). The halo kernels above
-// stream every tap's [128 co][64 ch] weight slice through an LDS-DMA ring with one block barrier per tap; phase
-// clocks put 44 % of their tap loop in that stream (issuing 1-KB LDS-DMA pieces, 60-185 cycles each, and waiting
-// for them) and PMC put the MFMA pipe at a third of the SIMD cycles. Here a block computes 256 output pixels x 128
-// channels with 4 waves of 128 pixels x 64 channels (acc[4][8]: twice the MFMAs per weight byte of a 64 x 64 wave
-// tile), and each wave loads its own weight fragments straight into VGPRs with buffer loads, two K-stages ahead
-// (the packed weight rows are [co][tap][Kc]: 16 co rows x 64 B per load). Only the activation halo lives in LDS,
-// as two 32-channel regions (64-byte rows, 16-byte chunk c of halo pixel h at physical chunk c ^ (2*((h>>2)&1)):
-// conflict-free ds_read_b128 for 16 consecutive pixels at any base, brute-force checked). A stage is (chunk c,
-// half hf, tap t) with K = 32: the 9 taps of half 0, then the 9 taps of half 1, so region 0 is free while half 1
-// computes and the next chunk's region 0 streams in then (and region 1 during the next chunk's half 0): a double-
-// buffered halo in the LDS of a single one, two block barriers per 64-channel chunk and none per tap. <= 76 KB of
-// LDS, <= 256 VGPRs: two blocks per CU. The epilogue is the shared LDS-staged one, in two 128-pixel halves.
-#ifndef HW_PD
-#define HW_PD 2
-#endif
-DMC_DEV int hw_swz(int h) { return ((h >> 2) & 1) << 1; }
-#ifndef HW_ACC
-#define HW_ACC "a"
-#endif
-DMC_DEV void mfma_bf16_tied(v4f& acc, const v4i& a, const v4i& b) {
-  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+" HW_ACC(acc) : "v"(a), "v"(b));
-}
-DMC_DEV void mfma_bf16_init(v4f& acc, const v4i& a, const v4i& b) {
-  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=" HW_ACC(acc) : "v"(a), "v"(b));
-}
-template <typename F, int... Rs>
-DMC_DEV void unroll_seq(F& f, std::integer_sequence<int, Rs...>) {
-  (f(std::integral_constant<int, Rs>{}), ...);
-}
-
-template <int HP, bool PRO>
-__global__ __launch_bounds__(256, 2) void conv3x3_hw_kernel(ConvK a, int R, int nimg) {
-  using T = bf16_t;
-  constexpr int NW = 4, BN = 128, HALF = 128;
-  constexpr int RB = HP * NW * 1024;                  // bytes of one 32-channel halo region
-  constexpr int EP = BN * 4 + 16;                     // epilogue row pitch (fp32)
-  constexpr int STATS = NW * (HALF / 64) * 16 * 64;   // GroupNorm (backward) partial scratch past the tile
-  constexpr int LDS_BYTES = 2 * RB > HALF * EP + STATS ? 2 * RB : HALF * EP + STATS;
-  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave & 1, wn = wave >> 1;
-  int mb = blockIdx.x, nb = blockIdx.y;
-  if (gridDim.y == 1) xcd_tile((a.Cout + BN - 1) / BN, mb, nb);
-  const int m0 = mb * 256, n0 = nb * BN;
-  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
-  const int n_first = m0 / a.OHW;
-  const int r0 = (m0 - n_first * a.OHW) / OW;
-  const int fr = lane & 15, fh = lane >> 4;
-  const int nch = a.Kc / 64;
-
-  // halo DMA: piece p of this wave holds halo pixels (wave*HP + p)*16 + lane/4; the lane fetches logical chunk lc
-  const int lc = (lane & 3) ^ (((lane >> 4) & 1) << 1);
-  int sp[HP];
-#pragma unroll
-  for (int p = 0; p < HP; ++p) {
-    const int h = (wave * HP + p) * 16 + (lane >> 2);
-    sp[p] = -1;
-    if (h < npix) {
-      const int img = h / segpix, rem = h - img * segpix;
-      const int hr = rem / HW, hc = rem - hr * HW;
-      const int iy = r0 + hr - 1, ix = hc - 1;
-      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) sp[p] = ((n_first + img) * a.H + iy) * a.W + ix;
-    }
-  }
-  // weight fragment i: rows co = n0 + wn*64 + i*16 + fr, 16 bytes at channel fh*8 of the stage's 32
-  const unsigned wrow = 9u * (unsigned)a.Kc;
-  unsigned wo[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int co = n0 + wn * 64 + i * 16 + fr;
-    wo[i] = co < a.Cout ? ((unsigned)co * wrow + fh * 8) * 2u : kOOB;
-  }
-  // pixel fragment j (tile pixels wm*128 + j*16 + fr) -> halo pixel hu[j] + lp (hu wave-uniform)
-  const int OWc = OW < 16 ? OW : 16;
-  const int lp = (fr / OWc) * HW + (fr - (fr / OWc) * OWc);
-  int hu[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int p0 = wm * HALF + j * 16;
-    const int img = p0 / (R * OW), rem = p0 - img * (R * OW);
-    const int row = rem / OW, col = rem - row * OW;
-    hu[j] = img * segpix + (row + 1) * HW + col + 1;
-  }
-  const int trot = a.trot ? (int)(blockIdx.x % 9) : 0;
-  auto tap_of = [&](int t) __attribute__((always_inline)) { return t + trot >= 9 ? t + trot - 9 : t + trot; };
-
-  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.w_bytes, 0x00020000);
-  constexpr int PD = HW_PD;   // weight prefetch distance in stages
-  v4i wb[PD + 1][4];
-  // The per-stage offsets below are derived from values passed through an empty asm at each use: otherwise hipcc
-  // hoists every stage's 8 fragment addresses and 4 weight offsets out of the chunk loop (> 100 live VGPRs, spills).
-  auto load_w = [&](v4i* dst, int c, int hf, int t) __attribute__((always_inline)) {
-    const int koff = (tap_of(t) * a.Kc + c * 64 + hf * 32) * 2;
-#if defined(HW_ABL) && HW_ABL == 3
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { unsigned o = wo[i] + koff; asm volatile("" : "+v"(o)); dst[i] = v4i{(int)o, 1, 2, 3}; }
-#else
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      unsigned o = wo[i];
-      asm volatile("" : "+v"(o));
-      dst[i] = (v4i)__builtin_amdgcn_raw_buffer_load_b128(rw, o, koff, 0);
-    }
-#endif
-  };
-  // one LDS-DMA piece of region hf for chunk cc (cc >= nch: zeros into a region nobody reads any more)
-  auto halo_piece = [&](int p, int cc, int hf) __attribute__((always_inline)) {
-    const int cb = cc * 64 + hf * 32;
-    const bool first = cb < a.C1;
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        first ? (void*)a.x1 : (void*)a.x2, (short)0, first ? a.x1_bytes : a.x2_bytes, 0x00020000);
-    const int ld = first ? a.ld1 : a.ld2;
-    int spp = sp[p];
-    asm volatile("" : "+v"(spp));
-    const unsigned off = (spp >= 0 && cc < nch)
-                             ? ((unsigned)spp * (unsigned)ld + (unsigned)((first ? cb : cb - a.C1) + lc * 8)) * 2u
-                             : kOOB;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(lds + hf * RB + (wave * HP + p) * 1024), 16, off, 0, 0, 0);
-  };
-  v4f st[4];
-  auto pro_load = [&](int cc, int hf) __attribute__((always_inline)) {
-    if constexpr (PRO) {
-      const int ch = (cc < nch ? cc : 0) * 64 + hf * 32 + lc * 8;
-      const float* sc = a.psc + (size_t)n_first * a.ldp + ch;
-      const float* sh = a.psh + (size_t)n_first * a.ldp + ch;
-      st[0] = *(const v4f*)sc; st[1] = *(const v4f*)(sc + 4);
-      st[2] = *(const v4f*)sh; st[3] = *(const v4f*)(sh + 4);
-    }
-  };
-  // inference prologue on the landed region: SiLU(x * scale + shift), the op sequence of gn_apply_kernel
-  auto pro_apply = [&](int hf) __attribute__((always_inline)) {
-    if constexpr (PRO) {
-      const float ss[8] = {st[0][0], st[0][1], st[0][2], st[0][3], st[1][0], st[1][1], st[1][2], st[1][3]};
-      const float tt[8] = {st[2][0], st[2][1], st[2][2], st[2][3], st[3][0], st[3][1], st[3][2], st[3][3]};
-#pragma unroll
-      for (int p = 0; p < HP; ++p) {
-        if (sp[p] < 0) continue;
-        char* q = lds + hf * RB + (wave * HP + p) * 1024 + lane * 16;
-        float f[8];
-        Chunk<bf16_t>::unpack(lds_read_b128_sync(q), f);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] = silu_f(fmaf(f[e], ss[e], tt[e]));
-        lds_write_b128(q, Chunk<bf16_t>::pack(f));
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-  };
-
-  // 128 accumulators per lane: the MFMAs are issued through inline asm with the accumulator tied to the
-  // destination (hipcc's own allocation of the builtin's results renamed them every stage and spilled); the first
-  // stage writes them from a zero srcC, and the epilogue waits out the MFMA->VALU hazard itself
-  v4f acc[4][8];
-
-  // prologue: region 0 of chunk 0, the first two stages' weights
-  pro_load(0, 0);
-#pragma unroll
-  for (int p = 0; p < HP; ++p) halo_piece(p, 0, 0);
-#pragma unroll
-  for (int q = 0; q < PD; ++q) load_w(wb[q], 0, 0, q);
-
-  // VMEM instructions issued after stage r's weights by the time stage r waits for them (stage r-2's pieces and
-  // scale/shift loads, stage r-1's weights + pieces + loads, stage r's weights + loads)
-  auto npc = [](int r) { r = (r + 18) % 18; return (r < HP || (r >= 9 && r < 9 + HP)) ? 1 : 0; };
-  auto npr = [](int r) { r = (r + 18) % 18; return (PRO && (r == 5 || r == 14)) ? 4 : 0; };
-
-  for (int c = 0; c < nch; ++c) {
-    auto stage = [&](auto RR) __attribute__((always_inline)) {
-      constexpr int r = decltype(RR)::value;
-      constexpr int hf = r / 9, t = r % 9;
-      {   // weights of stage s+PD (past the last chunk: loads nobody uses)
-        constexpr int r2 = (r + PD) % 18;
-        load_w(wb[(r + PD) % (PD + 1)], c + (r + PD) / 18, r2 / 9, r2 % 9);
-      }
-      __builtin_amdgcn_sched_barrier(0);   // keep each stage's loads and reads inside the stage (register pressure)
-      if constexpr (r == 14) pro_load(c + 1, 0);
-      if constexpr (r == 5) pro_load(c, 1);
-      {
-        constexpr int n = PD == 2 ? 8 + npc(r - 2) + npc(r - 1) + npr(r - 2) + npr(r - 1) + npr(r)
-                                  : 4 + npc(r - 1) + npr(r - 1) + npr(r);
-        __builtin_amdgcn_s_waitcnt(waitcnt_vm(n));
-      }
-      if constexpr (t == 0) {
-        // region hf of chunk c has landed (this wave's pieces: the wait above); the other waves' pieces and
-        // every wave being done with the other region's previous contents: the barrier
-        pro_apply(hf);
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("" ::: "memory");
-      }
-      if constexpr (r < HP) halo_piece(r, c, 1);               // region 1 of this chunk
-      if constexpr (r >= 9 && r < 9 + HP) halo_piece(r - 9, c + 1, 0);   // region 0 of the next chunk
-      const int tr = tap_of(t), ty = tr / 3, tx = tr - ty * 3;
-      const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
-      const char* reg = lds + hf * RB;
-      const v4i* w = wb[r % (PD + 1)];
-      int lpd = lp;
-      asm volatile("" : "+v"(lpd));
-      lpd += delta;
-      const bool first = (r == 0) && c == 0;
-      // all 8 pixel fragments are read before the first MFMA (counted lgkmcnt waits follow); left to itself hipcc
-      // interleaves each read with its 4 MFMAs and waits lgkmcnt(0) on every one
-      v4i bf[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int h = hu[j] + lpd;
-        bf[j] = *(const v4i*)(reg + h * 64 + ((fh ^ hw_swz(h)) << 4));
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const v4i b = bf[j];
-#if defined(HW_ABL) && HW_ABL == 1
-        if (first) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[i][j] = v4f{(float)b[0], (float)w[i][0], 0.f, 0.f};
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[i][j][0] += (float)(b[1] ^ w[i][1]);
-        }
-#else
-        if (first) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) mfma_bf16_init(acc[i][j], w[i], b);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) mfma_bf16_tied(acc[i][j], w[i], b);
-        }
-#endif
-      }
-    };
-    unroll_seq(stage, std::make_integer_sequence<int, 18>{});
-  }
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // last MFMA write -> VALU / DS read of acc
-  // every DMA landed (the last chunk's trailing zero pieces included) before the tile reuses the LDS
-  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-  __syncthreads();
-  // Two rounds, each parking the same share of every wave's accumulators (fragments j = 4q..4q+3: pixels 64q..64q+63
-  // of both 128-pixel halves), so that a round's epilogue never runs beside 128 live accumulators; each round is two
-  // 64-pixel sub-tiles through the shared epilogue (GroupNorm partial scratch past the 128 staged rows).
-  // (the accumulators are only ever indexed with compile-time indices -- park<Q> -- and the epilogue itself is one
-  // runtime loop, so hipcc keeps acc in registers: a runtime index anywhere moves the whole array to scratch)
-  char* const scratch = lds + HALF * EP;
-  auto park = [&](auto QQ) __attribute__((always_inline)) {
-    constexpr int q = decltype(QQ)::value;
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        *(v4f*)(lds + (wm * 64 + jj * 16 + fr) * EP + (wn * 64 + i * 16 + fh * 4) * 4) = acc[i][q * 4 + jj];
-  };
-  park(std::integral_constant<int, 0>{});
-#pragma nounroll
-  for (int e = 0; e < 4; ++e) {          // round e / 2, sub-tile e % 2
-    __syncthreads();
-    if (e == 2) {
-      park(std::integral_constant<int, 1>{});
-      __syncthreads();
-    }
-#if !(defined(HW_ABL) && HW_ABL == 2)
-    tile_epilogue<T, 64, BN, NW * 64>(a, lds + (e & 1) * 64 * EP, EP, m0 + (e & 1) * HALF + (e >> 1) * 64, n0, scratch);
-#endif
-  }
-}
-
-// Geometry of the register-weight kernel (256-pixel tiles): halo pieces per wave per region (<= 7), 0 if it does
-// not apply. Used where it gives >= 2 blocks per CU (the 32x32 and 64x64 levels at B = 128).
-int hw_plan(const ConvK& k, int* R, int* nimg) {
-  if (k.mode != DMC_MODE_NORMAL || k.stride != 1 || k.ntaps != 9 || k.tkw != 3) return 0;
-  if (!((k.tdy0 == -1 && k.tsy == 1) || (k.tdy0 == 1 && k.tsy == -1))) return 0;
-  if (!((k.tdx0 == -1 && k.tsx == 1) || (k.tdx0 == 1 && k.tsx == -1))) return 0;
-  if (k.OH != k.H || k.OW != k.W || k.C1 % 32 || k.C2 % 32) return 0;
-  const int ohw = k.OH * k.OW;
-  if (ohw % 256 == 0 && 256 % k.OW == 0) { *nimg = 1; *R = 256 / k.OW; }
-  else if (256 % ohw == 0 && k.N % (256 / ohw) == 0) { *nimg = 256 / ohw; *R = k.OH; }
-  else return 0;
-  if ((long)(k.M / 256) * dmc::cdiv(k.Cout, 128) < dmc::opt(dmc::OPT_HW_MINBLK)) return 0;
-  const int npix = *nimg * (*R + 2) * (k.OW + 2);
-  return npix <= 6 * 64 ? 6 : npix <= 7 * 64 ? 7 : 0;
 }
 
 // Geometry of the halo kernel for this conv, or false if it does not apply.
@@ -2480,8 +2185,7 @@ int halo2_pro_plan(const ConvK& k, int* R, int* nimg) {
 }
 
 template <bool PRO>
-void launch_halo2(ConvK k, int hp, int R, int nimg, hipStream_t s) {
-  k.trot = (int)dmc::opt(dmc::OPT_HALO_ROT);
+void launch_halo2(const ConvK& k, int hp, int R, int nimg, hipStream_t s) {
   const dim3 g = dmc::opt(dmc::OPT_NO_XCD) ? dim3(k.M / 128, dmc::cdiv(k.Cout, 128))
                                           : dim3(k.M / 128 * dmc::cdiv(k.Cout, 128));
   if (dmc::opt(dmc::OPT_HALO_NOSCHED)) {   // A/B: the compiler's own fragment-read schedule
@@ -2493,20 +2197,6 @@ void launch_halo2(ConvK k, int hp, int R, int nimg, hipStream_t s) {
   if (hp == 6) conv3x3_halo2_kernel<6, 3, PRO><<<g, 256, 0, s>>>(k, R, nimg);
   else if (hp == 7) conv3x3_halo2_kernel<7, 3, PRO><<<g, 256, 0, s>>>(k, R, nimg);
   else conv3x3_halo2_kernel<9, 2, PRO><<<g, 256, 0, s>>>(k, R, nimg);
-}
-
-template <bool PRO>
-void launch_hw(ConvK k, int hp, int R, int nimg, hipStream_t s) {
-  k.trot = (int)dmc::opt(dmc::OPT_HALO_ROT);
-  const dim3 g(k.M / 256 * dmc::cdiv(k.Cout, 128));
-  if (hp == 6) conv3x3_hw_kernel<6, PRO><<<g, 256, 0, s>>>(k, R, nimg);
-  else conv3x3_hw_kernel<7, PRO><<<g, 256, 0, s>>>(k, R, nimg);
-}
-
-// the register-weight kernel where it applies and DMC_HALO_VER selects it
-int hw_pick(const ConvK& k, int* R, int* nimg) {
-  if (dmc::opt(dmc::OPT_HALO_VER) != 4) return 0;
-  return hw_plan(k, R, nimg);
 }
 
 template <bool BUF>
@@ -2651,13 +2341,7 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
   if (sizeof(T) == 2 && k.prologue == DMC_PRO_AFFINE_SILU) {
     int R, nimg;
     const int hp2 = halo2_pro_plan(k, &R, &nimg);
-    if (hp2) {
-      int R4, nimg4;
-      const int hp4 = hw_pick(k, &R4, &nimg4);
-      if (hp4 && nimg4 == 1) launch_hw<true>(k, hp4, R4, nimg4, s);
-      else launch_halo2<true>(k, hp2, R, nimg, s);
-      return dmc::check_launch("dmc_conv2d");
-    }
+    if (hp2) { launch_halo2<true>(k, hp2, R, nimg, s); return dmc::check_launch("dmc_conv2d"); }
   }
   if (sizeof(T) == 2 && k.prologue == DMC_PRO_NONE && !dmc::opt(dmc::OPT_NO_GLDS)) {
     // bf16, plain operands: LDS-DMA pipelined kernel
@@ -2668,10 +2352,7 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
                      (k.C2 == 0 || k.x2_bytes > 0) && k.w_bytes > 0 && !dmc::opt(dmc::OPT_NO_BUFLDS);
     int R2, nimg2;
     const int hp2 = (buf && p.splits == 1 && !dmc::opt(dmc::OPT_NO_HALO)) ? halo2_plan(k, &R2, &nimg2) : 0;
-    int R4 = 0, nimg4 = 0;
-    const int hp4 = hp2 ? hw_pick(k, &R4, &nimg4) : 0;
-    if (hp4) launch_hw<false>(k, hp4, R4, nimg4, s);
-    else if (hp2) launch_halo2<false>(k, hp2, R2, nimg2, s);
+    if (hp2) launch_halo2<false>(k, hp2, R2, nimg2, s);
     else if (buf) launch_glds<true>(k, p, s);
     else launch_glds<false>(k, p, s);
     return dmc::check_launch("dmc_conv2d");

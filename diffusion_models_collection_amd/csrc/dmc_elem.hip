@@ -42,8 +42,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"DMC_WG_1X1", 1}, {"DMC_GN_BWD_SLICES", 2},
     {"DMC_WG_TAPS", 0}, {"DMC_NO_SKGN", 0},
     {"DMC_WG_HALO_TARGET", 256},
-    {"DMC_STAMP_PTR", 0}, {"DMC_HALO_ROT", 0}, {"DMC_HALO_VER", 2},
-    {"DMC_HW_MINBLK", 480},
+    {"DMC_STAMP_PTR", 0},
 };
 struct OptTable {
   long v[OPT_COUNT];

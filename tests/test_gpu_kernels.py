@@ -123,14 +123,12 @@ def test_upsample2x_nhwc_bitwise(dt):
     assert torch.equal(y.permute(0, 3, 1, 2).float(), ref)
 
 
-@pytest.mark.parametrize("variant", ["halo2", "hw"])
 @pytest.mark.parametrize("case", ["c32_two_sources", "c16_wide", "c32_384", "c8_multi_image"])
-def test_conv3x3_halo_gn_silu_prologue(case, variant, monkeypatch, dmc_opt):
-    """Inference prologue on the halo kernels: conv(SiLU(x*scale+shift)) with the GroupNorm affine + SiLU
+def test_conv3x3_halo_gn_silu_prologue(case, monkeypatch, dmc_opt):
+    """Inference prologue on the halo kernel: conv(SiLU(x*scale+shift)) with the GroupNorm affine + SiLU
     applied to the LDS-resident halo equals, BITWISE, dmc_gn_apply materialisation followed by the plain halo
     conv (same op sequence and bf16 rounding), and the fp32 torch reference within bf16 tolerance."""
     L, K = _lib()
-    _halo_variant(dmc_opt, variant)
     dmc_opt("DMC_NO_SPLITK", 1)   # small N: keep the planner on the halo kernel
     dmc_opt("DMC_HALO_PRO", 1)    # the halo prologue path (default on)
     dt = torch.bfloat16
@@ -229,26 +227,16 @@ def test_conv_dgrad_wgrad(dt, case):
     assert rel_err(db.cpu(), g.sum((0, 2, 3))) < 1e-5
 
 
-def _halo_variant(dmc_opt, variant):
-    """halo2 / halo2_nosched: conv3x3_halo2_kernel (scheduled fragment reads, or the compiler's own schedule);
-    hw / hw_rot: conv3x3_hw_kernel (weights in registers, 256-pixel tiles; block-rotated tap order), taken at any
-    grid size here (DMC_HW_MINBLK=0; the planner keeps it to >= 480 blocks)."""
-    dmc_opt("DMC_HALO_NOSCHED", 1 if variant == "halo2_nosched" else 0)
-    dmc_opt("DMC_HALO_VER", 4 if variant.startswith("hw") else 2)
-    dmc_opt("DMC_HW_MINBLK", 0)
-    dmc_opt("DMC_HALO_ROT", 1 if variant.endswith("_rot") else 0)
-
-
-@pytest.mark.parametrize("variant", ["halo2", "halo2_nosched", "hw", "hw_rot"])
+@pytest.mark.parametrize("variant", ["halo2", "halo2_nosched"])
 @pytest.mark.parametrize("case", ["fwd32_concat", "fwd16_ragged_cout", "dgrad32", "fwd8_multi_image", "fallback_4x4",
                                   "fwd8_concat_b128", "fwd64_rows"])
 def test_conv3x3_halo_kernel(case, variant, monkeypatch, dmc_opt):
-    """bf16 3x3 stride-1 convs on the LDS-halo kernels (conv3x3_halo2_kernel: 128-pixel tiles of whole rows or
-    whole images, two blocks per CU; conv3x3_hw_kernel: 256-pixel tiles, weights in registers) vs an fp32 reference
-    and vs the per-tap kernel (DMC_NO_HALO) on the same inputs; the weight-gradient twin (wgrad3x3_halo2_kernel)
-    likewise."""
+    """bf16 3x3 stride-1 convs on the LDS-halo kernel (conv3x3_halo2_kernel: 128-pixel tiles of whole rows or
+    whole images, two blocks per CU) vs an fp32 reference and vs the per-tap kernel (DMC_NO_HALO) on the same
+    inputs; its weight-gradient twin (wgrad3x3_halo2_kernel) likewise. Variants: the scheduled fragment reads
+    (default) and the compiler's own schedule (DMC_HALO_NOSCHED)."""
     L, K = _lib()
-    _halo_variant(dmc_opt, variant)
+    dmc_opt("DMC_HALO_NOSCHED", 1 if variant == "halo2_nosched" else 0)
     # at these small M the planner would split K over the LDS-DMA kernel instead; the halo kernel is what the
     # B=128 model runs, so keep split-K off here to exercise it
     dmc_opt("DMC_NO_SPLITK", 1)
@@ -686,7 +674,7 @@ def test_conv_fp32_gemm_splitk_silu_pre(Cin, Cout):
     assert rel_err(y.view(N, Cout).cpu(), ref) < 1e-5
 
 
-@pytest.mark.parametrize("case", ["halo2_3x3", "hw_3x3", "glds1x1", "splitk_small", "fp32_reg", "concat_two"])
+@pytest.mark.parametrize("case", ["halo2_3x3", "glds1x1", "splitk_small", "fp32_reg", "concat_two"])
 def test_conv_epilogue_groupnorm_partials(case, dmc_opt):
     """dmc_conv_desc.gn_part + dmc_gn_finalize (the conv epilogue's GroupNorm partials: in-kernel on the halo and
     LDS-DMA paths, one pass over the output elsewhere) give the statistics dmc_gn_stats computes over the stored
@@ -694,10 +682,9 @@ def test_conv_epilogue_groupnorm_partials(case, dmc_opt):
     from diffusion_models_collection_amd import _lib as L, kernels as K
     gen = torch.Generator().manual_seed(11)
     dt = torch.float32 if case == "fp32_reg" else torch.bfloat16
-    _halo_variant(dmc_opt, "hw" if case.startswith("hw") else "halo2")
     # (the halo cases need >= 240 256x128 tiles: fewer take the split-K path, whose partials come from one pass)
     N, H, W, Cin, Cout, taps = {"glds1x1": (8, 16, 16, 256, 256, K.TAPS1),
-                                "halo2_3x3": (32, 32, 32, 128, 256, K.TAPS3), "hw_3x3": (32, 32, 32, 128, 256, K.TAPS3),
+                                "halo2_3x3": (32, 32, 32, 128, 256, K.TAPS3),
                                 "splitk_small": (2, 8, 8, 256, 256, K.TAPS3), "fp32_reg": (2, 16, 16, 64, 128, K.TAPS3),
                                 "concat_two": (4, 16, 16, 128, 128, K.TAPS3)}[case]
     G = 8
@@ -724,7 +711,7 @@ def test_conv_epilogue_groupnorm_partials(case, dmc_opt):
         dmc_opt("DMC_NO_SKGN", 0)
         torch.cuda.synchronize()
         assert torch.equal(y1, y1s) and torch.equal(p1, p1s)
-    if case in ("halo2_3x3", "hw_3x3"):
+    if case == "halo2_3x3":
         d = K.make_desc(dt, N, H, W, Cin, 0, Cin, 0, L.kc_for(Cin, dt), H, W, Cout, taps)
         K.set_epilogue(d, ldy1=Cout)
         assert K.conv_fused(d) & L.FUSED_GN_STATS, case
@@ -741,7 +728,7 @@ def test_conv_epilogue_groupnorm_partials(case, dmc_opt):
         assert rel_err(got, ref) < 2e-5, (case, rel_err(got, ref))
 
 
-@pytest.mark.parametrize("case", ["halo2_3x3", "hw_3x3", "glds1x1_2b", "glds1x1_8wave", "splitk_small", "concat_two",
+@pytest.mark.parametrize("case", ["halo2_3x3", "glds1x1_2b", "glds1x1_8wave", "splitk_small", "concat_two",
                                   "cfg2_small"])
 @pytest.mark.parametrize("silu,dropout", [(True, False), (True, True), (False, False)])
 def test_conv_epilogue_groupnorm_backward_partials(case, silu, dropout, dmc_opt):
@@ -753,10 +740,8 @@ def test_conv_epilogue_groupnorm_backward_partials(case, silu, dropout, dmc_opt)
     import numpy as np
     from diffusion_models_collection_amd import _lib as L, kernels as K
     dmc_opt("DMC_GLDS_2B", 0 if case == "glds1x1_8wave" else 1)
-    _halo_variant(dmc_opt, "hw" if case.startswith("hw") else "halo2")
     N, H, W, Cin, C1, C2, taps = {
-        "halo2_3x3": (32, 32, 32, 128, 256, 0, K.TAPS3), "hw_3x3": (32, 32, 32, 128, 256, 0, K.TAPS3),
-        "glds1x1_2b": (128, 16, 16, 256, 256, 0, K.TAPS1),
+        "halo2_3x3": (32, 32, 32, 128, 256, 0, K.TAPS3), "glds1x1_2b": (128, 16, 16, 256, 256, 0, K.TAPS1),
         "glds1x1_8wave": (128, 16, 16, 256, 256, 0, K.TAPS1),
         "splitk_small": (2, 8, 8, 256, 256, 0, K.TAPS3), "concat_two": (64, 16, 16, 128, 128, 128, K.TAPS3),
         "cfg2_small": (2, 16, 16, 128, 128, 0, K.TAPS1)}[case]
@@ -780,7 +765,7 @@ def test_conv_epilogue_groupnorm_backward_partials(case, silu, dropout, dmc_opt)
     g = torch.empty(N, H, W, C, dtype=dt, device=DEV)
     d = K.make_desc(dt, N, H, W, Cin, 0, Cin, 0, Kc, H, W, C, taps)
     K.set_epilogue(d, ldy1=C, gnb=gnb)
-    fused = case in ("halo2_3x3", "hw_3x3", "glds1x1_2b", "concat_two", "cfg2_small")
+    fused = case in ("halo2_3x3", "glds1x1_2b", "concat_two", "cfg2_small")
     assert bool(K.conv_fused(d) & L.FUSED_GN_BWD) == fused, case
     K.conv(d, dy, None, wp, g)
     g_ref = torch.empty_like(g)
