@@ -335,28 +335,26 @@ def data_line(trainer, dev, B, steps):
                                        "(one reference DataLoader worker's transform work; the reference runs 4)"}}
 
 
-def rccl_one_rank_line(mp, dtype, dev, pool, steps, base_ms):
+def rccl_one_rank_line(args, base_ms):
     """The data-parallel step (GradSync + the segmented HIP-graph step: graphs cut at the gradient all-reduce
-    points, RCCL all-reduce(AVG) of each 25 MB bucket issued between the replays) on a world_size-1 'nccl' (RCCL)
+    points, RCCL all-reduce of each 25 MB bucket issued between the replays) on a world_size-1 'nccl' (RCCL)
     process group, timed like the headline beside it: what the distributed plumbing costs per step on one GPU
-    (segment launches + collective calls + the stream waits), with no inter-GPU traffic."""
-    import socket
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
-    try:
-        model, tr = make_trainer(mp, dtype, dev, 0, 1)
-        tr.enable_grad_sync()
-        model.train()
-        el, _ = train_rate(tr, pool, steps, 5, 1)
-        segs = len(tr._graph.segs) if tr._graph is not None and tr._graph.segs else 0
-    finally:
-        dist.destroy_process_group()
-    ms = el / steps * 1e3
-    return {"train_img_s": round(pool[0].shape[0] * steps / el, 2), "ms_per_step": round(ms, 3),
-            "overhead_ms_per_step": round(ms - base_ms, 3), "graph_segments": segs, "steps": steps,
-            "note": "world_size-1 RCCL group: GradSync buckets + segmented graph replay vs the single-graph headline"}
+    (segment launches + collective calls + the stream waits), with no inter-GPU traffic. Run as a child process
+    (`bench.py --dist-one-rank`): a failure inside RCCL or its watchdog thread aborts that process, never the
+    headline run."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--dist-one-rank", "--no-sample", "--no-extra", "--no-dit",
+           "--no-cpu", "--no-roofline", "--steps", str(args.steps), "--warmup", str(args.warmup), "--dtype", args.dtype]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    if r.returncode != 0:
+        return {"error": f"exit {r.returncode}: " + (r.stderr or "")[-400:]}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    ms = d["ms_per_step"]
+    return {"train_img_s": d["value"], "ms_per_step": ms, "overhead_ms_per_step": round(ms - base_ms, 3),
+            "graph_segments": d.get("graph_segments"), "steps": args.steps,
+            "note": "world_size-1 RCCL group (child process): GradSync buckets + segmented graph replay vs the "
+                    "single-graph headline"}
 
 
 DIT_S2 = dict(img_size=(32, 32), patch_size=2, in_channels=3, hidden_size=384, depth=12, num_heads=6, mlp_ratio=4.0)
@@ -502,10 +500,12 @@ def main():
            "train_tflops_per_gpu": round(value / world * gflop / 1e3, 2)}
     if args.no_train:
         out["value"] = None
+    if trainer.grad_sync is not None and trainer._graph is not None and trainer._graph.segs:
+        out["graph_segments"] = len(trainer._graph.segs)
     if args.extra and S == 32 and not args.no_train and world == 1:
         out["data_loader"] = data_line(trainer, dev, B, args.steps)
         try:
-            out["dp1_rccl"] = rccl_one_rank_line(mp, args.dtype, dev, pool, args.steps, ms)
+            out["dp1_rccl"] = rccl_one_rank_line(args, ms)
         except Exception as e:  # noqa: BLE001 -- a side line must never hide the headline
             out["dp1_rccl"] = {"error": repr(e)}
 

@@ -1290,7 +1290,27 @@ __global__ __launch_bounds__(256) void conv_narrow_out_kernel(ConvK a) {
 }
 
 // split-K reduction + the regular epilogue: out(pix, co..co+3) = epilogue(sum_z slab[z][pix][co..])
-template <typename T>
+// Sum of a split-K slab column: SP > 0 = the split count at compile time, every slab load issued before the first add
+// (a runtime-bounded loop left each load behind the previous add: SP dependent L2 round trips per element);
+// SP == 0: any count. The splits are added in ascending order either way (bitwise the same sums).
+template <int SP>
+DMC_DEV v4f splitk_sum(const float* p, size_t zs, int splits) {
+  if constexpr (SP > 0) {
+    v4f v[SP];
+#pragma unroll
+    for (int z = 0; z < SP; ++z) v[z] = *(const v4f*)(p + z * zs);
+    v4f t = v[0];
+#pragma unroll
+    for (int z = 1; z < SP; ++z) t += v[z];
+    return t;
+  } else {
+    v4f t = *(const v4f*)p;
+    for (int z = 1; z < splits; ++z) t += *(const v4f*)(p + z * zs);
+    return t;
+  }
+}
+
+template <typename T, int SP>
 __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvK a, int splits, int Cpad) {
   const int cg_per_row = Cpad / 4;
   const long total = (long)a.M * cg_per_row;
@@ -1299,18 +1319,11 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvK a, int 
     const int pix = idx / cg_per_row;
     const int co = (idx - (long)pix * cg_per_row) * 4;
     if (co >= a.Cout) continue;
-    const float* p = a.sk + (size_t)pix * Cpad + co;
-    v4f v = *(const v4f*)p;
-    for (int z = 1; z < splits; ++z) v += *(const v4f*)(p + z * zs);
+    const v4f v = splitk_sum<SP>(a.sk + (size_t)pix * Cpad + co, zs, splits);
     conv_store_tile<T>(a, v, pix, co);
   }
 }
-
-// ... and the GroupNorm partials of the stored output in the same pass (the input of the next GroupNorm, as
-// tile_epilogue8 emits them for the unsplit kernels): one wave per (64-pixel segment, 8-channel chunk), lane =
-// pixel; the statistics are those gn_part_kernel computes from the stored values (bitwise: same reads, same
-// reduction). Needs M % 64 == 0, Cout % 8 == 0 and one NHWC output (the planner checks).
-template <typename T>
+template <typename T, int SP>
 __global__ __launch_bounds__(256) void conv_splitk_epi_gn_kernel(ConvK a, int splits, int Cpad) {
   const int lane = threadIdx.x & 63;
   const int nch = a.Cout / 8;
@@ -1320,8 +1333,7 @@ __global__ __launch_bounds__(256) void conv_splitk_epi_gn_kernel(ConvK a, int sp
   const int pix = seg * 64 + lane, co = ch * 8;
   const size_t zs = (size_t)a.M * Cpad;
   const float* p = a.sk + (size_t)pix * Cpad + co;
-  v4f v0 = *(const v4f*)p, v1 = *(const v4f*)(p + 4);
-  for (int z = 1; z < splits; ++z) { v0 += *(const v4f*)(p + z * zs); v1 += *(const v4f*)(p + 4 + z * zs); }
+  const v4f v0 = splitk_sum<SP>(p, zs, splits), v1 = splitk_sum<SP>(p + 4, zs, splits);
   conv_store_tile<T>(a, v0, pix, co);
   conv_store_tile<T>(a, v1, pix, co + 4);
   // read back what this lane stored (its own writes) and reduce exactly as gn_part_kernel
@@ -1338,6 +1350,34 @@ __global__ __launch_bounds__(256) void conv_splitk_epi_gn_kernel(ConvK a, int sp
   for (int e = 0; e < 8; ++e) q = fmaf(f[e] - m, f[e] - m, q);
   q = wave_sum(q);
   if (lane == 0) { a.gsk[w * 2] = m; a.gsk[w * 2 + 1] = q; }
+}
+
+// launch helpers: the split count as a template argument where the planners produce it (2..8; else generic)
+template <typename T>
+void launch_splitk_epilogue(const ConvK& k, int splits, int Cpad, int blocks, hipStream_t s) {
+  switch (splits) {
+    case 2: conv_splitk_epilogue_kernel<T, 2><<<blocks, 256, 0, s>>>(k, splits, Cpad); break;
+    case 3: conv_splitk_epilogue_kernel<T, 3><<<blocks, 256, 0, s>>>(k, splits, Cpad); break;
+    case 4: conv_splitk_epilogue_kernel<T, 4><<<blocks, 256, 0, s>>>(k, splits, Cpad); break;
+    case 5: conv_splitk_epilogue_kernel<T, 5><<<blocks, 256, 0, s>>>(k, splits, Cpad); break;
+    case 6: conv_splitk_epilogue_kernel<T, 6><<<blocks, 256, 0, s>>>(k, splits, Cpad); break;
+    case 7: conv_splitk_epilogue_kernel<T, 7><<<blocks, 256, 0, s>>>(k, splits, Cpad); break;
+    case 8: conv_splitk_epilogue_kernel<T, 8><<<blocks, 256, 0, s>>>(k, splits, Cpad); break;
+    default: conv_splitk_epilogue_kernel<T, 0><<<blocks, 256, 0, s>>>(k, splits, Cpad); break;
+  }
+}
+void launch_splitk_epi_gn(const ConvK& k, int splits, int Cpad, hipStream_t s) {
+  const int blocks = (int)(((long)(k.M / 64) * (k.Cout / 8) + 3) / 4);
+  switch (splits) {
+    case 2: conv_splitk_epi_gn_kernel<bf16_t, 2><<<blocks, 256, 0, s>>>(k, splits, Cpad); break;
+    case 3: conv_splitk_epi_gn_kernel<bf16_t, 3><<<blocks, 256, 0, s>>>(k, splits, Cpad); break;
+    case 4: conv_splitk_epi_gn_kernel<bf16_t, 4><<<blocks, 256, 0, s>>>(k, splits, Cpad); break;
+    case 5: conv_splitk_epi_gn_kernel<bf16_t, 5><<<blocks, 256, 0, s>>>(k, splits, Cpad); break;
+    case 6: conv_splitk_epi_gn_kernel<bf16_t, 6><<<blocks, 256, 0, s>>>(k, splits, Cpad); break;
+    case 7: conv_splitk_epi_gn_kernel<bf16_t, 7><<<blocks, 256, 0, s>>>(k, splits, Cpad); break;
+    case 8: conv_splitk_epi_gn_kernel<bf16_t, 8><<<blocks, 256, 0, s>>>(k, splits, Cpad); break;
+    default: conv_splitk_epi_gn_kernel<bf16_t, 0><<<blocks, 256, 0, s>>>(k, splits, Cpad); break;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1860,9 +1900,14 @@ __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char*
 // dw[co][c][t] = scale * sum_z slab[z][co][t*Kc + c]; threads walk the slab contiguously (k fastest)
 // ... and with bslab: dbias[co] = scale * sum_z bslab[z][co], one wave per co in the blocks past wblocks (lanes
 // take z = lane, lane + 64, ...; fixed xor tree: deterministic)
-__global__ void wgrad_reduce_kernel(const float* slab, int splits, int KK, int Cpad, int Cout, int Ctot,
-                                    int ntaps, int Kc, float scale, float* dw, const float* bslab, float* dbias,
-                                    int wblocks) {
+// Sum of the per-split fp32 slabs [split][Cpad][KK] into the reference-layout weight gradient dw[co][c][t] (x scale),
+// plus the bias gradient from the per-split bias slab (one wave per channel, blocks past wblocks). A thread owns 4
+// consecutive (co, k) outputs (16-byte slab loads, 16 in flight) and adds the splits in ascending order, one fp32
+// add per split and output: the same sums, bit for bit, as one output per thread (the round-1/2 form), at a quarter
+// of the load instructions and 8x the bytes in flight per thread (the reduce was latency-bound at 1.3-2.7 TB/s).
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slab, int splits, int KK, int Cpad, int Cout,
+                                                           int Ctot, int ntaps, int Kc, float scale, float* dw,
+                                                           const float* bslab, float* dbias, int wblocks) {
   if ((int)blockIdx.x >= wblocks) {
     const int co = ((int)blockIdx.x - wblocks) * (blockDim.x / 64) + (int)(threadIdx.x >> 6);
     if (co >= Cout) return;
@@ -1872,25 +1917,37 @@ __global__ void wgrad_reduce_kernel(const float* slab, int splits, int KK, int C
     if ((threadIdx.x & 63) == 0) dbias[co] = s * scale;
     return;
   }
-  const int total = Cout * KK;   // < 2^31: weights of one conv
-  const size_t zstride = (size_t)Cpad * KK;
-  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += wblocks * blockDim.x) {
+  const int total4 = Cout * KK / 4;   // KK = ntaps * Kc, Kc a multiple of 32: 4 | KK
+  const size_t zs = (size_t)Cpad * KK / 4;
+  const v4f* s4 = (const v4f*)slab;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < total4; q += wblocks * blockDim.x) {
+    const int o = q * 4;
     const int co = o / KK;
     const int k = o - co * KK;
-    const int t = k / Kc, c = k - t * Kc;
+    const int t = k / Kc, c = k - t * Kc;   // 4 | Kc: the 4 outputs share co and t
     if (c >= Ctot) continue;
-    float s = 0.f;
-    // 8 independent loads in flight (fixed order: deterministic)
+    v4f s = {0.f, 0.f, 0.f, 0.f};
     int z = 0;
-    for (; z + 8 <= splits; z += 8) {
-      float v[8];
+    for (; z + 16 <= splits; z += 16) {
+      v4f v[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = slab[(size_t)(z + u) * zstride + o];
+      for (int u = 0; u < 16; ++u) v[u] = s4[(size_t)(z + u) * zs + q];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += v[u];
+    }
+    if (z + 8 <= splits) {
+      v4f v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = s4[(size_t)(z + u) * zs + q];
 #pragma unroll
       for (int u = 0; u < 8; ++u) s += v[u];
+      z += 8;
     }
-    for (; z < splits; ++z) s += slab[(size_t)z * zstride + o];
-    dw[((size_t)co * Ctot + c) * ntaps + t] = s * scale;
+    for (; z < splits; ++z) s += s4[(size_t)z * zs + q];
+    float* d = dw + ((size_t)co * Ctot + c) * ntaps + t;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (c + e < Ctot) d[(size_t)e * ntaps] = s[e] * scale;
   }
 }
 
@@ -2205,14 +2262,13 @@ void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
     conv_fwd_glds_kernel<2, 2, BUF><<<dim3(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128), p.splits), 256, 0, s>>>(k);
     const int Cpad = dmc::cdiv(k.Cout, 128) * 128;
     if (k.gsk && k.M % 64 == 0 && k.Cout % 8 == 0 && !k.out_f32 && !k.out_nchw && k.Csplit == k.Cout) {
-      conv_splitk_epi_gn_kernel<bf16_t><<<(int)(((long)(k.M / 64) * (k.Cout / 8) + 3) / 4), 256, 0, s>>>(k, p.splits,
-                                                                                                       Cpad);
+      launch_splitk_epi_gn(k, p.splits, Cpad, s);
       if (k.gsk_done) *k.gsk_done = 1;
       return;
     }
     const long total = (long)k.M * Cpad / 4;
     const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
-    conv_splitk_epilogue_kernel<bf16_t><<<blocks, 256, 0, s>>>(k, p.splits, Cpad);
+    launch_splitk_epilogue<bf16_t>(k, p.splits, Cpad, blocks, s);
   } else {
     // 1-D grid: the kernel orders its tiles XCD-aware (xcd_tile); DMC_NO_XCD=1 keeps the 2-D grid (A/B)
     const int bm = p.cfg == 0 ? 256 : p.cfg == 1 ? 128 : 64;
@@ -2371,7 +2427,7 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     const int Cpad = dmc::cdiv(k.Cout, 64) * 64;
     const long total = (long)k.M * Cpad / 4;
     const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
-    conv_splitk_epilogue_kernel<T><<<blocks, 256, 0, s>>>(k, rp.splits, Cpad);
+    launch_splitk_epilogue<T>(k, rp.splits, Cpad, blocks, s);
   } else {
     dim3 g(dmc::cdiv(k.M, 64), dmc::cdiv(k.Cout, 64));
     conv_fwd_kernel<T, 64, 64><<<g, 256, 0, s>>>(k);
@@ -2569,7 +2625,7 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
     conv_wgrad_kernel<bf16_t><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (float*)workspace, KK, pps);
   if (dmc::check_launch("dmc_conv2d_wgrad")) return 2;
   const int Ctot = d->C1 + d->C2;
-  const long total = (long)d->Cout * KK;
+  const long total = (long)d->Cout * KK / 4;   // 4 outputs per thread
   const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
   const int bblocks = d->wg_bias ? dmc::cdiv(d->Cout, 4) : 0;   // one wave per bias channel
   wgrad_reduce_kernel<<<blocks + bblocks, 256, 0, s>>>((const float*)workspace, splits, KK, (int)g.y * 128, d->Cout,

@@ -18,7 +18,7 @@ class StepGraph:
     def __init__(self, fn, *inputs):
         self.static = [x.clone() for x in inputs]
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):   # see utils/trainer.py begin()
             self.out = fn(*self.static)
 
     def step(self, *inputs):

@@ -292,7 +292,7 @@ class GraphedTrainStep:
             return
         g = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 loss = tr.diffusion.p_losses(tr.model, self.x_s, self.t_s, self.y_s, noise=self.n_s,
                                              loss_type=tr.loss_type)
                 loss.backward()
@@ -329,7 +329,10 @@ class GraphedTrainStep:
 
         def begin():
             state["g"] = torch.cuda.CUDAGraph()
-            state["g"].capture_begin(pool=pool)
+            # thread-local capture: the process group's watchdog thread polls the earlier all-reduce events
+            # (hipEventQuery) while this thread captures; under the default global mode that query is illegal and
+            # aborts the process (seen on MI355X with a one-rank RCCL group)
+            state["g"].capture_begin(pool=pool, capture_error_mode="thread_local")
 
         def end(bucket):
             state["g"].capture_end()
