@@ -6,7 +6,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["DMC_LIB"] = os.path.join(ROOT, "probe_lib", "libdmc_stamp.so")
+os.environ["DMC_LIB"] = os.path.join(ROOT, "stamp_lib", "libdmc_stamp.so")
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 from diffusion_models_collection_amd import _lib as L, kernels as K  # noqa: E402
