@@ -2182,10 +2182,11 @@ FwdPlan plan_glds(const ConvK& k) {
   // small M: split K over grid.z (>= 4 stages per split) rather than shrinking the tile below 128x128
   long blocks = b22;
   p.cfg = 1;
-  int sp = (int)((240 + blocks - 1) / blocks);
+  const long target = dmc::opt(dmc::OPT_SK_TARGET);   // A/B knobs: blocks to aim for, split cap
+  int sp = (int)((target + blocks - 1) / blocks);
   const int maxs = nst / 4;
   if (sp > maxs) sp = maxs;
-  if (sp > 8) sp = 8;
+  if (sp > dmc::opt(dmc::OPT_SK_MAX)) sp = (int)dmc::opt(dmc::OPT_SK_MAX);
   if (sp >= 2) {
     p.splits = sp;
     p.per = (nst + sp - 1) / sp;
@@ -2259,7 +2260,9 @@ void launch_halo2(const ConvK& k, int hp, int R, int nimg, hipStream_t s) {
 template <bool BUF>
 void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
   if (p.splits > 1) {
-    conv_fwd_glds_kernel<2, 2, BUF><<<dim3(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128), p.splits), 256, 0, s>>>(k);
+    const dim3 gs(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128), p.splits);
+    if (dmc::opt(dmc::OPT_SK_2B)) conv_fwd_glds_kernel<2, 2, BUF, 2><<<gs, 256, 0, s>>>(k);   // two blocks per CU
+    else conv_fwd_glds_kernel<2, 2, BUF><<<gs, 256, 0, s>>>(k);
     const int Cpad = dmc::cdiv(k.Cout, 128) * 128;
     if (k.gsk && k.M % 64 == 0 && k.Cout % 8 == 0 && !k.out_f32 && !k.out_nchw && k.Csplit == k.Cout) {
       launch_splitk_epi_gn(k, p.splits, Cpad, s);
