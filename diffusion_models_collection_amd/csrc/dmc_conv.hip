@@ -2260,9 +2260,7 @@ void launch_halo2(const ConvK& k, int hp, int R, int nimg, hipStream_t s) {
 template <bool BUF>
 void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
   if (p.splits > 1) {
-    const dim3 gs(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128), p.splits);
-    if (dmc::opt(dmc::OPT_SK_2B)) conv_fwd_glds_kernel<2, 2, BUF, 2><<<gs, 256, 0, s>>>(k);   // two blocks per CU
-    else conv_fwd_glds_kernel<2, 2, BUF><<<gs, 256, 0, s>>>(k);
+    conv_fwd_glds_kernel<2, 2, BUF><<<dim3(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128), p.splits), 256, 0, s>>>(k);
     const int Cpad = dmc::cdiv(k.Cout, 128) * 128;
     if (k.gsk && k.M % 64 == 0 && k.Cout % 8 == 0 && !k.out_f32 && !k.out_nchw && k.Csplit == k.Cout) {
       launch_splitk_epi_gn(k, p.splits, Cpad, s);
