@@ -26,6 +26,8 @@ SHAPES = {
     "p1_16": (128, 16, 16, 256, 0, 256, "1"),
     "r256_8": (128, 8, 8, 256, 0, 256, "3"),
     "r256_4": (128, 4, 4, 256, 0, 256, "3"),
+    "nin_32": (128, 32, 32, 3, 0, 128, "3"),         # the UNet's first conv (3 -> 128, narrow-input kernel)
+    "nout_32": (128, 32, 32, 128, 0, 3, "3"),        # the output conv (128 -> 3, narrow-output kernel)
 }
 
 
@@ -35,13 +37,14 @@ def run(name, iters, epi="bias"):
     dev = "cuda"
     taps = K.TAPS3 if kind == "3" else K.TAPS1
     kk = 3 if kind == "3" else 1
-    x1 = torch.randn(B, H, W, C1, device=dev).to(dt)
+    ld1 = C1 if C1 >= 8 else 8    # a narrow source is stored at one 16-byte chunk per pixel
+    x1 = torch.randn(B, H, W, ld1, device=dev).to(dt)
     x2 = torch.randn(B, H, W, C2, device=dev).to(dt) if C2 else None
     w = torch.randn(Cout, C1 + C2, kk, kk, device=dev) * 0.03
     Kc = L.kc_for(C1 + C2, dt)
     wp = K.pack_weight(L.PACK_FWD, dt, w, Kc)
     y = torch.empty(B, H, W, Cout, device=dev, dtype=dt)
-    d = K.make_desc(dt, B, H, W, C1, C2, C1, C2, Kc, H, W, Cout, taps)
+    d = K.make_desc(dt, B, H, W, C1, C2, ld1, C2, Kc, H, W, Cout, taps)
     if epi == "full":   # ResBlock conv2 epilogue: bias + time embedding + residual
         resid = torch.randn(B, H, W, Cout, device=dev).to(dt)
         K.set_epilogue(d, bias=torch.randn(Cout, device=dev), addvec=torch.randn(B, Cout, device=dev), ld_add=Cout,
