@@ -238,6 +238,7 @@ def train_rate(trainer, pool, steps, warmup, world):
     torch.cuda.synchronize()
     g = getattr(trainer, "_graph", None)
     w0 = g.ring_wait_s if g is not None else 0.0
+    r0 = g.replays if g is not None else 0
     t0 = time.perf_counter()
     for i in range(steps):
         trainer.train_step(pool[i % len(pool)], 0)
@@ -247,7 +248,25 @@ def train_rate(trainer, pool, steps, warmup, world):
     # host enqueue = that time minus the waits on the graphed step's pinned-argument ring (which blocks the host
     # until step k-4 has run, i.e. paces the host to the GPU)
     ring = (g.ring_wait_s - w0) if g is not None else 0.0
+    trainer._bench_graphed = g is not None and g.replays - r0 == steps   # every timed step was a graph replay
     return max_over_ranks(el, world), (host_el - ring, ring)
+
+
+def exposed_comm(trainer, pool, steps=5):
+    """Data-parallel runs: after the timed region, `steps` more steps with GraphedTrainStep.measure_comm on (two
+    HIP events on the compute stream around its waits for the RCCL buckets, i.e. after the backward's last
+    bucketed segment): the mean ms per step the backward did not hide, max over ranks (None if not graphed)."""
+    g = getattr(trainer, "_graph", None)
+    if g is None or g.segs is None:
+        return None
+    g.measure_comm = True
+    try:
+        for i in range(steps):
+            trainer.train_step(pool[i % len(pool)], 0)
+        v = g.comm_ms()
+    finally:
+        g.measure_comm = False
+    return v
 
 
 def max_over_ranks(v, world):
@@ -343,8 +362,9 @@ def rccl_one_rank_line(args, base_ms):
     (`bench.py --dist-one-rank`): a failure inside RCCL or its watchdog thread aborts that process, never the
     headline run."""
     import subprocess
-    cmd = [sys.executable, os.path.abspath(__file__), "--dist-one-rank", "--no-sample", "--no-extra", "--no-dit",
-           "--no-cpu", "--no-roofline", "--steps", str(args.steps), "--warmup", str(args.warmup), "--dtype", args.dtype]
+    cmd = [sys.executable, os.path.abspath(__file__), "--dist-one-rank", "--dist-force-avg", "--no-sample", "--no-extra",
+           "--no-dit", "--no-cpu", "--no-roofline", "--steps", str(args.steps), "--warmup", str(args.warmup),
+           "--dtype", args.dtype, "--batch", str(args.batch), "--image-size", str(args.image_size)]
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     if r.returncode != 0:
@@ -352,9 +372,12 @@ def rccl_one_rank_line(args, base_ms):
     d = json.loads(r.stdout.strip().splitlines()[-1])
     ms = d["ms_per_step"]
     return {"train_img_s": d["value"], "ms_per_step": ms, "overhead_ms_per_step": round(ms - base_ms, 3),
-            "graph_segments": d.get("graph_segments"), "steps": args.steps,
-            "note": "world_size-1 RCCL group (child process): GradSync buckets + segmented graph replay vs the "
-                    "single-graph headline"}
+            "graph_segments": d.get("graph_segments"), "steps": args.steps, "batch": d["config"]["per_gpu_batch"],
+            "graphed": d.get("graphed"), "reduce_op": d.get("reduce_op"),
+            "exposed_comm_ms_per_step": d.get("exposed_comm_ms_per_step"),
+            "note": "world_size-1 RCCL group (child process), ReduceOp.AVG forced (the op every multi-rank run takes, "
+                    "with RCCL's averaging kernel): GradSync buckets + segmented graph replay vs the single-graph "
+                    "headline"}
 
 
 DIT_S2 = dict(img_size=(32, 32), patch_size=2, in_channels=3, hidden_size=384, depth=12, num_heads=6, mlp_ratio=4.0)
@@ -430,6 +453,8 @@ def main():
     ap.add_argument("--dit-only", action="store_true", help="only the DiT-S/2 line (profiling)")
     ap.add_argument("--dist-one-rank", action="store_true",
                     help="profiling: the headline step through GradSync + the segmented graph on a 1-rank RCCL group")
+    ap.add_argument("--dist-force-avg", action="store_true",
+                    help="with --dist-one-rank: all-reduce with ReduceOp.AVG (the multi-rank op) instead of SUM")
     args = ap.parse_args()
     if args.dit_only:
         torch.cuda.set_device(0)
@@ -469,7 +494,7 @@ def main():
             sk.bind(("127.0.0.1", 0))
             port = sk.getsockname()[1]
         dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
-        trainer.enable_grad_sync()
+        trainer.enable_grad_sync(force_avg=args.dist_force_avg)
     B = args.batch
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = [torch.rand(B, 3, S, S, device=dev, generator=gen) * 2 - 1 for _ in range(4)]
@@ -498,10 +523,22 @@ def main():
            "host_enqueue_ms_per_step": round(host_el / max(args.steps, 1) * 1e3, 3),
            "host_ring_wait_ms_per_step": round(ring_el / max(args.steps, 1) * 1e3, 3),
            "train_tflops_per_gpu": round(value / world * gflop / 1e3, 2)}
+    graphed = bool(getattr(trainer, "_bench_graphed", False))
+    out["graphed"] = graphed if not args.no_train else None
     if args.no_train:
         out["value"] = None
-    if trainer.grad_sync is not None and trainer._graph is not None and trainer._graph.segs:
-        out["graph_segments"] = len(trainer._graph.segs)
+    elif not graphed and os.environ.get("DMC_GRAPH", "1") != "0":
+        # the headline is the graph-replayed step: a timed step that ran eagerly means the capture was refused
+        raise SystemExit("bench: a timed training step was not a HIP graph replay (graph capture did not happen)")
+    if trainer.grad_sync is not None:
+        out["world_size"] = dist.get_world_size()
+        out["reduce_op"] = str(trainer.grad_sync.op).split(".")[-1]
+        if trainer._graph is not None and trainer._graph.segs:
+            out["graph_segments"] = len(trainer._graph.segs)
+        if not args.no_train:
+            # the part of the gradient all-reduce the backward did not hide (measured after the timed region)
+            v = exposed_comm(trainer, pool)
+            out["exposed_comm_ms_per_step"] = None if v is None else round(max_over_ranks(v, world), 4)
     if args.extra and S == 32 and not args.no_train and world == 1:
         out["data_loader"] = data_line(trainer, dev, B, args.steps)
         try:

@@ -961,20 +961,27 @@ DMC_DEV v4i lds_read_b128_sync(const char* p) {
 DMC_DEV void lds_write_b128(char* p, v4i v) {
   asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
 }
+// All HP pieces are read first and waited for once (one LDS round trip per chunk instead of one per piece).
 template <int HP>
 DMC_DEV void halo_affine_silu(char* buf, int wave, const unsigned* h1, const v4f* st) {
   const int lane = threadIdx.x & 63;
   const float ss[8] = {st[0][0], st[0][1], st[0][2], st[0][3], st[1][0], st[1][1], st[1][2], st[1][3]};
   const float tt[8] = {st[2][0], st[2][1], st[2][2], st[2][3], st[3][0], st[3][1], st[3][2], st[3][3]};
+  v4i v[HP];
+#pragma unroll
+  for (int p = 0; p < HP; ++p) {
+    const char* q = buf + (wave * HP + p) * 1024 + lane * 16;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v[p]) : "v"((unsigned)(uintptr_t)q) : "memory");
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
   for (int p = 0; p < HP; ++p) {
     if (h1[p] == kOOB) continue;
-    char* q = buf + (wave * HP + p) * 1024 + lane * 16;
     float f[8];
-    Chunk<bf16_t>::unpack(lds_read_b128_sync(q), f);
+    Chunk<bf16_t>::unpack(v[p], f);
 #pragma unroll
     for (int e = 0; e < 8; ++e) f[e] = silu_f(fmaf(f[e], ss[e], tt[e]));
-    lds_write_b128(q, Chunk<bf16_t>::pack(f));
+    lds_write_b128(buf + (wave * HP + p) * 1024 + lane * 16, Chunk<bf16_t>::pack(f));
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
@@ -2350,8 +2357,11 @@ __global__ __launch_bounds__(256) void gn_bwd_part_kernel(const char* gy, int ld
   }
 }
 
-// Whether dmc_conv2d's chosen kernel emits the GroupNorm partials in its epilogue (tile_epilogue8: the round-1
-// halo kernel and the non-split LDS-DMA kernel, bf16, one NHWC output, whole 256-pixel tiles, 128-channel tiles).
+// Whether dmc_conv2d's chosen kernel emits the GroupNorm partials in its epilogue (tile_epilogue8: bf16, one NHWC
+// output, 128-channel tiles, 64-pixel partial segments). The kernels that can: conv3x3_halo2_kernel (128-pixel
+// tiles, with or without the halo prologue) and the non-split LDS-DMA kernel (128- or 256-pixel tiles). M % 256 is
+// kept on purpose: it is what the 256-pixel LDS-DMA tile needs, and every UNet shape that reaches here meets it
+// (B * OH * OW with OH * OW >= 64 and B even), so one condition serves both kernels.
 bool epi_stats_ok(const ConvK& k, const void* ws, size_t ws_bytes) {
   if (k.dtype_bytes != 2 || k.out_f32 || k.out_nchw || k.silu_pre || k.Csplit != k.Cout || k.Cout % 128 ||
       k.M % 256 || k.OHW % 64 || ((k.Cout | k.ldy1 | k.ld_res) & 7))

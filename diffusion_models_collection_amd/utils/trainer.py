@@ -40,12 +40,17 @@ class GradSync:
 
     The executor lays gradients out in the order the backward finishes them and calls `hook(flat, hi,
     final)` after each layer with the length `hi` of the finished prefix. Every time >= bucket_bytes of new
-    finished gradients exist, an async all-reduce(AVG) of that slice is issued; RCCL waits on the compute
-    stream for the slice, then runs concurrently with the remaining backward kernels. At the end the compute
-    stream waits for all of them (no host synchronisation).
+    finished gradients exist, an async all-reduce of that slice is issued -- ReduceOp.AVG on RCCL (ncclAvg,
+    the op every multi-rank run takes), SUM then a division on gloo; RCCL waits on the compute stream for the
+    slice, then runs concurrently with the remaining backward kernels. At the end the compute stream waits for
+    all of them (no host synchronisation).
+
+    On a one-rank group the average is the identity and SUM is used (RCCL launches nothing for it, whereas a
+    one-rank AVG runs its premultiplied-average kernel, ~130 us per 25 MB bucket on MI355X); force_avg=True
+    keeps ReduceOp.AVG there too, so a single GPU exercises (and times) exactly the multi-rank code path.
     """
 
-    def __init__(self, executor, process_group=None, bucket_bytes=25 * 1024 * 1024):
+    def __init__(self, executor, process_group=None, bucket_bytes=25 * 1024 * 1024, force_avg=False):
         self.ex = executor
         self.pg = process_group
         self.bucket = bucket_bytes // 4
@@ -54,9 +59,7 @@ class GradSync:
         # RCCL/NCCL averages natively (ncclAvg); gloo (CPU tests) has no AVG: sum, then scale
         self.native_avg = dist.get_backend(process_group) == "nccl"
         self.world = dist.get_world_size(process_group)
-        # one rank: the average is the identity. SUM lets RCCL skip the launch it makes for a one-rank AVG (its
-        # premultiplied-average kernel, ~130 us per bucket on MI355X) -- the gradients stay bitwise unchanged
-        self.op = dist.ReduceOp.AVG if self.native_avg and self.world > 1 else dist.ReduceOp.SUM
+        self.op = dist.ReduceOp.AVG if self.native_avg and (self.world > 1 or force_avg) else dist.ReduceOp.SUM
         self.post_div = not self.native_avg and self.world > 1
         executor.grad_hook = self.hook
 
@@ -230,6 +233,10 @@ class FlatAdamW:
             self.ema.executor.wgen += 1
 
 
+class GraphCaptureError(RuntimeError):
+    """The training step's HIP graph capture failed (GraphedTrainStep.step)."""
+
+
 class GraphedTrainStep:
     """The training step captured once as a HIP graph and replayed (single process, fused optimizer path).
 
@@ -241,7 +248,14 @@ class GraphedTrainStep:
     draws it) and the nine AdamW/EMA scalars go to device memory with one pinned H2D copy per step; the
     captured kernels read them there (drop_seed_base, dmc_adamw_flat_dev). Replays are therefore bitwise
     identical to eager steps (tests/test_gpu_model.py). Captured after WARM eager steps, once per batch
-    shape; a step with another shape, or any capture failure, runs eagerly.
+    shape; a step with another shape runs eagerly. A capture failure raises GraphCaptureError: the failed
+    capture may have left the stream's error state poisoned, so the step is never retried eagerly on it (set
+    DMC_GRAPH=0 to train without graphs).
+
+    `replays` counts graph replays (bench.py records whether every timed step was one). With `measure_comm` set, a
+    data-parallel replay records two events on the compute stream: once the last segment that hands a bucket to
+    RCCL is enqueued, and after the compute stream's waits for every bucket -- their distance is the
+    communication the backward did not hide (comm_ms()).
     """
     WARM = 2
     RING = 4
@@ -249,10 +263,13 @@ class GraphedTrainStep:
     def __init__(self, trainer):
         self.tr = trainer
         self.calls = 0
+        self.replays = 0
         self.ring_wait_s = 0.0       # host seconds spent waiting for a pinned ring slot (paces the host to the GPU)
         self.graph = None
         self.failed = False
         self.key = None
+        self.measure_comm = False
+        self.comm_events = []
 
     @staticmethod
     def supported(trainer):
@@ -381,6 +398,7 @@ class GraphedTrainStep:
         self.flat = ex.flat
 
     def _replay(self):
+        self.replays += 1
         if self.segs is None:
             self.graph.replay()
             return
@@ -388,10 +406,17 @@ class GraphedTrainStep:
         works = []
         for g, bucket in self.segs:
             if bucket is None:
+                if self.measure_comm:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e0.record()       # after the backward's last bucketed segment
                 for seg, w in works:
                     w.wait()          # the compute stream waits for RCCL; no host sync
                     if gs.post_div:
                         seg.div_(gs.world)
+                if self.measure_comm:
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e1.record()
+                    self.comm_events.append((e0, e1))
             g.replay()
             if bucket is not None:
                 seg = self.flat[bucket[0]:bucket[1]]
@@ -410,16 +435,20 @@ class GraphedTrainStep:
         if self.graph is None or key != self.key:
             if self.graph is not None:
                 return None           # one captured shape (the last, ragged batch of an epoch runs eagerly)
+            prev = torch.cuda.current_stream()
             try:
                 self._capture(images, y)
                 self.key = key
-            except Exception:    # noqa: BLE001 -- any capture problem: stay eager
-                import traceback
+            except Exception as e:    # noqa: BLE001
+                # loud: round 3 saw the eager retry of a failed capture fail on the same stream ("operation
+                # failed due to a previous error during capture"). A capture_begin that raises inside
+                # torch.cuda.graph's __enter__ leaves its capture stream current: restore the caller's.
+                torch.cuda.set_stream(prev)
                 self.failed = True
                 self.graph = None
-                if tr.is_main_process:
-                    print("[dmc] training-step graph capture failed, running eagerly:\n" + traceback.format_exc())
-                return None
+                raise GraphCaptureError(
+                    "training-step HIP graph capture failed; the step is not retried eagerly on a possibly "
+                    "poisoned stream (set DMC_GRAPH=0 to train without graphs)") from e
         from ..models._unet_exec import _seed_from_torch
         self.x_s.copy_(images)
         self.t_s.copy_(t)
@@ -445,6 +474,15 @@ class GraphedTrainStep:
         self._replay()
         f.bump(ema_decay)
         return self.loss_s.clone()
+
+    def comm_ms(self):
+        """Mean exposed-communication ms over the replays measured since the last call (measure_comm)."""
+        if not self.comm_events:
+            return None
+        self.comm_events[-1][1].synchronize()
+        v = sum(a.elapsed_time(b) for a, b in self.comm_events) / len(self.comm_events)
+        self.comm_events = []
+        return v
 
 
 class DiffusionTrainer:
@@ -526,18 +564,30 @@ class DiffusionTrainer:
                          experiment_name=self.config.get('experiment_name', 'experiment'), config=self.config)
 
     # ------------------------------------------------------------------------------------------
-    def _make_grad_sync(self, config, process_group=None):
-        # bucket size: the reference's DDP default (25 MB); 'ddp_bucket_mb' (not a reference key) overrides
+    def _make_grad_sync(self, config, process_group=None, force_avg=False):
+        # bucket size: the reference's DDP default (25 MB); 'ddp_bucket_mb' (not a reference key) overrides.
+        # 'ddp_force_avg' (not a reference key): ReduceOp.AVG even on a one-rank RCCL group (GradSync)
         bmb = float((config or {}).get('ddp_bucket_mb', 25))
-        return GradSync(self.model.executor, process_group=process_group, bucket_bytes=int(bmb * 1024 * 1024))
+        force_avg = force_avg or bool((config or {}).get('ddp_force_avg', False))
+        return GradSync(self.model.executor, process_group=process_group, bucket_bytes=int(bmb * 1024 * 1024),
+                        force_avg=force_avg)
 
-    def enable_grad_sync(self, process_group=None):
+    def enable_grad_sync(self, process_group=None, force_avg=False):
         """Average gradients over `process_group` (default: the initialised default group) from inside the HIP
         backward even when this trainer was built with world_size 1 -- the data-parallel step (GradSync + the
-        segmented graph) on a one-rank group, used to exercise and time the RCCL path on a single GPU."""
+        segmented graph) on a one-rank group, used to exercise and time the RCCL path on a single GPU
+        (force_avg: the ReduceOp.AVG every multi-rank run takes instead of the one-rank SUM). On a group of more
+        ranks the parameters and buffers are first broadcast from the group's first rank, as the constructor's
+        distributed path does, and the trainer becomes distributed."""
         if not dist.is_initialized() or not _is_dmc_model(self._raw_model):
             raise RuntimeError("enable_grad_sync needs an initialised process group and a dmc backbone")
-        self.grad_sync = self._make_grad_sync(self.config, process_group)
+        if dist.get_world_size(process_group) > 1:
+            src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
+            with torch.no_grad():
+                for t in list(self._raw_model.parameters()) + list(self._raw_model.buffers()):
+                    dist.broadcast(t, src=src, group=process_group)
+            self.is_distributed = True
+        self.grad_sync = self._make_grad_sync(self.config, process_group, force_avg)
         self._graph = GraphedTrainStep(self) if GraphedTrainStep.supported(self) else None
         return self.grad_sync
 

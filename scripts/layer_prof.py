@@ -9,6 +9,7 @@ import sys
 from pathlib import Path
 
 os.environ.setdefault("DMC_LAYER_PROF", "1")
+os.environ["DMC_GRAPH"] = "0"     # eager steps: the per-call events must not be graph-captured
 import torch  # noqa: E402
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))

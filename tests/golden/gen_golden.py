@@ -475,16 +475,11 @@ K1_SEEDS = (41, 42, 43)           # numpy PCG64 seeds of x0 / t / noise; the tes
 
 
 def k1_inputs():
-    """The 1000 steps' inputs, host-independent: numpy PCG64 draws in step order (x0 ~ U(-1,1), t ~ U{0..999},
-    noise ~ N(0,1), float32)."""
-    rx, rt, rn = (np.random.default_rng(s) for s in K1_SEEDS)
-    shape = (K1_B, 3, 16, 16)
-    xs, ts, ns = [], [], []
-    for _ in range(K1_STEPS):
-        xs.append(torch.from_numpy(rx.random(shape, dtype=np.float32) * np.float32(2) - np.float32(1)))
-        ts.append(torch.from_numpy(rt.integers(0, 1000, (K1_B,), dtype=np.int64)))
-        ns.append(torch.from_numpy(rn.standard_normal(shape, dtype=np.float32)))
-    return xs, ts, ns
+    """The 1000 steps' inputs, host-independent (tests/k1_draws.py, shared with the tests): numpy PCG64 draws in
+    step order (x0 ~ U(-1,1), t ~ U{0..999}, noise ~ N(0,1), float32)."""
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    from k1_draws import k1_draws
+    return k1_draws(K1_SEEDS, K1_B, K1_STEPS)
 
 
 def _run_ref_1k(threads, capture):

@@ -22,6 +22,7 @@ import pytest
 import torch
 
 from conftest import load_golden
+from k1_draws import k1_inputs
 from test_gpu_model import cos, rel
 from test_oracle import DIT, DIT_S2, TINY, check_grad_summary, dit_s2_state_dict, split_params
 
@@ -36,20 +37,6 @@ CIFAR = dict(image_size=(32, 32), in_channels=3, model_channels=128, out_channel
 # ----------------------------------------------------------------------------------------------------------
 # 1000-step protocol
 # ----------------------------------------------------------------------------------------------------------
-def k1_inputs(g):
-    """tests/golden/gen_golden.py::k1_inputs: numpy PCG64 draws, step order, from the fixture's seeds."""
-    sx, st, sn = (int(s) for s in g["seeds"])
-    B = int(g["batch"])
-    rx, rt, rn = (np.random.default_rng(s) for s in (sx, st, sn))
-    shape = (B, 3, 16, 16)
-    xs, ts, ns = [], [], []
-    for _ in range(len(g["losses"])):
-        xs.append(torch.from_numpy(rx.random(shape, dtype=np.float32) * np.float32(2) - np.float32(1)))
-        ts.append(torch.from_numpy(rt.integers(0, 1000, (B,), dtype=np.int64)))
-        ns.append(torch.from_numpy(rn.standard_normal(shape, dtype=np.float32)))
-    return xs, ts, ns
-
-
 def _k1_trainer(tmp_path, theta, opt_state=None):
     from diffusion_models_collection_amd.models import UNet
     from diffusion_models_collection_amd.diffusion import DDPM
@@ -452,11 +439,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_rccl_single_rank_grad_sync_matches_single_process(tmp_path, monkeypatch):
+@pytest.mark.parametrize("force_avg", [False, True], ids=["sum", "avg"])
+def test_rccl_single_rank_grad_sync_matches_single_process(tmp_path, monkeypatch, force_avg):
     """The RCCL branch never exercised by the 2-rank gloo test (utils/helpers.py:88 backend 'nccl' + the DDP step
-    of utils/trainer.py:57-61): a world_size-1 'nccl' process group (RCCL on ROCm), GradSync with ReduceOp.AVG
-    issued from the executor's grad-ready hook on RCCL's stream, and the segmented HIP-graph step (graphs cut at
-    the all-reduce points, collectives issued between replays). Over 5 steps (bf16, dropout 0.1, EMA) the losses,
+    of utils/trainer.py:57-61): a world_size-1 'nccl' process group (RCCL on ROCm), GradSync issued from the
+    executor's grad-ready hook on RCCL's stream, and the segmented HIP-graph step (graphs cut at the all-reduce
+    points, collectives issued between replays). `sum`: the one-rank default (ReduceOp.SUM, RCCL launches
+    nothing); `avg`: ReduceOp.AVG forced (GradSync force_avg) -- ncclAvg with its averaging kernel, the op every
+    multi-rank run takes (utils/trainer.py GradSync). Over 5 steps (bf16, dropout 0.1, EMA) the losses,
     parameters and EMA equal the non-distributed graphed step's within 1e-6 (in practice bitwise: the average
     over one rank is the identity)."""
     import torch.distributed as dist
@@ -477,8 +467,9 @@ def test_rccl_single_rank_grad_sync_matches_single_process(tmp_path, monkeypatch
                "ddp_bucket_mb": 0.25}
         tr = DiffusionTrainer(m, DDPM(device=DEV), None, opt, None, device=DEV, config=cfg)
         if sync:
-            tr.enable_grad_sync()
+            tr.enable_grad_sync(force_avg=force_avg)
             assert tr.grad_sync is not None and tr.grad_sync.native_avg
+            assert tr.grad_sync.op == (dist.ReduceOp.AVG if force_avg else dist.ReduceOp.SUM)
         m.train()
         gen = torch.Generator().manual_seed(5)
         losses = []
@@ -501,6 +492,7 @@ def test_rccl_single_rank_grad_sync_matches_single_process(tmp_path, monkeypatch
         dist.destroy_process_group()
     tr = got[3]
     assert tr._graph is not None and tr._graph.segs is not None and len(tr._graph.segs) >= 3, "segmented step"
+    assert tr._graph.replays == 3, tr._graph.replays          # 5 steps: 2 eager warm-up steps, then replays
     bitwise = torch.equal(got[0], ref[0]) and all(torch.equal(got[1][k], ref[1][k]) for k in ref[1])
     print(f"RCCL 1-rank segmented step: {len(tr._graph.segs)} segments; bitwise equal to the single-process "
           f"graph: {bitwise}")
@@ -539,3 +531,93 @@ def test_dit_hidden768_backward_matches_oracle():
     assert abs(loss.item() - lref.item()) < 1e-5 * max(1.0, abs(lref.item()))
     for k, p in m.named_parameters():
         assert rel(p.grad, sd[k].grad) < 5e-4, (k, rel(p.grad, sd[k].grad))
+
+
+# ----------------------------------------------------------------------------------------------------------
+# A failed training-step capture is loud
+# ----------------------------------------------------------------------------------------------------------
+def test_graph_capture_failure_raises_and_restores_stream(tmp_path, monkeypatch):
+    """The first capture (step 3, after the 2 eager warm-up steps) fails -- capture_begin raises, as a refused
+    capture does -- so train_step raises GraphCaptureError instead of silently re-running the step eagerly on a
+    stream the failed capture may have poisoned; the caller's current stream is restored, the device stays usable,
+    and the trainer does not try to capture again."""
+    from diffusion_models_collection_amd.models import UNet
+    from diffusion_models_collection_amd.diffusion import DDPM
+    from diffusion_models_collection_amd.utils.trainer import DiffusionTrainer, GraphCaptureError
+    mp = dict(image_size=(16, 16), in_channels=3, model_channels=32, out_channels=3, num_res_blocks=1,
+              attention_resolutions=(8,), dropout=0.1, channel_mult=(1, 2), use_attention=True)
+    monkeypatch.setenv("DMC_GRAPH", "1")
+    torch.manual_seed(0)
+    m = UNet(**mp, compute_dtype="bf16").to(DEV).train()
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4)
+    cfg = {"epochs": 1, "save_dir": str(tmp_path / "c"), "sample_dir": str(tmp_path / "s"), "loss_type": "l2",
+           "use_ema": True, "ema_decay": 0.99, "model_type": "unet", "model_params": dict(mp)}
+    tr = DiffusionTrainer(m, DDPM(device=DEV), None, opt, None, device=DEV, config=cfg)
+    x = torch.rand(8, 3, 16, 16, device=DEV) * 2 - 1
+    for i in range(2):
+        assert torch.isfinite(tr.train_step(x, i)).all()      # eager warm-up steps
+
+    def refuse(self, *a, **kw):
+        raise RuntimeError("injected: operation not permitted when stream is capturing")
+
+    monkeypatch.setattr(torch.cuda.CUDAGraph, "capture_begin", refuse)
+    before = torch.cuda.current_stream()
+    with pytest.raises(GraphCaptureError) as ei:
+        tr.train_step(x, 2)
+    assert "injected" in repr(ei.value.__cause__)
+    assert torch.cuda.current_stream() == before
+    assert tr._graph.failed and tr._graph.graph is None and tr._graph.replays == 0
+    torch.cuda.synchronize()
+    assert torch.isfinite((x * 2).sum()).item()               # the device is still usable
+    # no second capture attempt: later steps run eagerly (nothing was captured, nothing poisoned)
+    assert torch.isfinite(tr.train_step(x, 3)).all()
+
+
+# ----------------------------------------------------------------------------------------------------------
+# The benchmarked plans (B=128) pinned to the oracle directly (VERDICT r3 #4)
+# ----------------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("mode", ["train", "eval"])
+def test_cifar_unet_b128_rows_match_oracle(dtype, mode):
+    """configs/cifar10_unet.py network at the benchmarked batch B=128 -- the launch plans the bench runs (bf16: the
+    halo, split-K and epilogue-statistics plans; eval: the GN+SiLU halo prologue) -- compared with the oracle
+    (models/unet.py:243-292) run on rows {0, 1, 127} alone, and the per-sample p_losses of those rows
+    (diffusion/ddpm.py:106-140: q_sample, forward, MSE over each image) with the oracle's. Dropout 0 so that the
+    training forward is deterministic. Tolerances: fp32 1e-4 of max |ref| on the outputs and 1e-4 relative on each
+    per-sample loss; bf16 5e-2 of max |ref| with cosine > 0.999 on the outputs, and 2e-2 relative per-sample loss
+    (bf16 storage of every activation)."""
+    from diffusion_models_collection_amd.models import UNet
+    from diffusion_models_collection_amd.diffusion import DDPM
+    from oracle.unet_oracle import make_oracle
+    from oracle import diffusion_oracle as DO
+    torch.manual_seed(42)
+    m = UNet(**CIFAR, compute_dtype=dtype).to(DEV)
+    m.train() if mode == "train" else m.eval()
+    orc, _ = make_oracle(m.state_dict(), CIFAR)
+    gen = torch.Generator().manual_seed(11)
+    x0 = torch.rand(128, 3, 32, 32, generator=gen) * 2 - 1
+    t = torch.randint(0, 1000, (128,), generator=gen)
+    noise = torch.randn(128, 3, 32, 32, generator=gen)
+    ddpm = DDPM(device=DEV)
+    xt = ddpm.q_sample(x0.to(DEV), t.to(DEV), noise.to(DEV))
+    if mode == "train":
+        xin = xt.clone().requires_grad_(True)          # the taped (training) forward and its plans
+        out = m(xin, t.to(DEV))
+    else:
+        with torch.no_grad():
+            out = m(xt, t.to(DEV))
+    out = out.detach().float().cpu()
+    rows = [0, 1, 127]
+    tab = DO.schedule()
+    xr = DO.q_sample(tab, x0[rows], t[rows], noise[rows])
+    with torch.no_grad():
+        ref = orc.forward(xr, t[rows], None)
+    got = out[rows]
+    lg = ((got - noise[rows]) ** 2).mean(dim=(1, 2, 3))
+    lr = ((ref - noise[rows]) ** 2).mean(dim=(1, 2, 3))
+    e, c, le = rel(got, ref), cos(got, ref), ((lg - lr).abs() / lr.abs()).max().item()
+    print(f"B=128 {dtype} {mode}: rows {rows} out rel {e:.3e} cos {c:.6f}; per-sample loss rel {le:.3e}")
+    if dtype == "fp32":
+        assert e < 1e-4 and le < 1e-4, (e, le)
+    else:
+        assert e < 5e-2 and c > 0.999 and le < 2e-2, (e, c, le)

@@ -311,7 +311,7 @@ def test_oracle_trainer_1k_snapshots():
     summaries within 1e-4 of each tensor's absmax; the inputs are regenerated from the fixture's seeds (numpy PCG64,
     host-independent); and the reference's two runs (8 vs 1 host threads) agree to 1e-5 per step."""
     import numpy as np
-    from test_gpu_protocol import k1_inputs
+    from k1_draws import k1_inputs
     g = load_golden("trainer_1k")
     xs, ts, ns = k1_inputs(g)
     assert len(xs) == 1000 and tuple(xs[0].shape) == (4, 3, 16, 16)
