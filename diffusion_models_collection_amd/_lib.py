@@ -24,7 +24,7 @@ _c_int, _c_p, _c_f, _c_u32, _c_long, _c_size = (ctypes.c_int, ctypes.c_void_p, c
 
 
 ACT_NONE, ACT_GELU, ACT_GELU_DROP, ACT_DGELU = 0, 1, 2, 3   # include/dmc.h DMC_ACT_*
-FUSED_GN_STATS, FUSED_GN_BWD = 1, 2   # dmc_conv2d_fused_epilogue bits
+FUSED_GN_STATS, FUSED_GN_BWD, FUSED_GN_FIN = 1, 2, 4   # dmc_conv2d_fused_epilogue bits
 
 
 class ConvDesc(ctypes.Structure):
@@ -39,7 +39,15 @@ class ConvDesc(ctypes.Structure):
         ("bias", _c_p), ("addvec", _c_p), ("ld_add", _c_int), ("resid", _c_p), ("ld_res", _c_int),
         ("silu_pre", _c_p), ("ld_silu", _c_int), ("Csplit", _c_int), ("ldy1", _c_int), ("ldy2", _c_int),
         ("out_f32", _c_int), ("out_nchw", _c_int), ("act", _c_int), ("y_pre", _c_p), ("ld_pre", _c_int),
-        ("gnb", _c_p), ("gn_part", _c_p), ("wg_bias", _c_p),
+        ("gnb", _c_p), ("gn_part", _c_p), ("wg_bias", _c_p), ("gn_fin", _c_p),
+    ]
+
+
+class GnFin(ctypes.Structure):
+    """include/dmc.h dmc_gn_fin: the next GroupNorm's statistics finalised by the producing conv's last blocks."""
+    _fields_ = [
+        ("counters", _c_p), ("part2", _c_p), ("C2", _c_int), ("G", _c_int), ("eps", _c_f),
+        ("gamma", _c_p), ("beta", _c_p), ("mean_rstd", _c_p), ("scale", _c_p), ("shift", _c_p),
     ]
 
 

@@ -167,6 +167,61 @@ DMC_DEV float wave_max(float v) {
   return v;
 }
 
+// ---- GroupNorm statistics from conv-epilogue partials (mean, M2 per 64-pixel segment x 8-channel chunk) ----
+// Chan's combination of (n, m, q) with (nb, mb, qb).
+DMC_DEV void gn_chan(float& n, float& m, float& q, float nb, float mb, float qb) {
+  const float tot = n + nb;
+  if (tot == 0.f) return;
+  const float d = mb - m, r = nb / tot;
+  m += d * r;
+  q += qb + d * d * n * r;
+  n = tot;
+}
+// One wave finalises GroupNorm group g of image n: lane l combines partials l, l+64, ... (segments outer, the
+// group's chunks inner; p1's chunks, then p2's), the lanes then combine over a fixed xor tree (deterministic), and
+// mean / rstd and the folded per-channel scale / shift are written. SC1: the partials of p1 were handed off inside
+// the running launch (write-through stores + an arrival counter): read them with agent-scope (sc1) loads.
+// Used by gn_finalize_kernel (dmc_norm.hip) and by the producing conv's last block (dmc_conv.hip): bitwise equal.
+template <bool SC1>
+DMC_DEV void gn_finalize_group(const float* p1, int nch1, const float* p2, int nch2, int n, int g, int spi, int G,
+                               float eps, const float* gamma, const float* beta, float* mean_rstd, float* scale,
+                               float* shift) {
+  const int lane = threadIdx.x & 63;
+  const int C = 8 * (nch1 + nch2), cpg = C / G, kpg = cpg / 8, np = spi * kpg;
+  float cn = 0.f, m = 0.f, q = 0.f;
+  for (int t = lane; t < np; t += 64) {
+    const int sg = n * spi + t / kpg, kc = g * kpg + t % kpg;
+    const float* pp = kc < nch1 ? p1 + ((size_t)sg * nch1 + kc) * 2 : p2 + ((size_t)sg * nch2 + (kc - nch1)) * 2;
+    float pm, pq;
+    if (SC1 && kc < nch1) {
+      pm = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pq = __hip_atomic_load(pp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      pm = pp[0];
+      pq = pp[1];
+    }
+    gn_chan(cn, m, q, 512.f, pm, pq);
+  }
+#pragma unroll
+  for (int sh = 1; sh < 64; sh <<= 1) {
+    const float nb = __shfl_xor(cn, sh), mb = __shfl_xor(m, sh), qb = __shfl_xor(q, sh);
+    // both lanes of a pair must end with the same value: combine in lane order (lower lane first)
+    if ((lane & sh) == 0) gn_chan(cn, m, q, nb, mb, qb);
+    else { float n2 = nb, m2 = mb, q2 = qb; gn_chan(n2, m2, q2, cn, m, q); cn = n2; m = m2; q = q2; }
+  }
+  const float mean = m;
+  const float var = fmaxf(q / cn, 0.f);
+  const float rstd = 1.0f / sqrtf(var + eps);
+  const size_t i = (size_t)n * G + g;
+  if (lane == 0 && mean_rstd) { mean_rstd[i * 2] = mean; mean_rstd[i * 2 + 1] = rstd; }
+  for (int c = g * cpg + lane; c < (g + 1) * cpg; c += 64) {
+    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    const float sc = rstd * gm;
+    scale[(size_t)n * C + c] = sc;
+    shift[(size_t)n * C + c] = bt - mean * sc;
+  }
+}
+
 // load / store one element of storage type T as float
 template <typename T> DMC_DEV float ld_as_f(const void* p, size_t i);
 template <> DMC_DEV float ld_as_f<float>(const void* p, size_t i) { return ((const float*)p)[i]; }

@@ -32,6 +32,8 @@ struct ConvK {
   float* gsk;  // split-K launches: GroupNorm partials written by the split-K epilogue (nullptr: off)
   unsigned long long* stamp;  // DMC_STAMP measurement builds only: per-wave phase clocks of the halo conv
   int* gsk_done;  // host flag: set when the launch path emitted gsk
+  int fin_on;     // finalise the next GroupNorm from gst in this launch (dmc_gn_fin in fin; needs gst)
+  dmc_gn_fin fin;
   int M;      // N*OH*OW output pixels
   int OHW;    // OH*OW
   float* sk;  // split-K partial slab (nullptr: no split)
@@ -368,11 +370,38 @@ DMC_DEV void chan_eq(float& m, float& q, float mb, float qb, float n) {
   m = 0.5f * (m + mb);
 }
 
+// The producing conv finalises the next GroupNorm (dmc_gn_fin, MI355X_MICROARCH.md "Valid forms" row 1): every
+// storing wave drains its write-through (sc1) partial stores, the block barriers, then one lane per image of the tile
+// adds to that image's arrival counter (agent scope, returning). The block whose add completes the count -- every
+// (pixel tile, channel tile) block of the image has stored its partials -- combines the image's partials with sc1
+// loads, one wave per GroupNorm group (gn_finalize_group: bitwise dmc_gn_finalize). No block ever waits for another.
+template <int BM, int BN, int NT>
+DMC_DEV void gn_fin_tail(const ConvK& a, const char* scratch, int m0) {
+  int* flag = (int*)scratch;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int nf = m0 / a.OHW, ni = (m0 + BM - 1) / a.OHW - nf + 1;   // images this tile covers
+  const unsigned expect = (unsigned)((a.OHW >= BM ? a.OHW / BM : 1) * (a.Cout / BN));
+  if ((int)threadIdx.x < ni) {
+    const unsigned old = __hip_atomic_fetch_add(a.fin.counters + nf + threadIdx.x, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    flag[threadIdx.x] = old == expect - 1;
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, spi = a.OHW / 64;
+  for (int i = 0; i < ni; ++i) {
+    if (!flag[i]) continue;
+    for (int g = wave; g < a.fin.G; g += NT / 64)
+      gn_finalize_group<true>(a.gst, a.Cout / 8, a.fin.part2, a.fin.C2 / 8, nf + i, g, spi, a.fin.G, a.fin.eps,
+                              a.fin.gamma, a.fin.beta, a.fin.mean_rstd, a.fin.scale, a.fin.shift);
+  }
+}
+
 template <int BM, int BN, int NT>
 DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int n0) {
   constexpr int CG = BN / 8, RS = NT / CG, IT = BM / RS;
   constexpr int SEG = 64, NSEG = BM / SEG, KPS = SEG / RS;   // GroupNorm partial segments of 64 pixels
-  static_assert(CG == 16 && SEG % RS == 0 && BM % SEG == 0, "GroupNorm partial geometry");
+  static_assert((CG == 16 || CG == 8) && SEG % RS == 0 && BM % SEG == 0, "GroupNorm partial geometry");
   const int cg = threadIdx.x % CG, r0 = threadIdx.x / CG;
   const int co = n0 + cg * 8;
   if (co >= a.Cout) return;
@@ -523,11 +552,11 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
     }
   }
   if (a.gb_on) {
-    // lanes with the same chunk (xor 16, 32), then waves through LDS past the epilogue tile, in fixed order
+    // lanes with the same chunk (xor CG, 2 CG, ...), then waves through LDS past the epilogue tile, in fixed order
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int NW = NT / 64;
 #pragma unroll
-    for (int sh = 16; sh < 64; sh <<= 1)
+    for (int sh = CG; sh < 64; sh <<= 1)
 #pragma unroll
       for (int j = 0; j < NSEG; ++j)
 #pragma unroll
@@ -562,7 +591,7 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
     float cnt = 8.f * KPS;
     if (a.gb_on) __syncthreads();                    // the scratch below is shared with the sums above
 #pragma unroll
-    for (int sh = 16; sh < 64; sh <<= 1) {          // the lanes of this wave with the same chunk
+    for (int sh = CG; sh < 64; sh <<= 1) {          // the lanes of this wave with the same chunk
 #pragma unroll
       for (int j = 0; j < NSEG; ++j) {
         const float mb = __shfl_xor(gm[j], sh), qb = __shfl_xor(gq[j], sh);
@@ -590,9 +619,15 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
         q += qb + d * d * (na * nb / (na + nb));
       }
       const size_t o = ((size_t)(m0 / SEG + j) * (a.Cout / 8) + (n0 / 8 + c)) * 2;
-      a.gst[o] = m;
-      a.gst[o + 1] = q;
+      if (a.fin_on) {   // handed off inside this launch: write-through (sc1), read by the last block with sc1 loads
+        __hip_atomic_store(a.gst + o, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.gst + o + 1, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        a.gst[o] = m;
+        a.gst[o + 1] = q;
+      }
     }
+    if (a.fin_on) gn_fin_tail<BM, BN, NT>(a, lds + BM * EP, m0);
   }
 }
 
@@ -611,7 +646,7 @@ DMC_DEV void tile_epilogue(const ConvK& a, const char* lds, int EP, int m0, int 
     for (int pl = r0; pl < BM; pl += RS) conv_store_tile<T>(a, *(const v4f*)(lds + pl * EP + cg * 16), m0 + pl, co);
     return;
   }
-  if constexpr (BN == 128) {
+  if constexpr ((BN == 128 || BN == 64) && BM % 64 == 0) {
     if (sizeof(T) == 2 && !a.out_f32 && !((a.Cout | a.Csplit | a.ldy1 | a.ldy2 | a.ld_res) & 7)) {
       tile_epilogue8<BM, BN, NT>(a, lds, EP, m0, n0);   // 16-byte stores: half the store instructions
       return;
@@ -1159,6 +1194,198 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
   tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Small-map 3x3 conv (forward or dgrad, stride 1) for the UNet's 8x8 and 4x4 levels (models/unet.py:28-72 at the
+// two deepest resolutions, their up-path concat convs and input gradients). There M is 8192 / 2048 pixels: the
+// 128-pixel x 128-channel tiles of the kernels above give 64-128 blocks for 256 CUs, and split-K to fill the chip
+// leaves every block a handful of K stages behind a fixed prologue / epilogue / slab cost (PMC of the 4x4 split
+// launch: MFMA busy 11 % of a wave's life). Here a block owns a tile of BM = 16 * MT output pixels (two whole
+// images) x 64 output channels over the FULL K, and its four waves split K instead of the tile: wave w takes the
+// input channels [w * CPW, (w + 1) * CPW), CPW = Cin / 4, for all nine taps. So:
+//   * each wave keeps its channel slice of the tile's halo (the images plus their zero border, 64-channel planes
+//     of 128-byte rows, the halo kernels' XOR swizzle) resident in wave-private LDS: loaded once (CPW = 64) or
+//     twice (CPW = 128), never shared, so the K loop has no block barrier at all;
+//   * the weight fragments come straight from global memory (L2) into registers, P k-steps ahead of their
+//     MFMAs (no LDS staging, no DMA issue in the loop);
+//   * the four partial tiles are summed through LDS in a fixed order ((w0 + w2) + (w1 + w3)), then the shared
+//     LDS-staged epilogue (bias, time embedding, residual, GroupNorm partials) runs once: no fp32 slab, no
+//     split-K epilogue launch.
+// Grid: (M / BM) x (Cout / 64) blocks = 256 at B = 128 (512 for 512 output channels). MT = 8 (8x8 maps) or
+// 2 (4x4 maps); HPC = halo DMA pieces (8 pixels) per wave-plane: 2 x 10 x 10 -> 25, 2 x 6 x 6 -> 9.
+template <int MT, int HPC, int NPL, int P>
+__global__ __launch_bounds__(256) void conv3x3_small_kernel(ConvK a) {
+  using T = bf16_t;
+  constexpr int BM = 16 * MT, BN = 64, NT = 256;
+  constexpr int PLB = HPC * 1024;                       // bytes of one wave's halo plane
+  constexpr int EP = BN * 4 + 16;                       // epilogue row pitch (fp32)
+  constexpr int RED = 2 * BM * EP + 4 * (BM / 64 > 0 ? BM / 64 : 1) * 16 * 64;   // 2 partial tiles + stats scratch
+  constexpr int LDS_BYTES = 4 * PLB > RED ? 4 * PLB : RED;
+  constexpr int S = NPL * 18;                           // k32 steps per wave: planes x 9 taps x 2 halves
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int NB = a.Cout / BN;
+  const int mb = blockIdx.x / NB, nb = blockIdx.x - mb * NB;
+  const int m0 = mb * BM, n0 = nb * BN;
+  const int OW = a.OW, HW = OW + 2, segpix = (a.OH + 2) * HW, nimg = BM / a.OHW;
+  const int n_first = m0 / a.OHW;
+  const int CPW = NPL * 64, cw0 = wave * CPW;           // this wave's input channels
+  const bool first = cw0 < a.C1;
+  const char* const xs = first ? a.x1 : a.x2;
+  const int xbytes = first ? a.x1_bytes : a.x2_bytes, ldx = first ? a.ld1 : a.ld2, cs = first ? cw0 : cw0 - a.C1;
+  char* const hbuf = lds + wave * PLB;
+  const int lrow = lane >> 3, lc = (lane & 7) ^ lrow;   // DMA piece: lane -> row lrow, logical chunk lc
+
+  // halo DMA of one 64-channel plane (pieces of 8 halo pixels x 128 B; out-of-image pixels read zeros)
+  auto halo_dma = [&](int pl) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)xs, (short)0, xbytes, 0x00020000);
+#pragma unroll
+    for (int p = 0; p < HPC; ++p) {
+      const int h = p * 8 + lrow;
+      unsigned off = kOOB;
+      if (h < nimg * segpix) {
+        const int img = h / segpix, rem = h - img * segpix;
+        const int hr = rem / HW, hc = rem - hr * HW;
+        const int iy = hr - 1, ix = hc - 1;
+        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+          off = ((unsigned)(((n_first + img) * a.H + iy) * a.W + ix) * ldx + cs + pl * 64 + lc * 8) * 2u;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(hbuf + p * 1024), 16, off, 0, 0, 0);
+    }
+  };
+
+  const int fr = lane & 15, fh = lane >> 4;
+  int hb[MT];
+#pragma unroll
+  for (int j = 0; j < MT; ++j) {
+    const int m = j * 16 + fr;
+    const int img = m / a.OHW, rem = m - img * a.OHW;
+    const int r = rem / OW, col = rem - r * OW;
+    hb[j] = img * segpix + (r + 1) * HW + col + 1;
+  }
+  // weight fragments: packed [Cout][9][Kc]; step s = (plane, tap, half) -> k = tap * Kc + cw0 + plane * 64 + half * 32
+  const char* wb = a.w + ((size_t)(n0 + fr) * (9 * a.Kc) + cw0 + fh * 8) * 2;
+  const size_t wrow16 = (size_t)16 * 9 * a.Kc * 2;      // 16 co rows
+  auto wload = [&](int s, v4i* f) {
+    const int pl = s / 18, rem = s - pl * 18, t = rem >> 1, hf = rem & 1;
+    const char* p = wb + ((size_t)t * a.Kc + pl * 64 + hf * 32) * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = *(const v4i*)(p + i * wrow16);
+  };
+
+  v4f acc[4][MT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < MT; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  halo_dma(0);
+  // the counted wait below needs the halo DMA issued before the weight loads: keep hipcc from reordering them
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  v4i wq[P][4];
+#pragma unroll
+  for (int q = 0; q < P; ++q) wload(q, wq[q]);
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(4 * P));        // the halo (issued first) has landed
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int pl = s / 18, rem = s - pl * 18, t = rem >> 1, hf = rem & 1;
+    if (pl > 0 && rem == 0) {
+      // next 64-channel plane into the same (wave-private) buffer: this wave's reads of the old plane are done
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      halo_dma(pl);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+      asm volatile("" ::: "memory");
+    }
+    const int ty = t / 3, tx = t - ty * 3;
+    const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
+    v4i fb[MT];
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      const int h = hb[j] + delta;
+      fb[j] = *(const v4i*)(hbuf + h * 128 + (((hf * 4 + fh) ^ (h & 7)) << 4));
+    }
+    v4i* fa = wq[s % P];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
+    if (s + P < S) wload(s + P, wq[s % P]);
+  }
+  // K reduction across the waves: (w0 + w2) + (w1 + w3) in fixed order, into tile 0
+  __syncthreads();
+  float* const t0 = (float*)lds;
+  float* const t1 = (float*)(lds + BM * EP);
+  float* const tw = (wave & 1) ? t1 : t0;
+  const int cfr = (threadIdx.x & 63) & 15;
+  if (wave < 2) {
+#pragma unroll
+    for (int j = 0; j < MT; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *(v4f*)((char*)tw + (j * 16 + cfr) * EP + (i * 16 + fh * 4) * 4) = acc[i][j];
+  }
+  __syncthreads();
+  if (wave >= 2) {
+#pragma unroll
+    for (int j = 0; j < MT; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v4f* q = (v4f*)((char*)tw + (j * 16 + cfr) * EP + (i * 16 + fh * 4) * 4);
+        *q = *q + acc[i][j];
+      }
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < BM * (BN / 4); idx += NT) {
+    const int r = idx / (BN / 4), c4 = idx - r * (BN / 4);
+    v4f* q0 = (v4f*)((char*)t0 + r * EP + c4 * 16);
+    *q0 = *q0 + *(const v4f*)((char*)t1 + r * EP + c4 * 16);
+  }
+  __syncthreads();
+  tile_epilogue<T, BM, BN, NT>(a, lds, EP, m0, n0);
+}
+
+// Whether the small-map kernel takes this conv: bf16 3x3 stride-1 forward / dgrad taps, 8x8 or 4x4 maps (two
+// whole images per tile), Cin a multiple of 256 (4 waves x 64-channel planes, each wave's slice inside one
+// source), Cout a multiple of 64, no prologue. Returns MT (16-pixel m-tiles per block) or 0.
+int small_plan(const ConvK& k) {
+  if (dmc::opt(dmc::OPT_NO_SMALL) || k.dtype_bytes != 2 || k.prologue != DMC_PRO_NONE) return 0;
+  if (k.mode != DMC_MODE_NORMAL || k.stride != 1 || k.ntaps != 9 || k.tkw != 3) return 0;
+  if (!((k.tdy0 == -1 && k.tsy == 1) || (k.tdy0 == 1 && k.tsy == -1))) return 0;
+  if (!((k.tdx0 == -1 && k.tsx == 1) || (k.tdx0 == 1 && k.tsx == -1))) return 0;
+  if (k.OH != k.H || k.OW != k.W || !((k.OH == 8 && k.OW == 8) || (k.OH == 4 && k.OW == 4))) return 0;
+  const int Cin = k.C1 + k.C2, cpw = Cin / 4;
+  // Cin = 256 only: with 512 input channels (two halo planes per wave) it measured slower than the split-K path
+  // (8x8: 93 vs 42 us; 4x4: 25 vs 22 us), with 256 faster (8x8: 23.7 vs 32.5 us; 4x4: 15.2 vs 21.1 us)
+  if (Cin != 256 || k.Kc != Cin || k.C1 % cpw || k.Cout % 64 || k.N % 2) return 0;
+  if (k.x1_bytes == 0 || (k.C2 && k.x2_bytes == 0) || k.w_bytes == 0 || k.silu_pre || k.act) return 0;
+  // DMC_SMALL_MASK: bit 0 8x8 forward, 1 8x8 input gradient, 2 4x4 forward, 3 4x4 input gradient. Default 1: in
+  // the train step / DDIM loop only the 8x8 forward at B = 128 (one round of 256 blocks) measured faster (+0.3 %);
+  // the input gradients (512 output channels: two rounds of 102 KB blocks), the 4x4 shapes and the 2B-row CFG
+  // forward measured neutral to slower than the split-K path (profiles/r4_small_ab.txt)
+  const int bit = (k.OH == 8 ? 0 : 2) + (k.tdy0 == 1 ? 1 : 0);
+  if (!((dmc::opt(dmc::OPT_SMALL_MASK) >> bit) & 1)) return 0;
+  if (k.OH == 8 && k.M / 128 * (k.Cout / 64) > 256 && dmc::opt(dmc::OPT_SMALL_MASK) == 1) return 0;
+  return k.OH == 8 ? 8 : 2;
+}
+
+void launch_small(const ConvK& k, int mt, hipStream_t s) {
+  const int npl = (k.C1 + k.C2) / 256;
+  const dim3 g(k.M / (16 * mt) * (k.Cout / 64));
+  if (mt == 8) {
+    if (npl == 1) conv3x3_small_kernel<8, 25, 1, 4><<<g, 256, 0, s>>>(k);
+    else conv3x3_small_kernel<8, 25, 2, 4><<<g, 256, 0, s>>>(k);
+  } else {
+    if (npl == 1) conv3x3_small_kernel<2, 9, 1, 6><<<g, 256, 0, s>>>(k);
+    else conv3x3_small_kernel<2, 9, 2, 6><<<g, 256, 0, s>>>(k);
+  }
+}
+
 // Geometry of the halo kernel for this conv, or false if it does not apply.
 // Returns the DMA pieces per wave (6 or 7) the halo needs, 0 if the halo kernels do not apply.
 int halo_plan(const ConvK& k, int* R, int* nimg) {
@@ -1187,6 +1414,23 @@ int halo2_plan(const ConvK& k, int* R, int* nimg) {
   else return 0;
   const int npix = *nimg * (*R + 2) * (k.OW + 2);
   return npix <= 6 * 32 ? 6 : npix <= 7 * 32 ? 7 : npix <= 9 * 32 ? 9 : 0;
+}
+
+// The halo'd narrow kernels (conv3x3_nin_kernel / conv3x3_nout_kernel, below): bf16, 3x3 stride 1 on halo2_plan's
+// 128-pixel geometry. nin: one source of <= 8 channels (one chunk per pixel), Cout a multiple of 128. nout: Cout <=
+// 16, 64-aligned sources of <= 128 channels in all. Return the halo pieces per wave (6/7/9), or 0.
+int nin_plan(const ConvK& k, int* R, int* nimg) {
+  if (dmc::opt(dmc::OPT_NO_NHALO) || k.dtype_bytes != 2 || k.prologue != DMC_PRO_NONE || k.C2 != 0 || k.C1 > 8 ||
+      k.ld1 != 8 || k.Cout % 128 || k.silu_pre || k.act)
+    return 0;
+  return halo2_plan(k, R, nimg);
+}
+int nout_plan(const ConvK& k, int* R, int* nimg) {
+  if (dmc::opt(dmc::OPT_NO_NHALO) || k.dtype_bytes != 2 || k.prologue != DMC_PRO_NONE || k.Cout > 16 ||
+      k.C1 % 64 || k.C2 % 64 || k.C1 + k.C2 > 128 || k.Kc != k.C1 + k.C2 || k.x1_bytes == 0 ||
+      (k.C2 && k.x2_bytes == 0) || k.w_bytes == 0 || k.act)
+    return 0;
+  return halo2_plan(k, R, nimg);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1294,6 +1538,167 @@ __global__ __launch_bounds__(256) void conv_narrow_out_kernel(ConvK a) {
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) conv_store_tile<T>(a, acc[j], p0 + 16 * j + fr, fh * 4);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Halo'd narrow convs (bf16, 3x3 stride 1, 128-pixel tiles of whole rows / whole images: halo2_plan's geometry).
+// The global-fragment kernels above gather every input row once per tap (9x through the texture path: ~377 MB per
+// launch for the 128->3 output conv, whose inputs are 33.5 MB). Here each block DMAs its tile's halo into LDS
+// once and all nine taps read their fragments from it.
+//
+// Narrow output (Cout <= 16; the UNet's output conv models/unet.py:241, 128 -> 3): the halo of every 64-channel
+// plane of the input (NPL planes, HP pieces per wave each, halo2's 128-byte swizzled rows) is resident; wave w owns
+// pixel tiles 2w, 2w+1 and walks K = planes x taps x 64 with the weight fragments (16 rows, Cout real) from L1/L2.
+template <int HP, int NPL>
+__global__ __launch_bounds__(256) void conv3x3_nout_kernel(ConvK a, int R, int nimg) {
+  using T = bf16_t;
+  constexpr int PB = HP * 4 * 1024;              // bytes of one plane's halo
+  __shared__ __attribute__((aligned(16))) char lds[NPL * PB];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int m0 = blockIdx.x * 128;
+  const int lrow = lane >> 3, lc = (lane & 7) ^ lrow;
+  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
+  const int n_first = m0 / a.OHW, r0 = (m0 - n_first * a.OHW) / OW;
+#pragma unroll
+  for (int pl = 0; pl < NPL; ++pl) {
+    const int c = pl * 64;
+    const bool first = c < a.C1;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        first ? (void*)a.x1 : (void*)a.x2, (short)0, first ? a.x1_bytes : a.x2_bytes, 0x00020000);
+    const int ldx = first ? a.ld1 : a.ld2, cs = first ? c : c - a.C1;
+#pragma unroll
+    for (int p = 0; p < HP; ++p) {
+      const int h = (wave * HP + p) * 8 + lrow;
+      unsigned off = kOOB;
+      if (h < npix) {
+        const int img = h / segpix, rem = h - img * segpix;
+        const int hr = rem / HW, hc = rem - hr * HW;
+        const int iy = r0 + hr - 1, ix = hc - 1;
+        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+          off = ((unsigned)(((n_first + img) * a.H + iy) * a.W + ix) * ldx + cs + lc * 8) * 2u;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(lds + pl * PB + (wave * HP + p) * 1024), 16, off, 0,
+                                               0, 0);
+    }
+  }
+  const int fr = lane & 15, fh = lane >> 4;
+  int hb[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int m = (wave * 2 + j) * 16 + fr;
+    const int img = m / (R * OW), rem = m - img * (R * OW);
+    const int rr = rem / OW, col = rem - rr * OW;
+    hb[j] = img * segpix + (rr + 1) * HW + col + 1;
+  }
+  const bool wok = fr < a.Cout;
+  const char* wbase = a.w + ((size_t)(wok ? fr : 0) * 9 * a.Kc + fh * 8) * 2;
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+  __syncthreads();
+  v4f acc[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int pl = 0; pl < NPL; ++pl) {
+    v4i wf[18];
+#pragma unroll
+    for (int q = 0; q < 18; ++q) {
+      const int t = q >> 1, ks = q & 1;
+      wf[q] = *(const v4i*)(wbase + ((size_t)t * a.Kc + pl * 64 + ks * 32) * 2);
+      if (!wok) wf[q] = v4i{0, 0, 0, 0};
+    }
+    const char* buf = lds + pl * PB;
+#pragma unroll
+    for (int q = 0; q < 18; ++q) {
+      const int t = q >> 1, ks = q & 1;
+      const int ty = t / 3, tx = t - ty * 3;
+      const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int h = hb[j] + delta;
+        const v4i fb = *(const v4i*)(buf + h * 128 + (((ks * 4 + fh) ^ (h & 7)) << 4));
+        acc[j] = mma16<T>(acc[j], wf[q], fb);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) conv_store_tile<T>(a, acc[j], m0 + (wave * 2 + j) * 16 + fr, fh * 4);
+}
+
+// Narrow input (one source of <= 8 channels, stored as one 16-byte chunk per pixel; Cout a multiple of 128: the
+// UNet's input conv models/unet.py:188 and the input gradient of its output conv): the tile's halo (one masked
+// chunk per pixel, a few KB) is staged in LDS by plain loads; a k32 step is four taps x the chunk (tap >= 9: zero
+// weights), three steps in all. Wave w owns output channels [32w, 32w+32) of the 128-channel tile over its 128
+// pixels; the tile goes through the shared LDS epilogue (16-byte NHWC stores, bias / time embedding, the
+// GroupNorm partials of the stored output).
+__global__ __launch_bounds__(256) void conv3x3_nin_kernel(ConvK a, int R, int nimg) {
+  using T = bf16_t;
+  constexpr int BM = 128, BN = 128, EP = BN * 4 + 16;
+  constexpr int HALO = 320;                        // >= nimg * (R + 2) * (OW + 2) for every halo2_plan geometry
+  constexpr int LDS_BYTES = BM * EP + 4 * 2 * 16 * 64 > HALO * 16 ? BM * EP + 4 * 2 * 16 * 64 : HALO * 16;
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
+  const int n_first = m0 / a.OHW, r0 = (m0 - n_first * a.OHW) / OW;
+  for (int h = threadIdx.x; h < HALO; h += 256) {
+    v4i v = {0, 0, 0, 0};
+    if (h < npix) {
+      const int img = h / segpix, rem = h - img * segpix;
+      const int hr = rem / HW, hc = rem - hr * HW;
+      const int iy = r0 + hr - 1, ix = hc - 1;
+      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+        v = mask_chunk<T>(*(const v4i*)(a.x1 + (size_t)(((n_first + img) * a.H + iy) * a.W + ix) * a.ld1 * 2), a.C1);
+    }
+    *(v4i*)(lds + h * 16) = v;
+  }
+  const int fr = lane & 15, fh = lane >> 4;
+  // weights: rows co = n0 + 32 wave + 16 i + fr; the k32 step s covers taps 4s .. 4s+3, lane group fh takes tap 4s+fh
+  v4i fa[3][2];
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int co = n0 + wave * 32 + 16 * i + fr, tap = 4 * s + fh;
+      const bool ok = co < a.Cout && tap < 9;
+      v4i w = *(const v4i*)(a.w + ((size_t)(ok ? co : 0) * 9 * a.Kc + (size_t)(ok ? tap : 0) * a.Kc) * 2);
+      fa[s][i] = ok ? w : v4i{0, 0, 0, 0};
+    }
+  int hb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int m = j * 16 + fr;
+    const int img = m / (R * OW), rem = m - img * (R * OW);
+    const int rr = rem / OW, col = rem - rr * OW;
+    hb[j] = img * segpix + (rr + 1) * HW + col + 1;
+  }
+  int dl[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const int t = 4 * s + fh < 9 ? 4 * s + fh : 0, ty = t / 3, tx = t - ty * 3;
+    dl[s] = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
+  }
+  __syncthreads();
+  v4f acc[2][8];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const v4i fb = *(const v4i*)(lds + (hb[j] + dl[s]) * 16);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[i][j] = mma16<T>(acc[i][j], fa[s][i], fb);
+    }
+  __syncthreads();                                 // the halo is dead: the epilogue tile takes the LDS
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      *(v4f*)(lds + (j * 16 + fr) * EP + (wave * 32 + i * 16 + fh * 4) * 4) = acc[i][j];
+  __syncthreads();
+  tile_epilogue<T, BM, BN, 256>(a, lds, EP, m0, n0);
 }
 
 // split-K reduction + the regular epilogue: out(pix, co..co+3) = epilogue(sum_z slab[z][pix][co..])
@@ -2156,6 +2561,8 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
   k.gb_on = 0;       // likewise for the GroupNorm-backward partials
   k.wgb = nullptr;   // set by dmc_conv2d_wgrad when the bias gradient is requested
   k.gsk = nullptr; k.gsk_done = nullptr;
+  k.fin_on = 0;      // set by dmc_conv2d with gst
+  k.fin = d->gn_fin ? *d->gn_fin : dmc_gn_fin{};
   k.stamp = (unsigned long long*)dmc::opt(dmc::OPT_STAMP_PTR);   // 0 unless a DMC_STAMP probe sets it
   k.M = d->N * d->OH * d->OW; k.OHW = d->OH * d->OW;
   k.sk = nullptr; k.sk_per = 0;
@@ -2366,9 +2773,13 @@ bool epi_stats_ok(const ConvK& k, const void* ws, size_t ws_bytes) {
   if (k.dtype_bytes != 2 || k.out_f32 || k.out_nchw || k.silu_pre || k.Csplit != k.Cout || k.Cout % 128 ||
       k.M % 256 || k.OHW % 64 || ((k.Cout | k.ldy1 | k.ld_res) & 7))
     return false;
-  if (!dmc::opt(dmc::OPT_NO_NARROW) && ((k.C2 == 0 && k.C1 <= 8 && k.Cout >= 16) || k.Cout <= 8)) return false;
+  if (!dmc::opt(dmc::OPT_NO_NARROW) && ((k.C2 == 0 && k.C1 <= 8 && k.Cout >= 16) || k.Cout <= 8)) {
+    int R, nimg;   // the halo'd narrow-input kernel runs the shared LDS epilogue (128-channel tiles)
+    return nin_plan(k, &R, &nimg) != 0;
+  }
   if (dmc::opt(dmc::OPT_NO_GLDS) || dmc::opt(dmc::OPT_NO_EPI_STATS))
     return false;
+  if (small_plan(k) == 8) return true;   // conv3x3_small_kernel: 128-pixel tiles of two 8x8 images
   if (k.prologue == DMC_PRO_AFFINE_SILU) {
     int R, nimg;
     return halo2_pro_plan(k, &R, &nimg) != 0;
@@ -2395,6 +2806,22 @@ bool epi_gnb_ok(const ConvK& k, const void* ws, size_t ws_bytes) {
 template <typename T>
 int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
   constexpr int EPC = TT<T>::KPL;
+  if (!dmc::opt(dmc::OPT_NO_NARROW) && sizeof(T) == 2) {
+    int R, nimg;
+    if (k.C2 == 0 && k.C1 <= EPC && k.Cout >= 16 && nin_plan(k, &R, &nimg)) {
+      conv3x3_nin_kernel<<<dim3(k.M / 128, k.Cout / 128), 256, 0, s>>>(k, R, nimg);
+      return dmc::check_launch("dmc_conv2d");
+    }
+    const int hp = k.Cout <= 8 ? nout_plan(k, &R, &nimg) : 0;
+    if (hp) {
+      const int npl = (k.C1 + k.C2) / 64;
+      const dim3 g(k.M / 128);
+      if (hp == 6) { if (npl == 1) conv3x3_nout_kernel<6, 1><<<g, 256, 0, s>>>(k, R, nimg); else conv3x3_nout_kernel<6, 2><<<g, 256, 0, s>>>(k, R, nimg); }
+      else if (hp == 7) { if (npl == 1) conv3x3_nout_kernel<7, 1><<<g, 256, 0, s>>>(k, R, nimg); else conv3x3_nout_kernel<7, 2><<<g, 256, 0, s>>>(k, R, nimg); }
+      else { if (npl == 1) conv3x3_nout_kernel<9, 1><<<g, 256, 0, s>>>(k, R, nimg); else conv3x3_nout_kernel<9, 2><<<g, 256, 0, s>>>(k, R, nimg); }
+      return dmc::check_launch("dmc_conv2d");
+    }
+  }
   if (!dmc::opt(dmc::OPT_NO_NARROW)) {
     if (k.C2 == 0 && k.C1 <= EPC && k.Cout >= 16) {
       conv_narrow_in_kernel<T><<<dim3(dmc::cdiv(k.M, 256), dmc::cdiv(k.Cout, 32)), 256, 0, s>>>(k);
@@ -2404,6 +2831,10 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
       conv_narrow_out_kernel<T><<<dmc::cdiv(k.M, 256), 256, 0, s>>>(k);
       return dmc::check_launch("dmc_conv2d");
     }
+  }
+  if (sizeof(T) == 2) {
+    const int mt = small_plan(k);
+    if (mt) { launch_small(k, mt, s); return dmc::check_launch("dmc_conv2d"); }
   }
   if (sizeof(T) == 2 && k.prologue == DMC_PRO_AFFINE_SILU) {
     int R, nimg;
@@ -2481,7 +2912,7 @@ extern "C" int dmc_conv2d_fused_epilogue(const dmc_conv_desc* d, size_t ws_bytes
   // the planners only ask whether a workspace of ws_bytes is present
   const void* ws = ws_bytes ? (const void*)d : nullptr;
   int f = 0;
-  if (k.OHW % 64 == 0 && k.Cout % 8 == 0 && epi_stats_ok(k, ws, ws_bytes)) f |= DMC_FUSED_GN_STATS;
+  if (k.OHW % 64 == 0 && k.Cout % 8 == 0 && epi_stats_ok(k, ws, ws_bytes)) f |= DMC_FUSED_GN_STATS | DMC_FUSED_GN_FIN;
   if (k.OHW % 64 == 0 && k.Cout % 8 == 0 && epi_gnb_ok(k, ws, ws_bytes)) f |= DMC_FUSED_GN_BWD;
   return f;
 }
@@ -2504,6 +2935,15 @@ extern "C" int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2
     DMC_REQUIRE(k.OHW % 64 == 0 && k.Cout % 8 == 0 && k.Csplit == k.Cout && !k.out_nchw && k.ldy1 % 4 == 0,
                 "conv: GroupNorm partials need OH*OW %% 64 == 0, Cout %% 8 == 0 and one NHWC output");
     k.gst = epi_stats_ok(k, workspace, ws_bytes) ? part : nullptr;
+  }
+  if (d->gn_fin) {
+    const dmc_gn_fin& f = *d->gn_fin;
+    const int C = k.Cout + f.C2;
+    DMC_REQUIRE(k.gst != nullptr, "conv: gn_fin needs gn_part from a kernel that emits it (DMC_FUSED_GN_FIN)");
+    DMC_REQUIRE(f.counters && f.G > 0 && C % f.G == 0 && (C / f.G) % 8 == 0 && f.C2 % 8 == 0 && (f.C2 == 0 || f.part2) &&
+                    f.scale && f.shift,
+                "conv: gn_fin: G %d over %d channels (8-channel chunks inside groups), counters and outputs", f.G, C);
+    k.fin_on = 1;
   }
   // split-K launches: the split-K epilogue emits the partials in its pass (DMC_NO_SKGN=1: a separate pass)
   int gsk_done = 0;

@@ -823,47 +823,14 @@ namespace {
 // partials l, l+64, ... of image n's 64-pixel segments x the group's 8-channel chunks (segments outer, chunks
 // inner; source 1's chunks, then source 2's), then the lanes combine by Chan's formula over a fixed xor tree
 // (deterministic); mean / rstd and the folded per-channel scale / shift are written exactly as gn_stats does.
-DMC_DEV void chan(float& n, float& m, float& q, float nb, float mb, float qb) {
-  const float tot = n + nb;
-  if (tot == 0.f) return;
-  const float d = mb - m, r = nb / tot;
-  m += d * r;
-  q += qb + d * d * n * r;
-  n = tot;
-}
-
 __global__ __launch_bounds__(256) void gn_finalize_kernel(const float* p1, int nch1, const float* p2, int nch2, int N,
                                                           int spi, int G, float eps, const float* gamma,
                                                           const float* beta, float* mean_rstd, float* scale,
                                                           float* shift) {
-  const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= N * G) return;
   const int n = i / G, g = i - n * G;
-  const int C = 8 * (nch1 + nch2), cpg = C / G, kpg = cpg / 8, np = spi * kpg;
-  float cn = 0.f, m = 0.f, q = 0.f;
-  for (int t = lane; t < np; t += 64) {
-    const int sg = n * spi + t / kpg, kc = g * kpg + t % kpg;
-    const float* pp = kc < nch1 ? p1 + ((size_t)sg * nch1 + kc) * 2 : p2 + ((size_t)sg * nch2 + (kc - nch1)) * 2;
-    chan(cn, m, q, 512.f, pp[0], pp[1]);
-  }
-#pragma unroll
-  for (int sh = 1; sh < 64; sh <<= 1) {
-    const float nb = __shfl_xor(cn, sh), mb = __shfl_xor(m, sh), qb = __shfl_xor(q, sh);
-    // both lanes of a pair must end with the same value: combine in lane order (lower lane first)
-    if ((lane & sh) == 0) chan(cn, m, q, nb, mb, qb);
-    else { float n2 = nb, m2 = mb, q2 = qb; chan(n2, m2, q2, cn, m, q); cn = n2; m = m2; q = q2; }
-  }
-  const float mean = m;
-  const float var = fmaxf(q / cn, 0.f);
-  const float rstd = 1.0f / sqrtf(var + eps);
-  if (lane == 0 && mean_rstd) { mean_rstd[(size_t)i * 2] = mean; mean_rstd[(size_t)i * 2 + 1] = rstd; }
-  for (int c = g * cpg + lane; c < (g + 1) * cpg; c += 64) {
-    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-    const float sc = rstd * gm;
-    scale[(size_t)n * C + c] = sc;
-    shift[(size_t)n * C + c] = bt - mean * sc;
-  }
+  gn_finalize_group<false>(p1, nch1, p2, nch2, n, g, spi, G, eps, gamma, beta, mean_rstd, scale, shift);
 }
 }  // namespace
 

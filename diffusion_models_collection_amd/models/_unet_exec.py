@@ -32,12 +32,13 @@ from .. import kernels as K
 class Act:
     """An NHWC activation [N, H, W, C] (contiguous, pitch C) plus its gradient buffer."""
 
-    __slots__ = ("t", "H", "W", "C", "grad", "part")
+    __slots__ = ("t", "H", "W", "C", "grad", "part", "fin")
 
     def __init__(self, t, H, W, C):
         self.t, self.H, self.W, self.C = t, H, W, C
         self.grad = None
         self.part = None    # GroupNorm partials written by the conv that produced t (dmc_conv_desc.gn_part)
+        self.fin = None     # (GroupNorm, concat partner, (scale, shift, mean_rstd)) finalised by that conv (gn_fin)
 
 
 # GroupNorm statistics from the conv epilogues (A/B: DMC_GN_PARTIALS=0 computes them with dmc_gn_stats passes)
@@ -47,6 +48,11 @@ _GN_PARTIALS = os.environ.get("DMC_GN_PARTIALS", "1") not in ("", "0")
 # gn_bwd_one / gn_bwd_partial passes saved (halo2 <7,3> 56 -> 66 us; train 8253 vs 8284 img/s, 8256 vs 8290)
 _GNB_PARTIALS = _GN_PARTIALS and os.environ.get("DMC_GNB_PARTIALS", "0") not in ("", "0")
 _GNB_DROP = os.environ.get("DMC_GNB_DROP", "1") not in ("", "0")   # ... also at the dropout sites
+# The next GroupNorm's statistics finalised by the conv that produces its input (dmc_gn_fin: the producing launch's
+# last block per image combines the epilogue partials) instead of a dmc_gn_finalize launch. Opt-in (DMC_GN_FIN=1):
+# measured slower on MI355X (same box, B=128: train 8595 vs 8684 img/s, DDIM-50 621 vs 646) -- every block drains
+# its stores before its arrival add, and the image's last block runs the combine on the kernel's critical path
+_GN_FIN = _GN_PARTIALS and os.environ.get("DMC_GN_FIN", "0") not in ("", "0")
 
 
 class GnbReq:
@@ -140,11 +146,13 @@ class ExecCore:
     def _conv(self, srcs, conv, taps, OH, OW, Cout, mode=L.MODE_NORMAL, stride=1, pro=None, drop=None,
               bias=None, addvec=None, ld_add=0, resid=None, out=None, out_f32=False, out_nchw=False,
               dtype=None, packmode=L.PACK_FWD, w=None, Kc=None, silu_pre=None, ld_silu=0, split=None,
-              act=L.ACT_NONE, y_pre=None, stats=None, gnb=None):
+              act=L.ACT_NONE, y_pre=None, stats=None, gnb=None, fin=None):
         """Generic implicit-GEMM conv over 1-2 NHWC sources. pro = (kind, scale, shift). stats = the output Act:
         in bf16 mode it gets the GroupNorm partials of the stored output (the next GroupNorm then needs no
         statistics pass over it, see _gn). gnb = the dmc_gn_bwd_epi from _gnb_epi when the output is the gradient
-        a GroupNorm backward consumes: the conv also writes that backward's reduction sums."""
+        a GroupNorm backward consumes: the conv also writes that backward's reduction sums. fin = (GroupNorm, concat
+        partner Act or None) that reads this output next: where the kernel allows, the conv also finalises that
+        GroupNorm's statistics (_attach_fin)."""
         dtype = dtype or self.dt
         gn_part = None
         if (stats is not None and _GN_PARTIALS and dtype == torch.bfloat16 and (OH * OW) % 64 == 0 and Cout % 8 == 0
@@ -181,6 +189,8 @@ class ExecCore:
                        ld_res=(0 if resid is None or out_nchw else resid.shape[-1]), silu_pre=silu_pre,
                        ld_silu=ld_silu, ldy1=ldy1, ldy2=ldy2, Csplit=csplit, out_f32=out_f32, out_nchw=out_nchw,
                        act=act, y_pre=y_pre, ld_pre=0 if y_pre is None else y_pre.shape[-1], gn_part=gn_part)
+        if fin is not None and gn_part is not None:
+            self._attach_fin(d, fin, stats, N, OH * OW, Cout)
         if gnb is not None:
             if K.conv_fused(d) & L.FUSED_GN_BWD:
                 d.gnb = ctypes.addressof(gnb.epi)
@@ -189,6 +199,42 @@ class ExecCore:
                 gnb.part = None
         K.conv(d, a.t, srcs[1].t if len(srcs) > 1 else None, w, y1, y2)
         return d
+
+    def _fin_counters(self, N):
+        """A fresh set of N zeroed arrival counters for one gn_fin launch: slices of one buffer zeroed per forward
+        (one fill launch; captured into the step's graph like every other launch)."""
+        buf, i = self._fin_state
+        if buf is None or (i + 1) * N > buf.numel():
+            buf, i = torch.zeros(64 * N, dtype=torch.int32, device=self.device), 0
+        self._fin_state = (buf, i + 1)
+        return buf[i * N:(i + 1) * N]
+
+    def _attach_fin(self, d, fin, out, N, HW, Cout):
+        """Let the conv described by d finalise GroupNorm gn over [out | partner] (include/dmc.h dmc_gn_fin): out.fin
+        then holds (gn, partner, (scale, shift, mean_rstd)) for _gn. Skipped (the finalize launch stays) where the
+        kernel does not emit the partials or the group layout / partner partials do not allow it."""
+        gn, partner = fin
+        if not _GN_FIN or self.dt != torch.bfloat16:
+            return
+        C2 = partner.C if partner is not None else 0
+        C, G = Cout + C2, gn.num_groups
+        if C % G or (C // G) % 8 or C2 % 8 or (partner is not None and (partner.part is None or
+                                                                          partner.H * partner.W != HW)):
+            return
+        if not K.conv_fused(d) & L.FUSED_GN_FIN:
+            return
+        dev = self.device
+        mr = torch.empty(N * G * 2, dtype=torch.float32, device=dev)
+        sc = torch.empty(N * C, dtype=torch.float32, device=dev)
+        sh = torch.empty(N * C, dtype=torch.float32, device=dev)
+        f = L.GnFin()
+        ctr = self._fin_counters(N)
+        f.counters, f.part2, f.C2, f.G, f.eps = ctr.data_ptr(), L.ptr(partner.part if partner else None), C2, G, gn.eps
+        f.gamma, f.beta = L.ptr(gn.weight), L.ptr(gn.bias)
+        f.mean_rstd, f.scale, f.shift = mr.data_ptr(), sc.data_ptr(), sh.data_ptr()
+        d.gn_fin = ctypes.addressof(f)
+        d._keep_fin = (f, ctr, partner)
+        out.fin = (gn, partner, (sc, sh, mr))
 
     def _gnb_epi(self, x1, x2, C1, C2, ld1, ld2, mr, gn, silu, drop, N, HW):
         """(dmc_gn_bwd_epi, partials) for the input-gradient conv whose output g feeds gn_bwd over x = [x1 | x2]:
@@ -250,6 +296,19 @@ class UNetExecutor(ExecCore):
         self.use_side = os.environ.get("DMC_SIDE_STREAM", "0") not in ("", "0")
         self.side = None
         self._side_reads = {}
+        self._fin_state = (None, 0)
+        # the layer sequence of UNet.forward (models/unet.py:270-289): (layer, takes the [h, skip] concat, pushes a
+        # skip) -- walked with one step of lookahead so each conv knows which GroupNorm reads its output next
+        self.plan = []
+        for block in model.down_blocks:
+            for j, layer in enumerate(block):
+                self.plan.append((layer, False, j == len(block) - 1))
+        for layer in model.middle_block:
+            if type(layer).__name__ != "Identity":
+                self.plan.append((layer, False, False))
+        for block in model.up_blocks:
+            for j, layer in enumerate(block):
+                self.plan.append((layer, j == 0, False))
 
     # ---------------------------------------------------------------------------------------
     def _layout_grads(self):
@@ -338,10 +397,26 @@ class UNetExecutor(ExecCore):
                               jobs)
 
     # ---------------------------------------------------------------------------------------
+    def _next_gn(self, i, hs):
+        """(GroupNorm, concat partner) that reads the output of plan step i (the step after it: a ResidualBlock's
+        first GroupNorm -- over [h, skip] in the up path -- or an AttentionBlock's; the output GroupNorm after the
+        last step), or None (a Down/Upsample conv reads it)."""
+        if i + 1 >= len(self.plan):
+            return (self.m.output[0], None)
+        layer, cat, _ = self.plan[i + 1]
+        name = type(layer).__name__
+        if name == "ResidualBlock":
+            return (layer.conv1[0], hs[-1] if cat else None)
+        if name == "AttentionBlock":
+            return (layer.norm, None)
+        return None
+
     def _gn(self, srcs, gn, dtype=None):
         dtype = dtype or self.dt
         a = srcs[0]
         b = srcs[1] if len(srcs) > 1 else None
+        if a.fin is not None and a.fin[0] is gn and a.fin[1] is b:
+            return a.fin[2]          # finalised by the conv that produced a (dmc_gn_fin)
         N = a.t.shape[0]
         C = a.C + (b.C if b else 0)
         if (all(s.part is not None for s in srcs) and (a.H * a.W) % 64 == 0 and C % gn.num_groups == 0
@@ -490,23 +565,17 @@ class UNetExecutor(ExecCore):
         ldx = (Cin + self.chunk - 1) // self.chunk * self.chunk
         xin = Act(K.pack_input(dt, x, ldx), H, W, Cin)
         h = self._new(N, H, W, m.model_channels)
-        self._conv([xin], m.input_conv, K.TAPS3, H, W, m.model_channels, bias=m.input_conv.bias, out=h.t, stats=h)
+        self._fin_state = (None, 0)
+        self._conv([xin], m.input_conv, K.TAPS3, H, W, m.model_channels, bias=m.input_conv.bias, out=h.t, stats=h,
+                   fin=self._next_gn(-1, [h]))
         if keep:
             tape.append(("conv_in", xin, h, x.requires_grad))
         hs = [h]
-        for block in m.down_blocks:
-            for layer in block:
-                h = self._layer([h], layer, tape)
-            hs.append(h)
-        for layer in m.middle_block:
-            if type(layer).__name__ == "Identity":
-                continue
-            h = self._layer([h], layer, tape)
-        for block in m.up_blocks:
-            srcs = [h, hs.pop()]
-            for layer in block:
-                h = self._layer(srcs, layer, tape)
-                srcs = [h]
+        for i, (layer, cat, push) in enumerate(self.plan):
+            srcs = [h, hs.pop()] if cat else [h]
+            h = self._layer(srcs, layer, tape, self._next_gn(i, hs))
+            if push:
+                hs.append(h)
         # ---- output: GN -> SiLU -> conv3x3 -> NCHW fp32 ----
         gno, convo = m.output[0], m.output[2]
         sc, sh, mr = self._gn([h], gno)
@@ -517,17 +586,19 @@ class UNetExecutor(ExecCore):
             tape.append(("out", h, (sc, sh, mr), ao))
         return out, tape
 
-    def _layer(self, srcs, layer, tape):
+    def _layer(self, srcs, layer, tape, fin=None):
+        """One step of the plan; fin = (GroupNorm, partner) that reads its output next (see _next_gn)."""
         name = type(layer).__name__
         if name == "ResidualBlock":
-            return self._res_fwd(srcs, layer, tape)
+            return self._res_fwd(srcs, layer, tape, fin)
         if name == "AttentionBlock":
-            return self._attn_fwd(srcs[0], layer, tape)
+            return self._attn_fwd(srcs[0], layer, tape, fin)
         if name == "Downsample":
             a = srcs[0]
             OH, OW = (a.H + 2 - 3) // 2 + 1, (a.W + 2 - 3) // 2 + 1
             out = self._new(a.t.shape[0], OH, OW, a.C)
-            self._conv([a], layer.conv, K.TAPS3, OH, OW, a.C, stride=2, bias=layer.conv.bias, out=out.t, stats=out)
+            self._conv([a], layer.conv, K.TAPS3, OH, OW, a.C, stride=2, bias=layer.conv.bias, out=out.t, stats=out,
+                       fin=fin)
             if tape is not None:
                 tape.append(("down", layer, a, out))
             return out
@@ -535,13 +606,13 @@ class UNetExecutor(ExecCore):
             a = srcs[0]
             out = self._new(a.t.shape[0], 2 * a.H, 2 * a.W, a.C)
             self._conv([a], layer.conv, K.TAPS3, 2 * a.H, 2 * a.W, a.C, mode=L.MODE_UPSAMPLE, bias=layer.conv.bias,
-                       out=out.t, stats=out)
+                       out=out.t, stats=out, fin=fin)
             if tape is not None:
                 tape.append(("up", layer, a, out))
             return out
         raise TypeError(f"unexpected layer {name}")
 
-    def _res_fwd(self, srcs, rb, tape):
+    def _res_fwd(self, srcs, rb, tape, fin=None):
         a = srcs[0]
         N, H, W = a.t.shape[0], a.H, a.W
         Cout = rb.out_channels
@@ -555,11 +626,13 @@ class UNetExecutor(ExecCore):
         if tape is None and self._halo_pro_ok(srcs, Cout, st1):
             a1 = None
             self._conv(srcs, conv1, K.TAPS3, H, W, Cout, pro=(L.PRO_AFFINE_SILU, st1[0], st1[1]), bias=conv1.bias,
-                       addvec=self.addvec.view(N, -1)[:, off:], ld_add=self.temb_total, out=h1.t, stats=h1)
+                       addvec=self.addvec.view(N, -1)[:, off:], ld_add=self.temb_total, out=h1.t, stats=h1,
+                       fin=(gn2, None))
         else:
             a1 = self._apply(srcs, st1, silu=True)
             self._conv([a1], conv1, K.TAPS3, H, W, Cout, bias=conv1.bias,
-                       addvec=self.addvec.view(N, -1)[:, off:], ld_add=self.temb_total, out=h1.t, stats=h1)
+                       addvec=self.addvec.view(N, -1)[:, off:], ld_add=self.temb_total, out=h1.t, stats=h1,
+                       fin=(gn2, None))
         st2 = self._gn([h1], gn2)
         if isinstance(rb.shortcut, torch.nn.Conv2d):
             s = torch.empty(N, H, W, Cout, dtype=self.dt, device=self.device)
@@ -577,17 +650,17 @@ class UNetExecutor(ExecCore):
         if tape is None and drop is None and self._halo_pro_ok([h1], Cout, st2):
             a2 = None
             self._conv([h1], conv2, K.TAPS3, H, W, Cout, pro=(L.PRO_AFFINE_SILU, st2[0], st2[1]), bias=conv2.bias,
-                       resid=resid, out=out.t, stats=out)
+                       resid=resid, out=out.t, stats=out, fin=fin)
         else:
             a2 = self._apply([h1], st2, silu=True, drop=drop)
-            self._conv([a2], conv2, K.TAPS3, H, W, Cout, bias=conv2.bias, resid=resid, out=out.t, stats=out)
+            self._conv([a2], conv2, K.TAPS3, H, W, Cout, bias=conv2.bias, resid=resid, out=out.t, stats=out, fin=fin)
         st1 = (st1, a1)
         st2 = (st2, a2)
         if tape is not None:
             tape.append(("res", rb, srcs, h1, st1, st2, drop, out))
         return out
 
-    def _attn_fwd(self, a, ab, tape):
+    def _attn_fwd(self, a, ab, tape, fin=None):
         N, H, W, C = a.t.shape[0], a.H, a.W, a.C
         Lq = H * W
         heads = ab.num_heads
@@ -601,7 +674,7 @@ class UNetExecutor(ExecCore):
         lse = torch.empty(N * heads * Lq, dtype=torch.float32, device=self.device)
         K.attn_fwd(self.dt, qkv.t, 3 * C, N, Lq, heads, hd, o.t, C, lse)
         out = self._new(N, H, W, C)
-        self._conv([o], ab.proj, K.TAPS1, H, W, C, bias=ab.proj.bias, resid=a.t, out=out.t, stats=out)
+        self._conv([o], ab.proj, K.TAPS1, H, W, C, bias=ab.proj.bias, resid=a.t, out=out.t, stats=out, fin=fin)
         if tape is not None:
             tape.append(("attn", ab, a, st, qkv, o, lse, out))
         return out

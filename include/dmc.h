@@ -67,6 +67,24 @@ typedef struct dmc_gn_bwd_epi {
   float* part;               /* out: [M/64][Cout][2] */
 } dmc_gn_bwd_epi;
 
+/* GroupNorm statistics finalised by the conv that produces the GroupNorm's (last) input, in its own launch
+ * (dmc_conv_desc.gn_fin): the blocks hand their epilogue partials (gn_part) off through per-image arrival counters and
+ * the last block of each image combines them -- with the second source's partials for a virtual-concat GroupNorm
+ * -- exactly as dmc_gn_finalize does (bitwise), so the finalize launch disappears. Needs gn_part and a kernel that
+ * emits the partials in its epilogue (dmc_conv2d_fused_epilogue & DMC_FUSED_GN_FIN). */
+typedef struct dmc_gn_fin {
+  unsigned* counters;        /* [N] arrival counters, zero before the launch (one fresh set per launch) */
+  const float* part2;        /* partials of the second GroupNorm source [N*OH*OW/64][C2/8][2], or NULL */
+  int C2;                    /* its channels (the GroupNorm covers Cout + C2 channels) */
+  int G;
+  float eps;
+  const float* gamma;        /* [Cout + C2] or NULL */
+  const float* beta;
+  float* mean_rstd;          /* out: [N][G][2], as dmc_gn_finalize */
+  float* scale;              /* out: [N][Cout + C2] */
+  float* shift;
+} dmc_gn_fin;
+
 typedef struct dmc_conv_desc {
   int dtype;
   int N, H, W;               /* source batch and spatial size */
@@ -105,6 +123,7 @@ typedef struct dmc_conv_desc {
                               * OH*OW % 64 == 0, Cout % 8 == 0, one NHWC output. Finalised by dmc_gn_finalize. */
   float* wg_bias;            /* dmc_conv2d_wgrad only: if set, also the bias gradient wg_bias[co] = scale * sum over
                               * pixels of dy[pix][co] (nn.Conv2d bias), from the same pass over dy */
+  const struct dmc_gn_fin* gn_fin;   /* if set (with gn_part): finalise the next GroupNorm's statistics in this launch */
 } dmc_conv_desc;
 enum { DMC_ACT_NONE = 0, DMC_ACT_GELU = 1, DMC_ACT_GELU_DROP = 2, DMC_ACT_DGELU = 3 };
 /* DGELU: the backward of GELU_DROP / GELU on an input-gradient conv: out = round(acc) * mask * scale * gelu'(u) with
@@ -130,7 +149,7 @@ int dmc_conv_halo_prologue(const dmc_conv_desc* d);
  * executor asks before it records a layer, and asks for the GroupNorm-backward sums only where they come fused
  * (the extra pass costs more than dmc_gn_silu_bwd's own reduction). */
 int dmc_conv2d_fused_epilogue(const dmc_conv_desc* d, size_t ws_bytes);
-enum { DMC_FUSED_GN_STATS = 1, DMC_FUSED_GN_BWD = 2 };
+enum { DMC_FUSED_GN_STATS = 1, DMC_FUSED_GN_BWD = 2, DMC_FUSED_GN_FIN = 4 };
 int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2, const void* w,
                void* y1, void* y2, void* workspace, size_t ws_bytes, void* stream);
 

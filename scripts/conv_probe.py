@@ -26,6 +26,8 @@ SHAPES = {
     "p1_16": (128, 16, 16, 256, 0, 256, "1"),
     "r256_8": (128, 8, 8, 256, 0, 256, "3"),
     "r256_4": (128, 4, 4, 256, 0, 256, "3"),
+    "d512_8": (128, 8, 8, 256, 0, 512, "d"),       # input gradient of the 8x8 up-block conv1 (256 -> 512)
+    "d512_4": (128, 4, 4, 256, 0, 512, "d"),
     "nin_32": (128, 32, 32, 3, 0, 128, "3"),         # the UNet's first conv (3 -> 128, narrow-input kernel)
     "nout_32": (128, 32, 32, 128, 0, 3, "3"),        # the output conv (128 -> 3, narrow-output kernel)
 }
@@ -35,14 +37,16 @@ def run(name, iters, epi="bias"):
     B, H, W, C1, C2, Cout, kind = SHAPES[name]
     dt = torch.bfloat16
     dev = "cuda"
-    taps = K.TAPS3 if kind == "3" else K.TAPS1
-    kk = 3 if kind == "3" else 1
+    taps = K.TAPS3 if kind == "3" else K.TAPS3_DGRAD if kind == "d" else K.TAPS1
+    kk = 1 if kind == "1" else 3
     ld1 = C1 if C1 >= 8 else 8    # a narrow source is stored at one 16-byte chunk per pixel
     x1 = torch.randn(B, H, W, ld1, device=dev).to(dt)
     x2 = torch.randn(B, H, W, C2, device=dev).to(dt) if C2 else None
     w = torch.randn(Cout, C1 + C2, kk, kk, device=dev) * 0.03
     Kc = L.kc_for(C1 + C2, dt)
-    wp = K.pack_weight(L.PACK_FWD, dt, w, Kc)
+    if kind == "d":   # the forward conv Cout -> C1 read backwards: flipped / transposed pack
+        w = torch.randn(C1 + C2, Cout, kk, kk, device=dev) * 0.03
+    wp = K.pack_weight(L.PACK_DGRAD if kind == "d" else L.PACK_FWD, dt, w, Kc)
     y = torch.empty(B, H, W, Cout, device=dev, dtype=dt)
     d = K.make_desc(dt, B, H, W, C1, C2, ld1, C2, Kc, H, W, Cout, taps)
     if epi == "full":   # ResBlock conv2 epilogue: bias + time embedding + residual

@@ -303,6 +303,116 @@ def test_conv3x3_halo_kernel(case, variant, monkeypatch, dmc_opt):
         assert rel_err(dws[0], dws[1]) < 1e-3, rel_err(dws[0], dws[1])
 
 
+@pytest.mark.parametrize("case", ["in32", "in16_dgrad", "out32_nchw", "out64", "out8_multi_image"])
+def test_conv3x3_narrow_halo_kernels(case, dmc_opt):
+    """The halo'd narrow convs (conv3x3_nin_kernel: <= 8 input channels, the UNet's input conv and the input gradient
+    of its output conv, through the shared LDS epilogue with the GroupNorm partials; conv3x3_nout_kernel: <= 16 output
+    channels, the output conv with its NCHW fp32 store) vs the fp32 torch reference and vs the global-fragment narrow
+    kernels (DMC_NO_NHALO=1) on the same inputs."""
+    L, K = _lib()
+    dt = torch.bfloat16
+    torch.manual_seed(13)
+    N, H, Cin, Cout, taps, pm, nchw_out = {"in32": (8, 32, 3, 128, K.TAPS3, L.PACK_FWD, False),
+                                            "in16_dgrad": (8, 16, 3, 256, K.TAPS3_DGRAD, L.PACK_DGRAD, False),
+                                            "out32_nchw": (8, 32, 128, 3, K.TAPS3, L.PACK_FWD, True),
+                                            "out64": (4, 64, 128, 3, K.TAPS3, L.PACK_FWD, False),
+                                            "out8_multi_image": (16, 8, 64, 3, K.TAPS3, L.PACK_FWD, True)}[case]
+    W = H
+    x = q(torch.randn(N, Cin, H, W), dt)
+    if pm == L.PACK_DGRAD:
+        w = q(torch.randn(Cin, Cout, 3, 3) / math.sqrt(Cin * 9), dt)
+        yr = torch.nn.grad.conv2d_input((N, Cout, H, W), w, x, padding=1)
+    else:
+        w = q(torch.randn(Cout, Cin, 3, 3) / math.sqrt(Cin * 9), dt)
+        yr = F.conv2d(x, w, padding=1)
+    bias = torch.randn(Cout)
+    yr = yr + bias[:, None, None]
+    ld1 = 8 if Cin < 8 else Cin
+    xd = torch.full((N, H, W, ld1), 1e4, dtype=dt, device=DEV)   # padding channels hold garbage
+    xd[..., :Cin] = nhwc(x).to(dt).to(DEV)
+    wp = K.pack_weight(pm, dt, w.to(DEV), L.kc_for(Cin, dt))
+    stats = Cin < 8 and H * W % 64 == 0
+    outs, parts = [], []
+    for no_nhalo in (0, 1):
+        dmc_opt("DMC_NO_NHALO", no_nhalo)
+        d = K.make_desc(dt, N, H, W, Cin, 0, ld1, 0, L.kc_for(Cin, dt), H, W, Cout, taps)
+        part = torch.full((N * H * W // 64 * (Cout // 8) * 2,), float("nan"), device=DEV) if stats else None
+        if nchw_out:
+            y = torch.full((N, Cout, H, W), float("nan"), device=DEV)
+            K.set_epilogue(d, bias=bias.to(DEV), out_f32=True, out_nchw=True, gn_part=part)
+        else:
+            y = torch.full((N, H, W, Cout), float("nan"), dtype=dt, device=DEV)
+            K.set_epilogue(d, bias=bias.to(DEV), ldy1=Cout, gn_part=part)
+        K.conv(d, xd, None, wp, y)
+        torch.cuda.synchronize()
+        outs.append(y.float().cpu() if nchw_out else nchw(y.float().cpu()))
+        parts.append(part.cpu() if stats else None)
+    assert rel_err(outs[0], yr) < 2e-2, rel_err(outs[0], yr)
+    assert rel_err(outs[0], outs[1]) < 1e-2, rel_err(outs[0], outs[1])
+    if stats:
+        p0, p1 = parts[0].view(-1, 2), parts[1].view(-1, 2)
+        assert torch.isfinite(p0).all()
+        assert rel_err(p0[:, 0], p1[:, 0]) < 2e-2 and rel_err(p0[:, 1], p1[:, 1]) < 2e-2
+
+
+@pytest.mark.parametrize("case", ["f8_256", "f8_concat512", "d8_512out", "f4_256", "f4_concat512", "d4_512out"])
+def test_conv3x3_small_kernel(case, dmc_opt):
+    """The small-map 3x3 conv (conv3x3_small_kernel: two whole 8x8 / 4x4 images x 64 output channels per block,
+    K split over the block's four waves, wave-private LDS halos, weight fragments straight from L2, partial tiles
+    summed in LDS) at the UNet's B=128 shapes -- forward (one source and the up path's 256+256 concat) and the
+    input gradient with 512 output channels -- with the full epilogue (bias, time embedding, residual) and, at 8x8,
+    the GroupNorm partials: vs the fp32 torch reference, and vs the split-K LDS-DMA path it replaces
+    (DMC_NO_SMALL=1) on the same inputs."""
+    L, K = _lib()
+    dt = torch.bfloat16
+    torch.manual_seed(9)
+    H = 8 if case[1] == "8" else 4
+    N = 128
+    C1, C2, Cout, taps, pm = 256, 0, 256, K.TAPS3, L.PACK_FWD
+    if "concat512" in case:
+        C2 = 256
+    elif case.startswith("d"):
+        Cout, taps, pm = 512, K.TAPS3_DGRAD, L.PACK_DGRAD
+    W, Cin = H, C1 + C2
+    x = q(torch.randn(N, Cin, H, W), dt)
+    if pm == L.PACK_DGRAD:
+        w = q(torch.randn(Cin, Cout, 3, 3) / math.sqrt(Cin * 9), dt)   # the forward conv Cout -> Cin
+        yr = torch.nn.grad.conv2d_input((N, Cout, H, W), w, x, padding=1)
+    else:
+        w = q(torch.randn(Cout, Cin, 3, 3) / math.sqrt(Cin * 9), dt)
+        yr = F.conv2d(x, w, padding=1)
+    wp = K.pack_weight(pm, dt, w.to(DEV), L.kc_for(Cin, dt))
+    bias, addv = torch.randn(Cout), torch.randn(N, Cout)
+    resid = q(torch.randn(N, Cout, H, W), dt)
+    yr = yr + bias[:, None, None] + addv[:, :, None, None] + resid
+    xd = nhwc(x).to(dt).to(DEV)
+    x1d, x2d = (xd[..., :C1].contiguous(), xd[..., C1:].contiguous()) if C2 else (xd, None)
+    rd = nhwc(resid).to(dt).to(DEV)
+    outs, parts = [], []
+    for no_small in (0, 1):
+        dmc_opt("DMC_NO_SMALL", no_small)
+        d = K.make_desc(dt, N, H, W, C1, C2, C1, C2, L.kc_for(Cin, dt), H, W, Cout, taps)
+        part = torch.full((N * H * W // 64 * (Cout // 8) * 2,), float("nan"), device=DEV) if H == 8 else None
+        K.set_epilogue(d, bias=bias.to(DEV), addvec=addv.to(DEV), ld_add=Cout, resid=rd, ld_res=Cout, ldy1=Cout,
+                       gn_part=part)
+        y = torch.full((N, H, W, Cout), float("nan"), dtype=dt, device=DEV)
+        K.conv(d, x1d, x2d, wp, y)
+        torch.cuda.synchronize()
+        outs.append(nchw(y.float().cpu()))
+        parts.append(None if part is None else part.cpu())
+    assert rel_err(outs[0], yr) < 2e-2, rel_err(outs[0], yr)
+    assert rel_err(outs[0], outs[1]) < 1e-2, rel_err(outs[0], outs[1])
+    if H == 8:
+        # (mean, M2) per (64-pixel segment, 8-channel chunk) of the stored bf16 output, both paths
+        p0, p1 = parts[0].view(-1, 2), parts[1].view(-1, 2)
+        assert torch.isfinite(p0).all()
+        assert rel_err(p0[:, 0], p1[:, 0]) < 2e-2 and rel_err(p0[:, 1], p1[:, 1]) < 2e-2
+        yv = outs[0].permute(0, 2, 3, 1).reshape(N, 64, Cout // 8, 8)           # [segment][pixel][chunk][8]
+        mean = yv.mean(dim=(1, 3)).reshape(-1)
+        m2 = ((yv - yv.mean(dim=(1, 3), keepdim=True)) ** 2).sum(dim=(1, 3)).reshape(-1)
+        assert rel_err(p0[:, 0], mean) < 1e-4 and rel_err(p0[:, 1], m2) < 1e-4
+
+
 @pytest.mark.parametrize("shape", [(64, 8, 8, 256, 256), (128, 32, 32, 128, 0), (96, 16, 16, 136, 120),
                                    (64, 4, 4, 512, 0)])
 def test_groupnorm_stats_one_block_per_sample(shape, monkeypatch, dmc_opt):
