@@ -98,6 +98,9 @@ def _load():
                                      _c_p, _c_p]),
         "dmc_gn_apply": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p,
                                   _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_int, _c_p]),
+        "dmc_gn_apply_fin": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p,
+                                      _c_p, _c_int, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p, _c_int, _c_u32, _c_p, _c_u32,
+                                      _c_f, _c_p, _c_int, _c_p]),
         "dmc_gn_silu_bwd": (_c_int, [_c_int, _c_p, _c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int,
                                      _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_p,
                                      _c_int, _c_int, _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_p, _c_p, _c_p,

@@ -177,15 +177,13 @@ DMC_DEV void gn_chan(float& n, float& m, float& q, float nb, float mb, float qb)
   q += qb + d * d * n * r;
   n = tot;
 }
-// One wave finalises GroupNorm group g of image n: lane l combines partials l, l+64, ... (segments outer, the
-// group's chunks inner; p1's chunks, then p2's), the lanes then combine over a fixed xor tree (deterministic), and
-// mean / rstd and the folded per-channel scale / shift are written. SC1: the partials of p1 were handed off inside
-// the running launch (write-through stores + an arrival counter): read them with agent-scope (sc1) loads.
-// Used by gn_finalize_kernel (dmc_norm.hip) and by the producing conv's last block (dmc_conv.hip): bitwise equal.
+// One wave combines GroupNorm group g of image n: lane l takes partials l, l+64, ... (segments outer, the group's
+// chunks inner; p1's chunks, then p2's), the lanes then combine over a fixed xor tree (deterministic). Returns
+// (mean, rstd) in every lane. SC1: the partials of p1 were handed off inside the running launch (write-through
+// stores + an arrival counter): read them with agent-scope (sc1) loads.
 template <bool SC1>
-DMC_DEV void gn_finalize_group(const float* p1, int nch1, const float* p2, int nch2, int n, int g, int spi, int G,
-                               float eps, const float* gamma, const float* beta, float* mean_rstd, float* scale,
-                               float* shift) {
+DMC_DEV void gn_group_stats(const float* p1, int nch1, const float* p2, int nch2, int n, int g, int spi, int G,
+                            float eps, float& mean, float& rstd) {
   const int lane = threadIdx.x & 63;
   const int C = 8 * (nch1 + nch2), cpg = C / G, kpg = cpg / 8, np = spi * kpg;
   float cn = 0.f, m = 0.f, q = 0.f;
@@ -209,16 +207,32 @@ DMC_DEV void gn_finalize_group(const float* p1, int nch1, const float* p2, int n
     if ((lane & sh) == 0) gn_chan(cn, m, q, nb, mb, qb);
     else { float n2 = nb, m2 = mb, q2 = qb; gn_chan(n2, m2, q2, cn, m, q); cn = n2; m = m2; q = q2; }
   }
-  const float mean = m;
+  mean = m;
   const float var = fmaxf(q / cn, 0.f);
-  const float rstd = 1.0f / sqrtf(var + eps);
+  rstd = 1.0f / sqrtf(var + eps);
+}
+// The GroupNorm affine folded into a per-channel (scale, shift): z = x * scale + shift.
+DMC_DEV void gn_fold(float mean, float rstd, float gm, float bt, float& sc, float& sh) {
+  sc = rstd * gm;
+  sh = fmaf(-mean, sc, bt);
+}
+// One wave finalises group g of image n: gn_group_stats, then mean / rstd and the folded per-channel scale / shift.
+// Used by gn_finalize_kernel (dmc_norm.hip) and by the producing conv's last block (dmc_conv.hip): bitwise equal.
+template <bool SC1>
+DMC_DEV void gn_finalize_group(const float* p1, int nch1, const float* p2, int nch2, int n, int g, int spi, int G,
+                               float eps, const float* gamma, const float* beta, float* mean_rstd, float* scale,
+                               float* shift) {
+  const int lane = threadIdx.x & 63;
+  const int C = 8 * (nch1 + nch2), cpg = C / G;
+  float mean, rstd;
+  gn_group_stats<SC1>(p1, nch1, p2, nch2, n, g, spi, G, eps, mean, rstd);
   const size_t i = (size_t)n * G + g;
   if (lane == 0 && mean_rstd) { mean_rstd[i * 2] = mean; mean_rstd[i * 2 + 1] = rstd; }
   for (int c = g * cpg + lane; c < (g + 1) * cpg; c += 64) {
-    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-    const float sc = rstd * gm;
+    float sc, sh;
+    gn_fold(mean, rstd, gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f, sc, sh);
     scale[(size_t)n * C + c] = sc;
-    shift[(size_t)n * C + c] = bt - mean * sc;
+    shift[(size_t)n * C + c] = sh;
   }
 }
 

@@ -2175,6 +2175,199 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_halo2_kernel(ConvK a, const c
   }
 }
 
+// One-block-per-CU twin (round 4). PMC of wgrad3x3_halo2_kernel on the 32x32 128->128 layer: MFMA busy 26 %, waves
+// parked on waitcnt / barrier 32 % of their cycles, 233 MB of HBM-side traffic per launch for 67 MB of operands: the
+// single x-halo buffer is reloaded at every tile with both co-resident blocks stalling together, a 3-slot ring gives
+// each 64-pixel dy stage ~1 us of lead time, and the fp32 slab of 512 blocks x 64 x 576 partials is 75 MB written
+// + 75 MB re-read by the reduce. Here: 8 waves (2 per SIMD; wave = 32 co x 144 n: 2 x 9 accumulator tiles), the
+// SAME 64-co x (9 taps x 64 ci) block tile, one block per CU (256 blocks: half the slab), the next tile's x halo
+// DMA'd into a second buffer a whole tile ahead, and a DS-slot dy ring (DS - 1 stages of lead). Every wait is a
+// counted vmcnt derived from the issue order (no waits for younger DMA); one barrier per 64-pixel stage.
+// LDS: 2 x HPW x 8 KB (halo) + DS x 8 KB (dy) = 160 KB for (HPW, DS) = (6, 8) and (7, 6).
+DMC_DEV void wait_vm_upto16(int n) {
+  switch (n < 0 ? 0 : n) {
+    case 0: __builtin_amdgcn_s_waitcnt(waitcnt_vm(0)); break;
+    case 1: __builtin_amdgcn_s_waitcnt(waitcnt_vm(1)); break;
+    case 2: __builtin_amdgcn_s_waitcnt(waitcnt_vm(2)); break;
+    case 3: __builtin_amdgcn_s_waitcnt(waitcnt_vm(3)); break;
+    case 4: __builtin_amdgcn_s_waitcnt(waitcnt_vm(4)); break;
+    case 5: __builtin_amdgcn_s_waitcnt(waitcnt_vm(5)); break;
+    case 6: __builtin_amdgcn_s_waitcnt(waitcnt_vm(6)); break;
+    case 7: __builtin_amdgcn_s_waitcnt(waitcnt_vm(7)); break;
+    case 8: __builtin_amdgcn_s_waitcnt(waitcnt_vm(8)); break;
+    case 9: __builtin_amdgcn_s_waitcnt(waitcnt_vm(9)); break;
+    case 10: __builtin_amdgcn_s_waitcnt(waitcnt_vm(10)); break;
+    case 11: __builtin_amdgcn_s_waitcnt(waitcnt_vm(11)); break;
+    case 12: __builtin_amdgcn_s_waitcnt(waitcnt_vm(12)); break;
+    case 13: __builtin_amdgcn_s_waitcnt(waitcnt_vm(13)); break;
+    case 14: __builtin_amdgcn_s_waitcnt(waitcnt_vm(14)); break;
+    case 15: __builtin_amdgcn_s_waitcnt(waitcnt_vm(15)); break;
+    default: __builtin_amdgcn_s_waitcnt(waitcnt_vm(16)); break;   // waiting for more than needed stays correct
+  }
+}
+
+template <int HPW, int DS>
+__global__ __launch_bounds__(512, 1) void wgrad3x3_halo3_kernel(ConvK a, const char* dy, int ld_dy, int dy_bytes,
+                                                                float* slab, int R, int nimg, int tiles_per_split) {
+  using T = bf16_t;
+  constexpr int HB = HPW * 8 * 1024;     // one halo buffer: 8 waves x HPW pieces of 8 pixels x 128 B
+  constexpr int DB = 64 * 128;           // dy stage: 64 pixels x 64 co
+  __shared__ __attribute__((aligned(16))) char lds[2 * HB + DS * DB];
+  char* const dring = lds + 2 * HB;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ch = wave >> 2, nq = wave & 3;           // co half (32 co), n quarter (9 of the 36 16-wide n tiles)
+  const int c0 = blockIdx.x * 64, co0 = blockIdx.y * 64;
+  const int ntiles = a.M / 256;
+  const int t_begin = blockIdx.z * tiles_per_split, t_end = min(ntiles, t_begin + tiles_per_split);
+  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
+  const bool first = c0 < a.C1;
+  const int cs = first ? c0 : c0 - a.C1;
+  const int lds_x = first ? a.ld1 : a.ld2;
+
+  unsigned od;                                        // this wave's dy piece: stage rows wave*8 .. wave*8+7
+  {
+    const int row = wave * 8 + (lane >> 3);
+    const int pc = lane & 7;
+    const int lc = (((pc >> 1) ^ swz_x(row)) << 1) | (pc & 1);
+    const int co = co0 + lc * 8;
+    od = co < a.Cout ? ((unsigned)row * ld_dy + co) * 2u : kOOB;
+  }
+  auto halo_issue = [&](int tile, char* buf) {
+    const int m0 = tile * 256;
+    const int n_first = m0 / a.OHW;
+    const int r0 = (m0 - n_first * a.OHW) / OW;
+    unsigned hx[HPW];
+#pragma unroll
+    for (int p = 0; p < HPW; ++p) {
+      const int h = (wave * HPW + p) * 8 + (lane >> 3);
+      hx[p] = kOOB;
+      if (h < npix) {
+        const int img = h / segpix, rem = h - img * segpix;
+        const int hr = rem / HW, hc = rem - hr * HW;
+        const int iy = r0 + hr - 1, ix = hc - 1;
+        const int lc = ((((lane & 7) >> 1) ^ swz_x(h)) << 1) | (lane & 1);
+        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+          hx[p] = ((unsigned)(((n_first + img) * a.H + iy) * a.W + ix) * lds_x + cs + lc * 8) * 2u;
+      }
+    }
+    dma_pieces<HPW>(first ? (const void*)a.x1 : (const void*)a.x2, first ? a.x1_bytes : a.x2_bytes,
+                    buf + wave * HPW * 1024, hx, 0u, 0, HPW);
+  };
+  auto dy_issue = [&](int st) {
+    const int tile = t_begin + (st >> 2);
+    const unsigned base = (unsigned)(tile * 256 + (st & 3) * 64) * (unsigned)ld_dy * 2u;
+    dma_pieces<1>(dy, dy_bytes, dring + (st % DS) * DB + wave * 1024, &od, base, 0, 1);
+  };
+
+  const int fh = lane >> 4;
+  auto hrow = [&](int pl) {
+    const int img = pl / (R * OW), rem = pl - img * (R * OW);
+    const int r = rem / OW, col = rem - r * OW;
+    return img * segpix + (r + 1) * HW + col + 1;
+  };
+  const int hb0 = hrow(8 * fh), hz = hrow(0);
+  int dl[9];
+#pragma unroll
+  for (int u = 0; u < 9; ++u) {
+    const int nt = nq * 9 + u, t = nt >> 2;
+    const int ty = t / 3, tx = t - ty * 3;
+    dl[u] = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
+  }
+  v4f acc[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int u = 0; u < 9; ++u) acc[i][u] = v4f{0.f, 0.f, 0.f, 0.f};
+  const bool bias_on = a.wgb != nullptr && blockIdx.x == 0 && nq == 0;
+  const v4i ones = {0x3F803F80, 0x3F803F80, 0x3F803F80, 0x3F803F80};   // bf16 1.0 pairs
+  v4f accb[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
+
+  const int ntl = t_end - t_begin, nst = ntl * 4;
+  const int pro = min(DS - 1, nst);                  // dy stages issued in the prologue
+  // issue bookkeeping (per wave, wave-uniform): I(st) = DMA instructions issued before stage st's wait
+  auto issued_before = [&](int st) {
+    return HPW + pro + HPW * min(ntl - 1, (st + 3) >> 2) + min(st, max(0, nst - DS + 1));
+  };
+  auto pos_dy = [&](int s) {                         // issue position (1-based) of dy(s)
+    if (s < pro) return HPW + s + 1;
+    const int s1 = s - DS + 1;
+    const int h = ((s1 & 3) == 0 && (s1 >> 2) + 1 < ntl) ? HPW : 0;
+    return issued_before(s1) + h + 1;
+  };
+  auto pos_halo = [&](int tl) { return tl == 0 ? HPW : issued_before(4 * (tl - 1)) + HPW; };
+
+  halo_issue(t_begin, lds);
+  for (int q = 0; q < pro; ++q) dy_issue(q);
+  for (int st = 0; st < nst; ++st) {
+    const int tl = st >> 2, k = st & 3;
+    int need = pos_dy(st);
+    if (k == 0) need = max(need, pos_halo(tl));
+    wait_vm_upto16(issued_before(st) - need);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    // every wave is past stage st-1: its dy slot and (k == 0) the halo buffer of tile tl-1 are free
+    if (k == 0 && tl + 1 < ntl) halo_issue(t_begin + tl + 1, lds + ((tl + 1) & 1) * HB);
+    if (st + DS - 1 < nst) dy_issue(st + DS - 1);
+    const char* X = lds + (tl & 1) * HB;
+    const char* D = dring + (st % DS) * DB;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int j = k * 2 + ks;                      // 32-pixel group inside the tile
+      const int hj = __builtin_amdgcn_readfirstlane(hrow(32 * j) - hz);
+      v4i fa[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = tr_frag<128, false>(D, ks * 32 + 8 * fh, ch * 2 + i);
+      v4i fb = tr_frag<128, false>(X, hb0 + hj + dl[0], (nq * 9) & 3);
+#pragma unroll
+      for (int u = 0; u < 9; ++u) {
+        v4i fn = fb;
+        if (u + 1 < 9) fn = tr_frag<128, false>(X, hb0 + hj + dl[u + 1], (nq * 9 + u + 1) & 3);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[i][u] = mma16<T>(acc[i][u], fa[i], fb);
+        if (u + 1 < 9) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the next tile's reads
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // this tile's MFMAs
+        }
+        fb = fn;
+      }
+      if (bias_on) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) accb[i] = mma16<T>(accb[i], fa[i], ones);
+      }
+    }
+  }
+  const int Cpad = (a.Cout + 127) / 128 * 128;       // the slab layout of the other halo wgrad kernels
+  if (bias_on && (lane & 15) == 0) {                 // column 0: rows co = co0 + 16 (2 ch + i) + 4 fh + e
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int co = co0 + (ch * 2 + i) * 16 + fh * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (co + e < a.Cout) a.wgb[(size_t)blockIdx.z * Cpad + co + e] = accb[i][e];
+    }
+  }
+  const int KK = 9 * a.Kc;
+  float* out = slab + (size_t)blockIdx.z * Cpad * KK;
+  const int fr = lane & 15;
+#pragma unroll
+  for (int u = 0; u < 9; ++u) {
+    const int nt = nq * 9 + u, t = nt >> 2;
+    const int kk = t * a.Kc + c0 + (nt & 3) * 16 + fr;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int co = co0 + (ch * 2 + i) * 16 + fh * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (co + e < Cpad) out[(size_t)(co + e) * KK + kk] = acc[i][u][e];
+    }
+  }
+}
+
 // Weight gradient of a 1x1 stride-1 conv / Linear (bf16; the DiT linears, the UNet's 1x1 convs):
 // dW[co][ci] = sum_p dy[p][co] * x[p][ci]. Block = 128 co x 128 ci over a pixel range (split-K over grid.z); 4
 // waves, 2 (co halves) x 2 (ci halves) of 64 x 64. Both operands stream as SPX-pixel x 128-channel stages DMA'd
@@ -2977,10 +3170,11 @@ extern "C" int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2
 struct WgHaloPlan {
   bool ok;
   int R, nimg, splits, tps, hp;
+  bool v3;   // wgrad3x3_halo3_kernel (one 8-wave block per CU): splits for ~256 blocks
 };
 
 WgHaloPlan wgrad_halo_plan(const dmc_conv_desc* d) {
-  WgHaloPlan p{false, 0, 0, 1, 0, 0};
+  WgHaloPlan p{false, 0, 0, 1, 0, 0, false};
   if (d->dtype != DMC_BF16 || dmc::opt(dmc::OPT_NO_HALO)) return p;
   ConvK k;
   if (fill_convk(d, nullptr, nullptr, nullptr, nullptr, nullptr, k)) return p;
@@ -2996,6 +3190,16 @@ WgHaloPlan wgrad_halo_plan(const dmc_conv_desc* d) {
   p.tps = (ntiles + sp - 1) / sp;
   p.splits = (ntiles + p.tps - 1) / p.tps;
   p.ok = true;
+  if (dmc::opt(dmc::OPT_WG_HALO3)) {
+    // one block per CU: ~256 blocks of (64 ci, 64 co, tile range)
+    const int base3 = (k.Kc / 64) * dmc::cdiv(k.Cout, 64);
+    int sp3 = (256 + base3 - 1) / base3;
+    if (sp3 > ntiles) sp3 = ntiles;
+    if (sp3 < 1) sp3 = 1;
+    p.tps = (ntiles + sp3 - 1) / sp3;
+    p.splits = (ntiles + p.tps - 1) / p.tps;
+    p.v3 = true;
+  }
   return p;
 }
 
@@ -3049,7 +3253,14 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   if (halo) {
     // two blocks per CU: 64-co blocks, the same split count (twice the co tiles, half the block target's share)
     g = dim3(d->Kc / 64, dmc::cdiv(d->Cout, 64), splits);
-    if (hp.hp == 6)
+    if (hp.v3) {
+      if (hp.hp == 6)
+        wgrad3x3_halo3_kernel<6, 8><<<g, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R,
+                                                      hp.nimg, hp.tps);
+      else
+        wgrad3x3_halo3_kernel<7, 6><<<g, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R,
+                                                      hp.nimg, hp.tps);
+    } else if (hp.hp == 6)
       wgrad3x3_halo2_kernel<6><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
     else
       wgrad3x3_halo2_kernel<7><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);

@@ -553,6 +553,84 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(Src2 s, int HW, const flo
   }
 }
 
+// gn_apply_kernel with the GroupNorm statistics finalised in the same launch from the producing convs' epilogue
+// partials (dmc_conv_desc.gn_part): every block combines the partials of its image (one wave per group, exactly
+// gn_finalize_group's order: bitwise the dmc_gn_finalize statistics) while its first pixel rows are in flight, keeps
+// mean / rstd in LDS and folds scale / shift for its channels; the blocks of the first pixel split also store
+// mean_rstd (the GroupNorm backward reads it) and scale / shift. Replaces the finalize launch (~5 us + a dependent
+// kernel boundary per GroupNorm) at the price of a 2-4 KB L2 read per block.
+struct GnPart {
+  const float* p1; const float* p2; int nch1, nch2, G; float eps;
+  const float* gamma; const float* beta; float* mean_rstd; float* scale; float* shift;
+};
+template <typename T>
+__global__ __launch_bounds__(256) void gn_apply_fin_kernel(Src2 s, int HW, GnPart gp, int silu, uint32_t seed0,
+                                                           const uint32_t* seed_base, uint32_t thresh, float dscale,
+                                                           char* out, int ldo, int splits) {
+  __shared__ float smr[64][2];
+  const uint32_t seed = drop_seed(seed0, seed_base);
+  constexpr int EPC = TT<T>::KPL;
+  const int C = s.C1 + s.C2, CPR = C / EPC;
+  const int rpi = 256 / CPR;
+  const int col = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
+  const bool active = r0 < rpi;
+  const int n = blockIdx.x;
+  const int per = (HW + splits - 1) / splits;
+  const int pb = blockIdx.y * per, pe = min(HW, pb + per);
+  const int c0 = col * EPC;
+  v4i buf[UNR];
+  auto issue = [&](int p0) {
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      if (p0 + u * rpi < pe) buf[u] = load_chunk2<T>(s, n * HW + p0 + u * rpi, c0);
+  };
+  if (active && pb + r0 < pe) issue(pb + r0);   // in flight while the statistics are combined
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int g = wave; g < gp.G; g += 4) {
+    float mean, rstd;
+    gn_group_stats<false>(gp.p1, gp.nch1, gp.p2, gp.nch2, n, g, HW / 64, gp.G, gp.eps, mean, rstd);
+    if (lane == 0) {
+      smr[g][0] = mean;
+      smr[g][1] = rstd;
+      if (blockIdx.y == 0 && gp.mean_rstd) {
+        gp.mean_rstd[((size_t)n * gp.G + g) * 2] = mean;
+        gp.mean_rstd[((size_t)n * gp.G + g) * 2 + 1] = rstd;
+      }
+    }
+  }
+  __syncthreads();
+  if (!active) return;
+  const int cpg = C / gp.G;
+  float sc[EPC], sh[EPC];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) {
+    const int c = c0 + e, g = c / cpg;
+    gn_fold(smr[g][0], smr[g][1], gp.gamma ? gp.gamma[c] : 1.f, gp.beta ? gp.beta[c] : 0.f, sc[e], sh[e]);
+    if (blockIdx.y == 0 && r0 == 0 && gp.scale) {
+      gp.scale[(size_t)n * C + c] = sc[e];
+      gp.shift[(size_t)n * C + c] = sh[e];
+    }
+  }
+  for (int p0 = pb + r0; p0 < pe; p0 += UNR * rpi) {
+    if (p0 != pb + r0) issue(p0);
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      if (p0 + u * rpi >= pe) break;
+      const int pix = n * HW + p0 + u * rpi;
+      float f[EPC];
+      Chunk<T>::unpack(buf[u], f);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        float v = fmaf(f[e], sc[e], sh[e]);
+        if (silu) v = silu_f(v);
+        if (thresh) v = drop_keep((uint64_t)pix * C + c0 + e, seed, thresh) ? v * dscale : 0.f;
+        f[e] = v;
+      }
+      *(v4i*)(out + ((size_t)pix * ldo + c0) * sizeof(T)) = Chunk<T>::pack(f);
+    }
+  }
+}
+
 // dx = ka*dz + u*(x - mean) + w per element with the per-(n, c) coefficients of gn_bwd_final (vector loads).
 // Grid (N, pixel splits) like gn_apply_kernel: a thread owns one 16-byte channel chunk column of one
 // sample and walks pixels, streaming x, g in and dx out. Optionally (sum_part != NULL) it also reduces its
@@ -922,6 +1000,28 @@ extern "C" int dmc_channel_sum(int dtype, const void* dy, int N, int HW, int C, 
   else chsum_partial<bf16_t><<<g, 256, 0, s>>>((const char*)dy, HW, C, ld, splits, partial);
   chsum_finish(s, N, C, splits, partial, out_nc, ld_out, out_c, scale);
   return dmc::check_launch("dmc_channel_sum");
+}
+
+extern "C" int dmc_gn_apply_fin(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1,
+                                int ld2, const float* part1, const float* part2, int G, float eps, const float* gamma,
+                                const float* beta, float* mean_rstd, float* scale, float* shift, int silu,
+                                uint32_t drop_seed, const uint32_t* drop_seed_base, uint32_t drop_thresh,
+                                float drop_scale, void* out, int ld_out, void* stream) {
+  const int C = C1 + C2;
+  DMC_REQUIRE(dtype == DMC_BF16, "gn_apply_fin: bf16 (the conv-epilogue partials exist in bf16 mode only)");
+  DMC_REQUIRE(HW % 64 == 0 && C1 % 8 == 0 && C2 % 8 == 0 && G > 0 && G <= 64 && C % G == 0 && (C / G) % 8 == 0 &&
+                  (C2 == 0 || part2) && part1 && ld_out % 8 == 0 && C / 8 <= 256,
+              "gn_apply_fin: HW %d, C1 %d, C2 %d, G %d (64-pixel segments, 8-channel chunks inside groups)", HW, C1, C2,
+              G);
+  const int cpr = C / 8, rpi = 256 / cpr;
+  int splits = (2048 + N - 1) / N;
+  const int maxs = (HW + rpi - 1) / rpi;
+  splits = splits < maxs ? splits : maxs;
+  Src2 src{(const char*)x1, (const char*)x2, C1, C2, ld1, ld2};
+  GnPart gp{part1, part2, C1 / 8, C2 / 8, G, eps, gamma, beta, mean_rstd, scale, shift};
+  gn_apply_fin_kernel<bf16_t><<<dim3(N, splits), 256, 0, dmc::as_stream(stream)>>>(
+      src, HW, gp, silu, drop_seed, drop_seed_base, drop_thresh, drop_scale, (char*)out, ld_out, splits);
+  return dmc::check_launch("dmc_gn_apply_fin");
 }
 
 extern "C" int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1, int ld2,

@@ -234,13 +234,16 @@ def gn_stats(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, G, eps, gamma, beta):
     return sc, sh, mr
 
 
-def gn_finalize(p1, C1, p2, C2, N, HW, G, eps, gamma, beta):
-    """GroupNorm (scale, shift, mean_rstd) from the producing convs' partials (dmc_conv_desc.gn_part)."""
+def gn_finalize(p1, C1, p2, C2, N, HW, G, eps, gamma, beta, out=None):
+    """GroupNorm (scale, shift, mean_rstd) from the producing convs' partials (dmc_conv_desc.gn_part); out: the
+    three buffers to fill (allocated if None)."""
     dev = p1.device
     C = C1 + C2
-    mr = torch.empty(N * G * 2, dtype=torch.float32, device=dev)
-    sc = torch.empty(N * C, dtype=torch.float32, device=dev)
-    sh = torch.empty(N * C, dtype=torch.float32, device=dev)
+    if out is None:
+        out = (torch.empty(N * C, dtype=torch.float32, device=dev),
+               torch.empty(N * C, dtype=torch.float32, device=dev),
+               torch.empty(N * G * 2, dtype=torch.float32, device=dev))
+    sc, sh, mr = out
     check(LIB.dmc_gn_finalize(ptr(p1), C1, ptr(p2), C2, N, HW, G, eps, ptr(gamma), ptr(beta), ptr(mr), ptr(sc),
                               ptr(sh), L.stream()), "dmc_gn_finalize")
     return sc, sh, mr
@@ -255,6 +258,26 @@ def gn_apply(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, scale, shift, silu=True, dr
     check(LIB.dmc_gn_apply(L.dtype_code(dtype), ptr(x1), ptr(x2), N, HW, C1, C2, ld1, ld2, ptr(scale), ptr(shift),
                            int(silu), seed, base, thresh, dscale, ptr(out), C, L.stream()), "dmc_gn_apply")
     return out
+
+
+def gn_apply_fin(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, p1, p2, G, eps, gamma, beta, silu=True, drop=None,
+                 out=None, stats=None):
+    """gn_finalize + gn_apply in one launch (bitwise equal to the pair). stats: (scale, shift, mean_rstd) buffers
+    to fill, allocated if None. Returns (out, (scale, shift, mean_rstd))."""
+    C = C1 + C2
+    dev = x1.device
+    if stats is None:
+        stats = (torch.empty(N * C, dtype=torch.float32, device=dev),
+                 torch.empty(N * C, dtype=torch.float32, device=dev),
+                 torch.empty(N * G * 2, dtype=torch.float32, device=dev))
+    sc, sh, mr = stats
+    if out is None:
+        out = torch.empty(N * HW * C, dtype=dtype, device=dev)
+    seed, base, thresh, dscale = drop_args(drop)
+    check(LIB.dmc_gn_apply_fin(L.dtype_code(dtype), ptr(x1), ptr(x2), N, HW, C1, C2, ld1, ld2, ptr(p1), ptr(p2), G,
+                               eps, ptr(gamma), ptr(beta), ptr(mr), ptr(sc), ptr(sh), int(silu), seed, base, thresh,
+                               dscale, ptr(out), C, L.stream()), "dmc_gn_apply_fin")
+    return out, stats
 
 
 def gn_bwd(dtype, g, ld_g, x1, x2, N, HW, C1, C2, ld1, ld2, G, mr, gamma, beta, silu, drop, dx1, dx2, ld_dx1,

@@ -54,6 +54,42 @@ _GNB_DROP = os.environ.get("DMC_GNB_DROP", "1") not in ("", "0")   # ... also at
 # its stores before its arrival add, and the image's last block runs the combine on the kernel's critical path
 _GN_FIN = _GN_PARTIALS and os.environ.get("DMC_GN_FIN", "0") not in ("", "0")
 
+# GroupNorm statistics from epilogue partials finalised inside the apply launch (dmc_gn_apply_fin: each block
+# combines its image's partials while its first rows load) instead of a dmc_gn_finalize launch before it. A/B
+# switch DMC_GN_APPLY_FIN=0.
+_GN_APPLY_FIN = _GN_PARTIALS and os.environ.get("DMC_GN_APPLY_FIN", "1") not in ("", "0")
+
+
+class GnSt:
+    """GroupNorm statistics (scale, shift, mean_rstd) of one site, computed lazily from the producing convs'
+    partials: the apply that materialises the normalised activation finalises them in its own launch
+    (K.gn_apply_fin); a consumer that needs them earlier (a conv prologue) triggers dmc_gn_finalize. Indexes and
+    unpacks like the (scale, shift, mean_rstd) tuple of the other paths."""
+
+    __slots__ = ("args", "bufs", "done")
+
+    def __init__(self, args, N, C, G, dev):
+        self.args = args          # (p1, C1, p2, C2, N, HW, G, eps, gamma, beta)
+        self.bufs = (torch.empty(N * C, dtype=torch.float32, device=dev),
+                     torch.empty(N * C, dtype=torch.float32, device=dev),
+                     torch.empty(N * G * 2, dtype=torch.float32, device=dev))
+        self.done = False
+
+    def realize(self):
+        if not self.done:
+            K.gn_finalize(*self.args, out=self.bufs)
+            self.done = True
+        return self.bufs
+
+    def __getitem__(self, i):
+        return self.realize()[i]
+
+    def __iter__(self):
+        return iter(self.realize())
+
+    def __len__(self):
+        return 3
+
 
 class GnbReq:
     """A request for the GroupNorm-backward sums from an input-gradient conv (ExecCore._gnb_epi): epi is the
@@ -422,6 +458,9 @@ class UNetExecutor(ExecCore):
         if (all(s.part is not None for s in srcs) and (a.H * a.W) % 64 == 0 and C % gn.num_groups == 0
                 and (C // gn.num_groups) % 8 == 0):
             # statistics from the producing convs' epilogue partials: no pass over the activation
+            if _GN_APPLY_FIN and self.dt == torch.bfloat16 and gn.num_groups <= 64 and C <= 2048:
+                return GnSt((a.part, a.C, b.part if b else None, b.C if b else 0, N, a.H * a.W, gn.num_groups,
+                             gn.eps, gn.weight, gn.bias), N, C, gn.num_groups, a.t.device)
             return K.gn_finalize(a.part, a.C, b.part if b else None, b.C if b else 0, N, a.H * a.W, gn.num_groups,
                                  gn.eps, gn.weight, gn.bias)
         return K.gn_stats(dtype, a.t, b.t if b else None, N, a.H * a.W, a.C, b.C if b else 0, a.t.shape[-1],
@@ -433,6 +472,13 @@ class UNetExecutor(ExecCore):
         b = srcs[1] if len(srcs) > 1 else None
         N = a.t.shape[0]
         C = a.C + (b.C if b else 0)
+        if isinstance(st, GnSt) and not st.done:
+            p1, C1, p2, C2, _, HW, G, eps, gamma, beta = st.args
+            out, _ = K.gn_apply_fin(self.dt, a.t, b.t if b else None, N, HW, C1, C2, a.t.shape[-1],
+                                    b.t.shape[-1] if b else 0, p1, p2, G, eps, gamma, beta, silu=silu, drop=drop,
+                                    stats=st.bufs)
+            st.done = True
+            return Act(out.view(N, a.H, a.W, C), a.H, a.W, C)
         out = K.gn_apply(self.dt, a.t, b.t if b else None, N, a.H * a.W, a.C, b.C if b else 0, a.t.shape[-1],
                          b.t.shape[-1] if b else 0, st[0], st[1], silu=silu, drop=drop)
         return Act(out.view(N, a.H, a.W, C), a.H, a.W, C)
@@ -452,7 +498,8 @@ class UNetExecutor(ExecCore):
             C1, C2 = a.C, (b.C if b else 0)
             d = K.make_desc(self.dt, N, a.H, a.W, C1, C2, key[5], key[6], L.kc_for(C1 + C2, self.dt), a.H, a.W, Cout,
                             K.TAPS3)
-            K.set_prologue(d, L.PRO_AFFINE_SILU, st[0], st[1], C1 + C2)
+            bufs = st.bufs if isinstance(st, GnSt) else st     # pointers only: no statistics launch here
+            K.set_prologue(d, L.PRO_AFFINE_SILU, bufs[0], bufs[1], C1 + C2)
             ok = self._halo_pro_cache[key] = K.conv_halo_prologue(d)
         return ok
 
@@ -578,12 +625,12 @@ class UNetExecutor(ExecCore):
                 hs.append(h)
         # ---- output: GN -> SiLU -> conv3x3 -> NCHW fp32 ----
         gno, convo = m.output[0], m.output[2]
-        sc, sh, mr = self._gn([h], gno)
-        ao = self._apply([h], (sc, sh, mr), silu=True)
+        sto = self._gn([h], gno)
+        ao = self._apply([h], sto, silu=True)
         out = torch.empty(N, m.out_channels, H, W, dtype=f32, device=x.device)
         self._conv([ao], convo, K.TAPS3, H, W, m.out_channels, bias=convo.bias, out=out, out_f32=True, out_nchw=True)
         if keep:
-            tape.append(("out", h, (sc, sh, mr), ao))
+            tape.append(("out", h, sto, ao))
         return out, tape
 
     def _layer(self, srcs, layer, tape, fin=None):

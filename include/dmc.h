@@ -201,6 +201,15 @@ int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C
                  const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* out, int ld_out,
                  void* stream);
 
+/* dmc_gn_finalize + dmc_gn_apply in one launch: every block combines its image's partials (bitwise the
+ * dmc_gn_finalize statistics) while its first rows load; mean_rstd / scale / shift (may be NULL) are stored too.
+ * bf16 only (the conv-epilogue partials exist in bf16 mode). */
+int dmc_gn_apply_fin(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1, int ld2,
+                     const float* part1, const float* part2, int G, float eps, const float* gamma, const float* beta,
+                     float* mean_rstd, float* scale, float* shift, int silu, uint32_t drop_seed,
+                     const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* out, int ld_out,
+                     void* stream);
+
 /* Backward of a = dropout(SiLU(GroupNorm(x))) (silu=1) or a = GroupNorm(x) (silu=0, AttentionBlock
  * norm :80): g = dL/da (dtype, [pix][ld_g]); writes
  * dx (split into dx1/dx2 by channel like the sources; accumulate_k: add into existing),

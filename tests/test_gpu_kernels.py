@@ -838,6 +838,36 @@ def test_conv_epilogue_groupnorm_partials(case, dmc_opt):
         assert rel_err(got, ref) < 2e-5, (case, rel_err(got, ref))
 
 
+@pytest.mark.parametrize("N,HW,C1,C2", [(128, 1024, 128, 0), (128, 256, 256, 256), (128, 64, 512, 256),
+                                        (4, 1024, 256, 128), (3, 64, 64, 0)])
+@pytest.mark.parametrize("silu,dropout", [(True, False), (True, True), (False, False)])
+def test_gn_apply_fin_bitwise(N, HW, C1, C2, silu, dropout):
+    """dmc_gn_apply_fin (the finalize folded into the apply launch: every block combines its image's epilogue
+    partials itself) is BITWISE dmc_gn_finalize followed by dmc_gn_apply: output, mean_rstd, scale and shift."""
+    from diffusion_models_collection_amd import kernels as K
+    gen = torch.Generator().manual_seed(N * 7 + HW + C1 + C2)
+    G, dt, C = 8, torch.bfloat16, C1 + C2
+    x1 = torch.randn(N * HW, C1, generator=gen).to(DEV).to(dt)
+    x2 = torch.randn(N * HW, C2, generator=gen).to(DEV).to(dt) if C2 else None
+
+    def parts(c):     # [N*HW/64][c/8] (mean, M2) pairs of 512-element chunks
+        m = torch.randn(N * HW // 64, c // 8, 1, generator=gen) * 0.5 + 1.0
+        q = torch.rand(N * HW // 64, c // 8, 1, generator=gen) * 512.0
+        return torch.cat([m, q], -1).reshape(-1).to(DEV)
+
+    p1, p2 = parts(C1), (parts(C2) if C2 else None)
+    gamma = torch.randn(C, generator=gen).to(DEV)
+    beta = torch.randn(C, generator=gen).to(DEV)
+    drop = (1234, int(0.1 * 2 ** 32), 1.0 / 0.9) if dropout else None
+    sc, sh, mr = K.gn_finalize(p1, C1, p2, C2, N, HW, G, 1e-5, gamma, beta)
+    ref = K.gn_apply(dt, x1, x2, N, HW, C1, C2, C1, C2, sc, sh, silu=silu, drop=drop)
+    out, (sc2, sh2, mr2) = K.gn_apply_fin(dt, x1, x2, N, HW, C1, C2, C1, C2, p1, p2, G, 1e-5, gamma, beta,
+                                          silu=silu, drop=drop)
+    torch.cuda.synchronize()
+    assert torch.equal(mr, mr2) and torch.equal(sc, sc2) and torch.equal(sh, sh2)
+    assert torch.equal(ref, out)
+
+
 @pytest.mark.parametrize("case", ["halo2_3x3", "glds1x1_2b", "glds1x1_8wave", "splitk_small", "concat_two",
                                   "cfg2_small"])
 @pytest.mark.parametrize("silu,dropout", [(True, False), (True, True), (False, False)])

@@ -735,6 +735,7 @@ def test_groupnorm_finalize_in_producing_conv_bitwise(mode, monkeypatch):
         return orig(*a, **kw)
 
     monkeypatch.setattr(K, "gn_finalize", counted)
+    monkeypatch.setattr(UE, "_GN_APPLY_FIN", False)
     res = []
     for on in (True, False):
         monkeypatch.setattr(UE, "_GN_FIN", on)
@@ -750,6 +751,60 @@ def test_groupnorm_finalize_in_producing_conv_bitwise(mode, monkeypatch):
     (o1, g1, n1), (o0, g0, n0) = res
     print(f"{mode}: gn_finalize launches {n1} (fused) vs {n0}")
     assert n0 > 20 and n1 <= n0 // 4, (n1, n0)
+    assert torch.equal(o1, o0)
+    for k in g0:
+        assert torch.equal(g1[k], g0[k]), k
+
+
+@pytest.mark.parametrize("mode", ["eval", "train"])
+def test_groupnorm_finalize_in_apply_bitwise(mode, monkeypatch):
+    """The GroupNorm statistics finalised inside the apply launch (dmc_gn_apply_fin, every block combines its
+    image's epilogue partials) instead of a dmc_gn_finalize launch before dmc_gn_apply: the bf16 CIFAR UNet at
+    B=128 gives BITWISE the same output (eval) / loss and every gradient (train, dropout 0). In training every
+    finalize launch whose GroupNorm is materialised disappears; in eval the halo-prologue convs still finalise."""
+    from diffusion_models_collection_amd.models import UNet, _unet_exec as UE
+    from diffusion_models_collection_amd import kernels as K
+    cfg = dict(image_size=(32, 32), in_channels=3, model_channels=128, out_channels=3, num_res_blocks=2,
+               attention_resolutions=(16, 8), dropout=0.0, channel_mult=(1, 2, 2, 2), num_classes=None,
+               use_attention=True)
+    torch.manual_seed(42)
+    m = UNet(**cfg, compute_dtype="bf16").to(DEV)
+    m.train() if mode == "train" else m.eval()
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn(128, 3, 32, 32, generator=gen).to(DEV)
+    t = torch.randint(0, 1000, (128,), generator=gen).to(DEV)
+    calls = {"fin": 0, "apply_fin": 0}
+    orig_f, orig_a = K.gn_finalize, K.gn_apply_fin
+
+    def cf(*a, **kw):
+        calls["fin"] += 1
+        return orig_f(*a, **kw)
+
+    def ca(*a, **kw):
+        calls["apply_fin"] += 1
+        return orig_a(*a, **kw)
+
+    monkeypatch.setattr(K, "gn_finalize", cf)
+    monkeypatch.setattr(K, "gn_apply_fin", ca)
+    monkeypatch.setattr(UE, "_GN_FIN", False)
+    res = []
+    for on in (True, False):
+        monkeypatch.setattr(UE, "_GN_APPLY_FIN", on)
+        calls.update(fin=0, apply_fin=0)
+        m.zero_grad(set_to_none=True)
+        if mode == "train":
+            out = m(x.clone().requires_grad_(True), t)
+            (out.float() ** 2).mean().backward()
+            res.append((out.detach().clone(), {k: p.grad.clone() for k, p in m.named_parameters()}, dict(calls)))
+        else:
+            with torch.no_grad():
+                res.append((m(x, t).clone(), {}, dict(calls)))
+    (o1, g1, c1), (o0, g0, c0) = res
+    print(f"{mode}: fused {c1} vs separate {c0}")
+    assert c0["apply_fin"] == 0 and c1["apply_fin"] > 0
+    assert c1["fin"] + c1["apply_fin"] == c0["fin"], (c1, c0)
+    if mode == "train":
+        assert c1["fin"] == 0, c1
     assert torch.equal(o1, o0)
     for k in g0:
         assert torch.equal(g1[k], g0[k]), k
