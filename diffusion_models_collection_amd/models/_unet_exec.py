@@ -55,9 +55,11 @@ _GNB_DROP = os.environ.get("DMC_GNB_DROP", "1") not in ("", "0")   # ... also at
 _GN_FIN = _GN_PARTIALS and os.environ.get("DMC_GN_FIN", "0") not in ("", "0")
 
 # GroupNorm statistics from epilogue partials finalised inside the apply launch (dmc_gn_apply_fin: each block
-# combines its image's partials while its first rows load) instead of a dmc_gn_finalize launch before it. A/B
-# switch DMC_GN_APPLY_FIN=0.
-_GN_APPLY_FIN = _GN_PARTIALS and os.environ.get("DMC_GN_APPLY_FIN", "1") not in ("", "0")
+# combines its image's partials while its first rows load) instead of a dmc_gn_finalize launch before it. Opt-in
+# (DMC_GN_APPLY_FIN=1): measured slower on MI355X (same box, B=128, 2 reps: train 8418/8470 vs 8648/8693 img/s,
+# DDIM-50 599 vs 629; with the halo prologue off 558 vs 618) -- the 2048 blocks of an apply each repeat the
+# per-image combine (two dependent partial loads + 6 shuffle rounds per group) on their own critical path.
+_GN_APPLY_FIN = _GN_PARTIALS and os.environ.get("DMC_GN_APPLY_FIN", "0") not in ("", "0")
 
 
 class GnSt:

@@ -7,7 +7,7 @@ traces / PMC passes of the same command (the eager step's dispatch sequence is d
 
 Algorithmic work per op (each tensor read or written once; fp32 weight-gradient slabs, split-K partials and re-reads
 excluded): conv 2*M*Cout*taps*Cin FLOP, bytes = input + output (+ residual) + packed weights; wgrad the same FLOP,
-bytes = dy + x + fp32 dw; GroupNorm stats 1 read, apply 1 read + 1 write, backward x + g read, dx written (+ dx read
+bytes = dy + x + fp32 dw; GroupNorm stats 1 read, apply 1 read + 1 write (+ the epilogue partials when it finalises), backward x + g read, dx written (+ dx read
 when accumulating); attention 4*B*h*L^2*d FLOP forward / 8*B*h*L^2*d backward; AdamW+EMA 36 B per parameter, grad
 norm 4 B per parameter; weight pack 4 B read + 2 B written per element.
 
@@ -68,6 +68,11 @@ def a_gn_apply(dtype, x1, x2, N, HW, C1, C2, *a, **k):
     return 0.0, 2 * N * HW * (C1 + C2) * x1.element_size(), f"N{N} HW{HW} C{C1 + C2}"
 
 
+def a_gn_apply_fin(dtype, x1, x2, N, HW, C1, C2, *a, **k):
+    C = C1 + C2
+    return 0.0, 2 * N * HW * C * x1.element_size() + N * HW // 64 * C // 8 * 8, f"N{N} HW{HW} C{C}"
+
+
 def a_gn_bwd(dtype, g, ld_g, x1, x2, N, HW, C1, C2, ld1, ld2, G, mr, gamma, beta, silu, drop, dx1, dx2, ld_dx1,
              ld_dx2, acc1, acc2, *a, **k):
     e = g.element_size()
@@ -117,7 +122,7 @@ def wrap(mod, name, alg):
 
 
 for nm, alg in [("conv", a_conv), ("wgrad", a_wgrad), ("gn_stats", a_gn_stats), ("gn_finalize", a_gn_finalize),
-                ("gn_apply", a_gn_apply), ("gn_bwd", a_gn_bwd), ("attn_fwd", a_attn_fwd), ("attn_bwd", a_attn_bwd),
+                ("gn_apply", a_gn_apply), ("gn_apply_fin", a_gn_apply_fin), ("gn_bwd", a_gn_bwd), ("attn_fwd", a_attn_fwd), ("attn_bwd", a_attn_bwd),
                 ("adamw_flat_dev", a_adamw_dev), ("adamw_flat", a_adamw), ("grad_norm_flat", a_grad_norm), ("pack_input", a_gn_none),
                 ("loss_fwd", a_gn_none), ("loss_bwd", a_gn_none), ("add_", a_gn_none), ("upsample2x", a_gn_none),
                 ("channel_sum", a_gn_none), ("time_embed", a_gn_none), ("unpack_output", a_gn_none)]:
