@@ -783,6 +783,170 @@ __global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* cf, ch
   }
 }
 
+// gn_bwd_one + gn_bwd_apply in ONE launch for small samples (the 16x16 and smaller levels): a 1024-thread block owns
+// one channel slice of one sample, loads its x and g rows ONCE into registers (NR 16-byte chunks of each per
+// thread, NR <= 4), reduces the per-channel sums in exactly gn_bwd_one's order (same A / coefficients), then writes dx from
+// the registers with gn_bwd_apply's formula -- one HBM pass over x and g instead of two and one launch instead of
+// two. The per-(n, c) pixel sums of the stored dx (bias / time-embedding gradients) are reduced in-block and
+// written directly; dgamma / dbeta and the per-c sums are column sums over n (gn_bwd_finish_kernel).
+template <int NR>
+__global__ __launch_bounds__(1024) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]*/, char* dx1, char* dx2, int ld1,
+                                                     int ld2, int acc1, int acc2, float* sums /*[N][C]*/,
+                                                     float* out_nc, int ld_nc) {
+  using T = bf16_t;
+  constexpr int EPC = 8;
+  const int n = blockIdx.x;
+  const uint32_t dseed = drop_seed(b.dseed, b.dseed_base);
+  const int C = b.s.C1 + b.s.C2, cpg = C / b.G, G = b.G, HW = b.HW;
+  const int Cs = C / (int)gridDim.y, cb = (int)blockIdx.y * Cs, g0 = cb / cpg;
+  const int CPR = Cs / EPC, rpi = 1024 / CPR;
+  const int tid = threadIdx.x, col = tid % CPR, r0 = tid / CPR;
+  const bool active = r0 < rpi;
+  __shared__ float red[1024][2 * EPC];
+  __shared__ float sA[1024][2];
+  __shared__ float sm[64][2];
+  const int c0 = cb + col * EPC;
+  const bool first = c0 < b.s.C1;
+  char* const dst = first ? dx1 : dx2;
+  const int ldd = first ? ld1 : ld2, cd = first ? c0 : c0 - b.s.C1, acc = first ? acc1 : acc2;
+  v4i bx[NR], bg[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const int p = r0 + j * rpi;
+    if (active && p < HW) {
+      bx[j] = load_chunk2<T>(b.s, n * HW + p, c0);
+      bg[j] = *(const v4i*)(b.g + ((size_t)(n * HW + p) * b.ld_g + c0) * sizeof(T));
+    }
+  }
+  float mean[EPC], rstd[EPC], gm[EPC], bt[EPC], a1[EPC], a2[EPC];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) {
+    const int c = c0 + e, g = c / cpg;
+    mean[e] = b.mr[((size_t)n * G + g) * 2];
+    rstd[e] = b.mr[((size_t)n * G + g) * 2 + 1];
+    gm[e] = b.gamma ? b.gamma[c] : 1.f;
+    bt[e] = b.beta ? b.beta[c] : 0.f;
+    a1[e] = 0.f; a2[e] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const int p = r0 + j * rpi;
+    if (!(active && p < HW)) break;
+    const int pix = n * HW + p;
+    float x[EPC], gv[EPC];
+    Chunk<T>::unpack(bx[j], x);
+    Chunk<T>::unpack(bg[j], gv);
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      float g = gv[e];
+      if (b.dthresh) g = drop_keep((uint64_t)pix * C + c0 + e, dseed, b.dthresh) ? g * b.dscale : 0.f;
+      float xh;
+      const float dz = gn_dz(x[e], g, mean[e], rstd[e], gm[e], bt[e], xh, b.silu);
+      a1[e] += dz;
+      a2[e] = fmaf(dz, xh, a2[e]);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) { red[tid][2 * e] = active ? a1[e] : 0.f; red[tid][2 * e + 1] = active ? a2[e] : 0.f; }
+  __syncthreads();
+  onecta_chan_totals<EPC>(red, Cs, CPR, rpi, sA);   // sA[c - cb]
+  __syncthreads();
+  for (int c = tid; c < Cs; c += 1024) {
+    A[((size_t)n * C + cb + c) * 2] = sA[c][0];
+    A[((size_t)n * C + cb + c) * 2 + 1] = sA[c][1];
+  }
+  const float cnt = (float)cpg * (float)HW;
+  const int wv = tid >> 6, ln = tid & 63;
+  for (int gl = wv; gl < Cs / cpg; gl += 16) {   // one wave per group: gamma-weighted channel totals
+    const int g = g0 + gl;
+    float m1 = 0.f, m2 = 0.f;
+    for (int c = g * cpg + ln; c < (g + 1) * cpg; c += 64) {
+      const float g_ = b.gamma ? b.gamma[c] : 1.f;
+      m1 = fmaf(sA[c - cb][0], g_, m1); m2 = fmaf(sA[c - cb][1], g_, m2);
+    }
+    m1 = wave_sum(m1); m2 = wave_sum(m2);
+    if (ln == 0) { sm[gl][0] = m1 / cnt; sm[gl][1] = m2 / cnt; }
+  }
+  // the accumulate operand is read while the group sums finish
+  v4i bp[NR];
+  if (acc) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int p = r0 + j * rpi;
+      if (active && p < HW) bp[j] = *(const v4i*)(dst + ((size_t)(n * HW + p) * ldd + cd) * sizeof(T));
+    }
+  }
+  __syncthreads();
+  if (!active && !sums) return;
+  // gn_bwd_final's per-channel coefficients (same expressions)
+  float sc[EPC], sh[EPC], ka[EPC], ku[EPC], km[EPC], kw[EPC], sum[EPC];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) {
+    const int c = c0 + e, gl = c / cpg - g0;
+    const float rs = rstd[e], mu = mean[e];
+    sc[e] = rs * gm[e];
+    sh[e] = bt[e] - mu * sc[e];
+    ka[e] = sc[e];
+    ku[e] = -rs * rs * sm[gl][1];
+    km[e] = mu;
+    kw[e] = -rs * sm[gl][0];
+    sum[e] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const int p = r0 + j * rpi;
+    if (!(active && p < HW)) break;
+    const int pix = n * HW + p;
+    float x[EPC], gv[EPC], o[EPC];
+    Chunk<T>::unpack(bx[j], x);
+    Chunk<T>::unpack(bg[j], gv);
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      float gg = gv[e];
+      if (b.dthresh) gg = drop_keep((uint64_t)pix * C + c0 + e, dseed, b.dthresh) ? gg * b.dscale : 0.f;
+      float dz = gg;
+      if (b.silu) {
+        const float z = fmaf(x[e], sc[e], sh[e]);
+        const float sg = sigmoid_f(z);
+        dz = gg * sg * (1.f + z * (1.f - sg));
+      }
+      o[e] = fmaf(ka[e], dz, fmaf(ku[e], x[e] - km[e], kw[e]));
+    }
+    if (acc) {
+      float prev[EPC];
+      Chunk<T>::unpack(bp[j], prev);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) o[e] += prev[e];
+    }
+    const v4i packed = Chunk<T>::pack(o);
+    *(v4i*)(dst + ((size_t)pix * ldd + cd) * sizeof(T)) = packed;
+    if (sums) {
+      Chunk<T>::unpack(packed, o);   // sum what was stored
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) sum[e] += o[e];
+    }
+  }
+  if (!sums) return;
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) red[tid][e] = active ? sum[e] : 0.f;
+  __syncthreads();
+  for (int cl = tid; cl < Cs; cl += 1024) {
+    float v = 0.f;
+    for (int r = 0; r < rpi; ++r) v += red[r * CPR + cl / EPC][cl % EPC];
+    sums[(size_t)n * C + cb + cl] = v;
+    if (out_nc) out_nc[(size_t)n * ld_nc + cb + cl] = v;
+  }
+}
+
+// dgamma / dbeta (column sums of A over n) and, when asked, the per-c sums of dx (column sums of gn_bwd_fused's
+// [N][C] sums): one launch of 64-column blocks.
+__global__ __launch_bounds__(1024) void gn_bwd_finish_kernel(const float* A, const float* sums, int N, int C,
+                                                             float* dbeta, float* dgamma, float* out_c) {
+  const int nb = (C + 63) / 64;
+  if ((int)blockIdx.x < nb) colsum_block<16>(A, N, C, (long)C * 2, 2, blockIdx.x * 64, dbeta, dgamma, 1.f);
+  else colsum_block<16>(sums, N, C, C, 1, (blockIdx.x - nb) * 64, out_c, nullptr, 1.f);
+}
+
 // ---------------- per-channel pixel sums ----------------
 template <typename T>
 __global__ __launch_bounds__(256) void chsum_partial(const char* dy, int HW, int C, int ld, int splits, float* partial) {
@@ -954,6 +1118,29 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
   const bool want_sums = dx_sum_nc || dx_sum_c;
   dim3 gr(N, b.splits);
   const long one_max = dmc::opt(dmc::OPT_GN_BWD_ONE_MAX);   // A/B knob
+  // the one-pass fused kernel when a channel slice's rows fit NR <= DMC_GN_BWD_FUSED (<= 4) chunks per thread
+  // (S <= 8 channel slices of whole groups per sample, N*S >= 256 blocks to fill the chip)
+  const int fused_max = (int)dmc::opt(dmc::OPT_GN_BWD_FUSED);
+  if (!part && dtype != DMC_F32 && N >= 64 && fused_max > 0 && !dmc::opt(dmc::OPT_GN_BWD_SPLIT)) {
+    auto rows = [&](int s_) { const int rp = 1024 / (C / s_ / epc); return (HW + rp - 1) / rp; };
+    auto ok = [&](int s_) { return C % s_ == 0 && (C / s_) % (C / G) == 0 && (C / s_) % epc == 0; };
+    int S = 1;
+    while ((N * S < 256 || rows(S) > fused_max) && S < 8 && ok(S * 2)) S *= 2;
+    const int nr = rows(S);
+    if (nr <= fused_max && nr <= 4) {   // NR = 8 spills (x, g, accumulate operand and coefficients > 128 VGPRs)
+      float* ssum = want_sums ? sums : nullptr;
+      const dim3 gf(N, S);
+#define DMC_GNBF(NR_) gn_bwd_fused<NR_><<<gf, 1024, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
+                                                         accumulate1, accumulate2, ssum, dx_sum_nc, ld_sum_nc)
+      if (nr <= 1) DMC_GNBF(1);
+      else if (nr <= 2) DMC_GNBF(2);
+      else DMC_GNBF(4);
+#undef DMC_GNBF
+      const int nb = (C + 63) / 64 + (dx_sum_c ? (C + 63) / 64 : 0);
+      gn_bwd_finish_kernel<<<nb, 1024, 0, s>>>(A, ssum, N, C, dbeta, dgamma, dx_sum_c);
+      return dmc::check_launch("dmc_gn_silu_bwd");
+    }
+  }
   if (part) {
     // the per-(64-pixel segment, channel) sums came from the input-gradient conv's epilogue (dmc_gn_bwd_epi):
     // [n][HW/64][C][2] is gn_bwd_final's partial layout with HW/64 splits

@@ -488,6 +488,62 @@ def test_groupnorm_backward_one_block_per_sample(shape, monkeypatch, dmc_opt):
     assert rel_err(res[("0", False)][0], dxk) > 1e-2
 
 
+@pytest.mark.parametrize("shape", [(128, 32, 32, 128, 0), (128, 16, 16, 256, 256), (64, 8, 8, 256, 256),
+                                   (128, 4, 4, 256, 0), (128, 16, 16, 384, 0), (96, 8, 8, 512, 0)])
+def test_groupnorm_backward_fused_one_pass(shape, dmc_opt):
+    """bf16 at N >= 64: the one-pass GroupNorm backward (gn_bwd_fused: a channel slice of a sample per 1024-thread
+    block, x and g held in registers between the reduction and the dx pass) vs the two-pass kernels
+    (DMC_GN_BWD_FUSED=0) and torch fp32 autograd: dx with dropout and accumulation, dgamma / dbeta, and the fused
+    per-(n, c) / per-c pixel sums of the stored dx."""
+    L, K = _lib()
+    torch.manual_seed(8)
+    N, H, W, C1, C2 = shape
+    G, C, dt, HW = 8, C1 + C2, torch.bfloat16, shape[1] * shape[2]
+    x = q(torch.randn(N, C, H, W) * 1.3 + 0.4, dt).requires_grad_(True)
+    gamma = (torch.rand(C) + 0.5).requires_grad_(True)
+    beta = torch.randn(C).requires_grad_(True)
+    a = F.silu(F.group_norm(x, G, gamma, beta, 1e-5))
+    gout = q(torch.randn_like(a), dt)
+    a.backward(gout)
+    xd = nhwc(x.detach()).to(dt).to(DEV)
+    x1, x2 = xd[..., :C1].contiguous(), (xd[..., C1:].contiguous() if C2 else None)
+    gd, gm_d, bt_d = nhwc(gout).to(dt).to(DEV), gamma.detach().to(DEV), beta.detach().to(DEV)
+    _, _, mr = K.gn_stats(dt, x1, x2, N, HW, C1, C2, C1, C2, G, 1e-5, gm_d, bt_d)
+    prev = q(torch.randn(N, H, W, C), dt).to(dt).to(DEV)
+    res = {}
+    for fused in (4, 0):
+        dmc_opt("DMC_GN_BWD_FUSED", fused)
+        for drop in (None, (11, 1 << 30, 4.0 / 3.0)):
+            dx1, dx2 = torch.empty_like(x1), (torch.empty_like(x2) if C2 else None)
+            dg, db = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+            K.gn_bwd(dt, gd, C, x1, x2, N, HW, C1, C2, C1, C2, G, mr, gm_d, bt_d, True, drop, dx1, dx2, C1, C2,
+                     0, 0, dg, db)
+            out = [(torch.cat([dx1, dx2], -1) if C2 else dx1).float().cpu(), dg.cpu(), db.cpu()]
+            if not C2:   # single source: accumulate into dx and the fused pixel sums
+                dxs = prev.clone()
+                snc = torch.full((N, C + 8), -7.0, device=DEV)
+                sc_ = torch.empty(C, device=DEV)
+                K.gn_bwd(dt, gd, C, x1, None, N, HW, C, 0, C, 0, G, mr, gm_d, bt_d, True, drop, dxs, None, C, 0, 1, 0,
+                         dg, db, dx_sum_nc=snc, ld_sum_nc=C + 8, dx_sum_c=sc_)
+                torch.cuda.synchronize()
+                ref_nc = dxs.float().sum((1, 2))
+                tag = f"fused={fused} drop={drop is not None}"
+                assert rel_err(snc[:, :C], ref_nc) < 1e-4, (tag, rel_err(snc[:, :C], ref_nc),
+                                                            (snc[:, :C] == -7.0).float().mean().item())
+                assert (snc[:, C:] == -7.0).all(), tag
+                assert rel_err(sc_, ref_nc.sum(0)) < 1e-4, (tag, rel_err(sc_, ref_nc.sum(0)))
+                assert rel_err(dxs.float().cpu(), out[0] + prev.float().cpu()) < 1e-2
+                out.append(snc[:, :C].cpu())
+            res[(fused, drop is None)] = out
+    dxk, dgk, dbk = res[(4, True)][:3]
+    assert rel_err(nchw(dxk), x.grad) < 2e-2
+    assert rel_err(dgk, gamma.grad) < 1e-4 and rel_err(dbk, beta.grad) < 1e-4
+    for nodrop in (True, False):
+        for u, v in zip(res[(4, nodrop)], res[(0, nodrop)]):
+            assert rel_err(u, v) < 1e-2, (nodrop, rel_err(u, v))
+    assert rel_err(res[(4, False)][0], dxk) > 1e-2
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_groupnorm_stats_and_backward(dt):
     L, K = _lib()
