@@ -58,8 +58,11 @@ def build(force: bool = False, verbose: bool = True) -> Path:
         list(ex.map(run, jobs))
     objs = [BUILD / (Path(s).stem + ".o") for s in SOURCES]
     if force or jobs or _stale(LIB, objs):
-        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", str(LIB)] + [str(o) for o in objs]
+        # link to a temporary name and rename: a snapshot of the tree never holds a half-written library
+        tmp = LIB.with_name(LIB.name + ".tmp")
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", str(tmp)] + [str(o) for o in objs]
         run(cmd)
+        os.replace(tmp, LIB)
     return LIB
 
 

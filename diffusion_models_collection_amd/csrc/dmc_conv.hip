@@ -920,6 +920,159 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Persistent 1x1-conv GEMM (bf16, stride 1, bias-only epilogue): Y[M][Cout] = X[M][K] W[Cout][K]^T + bias -- the
+// AttentionBlock qkv projection (models/unet.py:83), the ResBlock 1x1 shortcuts (:70) and the 1x1 input gradients
+// that start a gradient buffer. With K = 256-768 a 128x128 tile has only 4-12 LDS-DMA stages, and the per-tile
+// kernel above spends most of a block on the latency of its first stages and on its LDS-staged epilogue (an 8x8
+// qkv launch: ~13 us per round of tiles). Here one block per CU walks a CONTIGUOUS range of tiles (the output-
+// channel tiles of one pixel tile adjacent: that tile comes from HBM once, then from L2) and streams their
+// K stages through an NS-slot ring that runs across tile boundaries; the epilogue (bias, bf16 pack, one 8-byte
+// store of 4 channels per accumulator) is done from the accumulators, without LDS, so the next tile's stages
+// keep landing under it. The stores count in vmcnt like the DMA: every wait is counted from the issue positions
+// (pos[] = the wave's VMEM instruction count after each stage's issue), never a drain.
+DMC_DEV void wait_vm_upto40(int n) {
+  switch (n < 0 ? 0 : n) {
+#define DMC_W(i) case i: __builtin_amdgcn_s_waitcnt(waitcnt_vm(i)); break;
+    DMC_W(0) DMC_W(1) DMC_W(2) DMC_W(3) DMC_W(4) DMC_W(5) DMC_W(6) DMC_W(7) DMC_W(8) DMC_W(9) DMC_W(10)
+    DMC_W(11) DMC_W(12) DMC_W(13) DMC_W(14) DMC_W(15) DMC_W(16) DMC_W(17) DMC_W(18) DMC_W(19) DMC_W(20)
+    DMC_W(21) DMC_W(22) DMC_W(23) DMC_W(24) DMC_W(25) DMC_W(26) DMC_W(27) DMC_W(28) DMC_W(29) DMC_W(30)
+    DMC_W(31) DMC_W(32) DMC_W(33) DMC_W(34) DMC_W(35) DMC_W(36) DMC_W(37) DMC_W(38) DMC_W(39)
+#undef DMC_W
+    default: __builtin_amdgcn_s_waitcnt(waitcnt_vm(40)); break;   // waiting for more than needed stays correct
+  }
+}
+
+template <int NS>
+__global__ __launch_bounds__(256, 1) void gemm1x1_persist_kernel(ConvK a, int ntiles, int NB, int tpb) {
+  using T = bf16_t;
+  constexpr int BM = 128, BN = 128, AI = 4, BI = 4, SB = (BM + BN) * 128;
+  __shared__ __attribute__((aligned(16))) char lds[NS * SB + 4096];
+  float* const sbias = (float*)(lds + NS * SB);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave % 2, wn = wave / 2;
+  const int lrow = lane >> 3, lc = (lane & 7) ^ lrow;
+  const int fr = lane & 15, fh = lane >> 4;
+  const int t_begin = blockIdx.x * tpb, t_end = min(ntiles, t_begin + tpb);
+  if (t_begin >= t_end) return;
+  const int kst = a.Kc / 64, total = (t_end - t_begin) * kst;
+  // every output channel's bias into LDS: the epilogue then reads no global memory
+  for (int c = threadIdx.x; c < NB * BN; c += 256) sbias[c] = (a.bias && c < a.Cout) ? a.bias[c] : 0.f;
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+
+  unsigned o1[AI], o2[AI], ob[BI];
+  int it_tile = -1;
+  auto issue = [&](int S) {
+    const int ti = t_begin + S / kst, k = S - (S / kst) * kst;
+    if (ti != it_tile) {   // the issue pointer entered a new tile: its rows' source offsets
+      it_tile = ti;
+      const int mb = ti / NB, nb = ti - mb * NB;
+#pragma unroll
+      for (int j = 0; j < AI; ++j) {
+        const unsigned pix = (unsigned)(mb * BM + (wave * AI + j) * 8 + lrow);
+        o1[j] = (pix * a.ld1 + lc * 8) * 2u;
+        o2[j] = (pix * a.ld2 + lc * 8) * 2u;
+      }
+#pragma unroll
+      for (int j = 0; j < BI; ++j) {
+        const unsigned co = (unsigned)(nb * BN + (wave * BI + j) * 8 + lrow);
+        ob[j] = (co * a.Kc + lc * 8) * 2u;
+      }
+    }
+    glds_issue_buf<AI, BI, BM>(a, lds + (S % NS) * SB, k * 64, (unsigned)k * 128u, wave, o1, o2, ob);
+  };
+  int nvm = 0;        // this wave's VMEM instructions so far
+  int pos[NS];        // nvm right after stage S's issue, slot S % NS
+#pragma unroll
+  for (int q = 0; q < NS; ++q) pos[q] = 0;
+  for (int q = 0; q < NS - 1 && q < total; ++q) {
+    issue(q);
+    nvm += AI + BI;
+    pos[q] = nvm;
+  }
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < total; ++s) {
+    // stage s has landed once at most the VMEM instructions issued after it are outstanding
+    int mine = 0;
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+      if (q == s % NS) mine = pos[q];
+    wait_vm_upto40(nvm - mine);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    if (s + NS - 1 < total) {
+      issue(s + NS - 1);
+      nvm += AI + BI;
+#pragma unroll
+      for (int q = 0; q < NS; ++q)
+        if (q == (s + NS - 1) % NS) pos[q] = nvm;
+    }
+    const char* A = lds + (s % NS) * SB;
+    const char* B = A + BM * 128;
+    v4i fa[2][4], fb[2][4];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = ks * 4 + fh;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wn * 64 + i * 16 + fr;
+        fa[ks][i] = *(const v4i*)(B + r * 128 + ((chunk ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = wm * 64 + j * 16 + fr;
+        fb[ks][j] = *(const v4i*)(A + r * 128 + ((chunk ^ (r & 7)) << 4));
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[ks][i], fb[ks][j]);
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+    if ((s + 1) % kst == 0) {
+      // tile done: bias + bf16 pack from the accumulators, 16 unconditional 8-byte stores per lane
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      const int t = t_begin + s / kst, mb = t / NB, nb = t - mb * NB;
+      const int m0 = mb * BM, n0 = nb * BN;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = n0 + wn * 64 + i * 16 + fh * 4;
+        const v4f bv = *(const v4f*)(sbias + co);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int px = m0 + wm * 64 + j * 16 + fr;
+          const v4f v = acc[i][j] + bv;
+          v2i o;
+          o[0] = (int)f2bf2(v[0], v[1]);
+          o[1] = (int)f2bf2(v[2], v[3]);
+          *(v2i*)(a.y1 + ((size_t)px * a.ldy1 + co) * 2) = o;
+          acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      nvm += 16;
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // 3x3 stride-1 conv (forward, or dgrad with the flipped tap grid) with the activation HALO resident in
 // LDS. A block computes 256 output pixels (whole rows: R rows x OW of nimg image segments) x 128
 // channels. Per 64-channel chunk, the (R+2) x (OW+2) halo of every segment is DMA'd into LDS once and
@@ -2882,11 +3035,15 @@ void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
     const int bm = p.cfg == 0 ? 256 : p.cfg == 1 ? 128 : 64;
     const int nb = dmc::cdiv(k.Cout, 128);
     const dim3 g = dmc::opt(dmc::OPT_NO_XCD) ? dim3(dmc::cdiv(k.M, bm), nb) : dim3(dmc::cdiv(k.M, bm) * nb);
-    if (p.cfg == 0 && dmc::opt(dmc::OPT_GLDS_2B)) {
+    if (p.cfg == 0 && (dmc::opt(dmc::OPT_GLDS_2B) & 1)) {
       // A/B: 128x128 tiles, 2-stage ring, two blocks per CU
       const dim3 g2 = dmc::opt(dmc::OPT_NO_XCD) ? dim3(dmc::cdiv(k.M, 128), nb) : dim3(dmc::cdiv(k.M, 128) * nb);
       conv_fwd_glds_kernel<2, 2, BUF, 2><<<g2, 256, 0, s>>>(k);
     } else if (p.cfg == 0) conv_fwd_glds_kernel<4, 2, BUF><<<g, 512, 0, s>>>(k);
+    else if (p.cfg == 1 && (dmc::opt(dmc::OPT_GLDS_2B) & 2) && (long)dmc::cdiv(k.M, 128) * nb > 256)
+      // more 128x128 tiles than CUs: the 2-stage ring fits two blocks per CU (one round instead of two; the
+      // 8x8 attention qkv GEMM: 384 tiles)
+      conv_fwd_glds_kernel<2, 2, BUF, 2><<<g, 256, 0, s>>>(k);
     else if (p.cfg == 1) conv_fwd_glds_kernel<2, 2, BUF><<<g, 256, 0, s>>>(k);
     else conv_fwd_glds_kernel<1, 2, BUF><<<g, 128, 0, s>>>(k);
   }
@@ -2993,7 +3150,23 @@ bool epi_gnb_ok(const ConvK& k, const void* ws, size_t ws_bytes) {
   if (split) return false;
   int R, nimg;
   if (buf && !dmc::opt(dmc::OPT_NO_HALO) && halo2_plan(k, &R, &nimg)) return true;
-  return p.splits > 1 || p.cfg != 0 || dmc::opt(dmc::OPT_GLDS_2B);
+  return p.splits > 1 || p.cfg != 0 || (dmc::opt(dmc::OPT_GLDS_2B) & 1);
+}
+
+// The persistent 1x1 GEMM applies (bf16 1x1 stride-1, 64-aligned channel sources, plain bias epilogue, whole
+// 128x128 tiles, enough tiles to give every CU one block): returns the tiles per block, or 0.
+int gemm1x1_plan(const ConvK& k) {
+  if (!dmc::opt(dmc::OPT_GEMM1X1) || k.dtype_bytes != 2 || k.ntaps != 1 || k.stride != 1 || k.mode != DMC_MODE_NORMAL ||
+      k.tdy0 || k.tdx0 || k.H != k.OH || k.W != k.OW || k.prologue != DMC_PRO_NONE)
+    return 0;
+  if (k.C1 % 64 || k.C2 % 64 || k.Kc != k.C1 + k.C2 || k.x1_bytes == 0 || (k.C2 && k.x2_bytes == 0) || k.w_bytes == 0)
+    return 0;
+  if (k.addvec || k.resid || k.silu_pre || k.gst || k.gsk || k.gb_on || k.fin_on || k.act != DMC_ACT_NONE || k.sk ||
+      k.Csplit != k.Cout || k.out_f32 || k.out_nchw || (k.ldy1 & 3) || k.M % 128 || k.Cout % 128 || k.Cout > 1024)
+    return 0;
+  const long ntiles = (long)(k.M / 128) * (k.Cout / 128);
+  if (ntiles < 128) return 0;
+  return (int)((ntiles + 255) / 256);
 }
 
 template <typename T>
@@ -3028,6 +3201,14 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
   if (sizeof(T) == 2) {
     const int mt = small_plan(k);
     if (mt) { launch_small(k, mt, s); return dmc::check_launch("dmc_conv2d"); }
+  }
+  if (sizeof(T) == 2) {
+    const int tpb = gemm1x1_plan(k);
+    if (tpb) {
+      const int NB = k.Cout / 128, ntiles = (k.M / 128) * NB;
+      gemm1x1_persist_kernel<4><<<dmc::cdiv(ntiles, tpb), 256, 0, s>>>(k, ntiles, NB, tpb);
+      return dmc::check_launch("dmc_conv2d");
+    }
   }
   if (sizeof(T) == 2 && k.prologue == DMC_PRO_AFFINE_SILU) {
     int R, nimg;
@@ -3081,6 +3262,17 @@ int wgrad_splits(const dmc_conv_desc* d, int* pps) {
   const long minpix = dmc::opt(dmc::OPT_WG_MINPIX) > 4 * sp ? dmc::opt(dmc::OPT_WG_MINPIX) : 4 * sp;
   const long max_splits = (M + minpix - 1) / minpix;
   if (splits > max_splits) splits = max_splits;
+  // the fp32 slab (splits x KK x Cout) against the operands (dy + x): on the small maps the split count that fills
+  // the chip writes and re-reads ~10x the operand bytes. DMC_WG_SLAB_RATIO caps the ratio (0 = no cap, the
+  // default): measured, every cap is slower (same box, B=128 train: no cap 9069/9070 img/s, 8: 9011/9028,
+  // 4: 8749/8763, 2: 8164/8157) -- the blocks the cap removes cost more than the slab bytes it saves
+  const long ratio = dmc::opt(dmc::OPT_WG_SLAB_RATIO);
+  if (ratio > 0) {
+    const long eb = d->dtype == DMC_F32 ? 4 : 2;
+    const long opnd = M * (d->Cout + (long)(d->C1 + d->C2) * d->stride * d->stride) * eb;
+    const long per_split = KK * d->Cout * 4;
+    while (splits > 1 && splits * per_split > ratio * opnd) splits = (splits + 1) / 2;
+  }
   if (splits < 1) splits = 1;
   long per = (M + splits - 1) / splits;
   per = (per + sp - 1) / sp * sp;
@@ -3186,6 +3378,12 @@ WgHaloPlan wgrad_halo_plan(const dmc_conv_desc* d) {
   const int target = (int)dmc::opt(dmc::OPT_WG_HALO_TARGET);   // blocks of 128 co (the 64-co kernel runs twice as many)
   int sp = (target + base - 1) / base;
   if (sp > ntiles) sp = ntiles;
+  {  // slab cap (see wgrad_splits): splits x 9 Kc x Cout fp32 against dy + x
+    const long ratio = dmc::opt(dmc::OPT_WG_SLAB_RATIO);
+    const long opnd = (long)k.M * (k.Cout + k.C1 + k.C2) * 2;
+    const long per_split = 9L * k.Kc * dmc::cdiv(k.Cout, 128) * 128 * 4;
+    while (ratio > 0 && sp > 1 && sp * per_split > ratio * opnd) sp = (sp + 1) / 2;
+  }
   if (sp < 1) sp = 1;
   p.tps = (ntiles + sp - 1) / sp;
   p.splits = (ntiles + p.tps - 1) / p.tps;

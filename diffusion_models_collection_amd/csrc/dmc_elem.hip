@@ -38,12 +38,12 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"DMC_NO_HALO", 0},    {"DMC_HALO_PRO", 1},
     {"DMC_GN_STATS_SPLIT", 0}, {"DMC_GN_BWD_SPLIT", 0}, {"DMC_ATTN_STAGED", 0},    {"DMC_ATTN_HG", 0},
     {"DMC_WG_BLOCKS", 512}, {"DMC_GN_STATS_ONE_MAX", 1l << 20}, {"DMC_GN_BWD_ONE_MAX", 65536},
-    {"DMC_NO_XCD", 0}, {"DMC_NO_EPI_STATS", 0}, {"DMC_HALO_NOSCHED", 0}, {"DMC_GLDS_2B", 1}, {"DMC_WG_MINPIX", 0},
+    {"DMC_NO_XCD", 0}, {"DMC_NO_EPI_STATS", 0}, {"DMC_HALO_NOSCHED", 0}, {"DMC_GLDS_2B", 3}, {"DMC_WG_MINPIX", 0},
     {"DMC_WG_1X1", 1}, {"DMC_GN_BWD_SLICES", 2},
     {"DMC_WG_TAPS", 0}, {"DMC_NO_SKGN", 0},
     {"DMC_WG_HALO_TARGET", 256},
     {"DMC_STAMP_PTR", 0},
-    {"DMC_SK_TARGET", 240}, {"DMC_SK_MAX", 8}, {"DMC_NO_SMALL", 0}, {"DMC_NO_NHALO", 0}, {"DMC_SMALL_MASK", 1}, {"DMC_WG_HALO3", 0}, {"DMC_GN_BWD_FUSED", 4},
+    {"DMC_SK_TARGET", 240}, {"DMC_SK_MAX", 8}, {"DMC_NO_SMALL", 0}, {"DMC_NO_NHALO", 0}, {"DMC_SMALL_MASK", 1}, {"DMC_WG_HALO3", 0}, {"DMC_GN_BWD_FUSED", 4}, {"DMC_WG_SLAB_RATIO", 0}, {"DMC_GEMM1X1", 1},
 };
 struct OptTable {
   long v[OPT_COUNT];

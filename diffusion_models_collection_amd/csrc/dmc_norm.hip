@@ -795,39 +795,50 @@ __global__ __launch_bounds__(1024) void gn_bwd_fused(GnBwd b, float* A /*[n][C][
                                                      float* out_nc, int ld_nc) {
   using T = bf16_t;
   constexpr int EPC = 8;
+  constexpr bool EARLY_ACC = NR <= 2;   // the accumulate operand loaded with x and g (register budget allows it)
   const int n = blockIdx.x;
   const uint32_t dseed = drop_seed(b.dseed, b.dseed_base);
   const int C = b.s.C1 + b.s.C2, cpg = C / b.G, G = b.G, HW = b.HW;
   const int Cs = C / (int)gridDim.y, cb = (int)blockIdx.y * Cs, g0 = cb / cpg;
   const int CPR = Cs / EPC, rpi = 1024 / CPR;
+  const int rows = rpi < HW ? rpi : HW;   // row-threads that hold pixels (the rest only add zeros)
   const int tid = threadIdx.x, col = tid % CPR, r0 = tid / CPR;
-  const bool active = r0 < rpi;
+  const bool active = r0 < rows;
   __shared__ float red[1024][2 * EPC];
   __shared__ float sA[1024][2];
   __shared__ float sm[64][2];
+  __shared__ float sG[1024];
   const int c0 = cb + col * EPC;
   const bool first = c0 < b.s.C1;
   char* const dst = first ? dx1 : dx2;
   const int ldd = first ? ld1 : ld2, cd = first ? c0 : c0 - b.s.C1, acc = first ? acc1 : acc2;
-  v4i bx[NR], bg[NR];
+  v4i bx[NR], bg[NR], bp[NR];
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
     const int p = r0 + j * rpi;
     if (active && p < HW) {
       bx[j] = load_chunk2<T>(b.s, n * HW + p, c0);
       bg[j] = *(const v4i*)(b.g + ((size_t)(n * HW + p) * b.ld_g + c0) * sizeof(T));
+      if (EARLY_ACC && acc) bp[j] = *(const v4i*)(dst + ((size_t)(n * HW + p) * ldd + cd) * sizeof(T));
     }
   }
-  float mean[EPC], rstd[EPC], gm[EPC], bt[EPC], a1[EPC], a2[EPC];
+  // a thread's 8 channels lie in one group (groups are whole 8-channel chunks): one (mean, rstd) pair
+  const int gt = c0 / cpg;
+  const float mean = b.mr[((size_t)n * G + gt) * 2], rstd = b.mr[((size_t)n * G + gt) * 2 + 1];
+  float gm[EPC], bt[EPC], a1[EPC], a2[EPC];
+  {
+    const v4f one = {1.f, 1.f, 1.f, 1.f}, zero = {0.f, 0.f, 0.f, 0.f};
+    const v4f g0v = b.gamma ? *(const v4f*)(b.gamma + c0) : one, g1v = b.gamma ? *(const v4f*)(b.gamma + c0 + 4) : one;
+    const v4f b0v = b.beta ? *(const v4f*)(b.beta + c0) : zero, b1v = b.beta ? *(const v4f*)(b.beta + c0 + 4) : zero;
 #pragma unroll
-  for (int e = 0; e < EPC; ++e) {
-    const int c = c0 + e, g = c / cpg;
-    mean[e] = b.mr[((size_t)n * G + g) * 2];
-    rstd[e] = b.mr[((size_t)n * G + g) * 2 + 1];
-    gm[e] = b.gamma ? b.gamma[c] : 1.f;
-    bt[e] = b.beta ? b.beta[c] : 0.f;
-    a1[e] = 0.f; a2[e] = 0.f;
+    for (int e = 0; e < 4; ++e) { gm[e] = g0v[e]; gm[e + 4] = g1v[e]; bt[e] = b0v[e]; bt[e + 4] = b1v[e]; }
   }
+  if (r0 == 0) {
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) sG[col * EPC + e] = gm[e];
+  }
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) { a1[e] = 0.f; a2[e] = 0.f; }
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
     const int p = r0 + j * rpi;
@@ -841,7 +852,7 @@ __global__ __launch_bounds__(1024) void gn_bwd_fused(GnBwd b, float* A /*[n][C][
       float g = gv[e];
       if (b.dthresh) g = drop_keep((uint64_t)pix * C + c0 + e, dseed, b.dthresh) ? g * b.dscale : 0.f;
       float xh;
-      const float dz = gn_dz(x[e], g, mean[e], rstd[e], gm[e], bt[e], xh, b.silu);
+      const float dz = gn_dz(x[e], g, mean, rstd, gm[e], bt[e], xh, b.silu);
       a1[e] += dz;
       a2[e] = fmaf(dz, xh, a2[e]);
     }
@@ -849,7 +860,7 @@ __global__ __launch_bounds__(1024) void gn_bwd_fused(GnBwd b, float* A /*[n][C][
 #pragma unroll
   for (int e = 0; e < EPC; ++e) { red[tid][2 * e] = active ? a1[e] : 0.f; red[tid][2 * e + 1] = active ? a2[e] : 0.f; }
   __syncthreads();
-  onecta_chan_totals<EPC>(red, Cs, CPR, rpi, sA);   // sA[c - cb]
+  onecta_chan_totals<EPC>(red, Cs, CPR, rows, sA);   // sA[c - cb] (rows past `rows` held zeros)
   __syncthreads();
   for (int c = tid; c < Cs; c += 1024) {
     A[((size_t)n * C + cb + c) * 2] = sA[c][0];
@@ -858,18 +869,15 @@ __global__ __launch_bounds__(1024) void gn_bwd_fused(GnBwd b, float* A /*[n][C][
   const float cnt = (float)cpg * (float)HW;
   const int wv = tid >> 6, ln = tid & 63;
   for (int gl = wv; gl < Cs / cpg; gl += 16) {   // one wave per group: gamma-weighted channel totals
-    const int g = g0 + gl;
     float m1 = 0.f, m2 = 0.f;
-    for (int c = g * cpg + ln; c < (g + 1) * cpg; c += 64) {
-      const float g_ = b.gamma ? b.gamma[c] : 1.f;
-      m1 = fmaf(sA[c - cb][0], g_, m1); m2 = fmaf(sA[c - cb][1], g_, m2);
+    for (int cl = gl * cpg + ln; cl < (gl + 1) * cpg; cl += 64) {
+      const float g_ = sG[cl];
+      m1 = fmaf(sA[cl][0], g_, m1); m2 = fmaf(sA[cl][1], g_, m2);
     }
     m1 = wave_sum(m1); m2 = wave_sum(m2);
     if (ln == 0) { sm[gl][0] = m1 / cnt; sm[gl][1] = m2 / cnt; }
   }
-  // the accumulate operand is read while the group sums finish
-  v4i bp[NR];
-  if (acc) {
+  if (!EARLY_ACC && acc) {   // read while the group sums finish
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       const int p = r0 + j * rpi;
@@ -879,17 +887,13 @@ __global__ __launch_bounds__(1024) void gn_bwd_fused(GnBwd b, float* A /*[n][C][
   __syncthreads();
   if (!active && !sums) return;
   // gn_bwd_final's per-channel coefficients (same expressions)
-  float sc[EPC], sh[EPC], ka[EPC], ku[EPC], km[EPC], kw[EPC], sum[EPC];
+  const int gl = gt - g0;
+  const float ku = -rstd * rstd * sm[gl][1], kw = -rstd * sm[gl][0];
+  float sc[EPC], sh[EPC], sum[EPC];
 #pragma unroll
   for (int e = 0; e < EPC; ++e) {
-    const int c = c0 + e, gl = c / cpg - g0;
-    const float rs = rstd[e], mu = mean[e];
-    sc[e] = rs * gm[e];
-    sh[e] = bt[e] - mu * sc[e];
-    ka[e] = sc[e];
-    ku[e] = -rs * rs * sm[gl][1];
-    km[e] = mu;
-    kw[e] = -rs * sm[gl][0];
+    sc[e] = rstd * gm[e];
+    sh[e] = bt[e] - mean * sc[e];
     sum[e] = 0.f;
   }
 #pragma unroll
@@ -910,7 +914,7 @@ __global__ __launch_bounds__(1024) void gn_bwd_fused(GnBwd b, float* A /*[n][C][
         const float sg = sigmoid_f(z);
         dz = gg * sg * (1.f + z * (1.f - sg));
       }
-      o[e] = fmaf(ka[e], dz, fmaf(ku[e], x[e] - km[e], kw[e]));
+      o[e] = fmaf(sc[e], dz, fmaf(ku, x[e] - mean, kw));
     }
     if (acc) {
       float prev[EPC];
@@ -927,12 +931,14 @@ __global__ __launch_bounds__(1024) void gn_bwd_fused(GnBwd b, float* A /*[n][C][
     }
   }
   if (!sums) return;
+  float (*red1)[2 * EPC] = red;
 #pragma unroll
-  for (int e = 0; e < EPC; ++e) red[tid][e] = active ? sum[e] : 0.f;
+  for (int e = 0; e < EPC; ++e) { red1[tid][2 * e] = active ? sum[e] : 0.f; red1[tid][2 * e + 1] = 0.f; }
+  __syncthreads();
+  onecta_chan_totals<EPC>(red, Cs, CPR, rows, sA);   // the same fixed-order lane-parallel channel totals
   __syncthreads();
   for (int cl = tid; cl < Cs; cl += 1024) {
-    float v = 0.f;
-    for (int r = 0; r < rpi; ++r) v += red[r * CPR + cl / EPC][cl % EPC];
+    const float v = sA[cl][0];
     sums[(size_t)n * C + cb + cl] = v;
     if (out_nc) out_nc[(size_t)n * ld_nc + cb + cl] = v;
   }

@@ -23,6 +23,7 @@ SHAPES = {
     "r512_4": (128, 4, 4, 256, 256, 256, "3"),
     "qkv_16": (128, 16, 16, 256, 0, 768, "1"),
     "p1_8": (128, 8, 8, 256, 0, 256, "1"),
+    "qkv_8": (128, 8, 8, 256, 0, 768, "1"),
     "p1_16": (128, 16, 16, 256, 0, 256, "1"),
     "r256_8": (128, 8, 8, 256, 0, 256, "3"),
     "r256_4": (128, 4, 4, 256, 0, 256, "3"),

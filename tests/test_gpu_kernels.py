@@ -894,6 +894,36 @@ def test_conv_epilogue_groupnorm_partials(case, dmc_opt):
         assert rel_err(got, ref) < 2e-5, (case, rel_err(got, ref))
 
 
+@pytest.mark.parametrize("N,H,C1,C2,Cout", [(128, 16, 256, 0, 768), (128, 8, 256, 0, 768), (128, 32, 256, 0, 128),
+                                           (128, 16, 256, 256, 256), (128, 16, 768, 0, 256), (64, 8, 512, 0, 256)])
+def test_gemm1x1_persistent_bitwise(N, H, C1, C2, Cout, dmc_opt):
+    """The persistent 1x1 GEMM (gemm1x1_persist_kernel: tiles streamed through one LDS-DMA ring across tile
+    boundaries, bias epilogue from the accumulators) is BITWISE the per-tile LDS-DMA kernel (DMC_GEMM1X1=0): same
+    fragments, same K order, same rounding; and both match an fp32 torch GEMM of the bf16 operands."""
+    from diffusion_models_collection_amd import _lib as L, kernels as K
+    gen = torch.Generator().manual_seed(N + H + C1 + C2 + Cout)
+    dt = torch.bfloat16
+    x1 = torch.randn(N, H, H, C1, generator=gen).to(dt).to(DEV)
+    x2 = torch.randn(N, H, H, C2, generator=gen).to(dt).to(DEV) if C2 else None
+    w = (torch.randn(Cout, C1 + C2, 1, 1, generator=gen) * 0.05).to(DEV)
+    b = torch.randn(Cout, generator=gen).to(DEV)
+    Kc = L.kc_for(C1 + C2, dt)
+    wp = K.pack_weight(L.PACK_FWD, dt, w, Kc)
+    outs = []
+    for on in (1, 0):
+        dmc_opt("DMC_GEMM1X1", on)
+        y = torch.full((N, H, H, Cout), 7.0, device=DEV, dtype=dt)
+        d = K.make_desc(dt, N, H, H, C1, C2, C1, C2, Kc, H, H, Cout, K.TAPS1)
+        K.set_epilogue(d, bias=b, ldy1=Cout)
+        K.conv(d, x1, x2, wp, y)
+        outs.append(y)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    xs = torch.cat([x1, x2], -1) if C2 else x1
+    ref = xs.float().reshape(-1, C1 + C2) @ w.view(Cout, -1).to(dt).float().t() + b
+    assert rel_err(outs[0].float().reshape(-1, Cout), ref) < 1e-2
+
+
 @pytest.mark.parametrize("N,HW,C1,C2", [(128, 1024, 128, 0), (128, 256, 256, 256), (128, 64, 512, 256),
                                         (4, 1024, 256, 128), (3, 64, 64, 0)])
 @pytest.mark.parametrize("silu,dropout", [(True, False), (True, True), (False, False)])
