@@ -930,6 +930,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
 // store of 4 channels per accumulator) is done from the accumulators, without LDS, so the next tile's stages
 // keep landing under it. The stores count in vmcnt like the DMA: every wait is counted from the issue positions
 // (pos[] = the wave's VMEM instruction count after each stage's issue), never a drain.
+// Ring depth (DMC_GEMM1X1): 2 = a 2-slot ring (68 KB), two blocks per CU, 512 blocks -- the default: same box, B=128:
+// train 9300/9306 img/s, DDIM-50 694/690 vs the per-tile kernel's 9123/9115, 665/660 (a 4-slot ring with one block
+// per CU, DMC_GEMM1X1=1: 9182/9194, 672/672). Kernel trace (scripts/conv_probe.py): the 16x16 qkv GEMM 30.5 us
+// (per-tile 35.9), 8x8 qkv 11.9 (14.2), 16x16 256->256 12.7 (15.4).
 DMC_DEV void wait_vm_upto40(int n) {
   switch (n < 0 ? 0 : n) {
 #define DMC_W(i) case i: __builtin_amdgcn_s_waitcnt(waitcnt_vm(i)); break;
@@ -943,7 +947,7 @@ DMC_DEV void wait_vm_upto40(int n) {
 }
 
 template <int NS>
-__global__ __launch_bounds__(256, 1) void gemm1x1_persist_kernel(ConvK a, int ntiles, int NB, int tpb) {
+__global__ __launch_bounds__(256, NS <= 2 ? 2 : 1) void gemm1x1_persist_kernel(ConvK a, int ntiles, int NB, int tpb) {
   using T = bf16_t;
   constexpr int BM = 128, BN = 128, AI = 4, BI = 4, SB = (BM + BN) * 128;
   __shared__ __attribute__((aligned(16))) char lds[NS * SB + 4096];
@@ -3020,7 +3024,10 @@ void launch_halo2(const ConvK& k, int hp, int R, int nimg, hipStream_t s) {
 template <bool BUF>
 void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
   if (p.splits > 1) {
-    conv_fwd_glds_kernel<2, 2, BUF><<<dim3(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128), p.splits), 256, 0, s>>>(k);
+    if (dmc::opt(dmc::OPT_SK_2B))   // A/B: the 2-stage ring, two split blocks per CU
+      conv_fwd_glds_kernel<2, 2, BUF, 2><<<dim3(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128), p.splits), 256, 0, s>>>(k);
+    else
+      conv_fwd_glds_kernel<2, 2, BUF><<<dim3(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128), p.splits), 256, 0, s>>>(k);
     const int Cpad = dmc::cdiv(k.Cout, 128) * 128;
     if (k.gsk && k.M % 64 == 0 && k.Cout % 8 == 0 && !k.out_f32 && !k.out_nchw && k.Csplit == k.Cout) {
       launch_splitk_epi_gn(k, p.splits, Cpad, s);
@@ -3166,7 +3173,8 @@ int gemm1x1_plan(const ConvK& k) {
     return 0;
   const long ntiles = (long)(k.M / 128) * (k.Cout / 128);
   if (ntiles < 128) return 0;
-  return (int)((ntiles + 255) / 256);
+  const long blocks = dmc::opt(dmc::OPT_GEMM1X1) == 2 ? 512 : 256;   // 2: the 2-slot ring, two blocks per CU
+  return (int)((ntiles + blocks - 1) / blocks);
 }
 
 template <typename T>
@@ -3206,7 +3214,10 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     const int tpb = gemm1x1_plan(k);
     if (tpb) {
       const int NB = k.Cout / 128, ntiles = (k.M / 128) * NB;
-      gemm1x1_persist_kernel<4><<<dmc::cdiv(ntiles, tpb), 256, 0, s>>>(k, ntiles, NB, tpb);
+      if (dmc::opt(dmc::OPT_GEMM1X1) == 2)
+        gemm1x1_persist_kernel<2><<<dmc::cdiv(ntiles, tpb), 256, 0, s>>>(k, ntiles, NB, tpb);
+      else
+        gemm1x1_persist_kernel<4><<<dmc::cdiv(ntiles, tpb), 256, 0, s>>>(k, ntiles, NB, tpb);
       return dmc::check_launch("dmc_conv2d");
     }
   }

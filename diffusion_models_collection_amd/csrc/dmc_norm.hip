@@ -1127,7 +1127,8 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
   // the one-pass fused kernel when a channel slice's rows fit NR <= DMC_GN_BWD_FUSED (<= 4) chunks per thread
   // (S <= 8 channel slices of whole groups per sample, N*S >= 256 blocks to fill the chip)
   const int fused_max = (int)dmc::opt(dmc::OPT_GN_BWD_FUSED);
-  if (!part && dtype != DMC_F32 && N >= 64 && fused_max > 0 && !dmc::opt(dmc::OPT_GN_BWD_SPLIT)) {
+  if (!part && dtype != DMC_F32 && N >= 64 && fused_max > 0 && !dmc::opt(dmc::OPT_GN_BWD_SPLIT) &&
+      HW <= dmc::opt(dmc::OPT_GN_BWD_FUSED_MAXHW)) {
     auto rows = [&](int s_) { const int rp = 1024 / (C / s_ / epc); return (HW + rp - 1) / rp; };
     auto ok = [&](int s_) { return C % s_ == 0 && (C / s_) % (C / G) == 0 && (C / s_) % epc == 0; };
     int S = 1;
