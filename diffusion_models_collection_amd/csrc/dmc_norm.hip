@@ -584,12 +584,44 @@ __global__ __launch_bounds__(256) void gn_apply_fin_kernel(Src2 s, int HW, GnPar
     for (int u = 0; u < UNR; ++u)
       if (p0 + u * rpi < pe) buf[u] = load_chunk2<T>(s, n * HW + p0 + u * rpi, c0);
   };
-  if (active && pb + r0 < pe) issue(pb + r0);   // in flight while the statistics are combined
+  // The partials are loaded FIRST (their values return ahead of the pixel rows: the combine never waits behind the
+  // rows), every group at once: LG = the group's partial count rounded up to a power of two lanes, 64 / LG groups per
+  // wave. The butterfly over LG lanes is gn_group_stats' 64-lane tree with its identity rounds (empty lanes) left
+  // out, so the statistics stay bitwise those of dmc_gn_finalize.
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int g = wave; g < gp.G; g += 4) {
-    float mean, rstd;
-    gn_group_stats<false>(gp.p1, gp.nch1, gp.p2, gp.nch2, n, g, HW / 64, gp.G, gp.eps, mean, rstd);
-    if (lane == 0) {
+  const int spi = HW / 64, Cp = 8 * (gp.nch1 + gp.nch2), kpg = Cp / gp.G / 8, np = spi * kpg;
+  int LG = 1;
+  while (LG < np && LG < 64) LG <<= 1;
+  const int gpw = 64 / LG;                     // groups per wave per pass
+  const int npass = (gp.G + 4 * gpw - 1) / (4 * gpw);
+  v2f pv[2][2];   // [pass][k]: this lane's partials t = lane % LG + 64 k (np <= 128)
+#pragma unroll
+  for (int ps = 0; ps < 2; ++ps)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      pv[ps][k] = v2f{0.f, 0.f};
+      const int g = (ps * 4 + wave) * gpw + lane / LG, t = lane % LG + 64 * k;
+      if (ps < npass && g < gp.G && t < np) {
+        const int sg = n * spi + t / kpg, kc = g * kpg + t % kpg;
+        const float* pp = kc < gp.nch1 ? gp.p1 + ((size_t)sg * gp.nch1 + kc) * 2
+                                       : gp.p2 + ((size_t)sg * gp.nch2 + (kc - gp.nch1)) * 2;
+        pv[ps][k] = *(const v2f*)pp;
+      }
+    }
+  if (active && pb + r0 < pe) issue(pb + r0);   // the first pixel rows, in flight while the statistics combine
+  for (int ps = 0; ps < npass && ps < 2; ++ps) {
+    float c_ = 0.f, m_ = 0.f, q_ = 0.f;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (lane % LG + 64 * k < np) gn_chan(c_, m_, q_, 512.f, pv[ps][k][0], pv[ps][k][1]);
+    for (int sh = 1; sh < LG; sh <<= 1) {
+      const float nb = __shfl_xor(c_, sh), mb = __shfl_xor(m_, sh), qb = __shfl_xor(q_, sh);
+      if ((lane & sh) == 0) gn_chan(c_, m_, q_, nb, mb, qb);
+      else { float n2 = nb, m2 = mb, q2 = qb; gn_chan(n2, m2, q2, c_, m_, q_); c_ = n2; m_ = m2; q_ = q2; }
+    }
+    const int g = (ps * 4 + wave) * gpw + lane / LG;
+    if (g < gp.G && lane % LG == 0) {
+      const float mean = m_, var = fmaxf(q_ / c_, 0.f), rstd = 1.0f / sqrtf(var + gp.eps);
       smr[g][0] = mean;
       smr[g][1] = rstd;
       if (blockIdx.y == 0 && gp.mean_rstd) {
@@ -1203,6 +1235,12 @@ extern "C" int dmc_gn_apply_fin(int dtype, const void* x1, const void* x2, int N
                                 float drop_scale, void* out, int ld_out, void* stream) {
   const int C = C1 + C2;
   DMC_REQUIRE(dtype == DMC_BF16, "gn_apply_fin: bf16 (the conv-epilogue partials exist in bf16 mode only)");
+  {  // the kernel combines every group in at most two passes of 4 waves x (64 / LG) groups
+    const int np = HW / 64 * ((C1 + C2) / G / 8);
+    int LG = 1;
+    while (LG < np && LG < 64) LG <<= 1;
+    DMC_REQUIRE(G <= 8 * (64 / LG) && np <= 128, "gn_apply_fin: G %d with %d partials per group", G, np);
+  }
   DMC_REQUIRE(HW % 64 == 0 && C1 % 8 == 0 && C2 % 8 == 0 && G > 0 && G <= 64 && C % G == 0 && (C / G) % 8 == 0 &&
                   (C2 == 0 || part2) && part1 && ld_out % 8 == 0 && C / 8 <= 256,
               "gn_apply_fin: HW %d, C1 %d, C2 %d, G %d (64-pixel segments, 8-channel chunks inside groups)", HW, C1, C2,
