@@ -122,10 +122,10 @@ __global__ void gn_stats_final(Src2 s, int HW, int G, int splits, const float* p
 // Channel totals of the 1024-thread one-block kernels: red[t][2e], [2e+1] hold thread t's two partial sums
 // of channel (t % CPR)*EPC + e over its pixel rows (row t / CPR). tpc adjacent lanes per channel split the
 // rpi rows and combine by xor-shuffles (fixed order), instead of one thread walking all rows.
-template <int EPC>
+template <int EPC, int NT = 1024>
 DMC_DEV void onecta_chan_totals(const float (*red)[2 * EPC], int C, int CPR, int rpi, float (*out)[2]) {
   int tpc = 1;
-  while (tpc * 2 * C <= 1024 && tpc < 16) tpc *= 2;
+  while (tpc * 2 * C <= NT && tpc < 16) tpc *= 2;
   const int c = threadIdx.x / tpc, q = threadIdx.x % tpc;
   float b1 = 0.f, b2 = 0.f;
   if (c < C) {
@@ -821,8 +821,8 @@ __global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* cf, ch
 // the registers with gn_bwd_apply's formula -- one HBM pass over x and g instead of two and one launch instead of
 // two. The per-(n, c) pixel sums of the stored dx (bias / time-embedding gradients) are reduced in-block and
 // written directly; dgamma / dbeta and the per-c sums are column sums over n (gn_bwd_finish_kernel).
-template <int NR>
-__global__ __launch_bounds__(1024) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]*/, char* dx1, char* dx2, int ld1,
+template <int NR, int NT>
+__global__ __launch_bounds__(NT) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]*/, char* dx1, char* dx2, int ld1,
                                                      int ld2, int acc1, int acc2, float* sums /*[N][C]*/,
                                                      float* out_nc, int ld_nc) {
   using T = bf16_t;
@@ -832,11 +832,11 @@ __global__ __launch_bounds__(1024) void gn_bwd_fused(GnBwd b, float* A /*[n][C][
   const uint32_t dseed = drop_seed(b.dseed, b.dseed_base);
   const int C = b.s.C1 + b.s.C2, cpg = C / b.G, G = b.G, HW = b.HW;
   const int Cs = C / (int)gridDim.y, cb = (int)blockIdx.y * Cs, g0 = cb / cpg;
-  const int CPR = Cs / EPC, rpi = 1024 / CPR;
+  const int CPR = Cs / EPC, rpi = NT / CPR;
   const int rows = rpi < HW ? rpi : HW;   // row-threads that hold pixels (the rest only add zeros)
   const int tid = threadIdx.x, col = tid % CPR, r0 = tid / CPR;
   const bool active = r0 < rows;
-  __shared__ float red[1024][2 * EPC];
+  __shared__ float red[NT][2 * EPC];
   __shared__ float sA[1024][2];
   __shared__ float sm[64][2];
   __shared__ float sG[1024];
@@ -892,15 +892,15 @@ __global__ __launch_bounds__(1024) void gn_bwd_fused(GnBwd b, float* A /*[n][C][
 #pragma unroll
   for (int e = 0; e < EPC; ++e) { red[tid][2 * e] = active ? a1[e] : 0.f; red[tid][2 * e + 1] = active ? a2[e] : 0.f; }
   __syncthreads();
-  onecta_chan_totals<EPC>(red, Cs, CPR, rows, sA);   // sA[c - cb] (rows past `rows` held zeros)
+  onecta_chan_totals<EPC, NT>(red, Cs, CPR, rows, sA);   // sA[c - cb] (rows past `rows` held zeros)
   __syncthreads();
-  for (int c = tid; c < Cs; c += 1024) {
+  for (int c = tid; c < Cs; c += NT) {
     A[((size_t)n * C + cb + c) * 2] = sA[c][0];
     A[((size_t)n * C + cb + c) * 2 + 1] = sA[c][1];
   }
   const float cnt = (float)cpg * (float)HW;
   const int wv = tid >> 6, ln = tid & 63;
-  for (int gl = wv; gl < Cs / cpg; gl += 16) {   // one wave per group: gamma-weighted channel totals
+  for (int gl = wv; gl < Cs / cpg; gl += NT / 64) {   // one wave per group: gamma-weighted channel totals
     float m1 = 0.f, m2 = 0.f;
     for (int cl = gl * cpg + ln; cl < (gl + 1) * cpg; cl += 64) {
       const float g_ = sG[cl];
@@ -967,9 +967,9 @@ __global__ __launch_bounds__(1024) void gn_bwd_fused(GnBwd b, float* A /*[n][C][
 #pragma unroll
   for (int e = 0; e < EPC; ++e) { red1[tid][2 * e] = active ? sum[e] : 0.f; red1[tid][2 * e + 1] = 0.f; }
   __syncthreads();
-  onecta_chan_totals<EPC>(red, Cs, CPR, rows, sA);   // the same fixed-order lane-parallel channel totals
+  onecta_chan_totals<EPC, NT>(red, Cs, CPR, rows, sA);   // the same fixed-order lane-parallel channel totals
   __syncthreads();
-  for (int cl = tid; cl < Cs; cl += 1024) {
+  for (int cl = tid; cl < Cs; cl += NT) {
     const float v = sA[cl][0];
     sums[(size_t)n * C + cb + cl] = v;
     if (out_nc) out_nc[(size_t)n * ld_nc + cb + cl] = v;
@@ -1161,16 +1161,23 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
   const int fused_max = (int)dmc::opt(dmc::OPT_GN_BWD_FUSED);
   if (!part && dtype != DMC_F32 && N >= 64 && fused_max > 0 && !dmc::opt(dmc::OPT_GN_BWD_SPLIT) &&
       HW <= dmc::opt(dmc::OPT_GN_BWD_FUSED_MAXHW)) {
-    auto rows = [&](int s_) { const int rp = 1024 / (C / s_ / epc); return (HW + rp - 1) / rp; };
-    auto ok = [&](int s_) { return C % s_ == 0 && (C / s_) % (C / G) == 0 && (C / s_) % epc == 0; };
+    // DMC_GN_BWD_NT: threads per block (1024, or 512: two blocks per CU, twice the channel slices)
+    const int NT = dmc::opt(dmc::OPT_GN_BWD_NT) == 512 ? 512 : 1024;
+    auto rows = [&](int s_) { const int rp = NT / (C / s_ / epc); return rp > 0 ? (HW + rp - 1) / rp : 1 << 30; };
+    auto ok = [&](int s_) { return C % s_ == 0 && (C / s_) % (C / G) == 0 && (C / s_) % epc == 0 && C / s_ <= NT; };
     int S = 1;
-    while ((N * S < 256 || rows(S) > fused_max) && S < 8 && ok(S * 2)) S *= 2;
+    const int Smax = NT == 512 ? 16 : 8;
+    while ((N * S < 256 * 1024 / NT || rows(S) > fused_max) && S < Smax && ok(S * 2)) S *= 2;
     const int nr = rows(S);
-    if (nr <= fused_max && nr <= 4) {   // NR = 8 spills (x, g, accumulate operand and coefficients > 128 VGPRs)
+    if (nr <= fused_max && nr <= 4 && ok(S)) {   // NR = 8 spills (x, g, accumulate operand and coefficients > 128 VGPRs)
       float* ssum = want_sums ? sums : nullptr;
       const dim3 gf(N, S);
-#define DMC_GNBF(NR_) gn_bwd_fused<NR_><<<gf, 1024, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
-                                                         accumulate1, accumulate2, ssum, dx_sum_nc, ld_sum_nc)
+#define DMC_GNBF(NR_) do { \
+        if (NT == 512) gn_bwd_fused<NR_, 512><<<gf, 512, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
+                                                           accumulate1, accumulate2, ssum, dx_sum_nc, ld_sum_nc); \
+        else gn_bwd_fused<NR_, 1024><<<gf, 1024, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
+                                                     accumulate1, accumulate2, ssum, dx_sum_nc, ld_sum_nc); \
+      } while (0)
       if (nr <= 1) DMC_GNBF(1);
       else if (nr <= 2) DMC_GNBF(2);
       else DMC_GNBF(4);

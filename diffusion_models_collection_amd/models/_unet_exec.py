@@ -58,7 +58,9 @@ _GN_FIN = _GN_PARTIALS and os.environ.get("DMC_GN_FIN", "0") not in ("", "0")
 # combines its image's partials while its first rows load) instead of a dmc_gn_finalize launch before it. Opt-in
 # (DMC_GN_APPLY_FIN=1): measured slower on MI355X (same box, B=128, 2 reps: train 8418/8470 vs 8648/8693 img/s,
 # DDIM-50 599 vs 629; with the halo prologue off 558 vs 618) -- the 2048 blocks of an apply each repeat the
-# per-image combine (two dependent partial loads + 6 shuffle rounds per group) on their own critical path.
+# per-image combine on their own critical path. A second form (partials loaded ahead of the rows, every group
+# combined in one pass of 64/LG groups per wave) measured the same: train 8904/8898 vs 9140/9169, DDIM-50 649/646
+# vs 676/672 (profiles/r4_ab_gemm_gn.txt).
 _GN_APPLY_FIN = _GN_PARTIALS and os.environ.get("DMC_GN_APPLY_FIN", "0") not in ("", "0")
 
 
