@@ -50,8 +50,12 @@ def run_loop(x, nsteps, make_inputs, fn, use_graph, record=None):
         if graph is None and use_graph and i >= 1:
             try:
                 graph = StepGraph(fn, *args)
-            except Exception:   # noqa: BLE001 -- capture problem: stay eager
-                use_graph = False
+            except Exception as e:   # noqa: BLE001
+                # loud, as the training step's capture (utils/trainer.py GraphCaptureError): the stream a failed
+                # capture ran on may be poisoned, so the loop does not silently carry on eagerly on it
+                # (torch.cuda.graph has already restored the caller's stream)
+                from ..utils.trainer import GraphCaptureError
+                raise GraphCaptureError(f"sampling step capture failed at step {i}: {e!r}") from e
         x = graph.step(*args) if graph is not None else fn(*args)
         if record is not None:
             record(i, x)

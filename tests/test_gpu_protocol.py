@@ -573,6 +573,34 @@ def test_graph_capture_failure_raises_and_restores_stream(tmp_path, monkeypatch)
     assert torch.isfinite(tr.train_step(x, 3)).all()
 
 
+def test_sampling_graph_capture_failure_raises(monkeypatch):
+    """The graphed sampling loop (diffusion/_graph.py, DMC_GRAPH=1) raises GraphCaptureError when its capture
+    fails instead of carrying on eagerly on a stream the failed capture may have poisoned; the caller's stream is
+    restored and the device stays usable."""
+    from diffusion_models_collection_amd.models import UNet
+    from diffusion_models_collection_amd.diffusion import DDIM
+    from diffusion_models_collection_amd.utils.trainer import GraphCaptureError
+    mp = dict(image_size=(16, 16), in_channels=3, model_channels=32, out_channels=3, num_res_blocks=1,
+              attention_resolutions=(8,), dropout=0.0, channel_mult=(1, 2), use_attention=True)
+    monkeypatch.setenv("DMC_GRAPH", "1")
+    torch.manual_seed(0)
+    m = UNet(**mp, compute_dtype="bf16").to(DEV).eval()
+    ddim = DDIM(num_inference_steps=5, device=DEV)
+
+    def refuse(self, *a, **kw):
+        raise RuntimeError("injected: capture refused")
+
+    monkeypatch.setattr(torch.cuda.CUDAGraph, "capture_begin", refuse)
+    before = torch.cuda.current_stream()
+    with pytest.raises(GraphCaptureError) as ei:
+        ddim.sample(m, (2, 3, 16, 16), None)
+    assert "injected" in repr(ei.value.__cause__)
+    assert torch.cuda.current_stream() == before
+    torch.cuda.synchronize()
+    x = torch.ones(4, device=DEV)
+    assert torch.isfinite((x * 2).sum()).item()
+
+
 # ----------------------------------------------------------------------------------------------------------
 # The benchmarked plans (B=128) pinned to the oracle directly (VERDICT r3 #4)
 # ----------------------------------------------------------------------------------------------------------
