@@ -51,6 +51,13 @@ class GnFin(ctypes.Structure):
     ]
 
 
+class ColsumJob(ctypes.Structure):
+    """include/dmc.h dmc_colsum_job"""
+    _fields_ = [("in_", ctypes.c_void_p), ("R", ctypes.c_int), ("C", ctypes.c_int), ("ld", ctypes.c_long),
+                ("stride", ctypes.c_int), ("out0", ctypes.c_void_p), ("out1", ctypes.c_void_p),
+                ("scale", ctypes.c_float)]
+
+
 class GnBwdEpi(ctypes.Structure):
     """include/dmc.h dmc_gn_bwd_epi: GroupNorm-backward partial sums from an input-gradient conv's epilogue."""
     _fields_ = [
@@ -105,6 +112,12 @@ def _load():
                                      _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_p,
                                      _c_int, _c_int, _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_p, _c_p, _c_p,
                                      _c_p]),
+        "dmc_gn_silu_bwd_deferred": (_c_int, [_c_int, _c_p, _c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int,
+                                              _c_int, _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_u32, _c_p, _c_u32,
+                                              _c_f, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p, _c_p,
+                                              _c_int, _c_p, _c_p, _c_p, _c_p, _c_p, ctypes.POINTER(ctypes.c_int),
+                                              _c_p]),
+        "dmc_colsum_batch": (_c_int, [ctypes.POINTER(ColsumJob), _c_int, _c_p]),
         "dmc_channel_sum_workspace": (_c_size, [_c_int, _c_int, _c_int]),
         "dmc_channel_sum": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_p, _c_int, _c_p, _c_f, _c_p,
                                      _c_p]),

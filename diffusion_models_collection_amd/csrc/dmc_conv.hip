@@ -40,6 +40,7 @@ struct ConvK {
   int sk_per; // K stages per split
   int x1_bytes, x2_bytes, w_bytes;  // operand extents for buffer resources (0: too large / absent)
   int dtype_bytes;  // 4 (fp32) or 2 (bf16) storage
+  int reg_epi;      // DMC_REG_EPI: the halo conv's epilogue straight from the accumulators (reg_epilogue)
 };
 
 // Source pixel of output pixel (n,oy,ox) under tap; returns -1 if it falls in the zero padding.
@@ -755,6 +756,107 @@ DMC_DEV void xcd_tile(int NB, int& mb, int& nb) {
   nb = t - mb * NB;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Epilogue straight from the accumulators of a 4-wave 128 x 128 tile (wave = (wm pixel half, wn channel half),
+// acc[i][j] = channel fragment i x pixel fragment j; lane (fr, fh) holds channels 4 fh .. 4 fh + 3 of pixel fr):
+// bias, time-embedding addvec and residual in tile_epilogue8's order, bf16 pack, one 8-byte store per accumulator,
+// and the GroupNorm partials of the stored values -- segment = the wave's 64-pixel half, 8-channel chunk = the lane
+// pair (fh, fh ^ 1) of one fragment -- folded over the lane's 4 pixels, then combined by xor shuffles with equal
+// counts (no LDS staging, no block barrier: the LDS-staged epilogue of the 2-blocks-per-CU halo conv runs with
+// both blocks of a CU in lockstep, so its staging and barriers were exposed). Same statistics as tile_epilogue8 up
+// to the fp32 summation order.
+DMC_DEV bool reg_epi_ok(const ConvK& a) {
+  return a.reg_epi && a.dtype_bytes == 2 && !a.out_f32 && !a.out_nchw && !a.silu_pre && a.Csplit == a.Cout &&
+         a.act == DMC_ACT_NONE && !a.gb_on && !a.fin_on && (a.Cout & 127) == 0 && (a.ldy1 & 7) == 0 &&
+         (!a.resid || (a.ld_res & 7) == 0) && (a.M & 127) == 0 && (!a.gst || a.OHW % 64 == 0);
+}
+DMC_DEV void reg_epilogue(const ConvK& a, v4f (&acc)[4][4], int m0, int n0, int wm, int wn) {
+  // Stores and residual loads are 16 bytes: the lane pair (fh, fh ^ 1) holds the two 4-channel halves of one
+  // 8-channel chunk, so for each pair of pixel fragments (j0, j1) one xor-16 exchange of 2 dwords gives the even
+  // lane the whole chunk of pixel j0 and the odd lane that of pixel j1 (8-byte stores are store-issue bound).
+  const int lane = threadIdx.x & 63, fr = lane & 15, fh = lane >> 4;
+  const bool odd = fh & 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int co = n0 + wn * 64 + i * 16 + fh * 4;
+    const int cc = co - (odd ? 4 : 0);   // first channel of the lane pair's 8-channel chunk
+    const v4f b = a.bias ? *(const v4f*)(a.bias + co) : v4f{0.f, 0.f, 0.f, 0.f};
+    float gm = 0.f, gq = 0.f;
+    int nimg = -1;
+    v4f ev = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      v2i o[2];
+      v4i rr = {0, 0, 0, 0};
+      if (a.resid) {   // 16 bytes of the chunk: pixel j0 (even lane) or j1 (odd lane)
+        const int px = m0 + wm * 64 + (2 * jp + (odd ? 1 : 0)) * 16 + fr;
+        rr = *(const v4i*)(a.resid + ((size_t)px * a.ld_res + cc) * 2);
+      }
+      // the other pixel's residual half: even lanes need their 4 channels of pixel j1, odd lanes of pixel j0
+      v2i rs;
+      rs[0] = __shfl_xor(odd ? rr[0] : rr[2], 16);
+      rs[1] = __shfl_xor(odd ? rr[1] : rr[3], 16);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = 2 * jp + h;
+        const int px = m0 + wm * 64 + j * 16 + fr;
+        v4f v = acc[i][j] + b;
+        if (a.addvec) {
+          const int n = px / a.OHW;
+          if (n != nimg) { nimg = n; ev = *(const v4f*)(a.addvec + (size_t)n * a.ld_add + co); }
+          v = v + ev;
+        }
+        float f[4] = {v[0], v[1], v[2], v[3]};
+        if (a.resid) {   // this lane's 4 channels of pixel j: own load (its pixel) or the partner's half
+          const bool own = (h == 1) == odd;
+          const uint32_t r0 = own ? (uint32_t)(odd ? rr[2] : rr[0]) : (uint32_t)rs[0];
+          const uint32_t r1 = own ? (uint32_t)(odd ? rr[3] : rr[1]) : (uint32_t)rs[1];
+          f[0] += bf2f(r0 & 0xffffu); f[1] += bf2f(r0 >> 16);
+          f[2] += bf2f(r1 & 0xffffu); f[3] += bf2f(r1 >> 16);
+        }
+        o[h][0] = (int)f2bf2(f[0], f[1]);
+        o[h][1] = (int)f2bf2(f[2], f[3]);
+        if (a.gst) {   // this pixel's 4 stored values, folded into the lane's j*4 earlier ones
+          const float g0 = bf2f((uint32_t)o[h][0] & 0xffffu), g1 = bf2f((uint32_t)o[h][0] >> 16);
+          const float g2 = bf2f((uint32_t)o[h][1] & 0xffffu), g3 = bf2f((uint32_t)o[h][1] >> 16);
+          const float mb = ((g0 + g1) + (g2 + g3)) * 0.25f;
+          const float qb =
+              fmaf(g3 - mb, g3 - mb, fmaf(g2 - mb, g2 - mb, fmaf(g1 - mb, g1 - mb, (g0 - mb) * (g0 - mb))));
+          if (j == 0) { gm = mb; gq = qb; }
+          else {
+            const float d = mb - gm, nn = 4.f * j;
+            gm += d * (4.f / (nn + 4.f));
+            gq += qb + d * d * (nn * 4.f / (nn + 4.f));
+          }
+        }
+      }
+      // exchange: the even lane sends its pixel-j1 half and receives the odd lane's pixel-j0 half
+      v2i send = odd ? o[0] : o[1], recv;
+      recv[0] = __shfl_xor(send[0], 16);
+      recv[1] = __shfl_xor(send[1], 16);
+      v4i outv;
+      if (!odd) { outv[0] = o[0][0]; outv[1] = o[0][1]; outv[2] = recv[0]; outv[3] = recv[1]; }
+      else { outv[0] = recv[0]; outv[1] = recv[1]; outv[2] = o[1][0]; outv[3] = o[1][1]; }
+      const int pxs = m0 + wm * 64 + (2 * jp + (odd ? 1 : 0)) * 16 + fr;
+      *(v4i*)(a.y1 + ((size_t)pxs * a.ldy1 + cc) * 2) = outv;
+    }
+    if (a.gst) {
+      float cnt = 16.f;
+#pragma unroll
+      for (int sh = 1; sh <= 16; sh <<= 1) {   // pixels (fr bits), then the chunk's second channel quad (fh ^ 1)
+        const float mb = __shfl_xor(gm, sh), qb = __shfl_xor(gq, sh);
+        chan_eq(gm, gq, mb, qb, cnt);
+        cnt *= 2.f;
+      }
+      if (fr == 0 && !odd) {
+        const size_t o = ((size_t)((m0 + wm * 64) / 64) * (a.Cout / 8) + cc / 8) * 2;
+        a.gst[o] = gm;
+        a.gst[o + 1] = gq;
+      }
+    }
+  }
+}
+
 // BUF = true: all operands through buffer resources (raw_ptr_buffer_load_lds), zero padding by the
 // hardware range check, per-row offsets precomputed once per tap -> one VALU add per DMA instruction.
 // Requires C1 % 64 == 0, C2 % 64 == 0, Kc == C1 + C2 (a stage never straddles the concat boundary).
@@ -895,10 +997,17 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_fwd_glds_kernel(ConvK a) {
     __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
   }
 #undef DMC_GLDS_ISSUE
-  // Epilogue through LDS: the block's fp32 tile is parked in the (now free) staging ring, then every
-  // thread finishes 4-channel groups of consecutive channels (coalesced NHWC stores; the epilogue loop is
-  // a runtime loop, which keeps hipcc from spilling the accumulators to scratch).
+  // Epilogue: from the accumulators where it applies (the 4-wave 128x128 tile, no split-K: reg_epilogue), else
+  // through LDS -- the block's fp32 tile is parked in the (now free) staging ring, then every thread finishes
+  // 4-channel groups of consecutive channels (coalesced NHWC stores; the epilogue loop is a runtime loop, which
+  // keeps hipcc from spilling the accumulators to scratch).
   constexpr int EP = BN * 4 + 16;
+  if constexpr (WM == 2 && WN == 2) {
+    if (!a.sk && reg_epi_ok(a) && n0 + BN <= a.Cout && m0 + BM <= a.M) {
+      reg_epilogue(a, acc, m0, n0, wm, wn);
+      return;
+    }
+  }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -1187,7 +1296,7 @@ DMC_DEV void halo_affine_silu(char* buf, int wave, const unsigned* h1, const v4f
 // overlaps the other's tap loop. At a chunk switch the block waits for its own next-chunk halo (the other block
 // keeps the CU busy). Tile geometry: R = 128 / OW rows of one image, or 128 / (OH*OW) whole images.
 template <int HP, int WS, bool PRO = false, bool SCHED = true>
-__global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int nimg) {
+__global__ __launch_bounds__(256, 2) void conv3x3_halo2_kernel(ConvK a, int R, int nimg) {
   using T = bf16_t;
   constexpr int NW = 4, WM = 2, BM = 128, BN = 128;
   constexpr int HB = HP * NW * 1024;             // bytes of the halo buffer
@@ -1342,6 +1451,10 @@ __global__ __launch_bounds__(256) void conv3x3_halo2_kernel(ConvK a, int R, int 
   }
 #endif
 #undef DMC_PH
+  if (reg_epi_ok(a)) {   // uniform: the epilogue from the accumulators (the trailing barrier above is kept: the
+    reg_epilogue(a, acc, m0, n0, wm, wn);   // MFMA tail drains there)
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -2912,6 +3025,7 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
   k.wgb = nullptr;   // set by dmc_conv2d_wgrad when the bias gradient is requested
   k.gsk = nullptr; k.gsk_done = nullptr;
   k.fin_on = 0;      // set by dmc_conv2d with gst
+  k.reg_epi = (int)dmc::opt(dmc::OPT_REG_EPI);
   k.fin = d->gn_fin ? *d->gn_fin : dmc_gn_fin{};
   k.stamp = (unsigned long long*)dmc::opt(dmc::OPT_STAMP_PTR);   // 0 unless a DMC_STAMP probe sets it
   k.M = d->N * d->OH * d->OW; k.OHW = d->OH * d->OW;

@@ -1128,13 +1128,15 @@ extern "C" int dmc_gn_finalize(const float* part1, int C1, const float* part2, i
   return dmc::check_launch("dmc_gn_finalize");
 }
 
-extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x1, const void* x2, int N, int HW, int C1,
-                               int C2, int ld1, int ld2, int G, const float* mean_rstd, const float* gamma,
-                               const float* beta, int silu, uint32_t drop_seed, const uint32_t* drop_seed_base,
-                               uint32_t drop_thresh, float drop_scale, void* dx1,
-                               void* dx2, int ld_dx1, int ld_dx2, int accumulate1, int accumulate2, float* dgamma,
-                               float* dbeta, float* dx_sum_nc, int ld_sum_nc, float* dx_sum_c, const float* part,
-                               void* workspace, void* stream) {
+namespace {
+int gn_silu_bwd_impl(int dtype, const void* g, int ld_g, const void* x1, const void* x2, int N, int HW, int C1,
+                     int C2, int ld1, int ld2, int G, const float* mean_rstd, const float* gamma,
+                     const float* beta, int silu, uint32_t drop_seed, const uint32_t* drop_seed_base,
+                     uint32_t drop_thresh, float drop_scale, void* dx1,
+                     void* dx2, int ld_dx1, int ld_dx2, int accumulate1, int accumulate2, float* dgamma,
+                     float* dbeta, float* dx_sum_nc, int ld_sum_nc, float* dx_sum_c, const float* part,
+                     void* workspace, void* stream, float* A_keep, float* sums_keep, int* deferred) {
+  if (deferred) *deferred = 0;
   const int epc = dtype == DMC_F32 ? 4 : 8;
   const int C = C1 + C2;
   DMC_REQUIRE(C % G == 0 && C <= 1024 && G <= 64, "gn_bwd: C %d / G %d", C, G);
@@ -1170,7 +1172,10 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
     while ((N * S < 256 * 1024 / NT || rows(S) > fused_max) && S < Smax && ok(S * 2)) S *= 2;
     const int nr = rows(S);
     if (nr <= fused_max && nr <= 4 && ok(S)) {   // NR = 8 spills (x, g, accumulate operand and coefficients > 128 VGPRs)
-      float* ssum = want_sums ? sums : nullptr;
+      // deferred column sums: A and the per-(n, c) sums go to the caller's buffers, the finish is its batch
+      const bool defer = A_keep && (!dx_sum_c || sums_keep);
+      if (defer) A = A_keep;
+      float* ssum = want_sums ? (defer && sums_keep ? sums_keep : sums) : nullptr;
       const dim3 gf(N, S);
 #define DMC_GNBF(NR_) do { \
         if (NT == 512) gn_bwd_fused<NR_, 512><<<gf, 512, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
@@ -1182,6 +1187,10 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
       else if (nr <= 2) DMC_GNBF(2);
       else DMC_GNBF(4);
 #undef DMC_GNBF
+      if (defer) {
+        if (deferred) *deferred = 1;
+        return dmc::check_launch("dmc_gn_silu_bwd");
+      }
       const int nb = (C + 63) / 64 + (dx_sum_c ? (C + 63) / 64 : 0);
       gn_bwd_finish_kernel<<<nb, 1024, 0, s>>>(A, ssum, N, C, dbeta, dgamma, dx_sum_c);
       return dmc::check_launch("dmc_gn_silu_bwd");
@@ -1215,6 +1224,68 @@ extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x
                                             want_sums ? sums : nullptr, A, dbeta, dgamma);
   if (want_sums) chsum_finish(s, N, C, b.splits, sums, dx_sum_nc, ld_sum_nc, dx_sum_c, 1.0f);
   return dmc::check_launch("dmc_gn_silu_bwd");
+}
+
+// Column sums of many small fp32 matrices in one launch (the deferred dgamma / dbeta / bias sums of the GroupNorm
+// backward): the jobs ride in the kernel arguments; block b runs 64 columns of the job whose block range holds b,
+// with colsum_block<16> -- bitwise gn_bwd_finish_kernel's sums.
+constexpr int kColsumJobs = 56;
+struct ColsumBatch {
+  int njobs;
+  int first[kColsumJobs + 1];   // block offsets
+  dmc_colsum_job j[kColsumJobs];
+};
+__global__ __launch_bounds__(1024) void colsum_batch_kernel(ColsumBatch cb) {
+  int k = 0;
+  while (k + 1 < cb.njobs && (int)blockIdx.x >= cb.first[k + 1]) ++k;
+  const dmc_colsum_job& J = cb.j[k];
+  colsum_block<16>(J.in, J.R, J.C, J.ld, J.stride, ((int)blockIdx.x - cb.first[k]) * 64, J.out0, J.out1, J.scale);
+}
+}  // namespace
+
+extern "C" int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x1, const void* x2, int N, int HW, int C1,
+                               int C2, int ld1, int ld2, int G, const float* mean_rstd, const float* gamma,
+                               const float* beta, int silu, uint32_t drop_seed, const uint32_t* drop_seed_base,
+                               uint32_t drop_thresh, float drop_scale, void* dx1,
+                               void* dx2, int ld_dx1, int ld_dx2, int accumulate1, int accumulate2, float* dgamma,
+                               float* dbeta, float* dx_sum_nc, int ld_sum_nc, float* dx_sum_c, const float* part,
+                               void* workspace, void* stream) {
+  return gn_silu_bwd_impl(dtype, g, ld_g, x1, x2, N, HW, C1, C2, ld1, ld2, G, mean_rstd, gamma, beta, silu, drop_seed,
+                          drop_seed_base, drop_thresh, drop_scale, dx1, dx2, ld_dx1, ld_dx2, accumulate1, accumulate2,
+                          dgamma, dbeta, dx_sum_nc, ld_sum_nc, dx_sum_c, part, workspace, stream, nullptr, nullptr,
+                          nullptr);
+}
+
+extern "C" int dmc_gn_silu_bwd_deferred(int dtype, const void* g, int ld_g, const void* x1, const void* x2, int N,
+                                        int HW, int C1, int C2, int ld1, int ld2, int G, const float* mean_rstd,
+                                        const float* gamma, const float* beta, int silu, uint32_t drop_seed,
+                                        const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale,
+                                        void* dx1, void* dx2, int ld_dx1, int ld_dx2, int accumulate1, int accumulate2,
+                                        float* dgamma, float* dbeta, float* dx_sum_nc, int ld_sum_nc, float* dx_sum_c,
+                                        const float* part, void* workspace, float* A_keep, float* sums_keep,
+                                        int* deferred, void* stream) {
+  DMC_REQUIRE(A_keep && deferred && (!dx_sum_c || sums_keep), "gn_silu_bwd_deferred: keep buffers / flag");
+  return gn_silu_bwd_impl(dtype, g, ld_g, x1, x2, N, HW, C1, C2, ld1, ld2, G, mean_rstd, gamma, beta, silu, drop_seed,
+                          drop_seed_base, drop_thresh, drop_scale, dx1, dx2, ld_dx1, ld_dx2, accumulate1, accumulate2,
+                          dgamma, dbeta, dx_sum_nc, ld_sum_nc, dx_sum_c, part, workspace, stream, A_keep, sums_keep,
+                          deferred);
+}
+
+extern "C" int dmc_colsum_batch(const dmc_colsum_job* jobs, int njobs, void* stream) {
+  DMC_REQUIRE(njobs >= 0 && njobs <= kColsumJobs, "colsum_batch: %d jobs (at most %d)", njobs, kColsumJobs);
+  if (njobs == 0) return 0;
+  ColsumBatch cb;
+  cb.njobs = njobs;
+  int nb = 0;
+  for (int k = 0; k < njobs; ++k) {
+    DMC_REQUIRE(jobs[k].in && jobs[k].out0 && jobs[k].R > 0 && jobs[k].C > 0, "colsum_batch: job %d", k);
+    cb.first[k] = nb;
+    cb.j[k] = jobs[k];
+    nb += (jobs[k].C + 63) / 64;
+  }
+  cb.first[njobs] = nb;
+  colsum_batch_kernel<<<nb, 1024, 0, dmc::as_stream(stream)>>>(cb);
+  return dmc::check_launch("dmc_colsum_batch");
 }
 
 extern "C" size_t dmc_channel_sum_workspace(int N, int HW, int C) {

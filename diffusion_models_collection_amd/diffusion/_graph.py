@@ -48,12 +48,14 @@ def run_loop(x, nsteps, make_inputs, fn, use_graph, record=None):
     for i in range(nsteps):
         args = make_inputs(i, x)
         if graph is None and use_graph and i >= 1:
+            prev = torch.cuda.current_stream()
             try:
                 graph = StepGraph(fn, *args)
             except Exception as e:   # noqa: BLE001
                 # loud, as the training step's capture (utils/trainer.py GraphCaptureError): the stream a failed
-                # capture ran on may be poisoned, so the loop does not silently carry on eagerly on it
-                # (torch.cuda.graph has already restored the caller's stream)
+                # capture ran on may be poisoned, so the loop does not silently carry on eagerly on it. A failure in
+                # capture_begin leaves torch.cuda.graph's side stream current (its __exit__ never runs): restore
+                torch.cuda.set_stream(prev)
                 from ..utils.trainer import GraphCaptureError
                 raise GraphCaptureError(f"sampling step capture failed at step {i}: {e!r}") from e
         x = graph.step(*args) if graph is not None else fn(*args)

@@ -281,16 +281,45 @@ def gn_apply_fin(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, p1, p2, G, eps, gamma, 
 
 
 def gn_bwd(dtype, g, ld_g, x1, x2, N, HW, C1, C2, ld1, ld2, G, mr, gamma, beta, silu, drop, dx1, dx2, ld_dx1,
-           ld_dx2, acc1, acc2, dgamma, dbeta, dx_sum_nc=None, ld_sum_nc=0, dx_sum_c=None, part=None):
+           ld_dx2, acc1, acc2, dgamma, dbeta, dx_sum_nc=None, ld_sum_nc=0, dx_sum_c=None, part=None, defer=None):
     """GroupNorm(+SiLU+dropout) backward; optionally also the per-(n,c) / per-c pixel sums of dx (the bias and
     time-embedding gradients of the layer that produced x), fused into the dx pass. part: the (sum dz,
     sum dz*xhat) partials the input-gradient conv that produced g wrote (gn_bwd_epi), skipping the reduction."""
     ws = SCRATCH.get(LIB.dmc_gn_workspace(N, C1 + C2, G, HW), g.device)
     seed, base, thresh, scale = drop_args(drop)
+    if defer is not None:
+        # the parameter column sums go to the caller's batch (colsum_batch) when the one-pass kernel takes the call
+        C = C1 + C2
+        a_keep = torch.empty(N * C * 2, dtype=torch.float32, device=g.device)
+        s_keep = torch.empty(N * C, dtype=torch.float32, device=g.device) if dx_sum_c is not None else None
+        flag = ctypes.c_int(0)
+        check(LIB.dmc_gn_silu_bwd_deferred(
+            L.dtype_code(dtype), ptr(g), ld_g, ptr(x1), ptr(x2), N, HW, C1, C2, ld1, ld2, G, ptr(mr), ptr(gamma),
+            ptr(beta), int(silu), seed, base, thresh, scale, ptr(dx1), ptr(dx2), ld_dx1, ld_dx2, int(acc1), int(acc2),
+            ptr(dgamma), ptr(dbeta), ptr(dx_sum_nc), ld_sum_nc, ptr(dx_sum_c), ptr(part), ptr(ws), ptr(a_keep),
+            ptr(s_keep), ctypes.byref(flag), L.stream()), "dmc_gn_silu_bwd_deferred")
+        if flag.value:
+            defer.append((a_keep, N, C, 2 * C, 2, dbeta, dgamma))
+            if s_keep is not None:
+                defer.append((s_keep, N, C, C, 1, dx_sum_c, None))
+        return
     check(LIB.dmc_gn_silu_bwd(L.dtype_code(dtype), ptr(g), ld_g, ptr(x1), ptr(x2), N, HW, C1, C2, ld1, ld2, G, ptr(mr),
                               ptr(gamma), ptr(beta), int(silu), seed, base, thresh, scale, ptr(dx1), ptr(dx2), ld_dx1,
                               ld_dx2, int(acc1), int(acc2), ptr(dgamma), ptr(dbeta), ptr(dx_sum_nc), ld_sum_nc,
                               ptr(dx_sum_c), ptr(part), ptr(ws), L.stream()), "dmc_gn_silu_bwd")
+
+
+def colsum_batch(jobs):
+    """Launch the column sums gn_bwd(defer=jobs) left behind (dmc_colsum_batch, <= 56 per launch) and clear the
+    list: out0[c] = sum_r in[r*ld + c*stride], out1 at +1 -- dgamma / dbeta / the bias sums."""
+    for k in range(0, len(jobs), 56):
+        chunk = jobs[k:k + 56]
+        arr = (L.ColsumJob * len(chunk))()
+        for j, (t, R, C, ld, stride, o0, o1) in enumerate(chunk):
+            arr[j].in_, arr[j].R, arr[j].C, arr[j].ld, arr[j].stride = ptr(t), R, C, ld, stride
+            arr[j].out0, arr[j].out1, arr[j].scale = ptr(o0), ptr(o1), 1.0
+        check(LIB.dmc_colsum_batch(arr, len(chunk), L.stream()), "dmc_colsum_batch")
+    jobs.clear()
 
 
 def gn_bwd_epi(x1, x2, C1, ld1, ld2, mr, gamma, beta, G, silu, drop, M, C):

@@ -62,6 +62,9 @@ _GN_FIN = _GN_PARTIALS and os.environ.get("DMC_GN_FIN", "0") not in ("", "0")
 # combined in one pass of 64/LG groups per wave) measured the same: train 8904/8898 vs 9140/9169, DDIM-50 649/646
 # vs 676/672 (profiles/r4_ab_gemm_gn.txt).
 _GN_APPLY_FIN = _GN_PARTIALS and os.environ.get("DMC_GN_APPLY_FIN", "0") not in ("", "0")
+# The GroupNorm backward's parameter column sums deferred to one dmc_colsum_batch per gradient segment (A/B switch
+# DMC_GN_DEFER=0: one finish launch per GroupNorm)
+_GN_DEFER = os.environ.get("DMC_GN_DEFER", "1") not in ("", "0")
 
 
 class GnSt:
@@ -744,6 +747,7 @@ class UNetExecutor(ExecCore):
         gv = lambda p: self._gview(flat, p)  # noqa: E731
         dx = None
         hook = self.grad_hook
+        self._gn_defer = [] if _GN_DEFER else None
         if hook is not None:
             order = sorted(range(len(self.params)), key=lambda i: self.goff[i])
             final = [False] * len(self.params)
@@ -769,8 +773,11 @@ class UNetExecutor(ExecCore):
                     cursor += 1
                 hi = self.goff[order[cursor]] if cursor < len(order) else self.gtotal
                 if getattr(hook, "wants", None) is None or hook.wants(hi, last):
+                    self._flush_gn()       # the deferred GroupNorm parameter sums of that prefix
                     self._join_side()      # the side stream's weight gradients of that prefix are written
                 hook(flat, hi, last)
+        self._flush_gn()
+        self._gn_defer = None
         self._join_side()
         self.daddvec = None
         grads = [self._gview(flat, p) for p in self.params]
@@ -822,7 +829,7 @@ class UNetExecutor(ExecCore):
                 self._conv([dya], convo, K.TAPS3_DGRAD, H, W, h.C, out=g, packmode=L.PACK_DGRAD,
                            Kc=L.kc_for(Co, dt), gnb=gnb)
                 buf, acc = self._grad_target(h)
-                K.gn_bwd(dt, g, h.C, h.t, None, N, H * W, h.C, 0, h.t.shape[-1], 0, gno.num_groups, mr, gno.weight,
+                self._gn_bwd(dt, g, h.C, h.t, None, N, H * W, h.C, 0, h.t.shape[-1], 0, gno.num_groups, mr, gno.weight,
                          gno.bias, True, None, buf, None, h.C, 0, acc, 0, gv(gno.weight), gv(gno.bias),
                          part=gnb and gnb.part)
             elif kind == "res":
@@ -926,7 +933,7 @@ class UNetExecutor(ExecCore):
         if self.daddvec is None:
             self.daddvec = torch.empty(N, self.temb_total, dtype=torch.float32, device=dout.device)
         dh1 = torch.empty(N, H, W, Cout, dtype=dt, device=dout.device)
-        K.gn_bwd(dt, g2, Cout, h1.t, None, N, HW, Cout, 0, Cout, 0, gn2.num_groups, st2[2], gn2.weight, gn2.bias, True,
+        self._gn_bwd(dt, g2, Cout, h1.t, None, N, HW, Cout, 0, Cout, 0, gn2.num_groups, st2[2], gn2.weight, gn2.bias, True,
                  drop, dh1, None, Cout, 0, 0, 0, gv(gn2.weight), gv(gn2.bias), dx_sum_nc=self.daddvec[:, off:],
                  ld_sum_nc=self.temb_total, dx_sum_c=gv(conv1.bias), part=gnb2 and gnb2.part)
         # conv1
@@ -944,9 +951,18 @@ class UNetExecutor(ExecCore):
             ld2 = srcs[1].t.shape[-1]
         else:
             b2, acc2, ld2 = None, 0, 0
-        K.gn_bwd(dt, g1, C1 + C2, a.t, srcs[1].t if len(srcs) > 1 else None, N, HW, C1, C2, a.t.shape[-1], ld2,
+        self._gn_bwd(dt, g1, C1 + C2, a.t, srcs[1].t if len(srcs) > 1 else None, N, HW, C1, C2, a.t.shape[-1], ld2,
                  gn1.num_groups, st1[2], gn1.weight, gn1.bias, True, None, b1, b2, a.t.shape[-1], ld2, acc1, acc2,
                  gv(gn1.weight), gv(gn1.bias), part=gnb1 and gnb1.part)
+
+    def _gn_bwd(self, *a, **kw):
+        """K.gn_bwd with its parameter column sums (dgamma / dbeta / the bias sums) deferred to one batched launch
+        per gradient segment (_flush_gn) -- 25 launches of ~4.7 us per B=128 training step became one."""
+        return K.gn_bwd(*a, defer=getattr(self, "_gn_defer", None), **kw)
+
+    def _flush_gn(self):
+        if getattr(self, "_gn_defer", None):
+            K.colsum_batch(self._gn_defer)
 
     def _scatter_add_concat(self, tmp, b1, acc1, b2, acc2, C1, C2):
         t1 = tmp[..., :C1].contiguous()
@@ -986,7 +1002,7 @@ class UNetExecutor(ExecCore):
         g = torch.empty(N, H, W, C, dtype=dt, device=dout.device)
         gnb = self._gnb_epi(a.t, None, C, 0, C, 0, st[2], ab.norm, False, None, N, HW)
         self._conv([Act(dqkv, H, W, 3 * C)], ab.qkv, K.TAPS1, H, W, C, out=g, packmode=L.PACK_DGRAD, gnb=gnb)
-        K.gn_bwd(dt, g, C, a.t, None, N, HW, C, 0, C, 0, ab.norm.num_groups, st[2], ab.norm.weight, ab.norm.bias,
+        self._gn_bwd(dt, g, C, a.t, None, N, HW, C, 0, C, 0, ab.norm.num_groups, st[2], ab.norm.weight, ab.norm.bias,
                  False, None, a.grad, None, C, 0, 1, 0, gv(ab.norm.weight), gv(ab.norm.bias), part=gnb and gnb.part)
 
     def _temb_bwd(self, rec, daddvec, gv):

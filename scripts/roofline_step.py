@@ -125,7 +125,7 @@ for nm, alg in [("conv", a_conv), ("wgrad", a_wgrad), ("gn_stats", a_gn_stats), 
                 ("gn_apply", a_gn_apply), ("gn_apply_fin", a_gn_apply_fin), ("gn_bwd", a_gn_bwd), ("attn_fwd", a_attn_fwd), ("attn_bwd", a_attn_bwd),
                 ("adamw_flat_dev", a_adamw_dev), ("adamw_flat", a_adamw), ("grad_norm_flat", a_grad_norm), ("pack_input", a_gn_none),
                 ("loss_fwd", a_gn_none), ("loss_bwd", a_gn_none), ("add_", a_gn_none), ("upsample2x", a_gn_none),
-                ("channel_sum", a_gn_none), ("time_embed", a_gn_none), ("unpack_output", a_gn_none)]:
+                ("channel_sum", a_gn_none), ("colsum_batch", a_gn_none), ("time_embed", a_gn_none), ("unpack_output", a_gn_none)]:
     wrap(K, nm, alg)
 _launch = K.PackBatch.launch
 

@@ -710,7 +710,7 @@ def test_ema_sampling_sees_unfused_ema_updates(tmp_path):
 
 
 @pytest.mark.parametrize("mode", ["eval", "train"])
-def test_groupnorm_finalize_in_producing_conv_bitwise(mode, monkeypatch):
+def test_groupnorm_finalize_in_producing_conv_bitwise(mode, monkeypatch, dmc_opt):
     """The GroupNorm statistics finalised by the conv that produces the GroupNorm's input (dmc_gn_fin: per-image
     arrival counters, the last block combines the epilogue partials with gn_finalize_group) instead of a
     dmc_gn_finalize launch: the bf16 CIFAR UNet at B=128 gives BITWISE the same output (eval) / loss and every
@@ -736,6 +736,9 @@ def test_groupnorm_finalize_in_producing_conv_bitwise(mode, monkeypatch):
 
     monkeypatch.setattr(K, "gn_finalize", counted)
     monkeypatch.setattr(UE, "_GN_APPLY_FIN", False)
+    # the producer-side finalize runs with the LDS-staged epilogue's partials (the halo conv's epilogue from the
+    # accumulators, DMC_REG_EPI, folds them in another order): compare both arms on that epilogue
+    dmc_opt("DMC_REG_EPI", 0)
     res = []
     for on in (True, False):
         monkeypatch.setattr(UE, "_GN_FIN", on)
