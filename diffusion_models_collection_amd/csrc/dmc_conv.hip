@@ -766,7 +766,10 @@ DMC_DEV void xcd_tile(int NB, int& mb, int& nb) {
 // both blocks of a CU in lockstep, so its staging and barriers were exposed). Same statistics as tile_epilogue8 up
 // to the fp32 summation order.
 DMC_DEV bool reg_epi_ok(const ConvK& a) {
-  return a.reg_epi && a.dtype_bytes == 2 && !a.out_f32 && !a.out_nchw && !a.silu_pre && a.Csplit == a.Cout &&
+  // DMC_REG_EPI: 1 = where the tile also emits GroupNorm partials (the LDS-staged form reduces them across the waves
+  // through LDS behind a second barrier; without partials it is the faster one: 52.5 vs 57.1 us on the 32x32 conv
+  // with bias + time embedding + residual, kernel trace), 2 = every eligible tile, 0 = never
+  return a.reg_epi && (a.gst || a.reg_epi == 2) && a.dtype_bytes == 2 && !a.out_f32 && !a.out_nchw && !a.silu_pre && a.Csplit == a.Cout &&
          a.act == DMC_ACT_NONE && !a.gb_on && !a.fin_on && (a.Cout & 127) == 0 && (a.ldy1 & 7) == 0 &&
          (!a.resid || (a.ld_res & 7) == 0) && (a.M & 127) == 0 && (!a.gst || a.OHW % 64 == 0);
 }

@@ -544,6 +544,39 @@ def test_groupnorm_backward_fused_one_pass(shape, dmc_opt):
     assert rel_err(res[(4, False)][0], dxk) > 1e-2
 
 
+@pytest.mark.parametrize("shape", [(128, 32, 32, 128), (128, 8, 8, 256), (64, 4, 4, 512)])
+def test_gn_bwd_deferred_column_sums_bitwise(shape):
+    """dmc_gn_silu_bwd_deferred + dmc_colsum_batch (the parameter column sums of several GroupNorm backwards in one
+    launch) give BITWISE the dgamma / dbeta / per-c dx sums of the immediate dmc_gn_silu_bwd, and the same dx and
+    per-(n, c) sums."""
+    L, K = _lib()
+    torch.manual_seed(9)
+    N, H, W, C = shape
+    G, dt, HW = 8, torch.bfloat16, H * W
+    x = (torch.randn(N, H, W, C) * 1.3 + 0.4).to(dt).to(DEV)
+    g = torch.randn(N, H, W, C).to(dt).to(DEV)
+    gamma, beta = (torch.rand(C) + 0.5).to(DEV), torch.randn(C).to(DEV)
+    _, _, mr = K.gn_stats(dt, x, None, N, HW, C, 0, C, 0, G, 1e-5, gamma, beta)
+    drop = (5, 1 << 29, 1.0 / 0.875)
+    outs = []
+    jobs = []
+    for defer in (None, jobs):
+        dx = torch.empty_like(x)
+        dg, db, sc_ = (torch.full((C,), -3.0, device=DEV) for _ in range(3))
+        snc = torch.empty(N, C, device=DEV)
+        K.gn_bwd(dt, g, C, x, None, N, HW, C, 0, C, 0, G, mr, gamma, beta, True, drop, dx, None, C, 0, 0, 0, dg, db,
+                 dx_sum_nc=snc, ld_sum_nc=C, dx_sum_c=sc_, defer=defer)
+        if defer is not None:
+            assert len(jobs) == 2                      # the one-pass kernel took it: A and the dx sums deferred
+            assert (dg == -3.0).all() and (sc_ == -3.0).all()
+            K.colsum_batch(jobs)
+            assert not jobs
+        torch.cuda.synchronize()
+        outs.append((dx, dg, db, sc_, snc))
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_groupnorm_stats_and_backward(dt):
     L, K = _lib()
