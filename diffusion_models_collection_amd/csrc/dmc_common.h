@@ -224,13 +224,19 @@ DMC_DEV void gn_finalize_group(const float* p1, int nch1, const float* p2, int n
                                float* shift) {
   const int lane = threadIdx.x & 63;
   const int C = 8 * (nch1 + nch2), cpg = C / G;
+  // the first (for cpg <= 64 the only) gamma / beta of this lane are loaded before the partials: their latency
+  // overlaps the statistics instead of following the mean_rstd store (which they could alias)
+  const int c_first = g * cpg + lane;
+  const bool has_first = c_first < (g + 1) * cpg;
+  const float gm0 = gamma && has_first ? gamma[c_first] : 1.f, bt0 = beta && has_first ? beta[c_first] : 0.f;
   float mean, rstd;
   gn_group_stats<SC1>(p1, nch1, p2, nch2, n, g, spi, G, eps, mean, rstd);
   const size_t i = (size_t)n * G + g;
   if (lane == 0 && mean_rstd) { mean_rstd[i * 2] = mean; mean_rstd[i * 2 + 1] = rstd; }
-  for (int c = g * cpg + lane; c < (g + 1) * cpg; c += 64) {
+  for (int c = c_first; c < (g + 1) * cpg; c += 64) {
     float sc, sh;
-    gn_fold(mean, rstd, gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f, sc, sh);
+    const bool f = c == c_first;
+    gn_fold(mean, rstd, f ? gm0 : gamma ? gamma[c] : 1.f, f ? bt0 : beta ? beta[c] : 0.f, sc, sh);
     scale[(size_t)n * C + c] = sc;
     shift[(size_t)n * C + c] = sh;
   }

@@ -767,9 +767,10 @@ DMC_DEV void xcd_tile(int NB, int& mb, int& nb) {
 // to the fp32 summation order.
 DMC_DEV bool reg_epi_ok(const ConvK& a) {
   // DMC_REG_EPI: 1 = where the tile also emits GroupNorm partials (the LDS-staged form reduces them across the waves
-  // through LDS behind a second barrier; without partials it is the faster one: 52.5 vs 57.1 us on the 32x32 conv
-  // with bias + time embedding + residual, kernel trace), 2 = every eligible tile, 0 = never
-  return a.reg_epi && (a.gst || a.reg_epi == 2) && a.dtype_bytes == 2 && !a.out_f32 && !a.out_nchw && !a.silu_pre && a.Csplit == a.Cout &&
+  // through LDS behind a second barrier; without partials it is the faster one in isolation: 52.5 vs 57.1 us on the
+  // 32x32 conv with bias + time embedding + residual, kernel trace), 2 = every eligible tile, 3 = every eligible
+  // tile but the inference (GroupNorm-prologue) halo kernel, 0 = never
+  return a.reg_epi && (a.gst || a.reg_epi >= 2) && a.dtype_bytes == 2 && !a.out_f32 && !a.out_nchw && !a.silu_pre && a.Csplit == a.Cout &&
          a.act == DMC_ACT_NONE && !a.gb_on && !a.fin_on && (a.Cout & 127) == 0 && (a.ldy1 & 7) == 0 &&
          (!a.resid || (a.ld_res & 7) == 0) && (a.M & 127) == 0 && (!a.gst || a.OHW % 64 == 0);
 }
@@ -1454,8 +1455,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo2_kernel(ConvK a, int R, i
   }
 #endif
 #undef DMC_PH
-  if (reg_epi_ok(a)) {   // uniform: the epilogue from the accumulators (the trailing barrier above is kept: the
-    reg_epilogue(a, acc, m0, n0, wm, wn);   // MFMA tail drains there)
+  if (!(PRO && a.reg_epi == 3) && reg_epi_ok(a)) {   // uniform: the epilogue from the accumulators (the trailing
+    reg_epilogue(a, acc, m0, n0, wm, wn);              // barrier above is kept: the MFMA tail drains there)
     return;
   }
 #pragma unroll

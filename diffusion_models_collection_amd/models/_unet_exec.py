@@ -337,6 +337,9 @@ class UNetExecutor(ExecCore):
         self.seed_ptr = None        # device address of the dropout seed word (graph-captured training step)
         # measured slower on MI355X (the overlapped kernels contend for LDS and CUs): opt-in only
         self.use_side = os.environ.get("DMC_SIDE_STREAM", "0") not in ("", "0")
+        # DMC_SIDE_MAXHW > 0: only weight gradients on maps of at most that many pixels go to the side stream (the
+        # 8x8 / 4x4 levels, whose latency-bound launches leave most CUs idle)
+        self.side_maxhw = int(os.environ.get("DMC_SIDE_MAXHW", "0"))
         self.side = None
         self._side_reads = {}
         self._fin_state = (None, 0)
@@ -527,7 +530,8 @@ class UNetExecutor(ExecCore):
     # wait for the side reads first); (2) the flat gradient buffer is complete only after a join.
     @contextlib.contextmanager
     def _side(self, *reads):
-        if not self.use_side:
+        if not self.use_side or (self.side_maxhw > 0 and reads[0].dim() == 4
+                                 and reads[0].shape[1] * reads[0].shape[2] > self.side_maxhw):
             yield
             return
         main = torch.cuda.current_stream()

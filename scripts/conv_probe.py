@@ -34,7 +34,7 @@ SHAPES = {
 }
 
 
-def run(name, iters, epi="bias"):
+def run(name, iters, epi="bias", cold=False):
     B, H, W, C1, C2, Cout, kind = SHAPES[name]
     dt = torch.bfloat16
     dev = "cuda"
@@ -61,15 +61,29 @@ def run(name, iters, epi="bias"):
         K.conv(d, x1, x2, wp, y)
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
-    for _ in range(iters):
-        K.conv(d, x1, x2, wp, y)
-    e1.record(s)
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / iters
+    if cold:
+        # every launch with L2 and the MALL evicted (a 1 GiB write in between, outside the timed pair)
+        flush = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+        small = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+        ms = 0.0
+        for _ in range(iters):
+            (flush if cold == "cold" else small).fill_(1)   # "hot1": the same per-launch timing, caches kept
+            e0.record(s)
+            K.conv(d, x1, x2, wp, y)
+            e1.record(s)
+            e1.synchronize()
+            ms += e0.elapsed_time(e1)
+        ms /= iters
+    else:
+        e0.record(s)
+        for _ in range(iters):
+            K.conv(d, x1, x2, wp, y)
+        e1.record(s)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / iters
     flops = 2.0 * B * H * W * Cout * (C1 + C2) * kk * kk
     print(f"{name:8s} M={B*H*W:7d} K={(C1+C2)*kk*kk:5d} N={Cout:4d} splitk_ws={ws/2**20:6.1f}MiB "
-          f"{ms*1e3:8.1f} us  {flops/ms/1e9:7.1f} TFLOP/s", flush=True)
+          f"{ms*1e3:8.1f} us{' ' + cold if cold else ''}  {flops/ms/1e9:7.1f} TFLOP/s", flush=True)
 
 
 def main():
@@ -77,9 +91,11 @@ def main():
     ap.add_argument("--shape", default="all")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--epi", default="bias", choices=["bias", "full"])
+    ap.add_argument("--cold", default="", choices=["", "cold", "hot1"],
+                    help="time launches one at a time, with L2 / MALL evicted before each (cold) or not (hot1)")
     a = ap.parse_args()
     for name in (SHAPES if a.shape == "all" else [a.shape]):
-        run(name, a.iters, a.epi)
+        run(name, a.iters, a.epi, a.cold)
 
 
 if __name__ == "__main__":
