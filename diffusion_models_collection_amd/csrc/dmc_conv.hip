@@ -3142,8 +3142,13 @@ void launch_halo2(const ConvK& k, int hp, int R, int nimg, hipStream_t s) {
 template <bool BUF>
 void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
   if (p.splits > 1) {
+    const dim3 gs(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128), p.splits);
     if (dmc::opt(dmc::OPT_SK_2B))   // A/B: the 2-stage ring, two split blocks per CU
-      conv_fwd_glds_kernel<2, 2, BUF, 2><<<dim3(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128), p.splits), 256, 0, s>>>(k);
+      conv_fwd_glds_kernel<2, 2, BUF, 2><<<gs, 256, 0, s>>>(k);
+    else if (dmc::opt(dmc::OPT_SK_STAGES) == 5)   // A/B: 4 stages in flight (160 KB ring): a split's stages at once
+      conv_fwd_glds_kernel<2, 2, BUF, 5><<<gs, 256, 0, s>>>(k);
+    else if (dmc::opt(dmc::OPT_SK_STAGES) == 4)
+      conv_fwd_glds_kernel<2, 2, BUF, 4><<<gs, 256, 0, s>>>(k);
     else
       conv_fwd_glds_kernel<2, 2, BUF><<<dim3(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128), p.splits), 256, 0, s>>>(k);
     const int Cpad = dmc::cdiv(k.Cout, 128) * 128;

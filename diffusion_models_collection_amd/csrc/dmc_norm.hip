@@ -821,14 +821,16 @@ __global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* cf, ch
 // the registers with gn_bwd_apply's formula -- one HBM pass over x and g instead of two and one launch instead of
 // two. The per-(n, c) pixel sums of the stored dx (bias / time-embedding gradients) are reduced in-block and
 // written directly; dgamma / dbeta and the per-c sums are column sums over n (gn_bwd_finish_kernel).
-template <int NR, int NT>
+// IPB = 2 (DMC_GN_BWD_IPB): a block runs two samples, the second one's x / g rows DMA'd into registers with the
+// first's, so they land while the first sample's reductions and dx stores run (with one sample per block the whole
+// grid loads, then reduces, then stores in lockstep); the per-sample arithmetic is unchanged (bitwise).
+template <int NR, int NT, int IPB = 1>
 __global__ __launch_bounds__(NT) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]*/, char* dx1, char* dx2, int ld1,
                                                      int ld2, int acc1, int acc2, float* sums /*[N][C]*/,
                                                      float* out_nc, int ld_nc) {
   using T = bf16_t;
   constexpr int EPC = 8;
   constexpr bool EARLY_ACC = NR <= 2;   // the accumulate operand loaded with x and g (register budget allows it)
-  const int n = blockIdx.x;
   const uint32_t dseed = drop_seed(b.dseed, b.dseed_base);
   const int C = b.s.C1 + b.s.C2, cpg = C / b.G, G = b.G, HW = b.HW;
   const int Cs = C / (int)gridDim.y, cb = (int)blockIdx.y * Cs, g0 = cb / cpg;
@@ -844,135 +846,150 @@ __global__ __launch_bounds__(NT) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]
   const bool first = c0 < b.s.C1;
   char* const dst = first ? dx1 : dx2;
   const int ldd = first ? ld1 : ld2, cd = first ? c0 : c0 - b.s.C1, acc = first ? acc1 : acc2;
-  v4i bx[NR], bg[NR], bp[NR];
-#pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    const int p = r0 + j * rpi;
-    if (active && p < HW) {
-      bx[j] = load_chunk2<T>(b.s, n * HW + p, c0);
-      bg[j] = *(const v4i*)(b.g + ((size_t)(n * HW + p) * b.ld_g + c0) * sizeof(T));
-      if (EARLY_ACC && acc) bp[j] = *(const v4i*)(dst + ((size_t)(n * HW + p) * ldd + cd) * sizeof(T));
-    }
-  }
-  // a thread's 8 channels lie in one group (groups are whole 8-channel chunks): one (mean, rstd) pair
-  const int gt = c0 / cpg;
-  const float mean = b.mr[((size_t)n * G + gt) * 2], rstd = b.mr[((size_t)n * G + gt) * 2 + 1];
-  float gm[EPC], bt[EPC], a1[EPC], a2[EPC];
-  {
-    const v4f one = {1.f, 1.f, 1.f, 1.f}, zero = {0.f, 0.f, 0.f, 0.f};
-    const v4f g0v = b.gamma ? *(const v4f*)(b.gamma + c0) : one, g1v = b.gamma ? *(const v4f*)(b.gamma + c0 + 4) : one;
-    const v4f b0v = b.beta ? *(const v4f*)(b.beta + c0) : zero, b1v = b.beta ? *(const v4f*)(b.beta + c0 + 4) : zero;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) { gm[e] = g0v[e]; gm[e + 4] = g1v[e]; bt[e] = b0v[e]; bt[e + 4] = b1v[e]; }
-  }
-  if (r0 == 0) {
-#pragma unroll
-    for (int e = 0; e < EPC; ++e) sG[col * EPC + e] = gm[e];
-  }
-#pragma unroll
-  for (int e = 0; e < EPC; ++e) { a1[e] = 0.f; a2[e] = 0.f; }
-#pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    const int p = r0 + j * rpi;
-    if (!(active && p < HW)) break;
-    const int pix = n * HW + p;
-    float x[EPC], gv[EPC];
-    Chunk<T>::unpack(bx[j], x);
-    Chunk<T>::unpack(bg[j], gv);
-#pragma unroll
-    for (int e = 0; e < EPC; ++e) {
-      float g = gv[e];
-      if (b.dthresh) g = drop_keep((uint64_t)pix * C + c0 + e, dseed, b.dthresh) ? g * b.dscale : 0.f;
-      float xh;
-      const float dz = gn_dz(x[e], g, mean, rstd, gm[e], bt[e], xh, b.silu);
-      a1[e] += dz;
-      a2[e] = fmaf(dz, xh, a2[e]);
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < EPC; ++e) { red[tid][2 * e] = active ? a1[e] : 0.f; red[tid][2 * e + 1] = active ? a2[e] : 0.f; }
-  __syncthreads();
-  onecta_chan_totals<EPC, NT>(red, Cs, CPR, rows, sA);   // sA[c - cb] (rows past `rows` held zeros)
-  __syncthreads();
-  for (int c = tid; c < Cs; c += NT) {
-    A[((size_t)n * C + cb + c) * 2] = sA[c][0];
-    A[((size_t)n * C + cb + c) * 2 + 1] = sA[c][1];
-  }
-  const float cnt = (float)cpg * (float)HW;
-  const int wv = tid >> 6, ln = tid & 63;
-  for (int gl = wv; gl < Cs / cpg; gl += NT / 64) {   // one wave per group: gamma-weighted channel totals
-    float m1 = 0.f, m2 = 0.f;
-    for (int cl = gl * cpg + ln; cl < (gl + 1) * cpg; cl += 64) {
-      const float g_ = sG[cl];
-      m1 = fmaf(sA[cl][0], g_, m1); m2 = fmaf(sA[cl][1], g_, m2);
-    }
-    m1 = wave_sum(m1); m2 = wave_sum(m2);
-    if (ln == 0) { sm[gl][0] = m1 / cnt; sm[gl][1] = m2 / cnt; }
-  }
-  if (!EARLY_ACC && acc) {   // read while the group sums finish
+  auto load_item = [&](int n, v4i* bx, v4i* bg, v4i* bp) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       const int p = r0 + j * rpi;
-      if (active && p < HW) bp[j] = *(const v4i*)(dst + ((size_t)(n * HW + p) * ldd + cd) * sizeof(T));
+      if (active && p < HW) {
+        bx[j] = load_chunk2<T>(b.s, n * HW + p, c0);
+        bg[j] = *(const v4i*)(b.g + ((size_t)(n * HW + p) * b.ld_g + c0) * sizeof(T));
+        if (EARLY_ACC && acc) bp[j] = *(const v4i*)(dst + ((size_t)(n * HW + p) * ldd + cd) * sizeof(T));
+      }
     }
-  }
-  __syncthreads();
-  if (!active && !sums) return;
-  // gn_bwd_final's per-channel coefficients (same expressions)
-  const int gl = gt - g0;
-  const float ku = -rstd * rstd * sm[gl][1], kw = -rstd * sm[gl][0];
-  float sc[EPC], sh[EPC], sum[EPC];
+  };
+  auto run_item = [&](int n, v4i* bx, v4i* bg, v4i* bp) __attribute__((always_inline)) {
+    // a thread's 8 channels lie in one group (groups are whole 8-channel chunks): one (mean, rstd) pair
+    const int gt = c0 / cpg;
+    const float mean = b.mr[((size_t)n * G + gt) * 2], rstd = b.mr[((size_t)n * G + gt) * 2 + 1];
+    float gm[EPC], bt[EPC], a1[EPC], a2[EPC];
+    {
+      const v4f one = {1.f, 1.f, 1.f, 1.f}, zero = {0.f, 0.f, 0.f, 0.f};
+      const v4f g0v = b.gamma ? *(const v4f*)(b.gamma + c0) : one, g1v = b.gamma ? *(const v4f*)(b.gamma + c0 + 4) : one;
+      const v4f b0v = b.beta ? *(const v4f*)(b.beta + c0) : zero, b1v = b.beta ? *(const v4f*)(b.beta + c0 + 4) : zero;
 #pragma unroll
-  for (int e = 0; e < EPC; ++e) {
-    sc[e] = rstd * gm[e];
-    sh[e] = bt[e] - mean * sc[e];
-    sum[e] = 0.f;
-  }
+      for (int e = 0; e < 4; ++e) { gm[e] = g0v[e]; gm[e + 4] = g1v[e]; bt[e] = b0v[e]; bt[e + 4] = b1v[e]; }
+    }
+    if (r0 == 0) {
 #pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    const int p = r0 + j * rpi;
-    if (!(active && p < HW)) break;
-    const int pix = n * HW + p;
-    float x[EPC], gv[EPC], o[EPC];
-    Chunk<T>::unpack(bx[j], x);
-    Chunk<T>::unpack(bg[j], gv);
+      for (int e = 0; e < EPC; ++e) sG[col * EPC + e] = gm[e];
+    }
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) { a1[e] = 0.f; a2[e] = 0.f; }
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int p = r0 + j * rpi;
+      if (!(active && p < HW)) break;
+      const int pix = n * HW + p;
+      float x[EPC], gv[EPC];
+      Chunk<T>::unpack(bx[j], x);
+      Chunk<T>::unpack(bg[j], gv);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        float g = gv[e];
+        if (b.dthresh) g = drop_keep((uint64_t)pix * C + c0 + e, dseed, b.dthresh) ? g * b.dscale : 0.f;
+        float xh;
+        const float dz = gn_dz(x[e], g, mean, rstd, gm[e], bt[e], xh, b.silu);
+        a1[e] += dz;
+        a2[e] = fmaf(dz, xh, a2[e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) { red[tid][2 * e] = active ? a1[e] : 0.f; red[tid][2 * e + 1] = active ? a2[e] : 0.f; }
+    __syncthreads();
+    onecta_chan_totals<EPC, NT>(red, Cs, CPR, rows, sA);   // sA[c - cb] (rows past `rows` held zeros)
+    __syncthreads();
+    for (int c = tid; c < Cs; c += NT) {
+      A[((size_t)n * C + cb + c) * 2] = sA[c][0];
+      A[((size_t)n * C + cb + c) * 2 + 1] = sA[c][1];
+    }
+    const float cnt = (float)cpg * (float)HW;
+    const int wv = tid >> 6, ln = tid & 63;
+    for (int gl = wv; gl < Cs / cpg; gl += NT / 64) {   // one wave per group: gamma-weighted channel totals
+      float m1 = 0.f, m2 = 0.f;
+      for (int cl = gl * cpg + ln; cl < (gl + 1) * cpg; cl += 64) {
+        const float g_ = sG[cl];
+        m1 = fmaf(sA[cl][0], g_, m1); m2 = fmaf(sA[cl][1], g_, m2);
+      }
+      m1 = wave_sum(m1); m2 = wave_sum(m2);
+      if (ln == 0) { sm[gl][0] = m1 / cnt; sm[gl][1] = m2 / cnt; }
+    }
+    if (!EARLY_ACC && acc) {   // read while the group sums finish
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        const int p = r0 + j * rpi;
+        if (active && p < HW) bp[j] = *(const v4i*)(dst + ((size_t)(n * HW + p) * ldd + cd) * sizeof(T));
+      }
+    }
+    __syncthreads();
+    if (!active && !sums) return;
+    // gn_bwd_final's per-channel coefficients (same expressions)
+    const int gl = gt - g0;
+    const float ku = -rstd * rstd * sm[gl][1], kw = -rstd * sm[gl][0];
+    float sc[EPC], sh[EPC], sum[EPC];
 #pragma unroll
     for (int e = 0; e < EPC; ++e) {
-      float gg = gv[e];
-      if (b.dthresh) gg = drop_keep((uint64_t)pix * C + c0 + e, dseed, b.dthresh) ? gg * b.dscale : 0.f;
-      float dz = gg;
-      if (b.silu) {
-        const float z = fmaf(x[e], sc[e], sh[e]);
-        const float sg = sigmoid_f(z);
-        dz = gg * sg * (1.f + z * (1.f - sg));
+      sc[e] = rstd * gm[e];
+      sh[e] = bt[e] - mean * sc[e];
+      sum[e] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int p = r0 + j * rpi;
+      if (!(active && p < HW)) break;
+      const int pix = n * HW + p;
+      float x[EPC], gv[EPC], o[EPC];
+      Chunk<T>::unpack(bx[j], x);
+      Chunk<T>::unpack(bg[j], gv);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        float gg = gv[e];
+        if (b.dthresh) gg = drop_keep((uint64_t)pix * C + c0 + e, dseed, b.dthresh) ? gg * b.dscale : 0.f;
+        float dz = gg;
+        if (b.silu) {
+          const float z = fmaf(x[e], sc[e], sh[e]);
+          const float sg = sigmoid_f(z);
+          dz = gg * sg * (1.f + z * (1.f - sg));
+        }
+        o[e] = fmaf(sc[e], dz, fmaf(ku, x[e] - mean, kw));
       }
-      o[e] = fmaf(sc[e], dz, fmaf(ku, x[e] - mean, kw));
-    }
-    if (acc) {
-      float prev[EPC];
-      Chunk<T>::unpack(bp[j], prev);
+      if (acc) {
+        float prev[EPC];
+        Chunk<T>::unpack(bp[j], prev);
 #pragma unroll
-      for (int e = 0; e < EPC; ++e) o[e] += prev[e];
-    }
-    const v4i packed = Chunk<T>::pack(o);
-    *(v4i*)(dst + ((size_t)pix * ldd + cd) * sizeof(T)) = packed;
-    if (sums) {
-      Chunk<T>::unpack(packed, o);   // sum what was stored
+        for (int e = 0; e < EPC; ++e) o[e] += prev[e];
+      }
+      const v4i packed = Chunk<T>::pack(o);
+      *(v4i*)(dst + ((size_t)pix * ldd + cd) * sizeof(T)) = packed;
+      if (sums) {
+        Chunk<T>::unpack(packed, o);   // sum what was stored
 #pragma unroll
-      for (int e = 0; e < EPC; ++e) sum[e] += o[e];
+        for (int e = 0; e < EPC; ++e) sum[e] += o[e];
+      }
     }
-  }
-  if (!sums) return;
-  float (*red1)[2 * EPC] = red;
+    if (!sums) return;
+    float (*red1)[2 * EPC] = red;
 #pragma unroll
-  for (int e = 0; e < EPC; ++e) { red1[tid][2 * e] = active ? sum[e] : 0.f; red1[tid][2 * e + 1] = 0.f; }
-  __syncthreads();
-  onecta_chan_totals<EPC, NT>(red, Cs, CPR, rows, sA);   // the same fixed-order lane-parallel channel totals
-  __syncthreads();
-  for (int cl = tid; cl < Cs; cl += NT) {
-    const float v = sA[cl][0];
-    sums[(size_t)n * C + cb + cl] = v;
-    if (out_nc) out_nc[(size_t)n * ld_nc + cb + cl] = v;
+    for (int e = 0; e < EPC; ++e) { red1[tid][2 * e] = active ? sum[e] : 0.f; red1[tid][2 * e + 1] = 0.f; }
+    __syncthreads();
+    onecta_chan_totals<EPC, NT>(red, Cs, CPR, rows, sA);   // the same fixed-order lane-parallel channel totals
+    __syncthreads();
+    for (int cl = tid; cl < Cs; cl += NT) {
+      const float v = sA[cl][0];
+      sums[(size_t)n * C + cb + cl] = v;
+      if (out_nc) out_nc[(size_t)n * ld_nc + cb + cl] = v;
+    }
+  };
+  const int nb = (int)blockIdx.x * IPB;
+  v4i bx0[NR], bg0[NR], bp0[NR];
+  load_item(nb, bx0, bg0, bp0);
+  if constexpr (IPB == 1) {
+    run_item(nb, bx0, bg0, bp0);
+  } else {
+    v4i bx1[NR], bg1[NR], bp1[NR];
+    load_item(nb + 1, bx1, bg1, bp1);
+    run_item(nb, bx0, bg0, bp0);
+    __syncthreads();   // the LDS reduction buffers are reused
+    run_item(nb + 1, bx1, bg1, bp1);
   }
 }
 
@@ -1164,7 +1181,10 @@ int gn_silu_bwd_impl(int dtype, const void* g, int ld_g, const void* x1, const v
   if (!part && dtype != DMC_F32 && N >= 64 && fused_max > 0 && !dmc::opt(dmc::OPT_GN_BWD_SPLIT) &&
       HW <= dmc::opt(dmc::OPT_GN_BWD_FUSED_MAXHW)) {
     // DMC_GN_BWD_NT: threads per block (1024, or 512: two blocks per CU, twice the channel slices)
-    const int NT = dmc::opt(dmc::OPT_GN_BWD_NT) == 512 ? 512 : 1024;
+    // (two samples per block, DMC_GN_BWD_IPB = 2, runs 512-thread blocks: with 1024 threads the second sample's rows
+    // do not fit the 128-VGPR budget at 4 chunks per thread)
+    const bool want2 = dmc::opt(dmc::OPT_GN_BWD_IPB) == 2;
+    const int NT = (dmc::opt(dmc::OPT_GN_BWD_NT) == 512 || want2) ? 512 : 1024;
     auto rows = [&](int s_) { const int rp = NT / (C / s_ / epc); return rp > 0 ? (HW + rp - 1) / rp : 1 << 30; };
     auto ok = [&](int s_) { return C % s_ == 0 && (C / s_) % (C / G) == 0 && (C / s_) % epc == 0 && C / s_ <= NT; };
     int S = 1;
@@ -1176,9 +1196,13 @@ int gn_silu_bwd_impl(int dtype, const void* g, int ld_g, const void* x1, const v
       const bool defer = A_keep && (!dx_sum_c || sums_keep);
       if (defer) A = A_keep;
       float* ssum = want_sums ? (defer && sums_keep ? sums_keep : sums) : nullptr;
-      const dim3 gf(N, S);
+      // DMC_GN_BWD_IPB = 2: two samples per block (needs N even and at least 256 blocks left)
+      const bool ipb2 = want2 && N % 2 == 0 && (N / 2) * S >= 256;
+      const dim3 gf(ipb2 ? N / 2 : N, S);
 #define DMC_GNBF(NR_) do { \
-        if (NT == 512) gn_bwd_fused<NR_, 512><<<gf, 512, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
+        if (ipb2) gn_bwd_fused<NR_, 512, 2><<<gf, 512, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
+                                                             accumulate1, accumulate2, ssum, dx_sum_nc, ld_sum_nc); \
+        else if (NT == 512) gn_bwd_fused<NR_, 512><<<gf, 512, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
                                                            accumulate1, accumulate2, ssum, dx_sum_nc, ld_sum_nc); \
         else gn_bwd_fused<NR_, 1024><<<gf, 1024, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
                                                      accumulate1, accumulate2, ssum, dx_sum_nc, ld_sum_nc); \

@@ -577,6 +577,37 @@ def test_gn_bwd_deferred_column_sums_bitwise(shape):
         assert torch.equal(u, v)
 
 
+@pytest.mark.parametrize("shape", [(128, 32, 32, 128), (128, 16, 16, 256), (128, 8, 8, 256), (128, 4, 4, 512)])
+def test_gn_bwd_two_samples_per_block_bitwise(shape, dmc_opt):
+    """gn_bwd_fused with two samples per block (DMC_GN_BWD_IPB=2: the second sample's rows loaded with the first's)
+    gives BITWISE the one-sample-per-block result at the same block size (512 threads): dx with dropout and
+    accumulation, the per-(n, c) / per-c dx sums, dgamma / dbeta."""
+    L, K = _lib()
+    torch.manual_seed(10)
+    N, H, W, C = shape
+    G, dt, HW = 8, torch.bfloat16, H * W
+    x = (torch.randn(N, H, W, C) * 1.3 + 0.4).to(dt).to(DEV)
+    g = torch.randn(N, H, W, C).to(dt).to(DEV)
+    prev = torch.randn(N, H, W, C).to(dt).to(DEV)
+    gamma, beta = (torch.rand(C) + 0.5).to(DEV), torch.randn(C).to(DEV)
+    _, _, mr = K.gn_stats(dt, x, None, N, HW, C, 0, C, 0, G, 1e-5, gamma, beta)
+    drop = (7, 1 << 29, 1.0 / 0.875)
+    outs = []
+    for ipb in (1, 2):
+        dmc_opt("DMC_GN_BWD_NT", 512)
+        dmc_opt("DMC_GN_BWD_IPB", ipb)
+        dx = prev.clone()
+        dg, db, sc_ = (torch.full((C,), -3.0, device=DEV) for _ in range(3))
+        snc = torch.empty(N, C, device=DEV)
+        K.gn_bwd(dt, g, C, x, None, N, HW, C, 0, C, 0, G, mr, gamma, beta, True, drop, dx, None, C, 0, 1, 0, dg, db,
+                 dx_sum_nc=snc, ld_sum_nc=C, dx_sum_c=sc_)
+        torch.cuda.synchronize()
+        outs.append((dx, dg, db, sc_, snc))
+    assert not torch.isnan(outs[1][0].float()).any()
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_groupnorm_stats_and_backward(dt):
     L, K = _lib()
