@@ -15,7 +15,7 @@ LIB_PATH = Path(os.environ.get("DMC_LIB", _PKG / "libdmc.so"))
 
 DMC_F32, DMC_BF16 = 0, 1
 MODE_NORMAL, MODE_UPSAMPLE, MODE_DILATE = 0, 1, 2
-PRO_NONE, PRO_AFFINE_SILU, PRO_SILU, PRO_AFFINE = 0, 1, 2, 3
+PRO_NONE, PRO_AFFINE_SILU, PRO_SILU, PRO_AFFINE, PRO_GN_SILU = 0, 1, 2, 3, 4
 LOSS = {"l1": 0, "l2": 1, "huber": 2}
 PACK_FWD, PACK_DGRAD, PACK_UPDGRAD = 0, 1, 2
 
@@ -40,6 +40,7 @@ class ConvDesc(ctypes.Structure):
         ("silu_pre", _c_p), ("ld_silu", _c_int), ("Csplit", _c_int), ("ldy1", _c_int), ("ldy2", _c_int),
         ("out_f32", _c_int), ("out_nchw", _c_int), ("act", _c_int), ("y_pre", _c_p), ("ld_pre", _c_int),
         ("gnb", _c_p), ("gn_part", _c_p), ("wg_bias", _c_p), ("gn_fin", _c_p),
+        ("pro_gn", _c_p),
     ]
 
 

@@ -169,13 +169,58 @@ DMC_DEV float wave_max(float v) {
 
 // ---- GroupNorm statistics from conv-epilogue partials (mean, M2 per 64-pixel segment x 8-channel chunk) ----
 // Chan's combination of (n, m, q) with (nb, mb, qb).
+// The fused / unfused steps are spelled out (no contraction left to the compiler): the combine runs in several
+// kernels (dmc_gn_finalize, the producing conv's last block, the GroupNorm-prologue conv) that must agree bitwise.
 DMC_DEV void gn_chan(float& n, float& m, float& q, float nb, float mb, float qb) {
-  const float tot = n + nb;
+  const float tot = __fadd_rn(n, nb);
   if (tot == 0.f) return;
-  const float d = mb - m, r = nb / tot;
-  m += d * r;
-  q += qb + d * d * n * r;
+  const float d = __fsub_rn(mb, m), r = __fdiv_rn(nb, tot);
+  m = __builtin_fmaf(d, r, m);
+  q = __fadd_rn(q, __builtin_fmaf(__fmul_rn(__fmul_rn(d, d), n), r, qb));
   n = tot;
+}
+// The wave-wide part of gn_group_stats: a fixed xor tree over the 64 lanes' (count, mean, M2), then (mean, rstd).
+DMC_DEV void gn_group_tree(float cn, float m, float q, float eps, float& mean, float& rstd) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int sh = 1; sh < 64; sh <<= 1) {
+    const float nb = __shfl_xor(cn, sh), mb = __shfl_xor(m, sh), qb = __shfl_xor(q, sh);
+    // both lanes of a pair must end with the same value: combine in lane order (lower lane first)
+    if ((lane & sh) == 0) gn_chan(cn, m, q, nb, mb, qb);
+    else { float n2 = nb, m2 = mb, q2 = qb; gn_chan(n2, m2, q2, cn, m, q); cn = n2; m = m2; q = q2; }
+  }
+  mean = m;
+  const float var = fmaxf(__fdiv_rn(q, cn), 0.f);
+  rstd = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(var, eps)));
+}
+// gn_group_stats in two halves for a caller that overlaps the loads with other memory traffic (the GroupNorm-prologue
+// halo conv): gn_group_fetch loads the lane's partials (t = lane, lane + 64: np <= 128), gn_group_reduce combines them
+// in gn_group_stats' order -- bitwise its (mean, rstd).
+struct GnLane { float m[2], q[2]; };
+DMC_DEV GnLane gn_group_fetch(const float* p1, int nch1, const float* p2, int nch2, int n, int g, int spi, int G) {
+  const int lane = threadIdx.x & 63;
+  const int C = 8 * (nch1 + nch2), cpg = C / G, kpg = cpg / 8, np = spi * kpg;
+  GnLane v = {{0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int t = lane + 64 * k;
+    if (t < np) {
+      const int sg = n * spi + t / kpg, kc = g * kpg + t % kpg;
+      const float* pp = kc < nch1 ? p1 + ((size_t)sg * nch1 + kc) * 2 : p2 + ((size_t)sg * nch2 + (kc - nch1)) * 2;
+      const v2f w = *(const v2f*)pp;
+      v.m[k] = w[0];
+      v.q[k] = w[1];
+    }
+  }
+  return v;
+}
+DMC_DEV void gn_group_reduce(const GnLane& v, int np, float eps, float& mean, float& rstd) {
+  const int lane = threadIdx.x & 63;
+  float cn = 0.f, m = 0.f, q = 0.f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+    if (lane + 64 * k < np) gn_chan(cn, m, q, 512.f, v.m[k], v.q[k]);
+  gn_group_tree(cn, m, q, eps, mean, rstd);
 }
 // One wave combines GroupNorm group g of image n: lane l takes partials l, l+64, ... (segments outer, the group's
 // chunks inner; p1's chunks, then p2's), the lanes then combine over a fixed xor tree (deterministic). Returns
@@ -200,16 +245,7 @@ DMC_DEV void gn_group_stats(const float* p1, int nch1, const float* p2, int nch2
     }
     gn_chan(cn, m, q, 512.f, pm, pq);
   }
-#pragma unroll
-  for (int sh = 1; sh < 64; sh <<= 1) {
-    const float nb = __shfl_xor(cn, sh), mb = __shfl_xor(m, sh), qb = __shfl_xor(q, sh);
-    // both lanes of a pair must end with the same value: combine in lane order (lower lane first)
-    if ((lane & sh) == 0) gn_chan(cn, m, q, nb, mb, qb);
-    else { float n2 = nb, m2 = mb, q2 = qb; gn_chan(n2, m2, q2, cn, m, q); cn = n2; m = m2; q = q2; }
-  }
-  mean = m;
-  const float var = fmaxf(q / cn, 0.f);
-  rstd = 1.0f / sqrtf(var + eps);
+  gn_group_tree(cn, m, q, eps, mean, rstd);
 }
 // The GroupNorm affine folded into a per-channel (scale, shift): z = x * scale + shift.
 DMC_DEV void gn_fold(float mean, float rstd, float gm, float bt, float& sc, float& sh) {

@@ -20,6 +20,9 @@ struct ConvK {
   int N, H, W, C1, C2, ld1, ld2, Kc, OH, OW, Cout, ntaps, mode, stride;
   int tkw, tdy0, tdx0, tsy, tsx;   // tap grid: tap t -> (tdy0 + tsy*(t / tkw), tdx0 + tsx*(t % tkw))
   int prologue; const float* psc; const float* psh; int ldp;
+  // DMC_PRO_GN_SILU (prologue = AFFINE_SILU, pro_part = 1): psc / psh are the GroupNorm partials of x1 / x2 and the
+  // scale / shift are combined per block (halo_gn_fetch / halo_gn_finish)
+  int pro_part; int pG; float peps; const float* pgam; const float* pbet;
   uint32_t dseed, dthresh; float dscale; int dld; const uint32_t* dseed_base;
   const float* bias; const float* addvec; int ld_add;
   const char* resid; int ld_res; const float* silu_pre; int ld_silu;
@@ -1255,6 +1258,46 @@ DMC_DEV void halo_pro_load(const ConvK& a, int n, int c0, v4f* st) {
   st[0] = *(const v4f*)sc; st[1] = *(const v4f*)(sc + 4);
   st[2] = *(const v4f*)sh; st[3] = *(const v4f*)(sh + 4);
 }
+// DMC_PRO_GN_SILU: the same (scale, shift) rows combined in the block from the partials, bitwise dmc_gn_finalize's
+// (gn_group_fetch / gn_group_reduce are gn_group_stats in two halves, gn_fold its fold). The fetch goes out before
+// the chunk's halo DMA and the combine runs while the halo lands: the wave combines every group of its 64-channel
+// chunk (<= 4: C/G >= 16) with the 64-lane tree, then each lane keeps its own 8 channels' group.
+struct HaloGn { GnLane gl[4]; v4f gb[4]; };
+DMC_DEV void halo_gn_fetch(const ConvK& a, int n, int c0, HaloGn& h) {
+  const int lane = threadIdx.x & 63, lrow = lane >> 3, lc = (lane & 7) ^ lrow;
+  const int C = a.C1 + a.C2, cpg = C / a.pG, g0 = c0 / cpg, spi = a.OHW / 64;
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    if ((g0 + s) * cpg < c0 + 64) h.gl[s] = gn_group_fetch(a.psc, a.C1 / 8, a.psh, a.C2 / 8, n, g0 + s, spi, a.pG);
+  const int c = c0 + lc * 8;
+  const v4f one = {1.f, 1.f, 1.f, 1.f}, zero = {0.f, 0.f, 0.f, 0.f};
+  h.gb[0] = a.pgam ? *(const v4f*)(a.pgam + c) : one;
+  h.gb[1] = a.pgam ? *(const v4f*)(a.pgam + c + 4) : one;
+  h.gb[2] = a.pbet ? *(const v4f*)(a.pbet + c) : zero;
+  h.gb[3] = a.pbet ? *(const v4f*)(a.pbet + c + 4) : zero;
+}
+DMC_DEV void halo_gn_finish(const ConvK& a, int c0, const HaloGn& h, v4f* st) {
+  const int lane = threadIdx.x & 63, lrow = lane >> 3, lc = (lane & 7) ^ lrow;
+  const int C = a.C1 + a.C2, cpg = C / a.pG, g0 = c0 / cpg, np = (a.OHW / 64) * (cpg / 8);
+  const int gl = (c0 + lc * 8) / cpg - g0;   // this lane's group slot
+  float mean = 0.f, rstd = 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if ((g0 + s) * cpg < c0 + 64) {
+      float m, r;
+      gn_group_reduce(h.gl[s], np, a.peps, m, r);
+      if (gl == s) { mean = m; rstd = r; }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float sc, sh;
+    gn_fold(mean, rstd, h.gb[0][e], h.gb[2][e], sc, sh);
+    st[0][e] = sc; st[2][e] = sh;
+    gn_fold(mean, rstd, h.gb[1][e], h.gb[3][e], sc, sh);
+    st[1][e] = sc; st[3][e] = sh;
+  }
+}
 // The rewrite's LDS accesses are inline asm: for plain C++ LDS stores hipcc inserts vmcnt(0) (they may alias
 // the in-flight LDS-DMA), draining the weight ring; a wave only touches the pieces its own, already-landed
 // DMA wrote, and nobody reads them before the next block barrier.
@@ -1382,10 +1425,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo2_kernel(ConvK a, int R, i
     if (t == 0) {
       // chunk c's halo into the single buffer: every wave is done with chunk c-1's taps
       if (c > 0) __syncthreads();
-      if (PRO) halo_pro_load(a, n_first, c * 64, pst);
+      HaloGn hg;
+      if (PRO) {
+        if (a.pro_part) halo_gn_fetch(a, n_first, c * 64, hg);
+        else halo_pro_load(a, n_first, c * 64, pst);
+      }
       halo_issue<HP>(a, lds, c * 64, wave, 0, HP, h1, h2);
       if (c == 0)
         for (int q = 0; q < WS - 1 && q < nst; ++q) issue_w(q);
+      if (PRO && a.pro_part) halo_gn_finish(a, c * 64, hg, pst);   // while the halo lands
       __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
       if (PRO) halo_affine_silu<HP>(lds, wave, h1, pst);
     } else {
@@ -3011,6 +3059,19 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
     DMC_REQUIRE(ok, "conv: taps must form a regular grid");
   }
   k.prologue = d->prologue; k.psc = d->pro_scale; k.psh = d->pro_shift; k.ldp = d->ld_pro;
+  k.pro_part = 0; k.pG = 0; k.peps = 0.f; k.pgam = nullptr; k.pbet = nullptr;
+  if (d->prologue == DMC_PRO_GN_SILU) {
+    const int C = d->C1 + d->C2, HW = d->H * d->W;
+    DMC_REQUIRE(d->pro_gn && d->pro_scale && (d->C2 == 0 || d->pro_shift), "conv: DMC_PRO_GN_SILU needs pro_gn and "
+                "the partials of every source");
+    const int G = d->pro_gn->G;
+    DMC_REQUIRE(G > 0 && C % G == 0 && (C / G) % 8 == 0 && C / G >= 16 && d->C1 % 8 == 0 && d->C2 % 8 == 0 && HW % 64 == 0 &&
+                    (HW / 64) * (C / G / 8) <= 128 && d->drop_thresh == 0,
+                "conv: DMC_PRO_GN_SILU: G %d over %d channels, H*W %d", G, C, HW);
+    k.prologue = DMC_PRO_AFFINE_SILU;
+    k.pro_part = 1; k.pG = G; k.peps = d->pro_gn->eps; k.pgam = d->pro_gn->gamma; k.pbet = d->pro_gn->beta;
+    k.ldp = C;   // (no scale / shift rows: keeps halo2_pro_plan's row check satisfied)
+  }
   k.dseed = d->drop_seed; k.dthresh = d->drop_thresh; k.dscale = d->drop_scale; k.dld = d->drop_ld;
   k.dseed_base = d->drop_seed_base;
   k.bias = d->bias; k.addvec = d->addvec; k.ld_add = d->ld_add; k.resid = (const char*)d->resid; k.ld_res = d->ld_res;
@@ -3349,6 +3410,7 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     const int hp2 = halo2_pro_plan(k, &R, &nimg);
     if (hp2) { launch_halo2<true>(k, hp2, R, nimg, s); return dmc::check_launch("dmc_conv2d"); }
   }
+  DMC_REQUIRE(!k.pro_part, "conv: DMC_PRO_GN_SILU runs only on the halo prologue kernel (dmc_conv_halo_prologue)");
   if (sizeof(T) == 2 && k.prologue == DMC_PRO_NONE && !dmc::opt(dmc::OPT_NO_GLDS)) {
     // bf16, plain operands: LDS-DMA pipelined kernel
     FwdPlan p = plan_glds(k);
@@ -3551,6 +3613,7 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   if (fill_convk(d, x1, x2, nullptr, nullptr, nullptr, k)) return 1;
   const int epc = d->dtype == DMC_F32 ? 4 : 8;
   DMC_REQUIRE(ld_dy % epc == 0, "wgrad: ld_dy %d alignment", ld_dy);
+  DMC_REQUIRE(!k.pro_part, "wgrad: no DMC_PRO_GN_SILU prologue");
   hipStream_t s = dmc::as_stream(stream);
   int pps;
   int splits = wgrad_splits(d, &pps);

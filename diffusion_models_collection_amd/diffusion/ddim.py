@@ -11,6 +11,8 @@ is done on device: if any t_next < 0, alpha_next = 1 for the whole batch, exactl
 CFG batches the cond/uncond forwards into one 2B forward and fuses combine + x0 + dynamic threshold
 (per-row torch.quantile restatement) into dmc_cfg_x0.
 """
+import os
+
 import torch
 from tqdm import tqdm
 
@@ -114,8 +116,14 @@ class DDIM:
             z = self._noise(noise, i, x)
             return (x, tab[i], tab[i + 1]) + ((z,) if z is not None else ())
 
+        # every sample shares the step's timestep: a model that takes a length-1 t (UNet.shared_timestep) runs its
+        # time-embedding MLPs once per step instead of once per image
+        shared_t = (y is None and getattr(model, "shared_timestep", False)
+                    and os.environ.get("DMC_SHARED_T", "1") != "0")   # A/B switch
+
         def fn(x, t, tn, z=None):
-            return self.p_sample(model, x, t, tn, y, noise=z)
+            eps = model(x, t[:1], None) if shared_t else None
+            return self.p_sample(model, x, t, tn, y, eps=eps, noise=z)
 
         def record(i, x):
             bar.update(1)

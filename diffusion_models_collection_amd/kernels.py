@@ -72,6 +72,19 @@ def set_prologue(d, kind=L.PRO_NONE, scale=None, shift=None, ld=0, drop=None, dr
     d.drop_ld = drop_ld if drop is not None else 0
 
 
+def set_prologue_gn(d, part1, part2, G, eps, gamma, beta, ld=0):
+    """Prologue DMC_PRO_GN_SILU: SiLU(GroupNorm) with the statistics combined in the conv from the producing convs'
+    partials (part1 / part2 of the two sources, dmc_conv_desc.gn_part layout); include/dmc.h."""
+    f = L.GnFin()
+    f.G, f.eps, f.gamma, f.beta = G, eps, ptr(gamma), ptr(beta)
+    d.prologue = L.PRO_GN_SILU
+    d._keep_pro = (part1, part2, gamma, beta, f)
+    d.pro_scale, d.pro_shift, d.ld_pro = ptr(part1), ptr(part2), ld
+    d.pro_gn = ctypes.addressof(f)
+    d.drop_seed, d.drop_seed_base, d.drop_thresh, d.drop_scale = 0, None, 0, 1.0
+    d.drop_ld = 0
+
+
 def set_epilogue(d, bias=None, addvec=None, ld_add=0, resid=None, ld_res=0, silu_pre=None, ld_silu=0,
                  ldy1=0, ldy2=0, Csplit=None, out_f32=False, out_nchw=False, act=L.ACT_NONE, y_pre=None, ld_pre=0,
                  gn_part=None, gnb=None):

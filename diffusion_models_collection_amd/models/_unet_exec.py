@@ -65,6 +65,10 @@ _GN_APPLY_FIN = _GN_PARTIALS and os.environ.get("DMC_GN_APPLY_FIN", "0") not in 
 # The GroupNorm backward's parameter column sums deferred to one dmc_colsum_batch per gradient segment (A/B switch
 # DMC_GN_DEFER=0: one finish launch per GroupNorm)
 _GN_DEFER = os.environ.get("DMC_GN_DEFER", "1") not in ("", "0")
+# Inference: the GroupNorm-prologue halo conv combines the GroupNorm statistics itself from the producing convs'
+# partials (dmc_conv_desc prologue DMC_PRO_GN_SILU), so those GroupNorms need no finalize launch (A/B switch
+# DMC_PRO_PART=0: dmc_gn_finalize + the scale / shift prologue)
+_PRO_PART = _GN_PARTIALS and os.environ.get("DMC_PRO_PART", "1") not in ("", "0")
 
 
 class GnSt:
@@ -214,7 +218,10 @@ class ExecCore:
         if w is None:
             w = self._wpack(conv, packmode, Kc, dtype)
         d = K.make_desc(dtype, N, a.H, a.W, C1, C2, ld1, ld2, Kc, OH, OW, Cout, taps, mode, stride)
-        if pro is not None:
+        if pro is not None and pro[0] == L.PRO_GN_SILU:
+            gn = pro[3]
+            K.set_prologue_gn(d, pro[1], pro[2], gn.num_groups, gn.eps, gn.weight, gn.bias)
+        elif pro is not None:
             K.set_prologue(d, pro[0], pro[1], pro[2], C1 + C2, drop, C1 + C2)
         elif drop is not None:
             if act not in (L.ACT_GELU_DROP, L.ACT_DGELU):
@@ -508,10 +515,28 @@ class UNetExecutor(ExecCore):
             C1, C2 = a.C, (b.C if b else 0)
             d = K.make_desc(self.dt, N, a.H, a.W, C1, C2, key[5], key[6], L.kc_for(C1 + C2, self.dt), a.H, a.W, Cout,
                             K.TAPS3)
+            if st is None:   # shape query only (_pro_gn): any valid pointers
+                st = (torch.empty(N * (C1 + C2), dtype=torch.float32, device=a.t.device),) * 2
             bufs = st.bufs if isinstance(st, GnSt) else st     # pointers only: no statistics launch here
             K.set_prologue(d, L.PRO_AFFINE_SILU, bufs[0], bufs[1], C1 + C2)
             ok = self._halo_pro_cache[key] = K.conv_halo_prologue(d)
         return ok
+
+    def _pro_gn(self, srcs, gn, Cout):
+        """pro = (PRO_GN_SILU, partials of srcs, gn) when the GroupNorm-prologue halo conv of SiLU(gn(srcs)) can
+        combine gn's statistics itself from the producing convs' partials (no finalize launch), else None."""
+        if not _PRO_PART or self.dt != torch.bfloat16 or any(s.part is None for s in srcs):
+            return None
+        a = srcs[0]
+        b = srcs[1] if len(srcs) > 1 else None
+        if a.fin is not None and a.fin[0] is gn:
+            return None                      # finalised by the producing conv already
+        C, G, HW = a.C + (b.C if b else 0), gn.num_groups, a.H * a.W
+        if C % G or (C // G) % 8 or C // G < 16 or HW % 64 or (HW // 64) * (C // G // 8) > 128:
+            return None
+        if not self._halo_pro_ok(srcs, Cout, None):
+            return None
+        return (L.PRO_GN_SILU, a.part, b.part if b else None, gn)
 
     def _grad_target(self, act):
         """(buffer, accumulate) for writing a gradient contribution into act.grad."""
@@ -594,12 +619,17 @@ class UNetExecutor(ExecCore):
         te = m.time_embed
         mc = te[0].dim
         tdim = te[1].out_features
-        e0 = torch.empty(N, mc, dtype=f32, device=x.device)
+        # a length-1 t at inference (the samplers' shared timestep, UNet.shared_timestep): the embedding rows are
+        # computed once and broadcast to every image by the consuming epilogues (ld_add = 0)
+        Nt = t.shape[0]
+        if Nt != N and not (Nt == 1 and not keep and (m.num_classes is None or y is None)):
+            raise ValueError(f"UNet: t has {Nt} entries for a batch of {N}")
+        e0 = torch.empty(Nt, mc, dtype=f32, device=x.device)
         K.time_embed(t, mc, e0)
-        A0 = Act(e0.view(N, 1, 1, mc), 1, 1, mc)
-        A1 = self._new(N, 1, 1, tdim, f32)
+        A0 = Act(e0.view(Nt, 1, 1, mc), 1, 1, mc)
+        A1 = self._new(Nt, 1, 1, tdim, f32)
         self._conv([A0], te[1], K.TAPS1, 1, 1, tdim, bias=te[1].bias, out=A1.t, dtype=f32)
-        A2 = self._new(N, 1, 1, tdim, f32)
+        A2 = self._new(Nt, 1, 1, tdim, f32)
         self._conv([A1], te[3], K.TAPS1, 1, 1, tdim, pro=(L.PRO_SILU, None, None), bias=te[3].bias, out=A2.t,
                    dtype=f32)
         Ay = None
@@ -608,7 +638,7 @@ class UNetExecutor(ExecCore):
             ye = torch.empty(N, tdim, dtype=f32, device=x.device)
             K.embed_fwd(y, m.label_embed.weight, ye)
             Ay = Act(ye.view(N, 1, 1, tdim), 1, 1, tdim)
-        addvec = torch.empty(N, 1, 1, self.temb_total, dtype=f32, device=x.device)
+        addvec = torch.empty(Nt, 1, 1, self.temb_total, dtype=f32, device=x.device)
         Kt = L.kc_for(tdim, f32)
         self._conv([A2], None, K.TAPS1, 1, 1, self.temb_total, pro=(L.PRO_SILU, None, None), bias=self._temb_bias(),
                    out=addvec, dtype=f32, w=self._temb_pack(0, f32), Kc=Kt)
@@ -616,6 +646,7 @@ class UNetExecutor(ExecCore):
             self._conv([Ay], None, K.TAPS1, 1, 1, self.temb_total, pro=(L.PRO_SILU, None, None), resid=addvec,
                        out=addvec, dtype=f32, w=self._temb_pack(1, f32), Kc=Kt)
         self.addvec = addvec
+        self._ld_add = self.temb_total if Nt == N else 0
         if keep:
             tape.append(("temb", t, y, A0, A1, A2, Ay, addvec))
 
@@ -678,20 +709,27 @@ class UNetExecutor(ExecCore):
         # a1 = SiLU(GN1(x)) materialised once (the 3x3 implicit GEMM reads every pixel 9x; the weight
         # gradient re-reads it in backward). Inference (no tape): where the halo kernel takes the conv, it
         # applies GN+SiLU to its LDS-resident halo instead and nothing is materialised.
-        st1 = self._gn(srcs, gn1)
+        pg1 = self._pro_gn(srcs, gn1, Cout) if tape is None else None
+        st1 = None if pg1 is not None else self._gn(srcs, gn1)
         h1 = self._new(N, H, W, Cout)
         off = self.temb_off[id(rb)]
-        if tape is None and self._halo_pro_ok(srcs, Cout, st1):
+        if pg1 is not None:
+            a1 = None
+            self._conv(srcs, conv1, K.TAPS3, H, W, Cout, pro=pg1, bias=conv1.bias,
+                       addvec=self.addvec.view(self.addvec.shape[0], -1)[:, off:], ld_add=self._ld_add, out=h1.t,
+                       stats=h1, fin=(gn2, None))
+        elif tape is None and self._halo_pro_ok(srcs, Cout, st1):
             a1 = None
             self._conv(srcs, conv1, K.TAPS3, H, W, Cout, pro=(L.PRO_AFFINE_SILU, st1[0], st1[1]), bias=conv1.bias,
-                       addvec=self.addvec.view(N, -1)[:, off:], ld_add=self.temb_total, out=h1.t, stats=h1,
+                       addvec=self.addvec.view(self.addvec.shape[0], -1)[:, off:], ld_add=self._ld_add, out=h1.t, stats=h1,
                        fin=(gn2, None))
         else:
             a1 = self._apply(srcs, st1, silu=True)
             self._conv([a1], conv1, K.TAPS3, H, W, Cout, bias=conv1.bias,
-                       addvec=self.addvec.view(N, -1)[:, off:], ld_add=self.temb_total, out=h1.t, stats=h1,
+                       addvec=self.addvec.view(self.addvec.shape[0], -1)[:, off:], ld_add=self._ld_add, out=h1.t, stats=h1,
                        fin=(gn2, None))
-        st2 = self._gn([h1], gn2)
+        pg2 = self._pro_gn([h1], gn2, Cout) if tape is None and self._drop is None else None
+        st2 = None if pg2 is not None else self._gn([h1], gn2)
         if isinstance(rb.shortcut, torch.nn.Conv2d):
             s = torch.empty(N, H, W, Cout, dtype=self.dt, device=self.device)
             self._conv(srcs, rb.shortcut, K.TAPS1, H, W, Cout, bias=rb.shortcut.bias, out=s)
@@ -705,7 +743,11 @@ class UNetExecutor(ExecCore):
                 drop = drop + (self.seed_ptr,)
         self._blk_idx += 1
         out = self._new(N, H, W, Cout)
-        if tape is None and drop is None and self._halo_pro_ok([h1], Cout, st2):
+        if pg2 is not None:
+            a2 = None
+            self._conv([h1], conv2, K.TAPS3, H, W, Cout, pro=pg2, bias=conv2.bias, resid=resid, out=out.t,
+                       stats=out, fin=fin)
+        elif tape is None and drop is None and self._halo_pro_ok([h1], Cout, st2):
             a2 = None
             self._conv([h1], conv2, K.TAPS3, H, W, Cout, pro=(L.PRO_AFFINE_SILU, st2[0], st2[1]), bias=conv2.bias,
                        resid=resid, out=out.t, stats=out, fin=fin)

@@ -196,8 +196,14 @@ class UNet(nn.Module):
         self._executor = None
         return self
 
+    # Inference with one timestep for the whole batch may pass t of shape (1,) (the reference's broadcasting of
+    # time_mlp(emb)[:, :, None, None] gives the same result): the time-embedding MLPs then run on one row, broadcast
+    # by the convs' epilogues. Not with class labels, not with autograd. The samplers use it when this is set.
+    shared_timestep = True
+
     def forward(self, x, t, y=None):
-        """x: (B, C, H, W) f32, t: (B,) i64, y: (B,) i64 class labels or None -> eps (B, C_out, H, W) f32."""
+        """x: (B, C, H, W) f32, t: (B,) i64 (or (1,), see shared_timestep), y: (B,) i64 class labels or None ->
+        eps (B, C_out, H, W) f32."""
         if not x.is_cuda:
             raise RuntimeError("UNet runs on the MI355X HIP kernels only: move the model and inputs to a cuda device")
         return self.executor.run(x, t, y if self.num_classes is not None else None)

@@ -25,7 +25,14 @@ extern "C" {
 
 enum { DMC_F32 = 0, DMC_BF16 = 1 };
 enum { DMC_MODE_NORMAL = 0, DMC_MODE_UPSAMPLE = 1, DMC_MODE_DILATE = 2 };
-enum { DMC_PRO_NONE = 0, DMC_PRO_AFFINE_SILU = 1, DMC_PRO_SILU = 2, DMC_PRO_AFFINE = 3 };
+enum { DMC_PRO_NONE = 0, DMC_PRO_AFFINE_SILU = 1, DMC_PRO_SILU = 2, DMC_PRO_AFFINE = 3, DMC_PRO_GN_SILU = 4 };
+/* DMC_PRO_GN_SILU: SiLU(GroupNorm(x)) with the statistics combined in the conv itself from the producing convs'
+ * partials (dmc_conv_desc.gn_part layout, [N*H*W/64][C/8][2]): pro_scale = the partials of x1 (C1 channels),
+ * pro_shift = those of x2 (C2) or NULL, pro_gn = the GroupNorm's G, eps, gamma, beta (its other fields unused).
+ * Every block combines its image's groups exactly as dmc_gn_finalize does, so the output is bitwise that of
+ * DMC_PRO_AFFINE_SILU with dmc_gn_finalize's scale / shift -- without the finalize launch (models/unet.py:33-35 at
+ * inference). Only on the halo prologue kernel (dmc_conv_halo_prologue(d) == 1; dmc_conv2d fails otherwise);
+ * needs H*W % 64 == 0, C / G a multiple of 8 and >= 16, (H*W / 64) * (C / G / 8) <= 128 and no dropout. */
 enum { DMC_LOSS_L1 = 0, DMC_LOSS_L2 = 1, DMC_LOSS_HUBER = 2 };
 enum { DMC_PACK_FWD = 0, DMC_PACK_DGRAD = 1, DMC_PACK_UPDGRAD = 2 };
 
@@ -124,6 +131,7 @@ typedef struct dmc_conv_desc {
   float* wg_bias;            /* dmc_conv2d_wgrad only: if set, also the bias gradient wg_bias[co] = scale * sum over
                               * pixels of dy[pix][co] (nn.Conv2d bias), from the same pass over dy */
   const struct dmc_gn_fin* gn_fin;   /* if set (with gn_part): finalise the next GroupNorm's statistics in this launch */
+  const struct dmc_gn_fin* pro_gn;   /* prologue DMC_PRO_GN_SILU: the GroupNorm (G, eps, gamma, beta) it applies */
 } dmc_conv_desc;
 enum { DMC_ACT_NONE = 0, DMC_ACT_GELU = 1, DMC_ACT_GELU_DROP = 2, DMC_ACT_DGELU = 3 };
 /* DGELU: the backward of GELU_DROP / GELU on an input-gradient conv: out = round(acc) * mask * scale * gelu'(u) with

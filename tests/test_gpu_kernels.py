@@ -166,6 +166,31 @@ def test_conv3x3_halo_gn_silu_prologue(case, monkeypatch, dmc_opt):
         assert rel_err(y.float(), y0.float()) < 1e-2
     yr = F.conv2d(F.silu(F.group_norm(x, G, gamma, beta, 1e-5)), w, bias, padding=1)
     assert rel_err(nchw(y.float().cpu()), yr) < 2e-2
+    if halo:
+        # DMC_PRO_GN_SILU: the statistics combined in the conv from (mean, M2) partials per 64-pixel segment x
+        # 8-channel chunk (any partials: here torch's of x) == dmc_gn_finalize of the same partials + the
+        # scale / shift prologue, bitwise
+        def parts(t, C_):
+            v = t.float().reshape(N * H * W // 64, 64, C_ // 8, 8).permute(0, 2, 1, 3).reshape(-1, C_ // 8, 512)
+            mu = v.mean(-1)
+            return torch.stack([mu, ((v - mu[..., None]) ** 2).sum(-1)], -1).contiguous()
+        p1 = parts(x1d, C1)
+        p2 = parts(x2d, C2) if C2 else None
+        scf, shf, _ = K.gn_finalize(p1, C1, p2, C2, N, H * W, G, 1e-5, gamma.to(DEV), beta.to(DEV))
+        d1 = K.make_desc(dt, N, H, W, C1, C2, C1, C2, Kc, H, W, Cout, K.TAPS3)
+        K.set_prologue(d1, L.PRO_AFFINE_SILU, scf, shf, Cin)
+        K.set_epilogue(d1, bias=bias.to(DEV), ldy1=Cout)
+        ya = torch.full((N, H, W, Cout), float("nan"), dtype=dt, device=DEV)
+        K.conv(d1, x1d, x2d, wp, ya)
+        d2 = K.make_desc(dt, N, H, W, C1, C2, C1, C2, Kc, H, W, Cout, K.TAPS3)
+        K.set_prologue_gn(d2, p1, p2, G, 1e-5, gamma.to(DEV), beta.to(DEV))
+        K.set_epilogue(d2, bias=bias.to(DEV), ldy1=Cout)
+        assert K.conv_halo_prologue(d2)
+        yb = torch.full((N, H, W, Cout), float("nan"), dtype=dt, device=DEV)
+        K.conv(d2, x1d, x2d, wp, yb)
+        torch.cuda.synchronize()
+        assert torch.equal(ya, yb), (ya.float() - yb.float()).abs().max().item()
+        assert rel_err(nchw(yb.float().cpu()), yr) < 2e-2
     dmc_opt("DMC_HALO_PRO", 0)
     assert not K.conv_halo_prologue(d)
 

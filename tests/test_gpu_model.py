@@ -108,6 +108,30 @@ def test_cifar_unet_inference_halo_prologue_bitwise(monkeypatch, dmc_opt):
     assert torch.equal(outs[0], outs[1])
 
 
+def test_cifar_unet_shared_timestep_broadcast():
+    """Inference with a length-1 t (UNet.shared_timestep: the time-embedding MLPs on one row, broadcast by the conv
+    epilogues with ld_add = 0) equals the per-image embedding with the same t in every row, within the fp32
+    summation order of the embedding GEMMs; a t of another length raises."""
+    from diffusion_models_collection_amd.models import UNet
+    torch.manual_seed(44)
+    cfg = dict(image_size=(32, 32), in_channels=3, model_channels=128, out_channels=3, num_res_blocks=2,
+               attention_resolutions=(16, 8), dropout=0.1, channel_mult=(1, 2, 2, 2), num_classes=None,
+               use_attention=True)
+    x = torch.randn(128, 3, 32, 32, device=DEV)
+    t1 = torch.tensor([417], device=DEV)
+    for dtype, lim in (("fp32", 1e-5), ("bf16", 2e-2)):
+        # fp32: the embedding GEMMs' summation order only; bf16: that difference flips bf16 roundings downstream
+        torch.manual_seed(44)
+        m = UNet(**cfg, compute_dtype=dtype).to(DEV).eval()
+        with torch.no_grad():
+            full = m(x, t1.expand(128).contiguous())
+            one = m(x, t1)
+        assert rel(one, full) < lim, (dtype, rel(one, full))
+    with pytest.raises(ValueError):
+        with torch.no_grad():
+            m(x, torch.tensor([1, 2], device=DEV))
+
+
 def test_cifar_unet_train_step_grads_match_oracle():
     """One training step's loss and parameter gradients (dropout 0) vs the oracle, fp32, B=2."""
     from diffusion_models_collection_amd.models import UNet
