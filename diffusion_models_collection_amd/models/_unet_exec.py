@@ -65,10 +65,11 @@ _GN_APPLY_FIN = _GN_PARTIALS and os.environ.get("DMC_GN_APPLY_FIN", "0") not in 
 # The GroupNorm backward's parameter column sums deferred to one dmc_colsum_batch per gradient segment (A/B switch
 # DMC_GN_DEFER=0: one finish launch per GroupNorm)
 _GN_DEFER = os.environ.get("DMC_GN_DEFER", "1") not in ("", "0")
-# Inference: the GroupNorm-prologue halo conv combines the GroupNorm statistics itself from the producing convs'
-# partials (dmc_conv_desc prologue DMC_PRO_GN_SILU), so those GroupNorms need no finalize launch (A/B switch
-# DMC_PRO_PART=0: dmc_gn_finalize + the scale / shift prologue)
-_PRO_PART = _GN_PARTIALS and os.environ.get("DMC_PRO_PART", "1") not in ("", "0")
+# Inference: the GroupNorm-prologue halo conv can combine the GroupNorm statistics itself from the producing convs'
+# partials (dmc_conv_desc prologue DMC_PRO_GN_SILU, bitwise the finalize path), so those GroupNorms need no finalize
+# launch. Opt-in (DMC_PRO_PART=1): every block combining its chunk's groups with the 64-lane tree costs more than the
+# launch it saves -- DDIM-50 623/624 vs 666/673 img/s, CFG 370/371 vs 410/410 (profiles/r4_ab_gemm_gn.txt, r4ab16)
+_PRO_PART = _GN_PARTIALS and os.environ.get("DMC_PRO_PART", "0") not in ("", "0")
 
 
 class GnSt:

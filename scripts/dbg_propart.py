@@ -49,8 +49,8 @@ def kernel_case(N, H, C1, C2, Cout, G=8):
 
 
 def main():
-    for case in ((128, 16, 256, 128, 256), (128, 16, 256, 128, 128), (128, 16, 384, 0, 256), (128, 16, 128, 256, 256),
-                 (128, 32, 256, 128, 256), (8, 16, 256, 128, 256)):
+    for case in ((128, 32, 128, 128, 128), (128, 32, 128, 0, 128), (128, 32, 256, 0, 128), (128, 32, 128, 128, 256),
+                 (128, 16, 256, 128, 256), (128, 16, 128, 256, 256), (128, 32, 256, 128, 256)):
         kernel_case(*case)
 
 
