@@ -179,6 +179,12 @@ DMC_DEV void gn_chan(float& n, float& m, float& q, float nb, float mb, float qb)
   q = __fadd_rn(q, __builtin_fmaf(__fmul_rn(__fmul_rn(d, d), n), r, qb));
   n = tot;
 }
+// (count, mean, M2) -> (mean, rstd), spelled out like gn_chan (every combine site must agree bitwise)
+DMC_DEV void gn_mean_rstd(float cn, float m, float q, float eps, float& mean, float& rstd) {
+  mean = m;
+  const float var = fmaxf(__fdiv_rn(q, cn), 0.f);
+  rstd = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(var, eps)));
+}
 // The wave-wide part of gn_group_stats: a fixed xor tree over the 64 lanes' (count, mean, M2), then (mean, rstd).
 DMC_DEV void gn_group_tree(float cn, float m, float q, float eps, float& mean, float& rstd) {
   const int lane = threadIdx.x & 63;
@@ -189,9 +195,7 @@ DMC_DEV void gn_group_tree(float cn, float m, float q, float eps, float& mean, f
     if ((lane & sh) == 0) gn_chan(cn, m, q, nb, mb, qb);
     else { float n2 = nb, m2 = mb, q2 = qb; gn_chan(n2, m2, q2, cn, m, q); cn = n2; m = m2; q = q2; }
   }
-  mean = m;
-  const float var = fmaxf(__fdiv_rn(q, cn), 0.f);
-  rstd = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(var, eps)));
+  gn_mean_rstd(cn, m, q, eps, mean, rstd);
 }
 // gn_group_stats in two halves for a caller that overlaps the loads with other memory traffic (the GroupNorm-prologue
 // halo conv): gn_group_fetch loads the lane's partials (t = lane, lane + 64: np <= 128), gn_group_reduce combines them

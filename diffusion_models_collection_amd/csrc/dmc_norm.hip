@@ -621,7 +621,8 @@ __global__ __launch_bounds__(256) void gn_apply_fin_kernel(Src2 s, int HW, GnPar
     }
     const int g = (ps * 4 + wave) * gpw + lane / LG;
     if (g < gp.G && lane % LG == 0) {
-      const float mean = m_, var = fmaxf(q_ / c_, 0.f), rstd = 1.0f / sqrtf(var + gp.eps);
+      float mean, rstd;
+      gn_mean_rstd(c_, m_, q_, gp.eps, mean, rstd);
       smr[g][0] = mean;
       smr[g][1] = rstd;
       if (blockIdx.y == 0 && gp.mean_rstd) {
