@@ -56,8 +56,9 @@ def log(*a):
 
 
 def conv_roofline(dtype, B=128):
-    """Time the dominant kernel (the ResBlock 3x3 conv 128->128 @32x32, B=128, bias + time-embedding epilogue;
-    its GN+SiLU input is materialised by the GN-apply pass, as in training; the halo kernel the library picks by
+    """Time the dominant kernel (the ResBlock 3x3 conv 128->128 @32x32, B=128, bias + time-embedding epilogue that
+    also emits the next GroupNorm's partials, as conv1 of a ResBlock does in the training step (models/_unet_exec.py
+    _res_fwd, stats=h1); its GN+SiLU input is materialised by the GN-apply pass, as in training; the halo kernel the library picks by
     default: conv3x3_halo2_kernel, two 128-pixel blocks per CU) with HIP events on the stream it is
     launched on. `achieved` / `avg_launch_ms`: the average of 50 launches issued back to back between two events
     (agrees with the rocprofv3 kernel-trace average, profiles/r3_roofline_kernel_stats.csv);
@@ -74,7 +75,9 @@ def conv_roofline(dtype, B=128):
     addv = torch.randn(B, C, device=dev)
     y = torch.empty(B, H, W, C, device=dev, dtype=dtype)
     d = K.make_desc(dtype, B, H, W, C, 0, C, 0, Kc, H, W, C, K.TAPS3)
-    K.set_epilogue(d, bias=bias, addvec=addv, ld_add=C, ldy1=C)
+    gpart = torch.empty(B * H * W // 64 * (C // 8) * 2, dtype=torch.float32, device=dev) \
+        if dtype == torch.bfloat16 else None
+    K.set_epilogue(d, bias=bias, addvec=addv, ld_add=C, ldy1=C, gn_part=gpart)
     for _ in range(5):
         K.conv(d, x, None, wp, y)
     s = torch.cuda.current_stream()
@@ -100,11 +103,12 @@ def conv_roofline(dtype, B=128):
     live = {"achieved": round(achieved, 2), "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
             "avg_launch_ms": round(b2b_ms, 4), "per_launch_events_ms": round(avg_ms, 4)}
     out = {"kernel": f"{kname} bf16 implicit GEMM (ResBlock 3x3 128->128 @32x32, B=128, "
-                     "bias+temb epilogue)" if dtype == torch.bfloat16 else "conv_fwd_kernel<f32,128,128>",
+                     "bias+temb epilogue + GroupNorm partials)" if dtype == torch.bfloat16 else "conv_fwd_kernel<f32,128,128>",
            "bound": "mfma", "achieved": live["achieved"], "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
            "frac": live["frac"], "traffic": pmc_traffic(), "flops_per_launch": flops,
            "avg_launch_ms": live["avg_launch_ms"], "per_launch_events_ms": live["per_launch_events_ms"],
-           "algorithmic_bytes_per_launch": 2 * (2 * B * H * W * C) + 2 * C * 9 * C, "source": "live"}
+           "algorithmic_bytes_per_launch": 2 * (2 * B * H * W * C) + 2 * C * 9 * C + B * H * W // 64 * (C // 8) * 8,
+           "source": "live"}
     rc = rocprof_committed(kname, flops) if dtype == torch.bfloat16 else None
     if rc and rc.get("frac"):
         # the headline is the figure a reader recomputes from profiles/ (the rocprofv3 kernel-trace average of this
