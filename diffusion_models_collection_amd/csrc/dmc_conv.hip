@@ -1710,7 +1710,7 @@ void launch_small(const ConvK& k, int mt, hipStream_t s) {
 
 // Geometry of the halo kernel for this conv, or false if it does not apply.
 // Returns the DMA pieces per wave (6 or 7) the halo needs, 0 if the halo kernels do not apply.
-int halo_plan(const ConvK& k, int* R, int* nimg) {
+int halo_plan(const ConvK& k, int* R, int* nimg, int maxhp = 7) {
   if (k.mode != DMC_MODE_NORMAL || k.stride != 1 || k.ntaps != 9 || k.tkw != 3) return 0;
   if (!((k.tdy0 == -1 && k.tsy == 1) || (k.tdy0 == 1 && k.tsy == -1))) return 0;
   if (!((k.tdx0 == -1 && k.tsx == 1) || (k.tdx0 == 1 && k.tsx == -1))) return 0;
@@ -1720,7 +1720,7 @@ int halo_plan(const ConvK& k, int* R, int* nimg) {
   else if (256 % ohw == 0 && k.N % (256 / ohw) == 0) { *nimg = 256 / ohw; *R = k.OH; }
   else return 0;
   const int npix = *nimg * (*R + 2) * (k.OW + 2);
-  return npix <= 6 * 64 ? 6 : npix <= 7 * 64 ? 7 : 0;
+  return npix <= 6 * 64 ? 6 : npix <= 7 * 64 ? 7 : (maxhp >= 9 && npix <= 9 * 64) ? 9 : 0;
 }
 
 // Geometry of the two-blocks-per-CU halo kernel (128-pixel tiles): halo pieces per wave (6, 7 or 9), 0 if it
@@ -2319,14 +2319,16 @@ DMC_DEV int swz_x(int row) { return ((row >> 1) & 1) | (((row >> 3) & 1) << 1); 
 
 // Transposed MFMA fragment (16 columns of segment `seg` x 8 k rows): the lane's k rows are
 // row0 + 4*half + q, q = (lane>>2)&3; RB = row pitch in bytes.
-template <int RB, bool DY>
-DMC_DEV v4i tr_frag(const char* img, int row0, int seg) {
+template <int RB, bool DY, bool TWO = false>
+DMC_DEV v4i tr_frag(const char* img, int row0, int seg, int row0b = 0) {
+  // TWO: row0b is the first row of the second 4-row half (the x halo of maps 4 pixels wide, whose 8-pixel k groups
+  // span two image rows; row0 + 4 otherwise)
   const int l = threadIdx.x & 63;
   const int q = (l >> 2) & 3, p = l & 3;
   v4i out;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
-    const int row = row0 + 4 * half + q;
+    const int row = (TWO && half ? row0b : row0 + 4 * half) + q;
     const int f = DY ? swz_dy(row) : swz_x(row);
     v4s rr = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS v4s*)(uintptr_t)(img + row * RB + ((seg ^ f) << 5) + p * 8));
     v2i ii = __builtin_bit_cast(v2i, rr);
@@ -2402,7 +2404,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_halo2_kernel(ConvK a, const c
     const int r = rem / OW, col = rem - r * OW;
     return img * segpix + (r + 1) * HW + col + 1;
   };
-  const int hb0 = hrow(8 * fh), hz = hrow(0);
+  const int hb0 = hrow(8 * fh), hb1 = hrow(8 * fh + 4), hz = hrow(0);   // hb1 = hb0 + 4 unless OW == 4
   int dl[9];
 #pragma unroll
   for (int u = 0; u < 9; ++u) {
@@ -2453,11 +2455,11 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_halo2_kernel(ConvK a, const c
       v4i fa[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) fa[i] = tr_frag<128, false>(D, ks * 32 + 8 * fh, i);
-      v4i fb = tr_frag<128, false>(X, hb0 + hj + dl[0], (wq * 9) & 3);
+      v4i fb = tr_frag<128, false, true>(X, hb0 + hj + dl[0], (wq * 9) & 3, hb1 + hj + dl[0]);
 #pragma unroll
       for (int u = 0; u < 9; ++u) {
         v4i fn = fb;
-        if (u + 1 < 9) fn = tr_frag<128, false>(X, hb0 + hj + dl[u + 1], (wq * 9 + u + 1) & 3);
+        if (u + 1 < 9) fn = tr_frag<128, false, true>(X, hb0 + hj + dl[u + 1], (wq * 9 + u + 1) & 3, hb1 + hj + dl[u + 1]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i][u] = mma16<T>(acc[i][u], fa[i], fb);
         if (u + 1 < 9) {
@@ -3567,7 +3569,9 @@ WgHaloPlan wgrad_halo_plan(const dmc_conv_desc* d) {
   ConvK k;
   if (fill_convk(d, nullptr, nullptr, nullptr, nullptr, nullptr, k)) return p;
   if (k.C1 % 64 || k.C2 % 64 || k.Kc != k.C1 + k.C2 || k.x1_bytes == 0 || (k.C2 && k.x2_bytes == 0)) return p;
-  p.hp = halo_plan(k, &p.R, &p.nimg);
+  // DMC_WG_HALO9: also the 4x4 maps (16 whole images per 256-pixel tile, a 576-pixel halo: 9 pieces per wave,
+  // 96 KB of LDS, one block per CU)
+  p.hp = halo_plan(k, &p.R, &p.nimg, dmc::opt(dmc::OPT_WG_HALO9) ? 9 : 7);
   if (!p.hp) return p;
   const int ntiles = k.M / 256;
   const int base = (k.Kc / 64) * dmc::cdiv(k.Cout, 128);
@@ -3584,7 +3588,7 @@ WgHaloPlan wgrad_halo_plan(const dmc_conv_desc* d) {
   p.tps = (ntiles + sp - 1) / sp;
   p.splits = (ntiles + p.tps - 1) / p.tps;
   p.ok = true;
-  if (dmc::opt(dmc::OPT_WG_HALO3)) {
+  if (dmc::opt(dmc::OPT_WG_HALO3) && p.hp != 9) {
     // one block per CU: ~256 blocks of (64 ci, 64 co, tile range)
     const int base3 = (k.Kc / 64) * dmc::cdiv(k.Cout, 64);
     int sp3 = (256 + base3 - 1) / base3;
@@ -3657,8 +3661,10 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
                                                       hp.nimg, hp.tps);
     } else if (hp.hp == 6)
       wgrad3x3_halo2_kernel<6><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
-    else
+    else if (hp.hp == 7)
       wgrad3x3_halo2_kernel<7><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
+    else
+      wgrad3x3_halo2_kernel<9><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
     g.y = dmc::cdiv(d->Cout, 128);   // the reduce's slab pitch: Cout rounded to 128
   } else if (w1x1) {
     g.z = splits;

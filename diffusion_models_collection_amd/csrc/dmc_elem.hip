@@ -43,7 +43,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"DMC_WG_TAPS", 0}, {"DMC_NO_SKGN", 0},
     {"DMC_WG_HALO_TARGET", 256},
     {"DMC_STAMP_PTR", 0},
-    {"DMC_SK_TARGET", 240}, {"DMC_SK_MAX", 8}, {"DMC_NO_SMALL", 0}, {"DMC_NO_NHALO", 0}, {"DMC_SMALL_MASK", 1}, {"DMC_WG_HALO3", 0}, {"DMC_GN_BWD_FUSED", 4}, {"DMC_WG_SLAB_RATIO", 0}, {"DMC_GEMM1X1", 2}, {"DMC_SK_2B", 0}, {"DMC_GN_BWD_FUSED_MAXHW", 1l << 30}, {"DMC_GN_BWD_NT", 1024}, {"DMC_REG_EPI", 3}, {"DMC_SK_STAGES", 0}, {"DMC_GN_BWD_IPB", 1},
+    {"DMC_SK_TARGET", 240}, {"DMC_SK_MAX", 8}, {"DMC_NO_SMALL", 0}, {"DMC_NO_NHALO", 0}, {"DMC_SMALL_MASK", 1}, {"DMC_WG_HALO3", 0}, {"DMC_GN_BWD_FUSED", 4}, {"DMC_WG_SLAB_RATIO", 0}, {"DMC_GEMM1X1", 2}, {"DMC_SK_2B", 0}, {"DMC_GN_BWD_FUSED_MAXHW", 1l << 30}, {"DMC_GN_BWD_NT", 1024}, {"DMC_REG_EPI", 3}, {"DMC_SK_STAGES", 0}, {"DMC_GN_BWD_IPB", 1}, {"DMC_WG_HALO9", 0},
 };
 struct OptTable {
   long v[OPT_COUNT];

@@ -254,7 +254,7 @@ def test_conv_dgrad_wgrad(dt, case):
 
 @pytest.mark.parametrize("variant", ["halo2", "halo2_nosched"])
 @pytest.mark.parametrize("case", ["fwd32_concat", "fwd16_ragged_cout", "dgrad32", "fwd8_multi_image", "fallback_4x4",
-                                  "fwd8_concat_b128", "fwd64_rows"])
+                                  "fwd8_concat_b128", "fwd64_rows", "wgrad4x4_halo9"])
 def test_conv3x3_halo_kernel(case, variant, monkeypatch, dmc_opt):
     """bf16 3x3 stride-1 convs on the LDS-halo kernel (conv3x3_halo2_kernel: 128-pixel tiles of whole rows or
     whole images, two blocks per CU) vs an fp32 reference and vs the per-tap kernel (DMC_NO_HALO) on the same
@@ -282,6 +282,11 @@ def test_conv3x3_halo_kernel(case, variant, monkeypatch, dmc_opt):
         N, H, C1, C2, Cout = 16, 64, 128, 0, 128  # 64-wide rows: 4-row tiles, 396 halo pixels (HP = 7)
     elif case == "fallback_4x4":
         N, H, C1, C2, Cout = 8, 4, 64, 0, 128     # halo of 16 images exceeds the LDS budget: per-tap kernel
+    elif case == "wgrad4x4_halo9":
+        # DMC_WG_HALO9: the weight gradient of 4x4 maps on the halo kernel (16 whole images per 256-pixel tile,
+        # 9 halo pieces per wave); the forward stays on the per-tap kernel
+        N, H, C1, C2, Cout = 32, 4, 128, 128, 256
+        dmc_opt("DMC_WG_HALO9", 1)
     W = H
     Cin = C1 + C2
     x = q(torch.randn(N, Cin, H, W), dt)
