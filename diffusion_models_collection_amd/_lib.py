@@ -15,7 +15,7 @@ LIB_PATH = Path(os.environ.get("DMC_LIB", _PKG / "libdmc.so"))
 
 DMC_F32, DMC_BF16 = 0, 1
 MODE_NORMAL, MODE_UPSAMPLE, MODE_DILATE = 0, 1, 2
-PRO_NONE, PRO_AFFINE_SILU, PRO_SILU, PRO_AFFINE, PRO_GN_SILU = 0, 1, 2, 3, 4
+PRO_NONE, PRO_AFFINE_SILU, PRO_SILU, PRO_AFFINE = 0, 1, 2, 3
 LOSS = {"l1": 0, "l2": 1, "huber": 2}
 PACK_FWD, PACK_DGRAD, PACK_UPDGRAD = 0, 1, 2
 
@@ -24,7 +24,7 @@ _c_int, _c_p, _c_f, _c_u32, _c_long, _c_size = (ctypes.c_int, ctypes.c_void_p, c
 
 
 ACT_NONE, ACT_GELU, ACT_GELU_DROP, ACT_DGELU = 0, 1, 2, 3   # include/dmc.h DMC_ACT_*
-FUSED_GN_STATS, FUSED_GN_BWD, FUSED_GN_FIN = 1, 2, 4   # dmc_conv2d_fused_epilogue bits
+FUSED_GN_STATS = 1   # dmc_conv2d_fused_epilogue bits
 
 
 class ConvDesc(ctypes.Structure):
@@ -39,16 +39,7 @@ class ConvDesc(ctypes.Structure):
         ("bias", _c_p), ("addvec", _c_p), ("ld_add", _c_int), ("resid", _c_p), ("ld_res", _c_int),
         ("silu_pre", _c_p), ("ld_silu", _c_int), ("Csplit", _c_int), ("ldy1", _c_int), ("ldy2", _c_int),
         ("out_f32", _c_int), ("out_nchw", _c_int), ("act", _c_int), ("y_pre", _c_p), ("ld_pre", _c_int),
-        ("gnb", _c_p), ("gn_part", _c_p), ("wg_bias", _c_p), ("gn_fin", _c_p),
-        ("pro_gn", _c_p),
-    ]
-
-
-class GnFin(ctypes.Structure):
-    """include/dmc.h dmc_gn_fin: the next GroupNorm's statistics finalised by the producing conv's last blocks."""
-    _fields_ = [
-        ("counters", _c_p), ("part2", _c_p), ("C2", _c_int), ("G", _c_int), ("eps", _c_f),
-        ("gamma", _c_p), ("beta", _c_p), ("mean_rstd", _c_p), ("scale", _c_p), ("shift", _c_p),
+        ("gn_part", _c_p), ("wg_bias", _c_p),
     ]
 
 
@@ -57,16 +48,6 @@ class ColsumJob(ctypes.Structure):
     _fields_ = [("in_", ctypes.c_void_p), ("R", ctypes.c_int), ("C", ctypes.c_int), ("ld", ctypes.c_long),
                 ("stride", ctypes.c_int), ("out0", ctypes.c_void_p), ("out1", ctypes.c_void_p),
                 ("scale", ctypes.c_float)]
-
-
-class GnBwdEpi(ctypes.Structure):
-    """include/dmc.h dmc_gn_bwd_epi: GroupNorm-backward partial sums from an input-gradient conv's epilogue."""
-    _fields_ = [
-        ("x1", _c_p), ("x2", _c_p), ("C1", _c_int), ("ld1", _c_int), ("ld2", _c_int),
-        ("mean_rstd", _c_p), ("gamma", _c_p), ("beta", _c_p), ("G", _c_int), ("silu", _c_int),
-        ("drop_seed", _c_u32), ("drop_seed_base", _c_p), ("drop_thresh", _c_u32), ("drop_scale", _c_f),
-        ("part", _c_p),
-    ]
 
 
 class PackJob(ctypes.Structure):
@@ -106,9 +87,6 @@ def _load():
                                      _c_p, _c_p]),
         "dmc_gn_apply": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p,
                                   _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_int, _c_p]),
-        "dmc_gn_apply_fin": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p,
-                                      _c_p, _c_int, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p, _c_int, _c_u32, _c_p, _c_u32,
-                                      _c_f, _c_p, _c_int, _c_p]),
         "dmc_gn_silu_bwd": (_c_int, [_c_int, _c_p, _c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int,
                                      _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_p,
                                      _c_int, _c_int, _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_p, _c_p, _c_p,

@@ -20,23 +20,15 @@ struct ConvK {
   int N, H, W, C1, C2, ld1, ld2, Kc, OH, OW, Cout, ntaps, mode, stride;
   int tkw, tdy0, tdx0, tsy, tsx;   // tap grid: tap t -> (tdy0 + tsy*(t / tkw), tdx0 + tsx*(t % tkw))
   int prologue; const float* psc; const float* psh; int ldp;
-  // DMC_PRO_GN_SILU (prologue = AFFINE_SILU, pro_part = 1): psc / psh are the GroupNorm partials of x1 / x2 and the
-  // scale / shift are combined per block (halo_gn_fetch / halo_gn_finish)
-  int pro_part; int pG; float peps; const float* pgam; const float* pbet;
   uint32_t dseed, dthresh; float dscale; int dld; const uint32_t* dseed_base;
   const float* bias; const float* addvec; int ld_add;
   const char* resid; int ld_res; const float* silu_pre; int ld_silu;
   int Csplit, ldy1, ldy2, out_f32, out_nchw;
   int act; char* ypre; int ldpre;   // DMC_ACT_GELU epilogue (+ optional pre-activation copy)
   float* gst;  // GroupNorm partials from the epilogue: [M/64][Cout/8] x (mean, M2) (nullptr: off)
-  int gb_on;   // GroupNorm-backward partials from the epilogue (dmc_gn_bwd_epi in gb)
-  dmc_gn_bwd_epi gb;
   float* wgb;  // wgrad: per-split bias partials [split][Cpad] = sum over the split's pixels of dy (nullptr: off)
   float* gsk;  // split-K launches: GroupNorm partials written by the split-K epilogue (nullptr: off)
-  unsigned long long* stamp;  // DMC_STAMP measurement builds only: per-wave phase clocks of the halo conv
   int* gsk_done;  // host flag: set when the launch path emitted gsk
-  int fin_on;     // finalise the next GroupNorm from gst in this launch (dmc_gn_fin in fin; needs gst)
-  dmc_gn_fin fin;
   int M;      // N*OH*OW output pixels
   int OHW;    // OH*OW
   float* sk;  // split-K partial slab (nullptr: no split)
@@ -358,47 +350,11 @@ DMC_DEV void conv_store_tile(const ConvK& a, const v4f accv, const int pix, cons
 // every residual load issued up front, and the embedding row is reloaded only when the image changes, so the
 // store phase pays one global round trip instead of one per row (it runs with no other block on the CU to
 // hide it).
-// dL/dz of one element of dropout(SiLU(GroupNorm(x))) from g = dL/d(output) (dmc_norm.hip gn_dz, same ops)
-DMC_DEV float gnb_dz(float x, float gv, float mean, float rstd, float gm, float bt, float& xhat, int silu) {
-  xhat = (x - mean) * rstd;
-  if (!silu) return gv;
-  const float z = fmaf(xhat, gm, bt);
-  const float sg = sigmoid_f(z);
-  return gv * sg * (1.f + z * (1.f - sg));
-}
-
 // Chan's combination of two (mean, M2) partials of equal count n: the count doubles.
 DMC_DEV void chan_eq(float& m, float& q, float mb, float qb, float n) {
   const float d = mb - m;
   q = q + qb + d * d * (0.5f * n);
   m = 0.5f * (m + mb);
-}
-
-// The producing conv finalises the next GroupNorm (dmc_gn_fin, MI355X_MICROARCH.md "Valid forms" row 1): every
-// storing wave drains its write-through (sc1) partial stores, the block barriers, then one lane per image of the tile
-// adds to that image's arrival counter (agent scope, returning). The block whose add completes the count -- every
-// (pixel tile, channel tile) block of the image has stored its partials -- combines the image's partials with sc1
-// loads, one wave per GroupNorm group (gn_finalize_group: bitwise dmc_gn_finalize). No block ever waits for another.
-template <int BM, int BN, int NT>
-DMC_DEV void gn_fin_tail(const ConvK& a, const char* scratch, int m0) {
-  int* flag = (int*)scratch;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int nf = m0 / a.OHW, ni = (m0 + BM - 1) / a.OHW - nf + 1;   // images this tile covers
-  const unsigned expect = (unsigned)((a.OHW >= BM ? a.OHW / BM : 1) * (a.Cout / BN));
-  if ((int)threadIdx.x < ni) {
-    const unsigned old = __hip_atomic_fetch_add(a.fin.counters + nf + threadIdx.x, 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    flag[threadIdx.x] = old == expect - 1;
-  }
-  __syncthreads();
-  const int wave = threadIdx.x >> 6, spi = a.OHW / 64;
-  for (int i = 0; i < ni; ++i) {
-    if (!flag[i]) continue;
-    for (int g = wave; g < a.fin.G; g += NT / 64)
-      gn_finalize_group<true>(a.gst, a.Cout / 8, a.fin.part2, a.fin.C2 / 8, nf + i, g, spi, a.fin.G, a.fin.eps,
-                              a.fin.gamma, a.fin.beta, a.fin.mean_rstd, a.fin.scale, a.fin.shift);
-  }
 }
 
 template <int BM, int BN, int NT>
@@ -415,35 +371,6 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
   float gm[NSEG], gq[NSEG];
 #pragma unroll
   for (int j = 0; j < NSEG; ++j) { gm[j] = 0.f; gq[j] = 0.f; }
-  // GroupNorm backward (a.gb_on): per (segment, channel) sums of dz and dz * xhat, dz recomputed from the GroupNorm
-  // input x (loaded up front, one 16-byte chunk per row) exactly as dmc_gn_silu_bwd does
-  float gs1[NSEG][8], gs2[NSEG][8];
-  v4i xr[IT];
-  float bgm[8], bbt[8];
-  int bG = 1, bcpg = 1;
-  if (a.gb_on) {
-#pragma unroll
-    for (int j = 0; j < NSEG; ++j)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { gs1[j][e] = 0.f; gs2[j][e] = 0.f; }
-    const bool in1 = co < a.gb.C1;
-    const char* xb = in1 ? (const char*)a.gb.x1 : (const char*)a.gb.x2;
-    const int xld = in1 ? a.gb.ld1 : a.gb.ld2, xc = in1 ? co : co - a.gb.C1;
-#pragma unroll
-    for (int k = 0; k < IT; ++k) {
-      const int pix = min(m0 + r0 + k * RS, a.M - 1);
-      xr[k] = *(const v4i*)(xb + ((size_t)pix * xld + xc) * 2);
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      bgm[e] = a.gb.gamma ? a.gb.gamma[co + e] : 1.f;
-      bbt[e] = a.gb.beta ? a.gb.beta[co + e] : 0.f;
-    }
-    bG = a.gb.G;
-    bcpg = a.Cout / bG;
-  }
-  const uint32_t bseed = (a.gb_on && a.gb.drop_thresh)
-                             ? a.gb.drop_seed + (a.gb.drop_seed_base ? *a.gb.drop_seed_base : 0u) : 0u;
   v4f b0 = {0.f, 0.f, 0.f, 0.f}, b1 = {0.f, 0.f, 0.f, 0.f};
   if (a.bias) { b0 = *(const v4f*)(a.bias + co); b1 = *(const v4f*)(a.bias + co + 4); }
   const bool first = co < a.Csplit;
@@ -509,28 +436,6 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
       }
       const v4i out = Chunk<bf16_t>::pack(f);
       *(v4i*)(y + ((size_t)pix * ldy + cy) * 2) = out;
-      if (a.gb_on) {
-        float gv[8], xv[8];
-        Chunk<bf16_t>::unpack(out, gv);
-        Chunk<bf16_t>::unpack(xr[k], xv);
-        const int nimg = pix / a.OHW, grp = co / bcpg;
-        const float mean = a.gb.mean_rstd[((size_t)nimg * bG + grp) * 2];
-        const float rstd = a.gb.mean_rstd[((size_t)nimg * bG + grp) * 2 + 1];
-#pragma unroll
-        for (int j = 0; j < NSEG; ++j) {
-          if (j != k / KPS) continue;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            float g = gv[e];
-            if (a.gb.drop_thresh)
-              g = drop_keep((uint64_t)pix * a.Cout + co + e, bseed, a.gb.drop_thresh) ? g * a.gb.drop_scale : 0.f;
-            float xh;
-            const float dz = gnb_dz(xv[e], g, mean, rstd, bgm[e], bbt[e], xh, a.gb.silu);
-            gs1[j][e] += dz;
-            gs2[j][e] = fmaf(dz, xh, gs2[j][e]);
-          }
-        }
-      }
       if (a.gst) {
         float g[8];
         Chunk<bf16_t>::unpack(out, g);
@@ -555,45 +460,10 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
       }
     }
   }
-  if (a.gb_on) {
-    // lanes with the same chunk (xor CG, 2 CG, ...), then waves through LDS past the epilogue tile, in fixed order
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr int NW = NT / 64;
-#pragma unroll
-    for (int sh = CG; sh < 64; sh <<= 1)
-#pragma unroll
-      for (int j = 0; j < NSEG; ++j)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { gs1[j][e] += __shfl_xor(gs1[j][e], sh); gs2[j][e] += __shfl_xor(gs2[j][e], sh); }
-    float* red = (float*)(lds + BM * EP);            // [NW][NSEG][CG][16]
-    if (lane < CG) {
-#pragma unroll
-      for (int j = 0; j < NSEG; ++j)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          red[((wave * NSEG + j) * CG + lane) * 16 + e] = gs1[j][e];
-          red[((wave * NSEG + j) * CG + lane) * 16 + 8 + e] = gs2[j][e];
-        }
-    }
-    __syncthreads();
-    // the thread of chunk cg (live: co < Cout) finishes (segment, channel) items r0, r0 + RS, ... of that chunk
-    for (int q = r0; q < NSEG * 8; q += RS) {
-      const int j = q / 8, c = cg, e = q % 8;
-      float v1 = 0.f, v2 = 0.f;
-      for (int w = 0; w < NW; ++w) {
-        v1 += red[((w * NSEG + j) * CG + c) * 16 + e];
-        v2 += red[((w * NSEG + j) * CG + c) * 16 + 8 + e];
-      }
-      const size_t o = ((size_t)(m0 / SEG + j) * a.Cout + n0 + c * 8 + e) * 2;
-      a.gb.part[o] = v1;
-      a.gb.part[o + 1] = v2;
-    }
-  }
   if (a.gst) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int NW = NT / 64;
     float cnt = 8.f * KPS;
-    if (a.gb_on) __syncthreads();                    // the scratch below is shared with the sums above
 #pragma unroll
     for (int sh = CG; sh < 64; sh <<= 1) {          // the lanes of this wave with the same chunk
 #pragma unroll
@@ -623,15 +493,9 @@ DMC_DEV void tile_epilogue8(const ConvK& a, const char* lds, int EP, int m0, int
         q += qb + d * d * (na * nb / (na + nb));
       }
       const size_t o = ((size_t)(m0 / SEG + j) * (a.Cout / 8) + (n0 / 8 + c)) * 2;
-      if (a.fin_on) {   // handed off inside this launch: write-through (sc1), read by the last block with sc1 loads
-        __hip_atomic_store(a.gst + o, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.gst + o + 1, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        a.gst[o] = m;
-        a.gst[o + 1] = q;
-      }
+      a.gst[o] = m;
+      a.gst[o + 1] = q;
     }
-    if (a.fin_on) gn_fin_tail<BM, BN, NT>(a, lds + BM * EP, m0);
   }
 }
 
@@ -774,7 +638,7 @@ DMC_DEV bool reg_epi_ok(const ConvK& a) {
   // 32x32 conv with bias + time embedding + residual, kernel trace), 2 = every eligible tile, 3 = every eligible
   // tile but the inference (GroupNorm-prologue) halo kernel, 0 = never
   return a.reg_epi && (a.gst || a.reg_epi >= 2) && a.dtype_bytes == 2 && !a.out_f32 && !a.out_nchw && !a.silu_pre && a.Csplit == a.Cout &&
-         a.act == DMC_ACT_NONE && !a.gb_on && !a.fin_on && (a.Cout & 127) == 0 && (a.ldy1 & 7) == 0 &&
+         a.act == DMC_ACT_NONE && (a.Cout & 127) == 0 && (a.ldy1 & 7) == 0 &&
          (!a.resid || (a.ld_res & 7) == 0) && (a.M & 127) == 0 && (!a.gst || a.OHW % 64 == 0);
 }
 DMC_DEV void reg_epilogue(const ConvK& a, v4f (&acc)[4][4], int m0, int n0, int wm, int wn) {
@@ -1258,46 +1122,6 @@ DMC_DEV void halo_pro_load(const ConvK& a, int n, int c0, v4f* st) {
   st[0] = *(const v4f*)sc; st[1] = *(const v4f*)(sc + 4);
   st[2] = *(const v4f*)sh; st[3] = *(const v4f*)(sh + 4);
 }
-// DMC_PRO_GN_SILU: the same (scale, shift) rows combined in the block from the partials, bitwise dmc_gn_finalize's
-// (gn_group_fetch / gn_group_reduce are gn_group_stats in two halves, gn_fold its fold). The fetch goes out before
-// the chunk's halo DMA and the combine runs while the halo lands: the wave combines every group of its 64-channel
-// chunk (<= 4: C/G >= 16) with the 64-lane tree, then each lane keeps its own 8 channels' group.
-struct HaloGn { GnLane gl[4]; v4f gb[4]; };
-DMC_DEV void halo_gn_fetch(const ConvK& a, int n, int c0, HaloGn& h) {
-  const int lane = threadIdx.x & 63, lrow = lane >> 3, lc = (lane & 7) ^ lrow;
-  const int C = a.C1 + a.C2, cpg = C / a.pG, g0 = c0 / cpg, spi = a.OHW / 64;
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-    if ((g0 + s) * cpg < c0 + 64) h.gl[s] = gn_group_fetch(a.psc, a.C1 / 8, a.psh, a.C2 / 8, n, g0 + s, spi, a.pG);
-  const int c = c0 + lc * 8;
-  const v4f one = {1.f, 1.f, 1.f, 1.f}, zero = {0.f, 0.f, 0.f, 0.f};
-  h.gb[0] = a.pgam ? *(const v4f*)(a.pgam + c) : one;
-  h.gb[1] = a.pgam ? *(const v4f*)(a.pgam + c + 4) : one;
-  h.gb[2] = a.pbet ? *(const v4f*)(a.pbet + c) : zero;
-  h.gb[3] = a.pbet ? *(const v4f*)(a.pbet + c + 4) : zero;
-}
-DMC_DEV void halo_gn_finish(const ConvK& a, int c0, const HaloGn& h, v4f* st) {
-  const int lane = threadIdx.x & 63, lrow = lane >> 3, lc = (lane & 7) ^ lrow;
-  const int C = a.C1 + a.C2, cpg = C / a.pG, g0 = c0 / cpg, np = (a.OHW / 64) * (cpg / 8);
-  const int gl = (c0 + lc * 8) / cpg - g0;   // this lane's group slot
-  float mean = 0.f, rstd = 0.f;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    if ((g0 + s) * cpg < c0 + 64) {
-      float m, r;
-      gn_group_reduce(h.gl[s], np, a.peps, m, r);
-      if (gl == s) { mean = m; rstd = r; }
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float sc, sh;
-    gn_fold(mean, rstd, h.gb[0][e], h.gb[2][e], sc, sh);
-    st[0][e] = sc; st[2][e] = sh;
-    gn_fold(mean, rstd, h.gb[1][e], h.gb[3][e], sc, sh);
-    st[1][e] = sc; st[3][e] = sh;
-  }
-}
 // The rewrite's LDS accesses are inline asm: for plain C++ LDS stores hipcc inserts vmcnt(0) (they may alias
 // the in-flight LDS-DMA), draining the weight ring; a wave only touches the pieces its own, already-landed
 // DMA wrote, and nobody reads them before the next block barrier.
@@ -1342,7 +1166,7 @@ DMC_DEV void halo_affine_silu(char* buf, int wave, const unsigned* h1, const v4f
 // and a WS-slot weight ring: <= 78 KB, two blocks per CU, so one block's prologue / chunk reload / epilogue
 // overlaps the other's tap loop. At a chunk switch the block waits for its own next-chunk halo (the other block
 // keeps the CU busy). Tile geometry: R = 128 / OW rows of one image, or 128 / (OH*OW) whole images.
-template <int HP, int WS, bool PRO = false, bool SCHED = true>
+template <int HP, int WS, bool PRO = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_halo2_kernel(ConvK a, int R, int nimg) {
   using T = bf16_t;
   constexpr int NW = 4, WM = 2, BM = 128, BN = 128;
@@ -1412,28 +1236,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo2_kernel(ConvK a, int R, i
     dma_pieces<4>(a.w, a.w_bytes, wring + (s % WS) * WB + wave * 4 * 1024, ob, koff, 0, 4);
   };
   v4f pst[4];
-#ifdef DMC_STAMP
-  // measurement build only (never in libdmc.so): clocks of the tap loop's phases, summed per wave
-  unsigned long long ph[5] = {0, 0, 0, 0, 0}, tq = __builtin_amdgcn_s_memtime();
-  const unsigned long long t_start = tq;
-#define DMC_PH(i) do { const unsigned long long tn_ = __builtin_amdgcn_s_memtime(); ph[i] += tn_ - tq; tq = tn_; } while (0)
-#else
-#define DMC_PH(i) do { } while (0)
-#endif
   for (int s = 0; s < nst; ++s) {
     const int c = s / 9, t = s - c * 9;
     if (t == 0) {
       // chunk c's halo into the single buffer: every wave is done with chunk c-1's taps
       if (c > 0) __syncthreads();
-      HaloGn hg;
-      if (PRO) {
-        if (a.pro_part) halo_gn_fetch(a, n_first, c * 64, hg);
-        else halo_pro_load(a, n_first, c * 64, pst);
-      }
+      if (PRO) halo_pro_load(a, n_first, c * 64, pst);
       halo_issue<HP>(a, lds, c * 64, wave, 0, HP, h1, h2);
       if (c == 0)
         for (int q = 0; q < WS - 1 && q < nst; ++q) issue_w(q);
-      if (PRO && a.pro_part) halo_gn_finish(a, c * 64, hg, pst);   // while the halo lands
       __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
       if (PRO) halo_affine_silu<HP>(lds, wave, h1, pst);
     } else {
@@ -1441,15 +1252,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo2_kernel(ConvK a, int R, i
       const int after = min(nst - 1, s + WS - 2) - s;
       wait_vm_dyn(4 * (after > 0 ? after : 0));
     }
-    DMC_PH(0);   // chunk halo / weight-slice wait
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
-    DMC_PH(1);   // block barrier
     if (s + WS - 1 < nst) issue_w(s + WS - 1);
-    DMC_PH(2);   // LDS-DMA issue of a later slice
     const char* Bw = wring + (s % WS) * WB;
     const int ty = t / 3, tx = t - ty * 3;
     const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
@@ -1477,7 +1285,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo2_kernel(ConvK a, int R, i
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[ks][i], fb[ks][j]);
-    if (SCHED) {
+    {
       __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);    // k-step 0 reads
 #pragma unroll
       for (int g = 0; g < 8; ++g) {
@@ -1486,23 +1294,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo2_kernel(ConvK a, int R, i
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);   // k-step 1 MFMAs
     }
-#ifdef DMC_STAMP
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-    DMC_PH(3);   // fragment reads + MFMA issue
   }
   __syncthreads();
-  DMC_PH(4);     // the MFMA tail + the epilogue barrier
-#ifdef DMC_STAMP
-  if (a.stamp && (threadIdx.x & 63) == 0) {
-    unsigned long long* o = a.stamp + ((size_t)blockIdx.x * NW + wave) * 8;
-    for (int q = 0; q < 5; ++q) o[q] = ph[q];
-    o[5] = t_start;
-    o[6] = __builtin_amdgcn_s_memtime();
-    o[7] = (unsigned long long)nst;
-  }
-#endif
-#undef DMC_PH
   if (!(PRO && a.reg_epi == 3) && reg_epi_ok(a)) {   // uniform: the epilogue from the accumulators (the trailing
     reg_epilogue(a, acc, m0, n0, wm, wn);              // barrier above is kept: the MFMA tail drains there)
     return;
@@ -2499,206 +2292,13 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_halo2_kernel(ConvK a, const c
   }
 }
 
-// One-block-per-CU twin (round 4). PMC of wgrad3x3_halo2_kernel on the 32x32 128->128 layer: MFMA busy 26 %, waves
-// parked on waitcnt / barrier 32 % of their cycles, 233 MB of HBM-side traffic per launch for 67 MB of operands: the
-// single x-halo buffer is reloaded at every tile with both co-resident blocks stalling together, a 3-slot ring gives
-// each 64-pixel dy stage ~1 us of lead time, and the fp32 slab of 512 blocks x 64 x 576 partials is 75 MB written
-// + 75 MB re-read by the reduce. Here: 8 waves (2 per SIMD; wave = 32 co x 144 n: 2 x 9 accumulator tiles), the
-// SAME 64-co x (9 taps x 64 ci) block tile, one block per CU (256 blocks: half the slab), the next tile's x halo
-// DMA'd into a second buffer a whole tile ahead, and a DS-slot dy ring (DS - 1 stages of lead). Every wait is a
-// counted vmcnt derived from the issue order (no waits for younger DMA); one barrier per 64-pixel stage.
-// LDS: 2 x HPW x 8 KB (halo) + DS x 8 KB (dy) = 160 KB for (HPW, DS) = (6, 8) and (7, 6).
-DMC_DEV void wait_vm_upto16(int n) {
-  switch (n < 0 ? 0 : n) {
-    case 0: __builtin_amdgcn_s_waitcnt(waitcnt_vm(0)); break;
-    case 1: __builtin_amdgcn_s_waitcnt(waitcnt_vm(1)); break;
-    case 2: __builtin_amdgcn_s_waitcnt(waitcnt_vm(2)); break;
-    case 3: __builtin_amdgcn_s_waitcnt(waitcnt_vm(3)); break;
-    case 4: __builtin_amdgcn_s_waitcnt(waitcnt_vm(4)); break;
-    case 5: __builtin_amdgcn_s_waitcnt(waitcnt_vm(5)); break;
-    case 6: __builtin_amdgcn_s_waitcnt(waitcnt_vm(6)); break;
-    case 7: __builtin_amdgcn_s_waitcnt(waitcnt_vm(7)); break;
-    case 8: __builtin_amdgcn_s_waitcnt(waitcnt_vm(8)); break;
-    case 9: __builtin_amdgcn_s_waitcnt(waitcnt_vm(9)); break;
-    case 10: __builtin_amdgcn_s_waitcnt(waitcnt_vm(10)); break;
-    case 11: __builtin_amdgcn_s_waitcnt(waitcnt_vm(11)); break;
-    case 12: __builtin_amdgcn_s_waitcnt(waitcnt_vm(12)); break;
-    case 13: __builtin_amdgcn_s_waitcnt(waitcnt_vm(13)); break;
-    case 14: __builtin_amdgcn_s_waitcnt(waitcnt_vm(14)); break;
-    case 15: __builtin_amdgcn_s_waitcnt(waitcnt_vm(15)); break;
-    default: __builtin_amdgcn_s_waitcnt(waitcnt_vm(16)); break;   // waiting for more than needed stays correct
-  }
-}
-
-template <int HPW, int DS>
-__global__ __launch_bounds__(512, 1) void wgrad3x3_halo3_kernel(ConvK a, const char* dy, int ld_dy, int dy_bytes,
-                                                                float* slab, int R, int nimg, int tiles_per_split) {
-  using T = bf16_t;
-  constexpr int HB = HPW * 8 * 1024;     // one halo buffer: 8 waves x HPW pieces of 8 pixels x 128 B
-  constexpr int DB = 64 * 128;           // dy stage: 64 pixels x 64 co
-  __shared__ __attribute__((aligned(16))) char lds[2 * HB + DS * DB];
-  char* const dring = lds + 2 * HB;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ch = wave >> 2, nq = wave & 3;           // co half (32 co), n quarter (9 of the 36 16-wide n tiles)
-  const int c0 = blockIdx.x * 64, co0 = blockIdx.y * 64;
-  const int ntiles = a.M / 256;
-  const int t_begin = blockIdx.z * tiles_per_split, t_end = min(ntiles, t_begin + tiles_per_split);
-  const int OW = a.OW, HW = OW + 2, segpix = (R + 2) * HW, npix = nimg * segpix;
-  const bool first = c0 < a.C1;
-  const int cs = first ? c0 : c0 - a.C1;
-  const int lds_x = first ? a.ld1 : a.ld2;
-
-  unsigned od;                                        // this wave's dy piece: stage rows wave*8 .. wave*8+7
-  {
-    const int row = wave * 8 + (lane >> 3);
-    const int pc = lane & 7;
-    const int lc = (((pc >> 1) ^ swz_x(row)) << 1) | (pc & 1);
-    const int co = co0 + lc * 8;
-    od = co < a.Cout ? ((unsigned)row * ld_dy + co) * 2u : kOOB;
-  }
-  auto halo_issue = [&](int tile, char* buf) {
-    const int m0 = tile * 256;
-    const int n_first = m0 / a.OHW;
-    const int r0 = (m0 - n_first * a.OHW) / OW;
-    unsigned hx[HPW];
-#pragma unroll
-    for (int p = 0; p < HPW; ++p) {
-      const int h = (wave * HPW + p) * 8 + (lane >> 3);
-      hx[p] = kOOB;
-      if (h < npix) {
-        const int img = h / segpix, rem = h - img * segpix;
-        const int hr = rem / HW, hc = rem - hr * HW;
-        const int iy = r0 + hr - 1, ix = hc - 1;
-        const int lc = ((((lane & 7) >> 1) ^ swz_x(h)) << 1) | (lane & 1);
-        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-          hx[p] = ((unsigned)(((n_first + img) * a.H + iy) * a.W + ix) * lds_x + cs + lc * 8) * 2u;
-      }
-    }
-    dma_pieces<HPW>(first ? (const void*)a.x1 : (const void*)a.x2, first ? a.x1_bytes : a.x2_bytes,
-                    buf + wave * HPW * 1024, hx, 0u, 0, HPW);
-  };
-  auto dy_issue = [&](int st) {
-    const int tile = t_begin + (st >> 2);
-    const unsigned base = (unsigned)(tile * 256 + (st & 3) * 64) * (unsigned)ld_dy * 2u;
-    dma_pieces<1>(dy, dy_bytes, dring + (st % DS) * DB + wave * 1024, &od, base, 0, 1);
-  };
-
-  const int fh = lane >> 4;
-  auto hrow = [&](int pl) {
-    const int img = pl / (R * OW), rem = pl - img * (R * OW);
-    const int r = rem / OW, col = rem - r * OW;
-    return img * segpix + (r + 1) * HW + col + 1;
-  };
-  const int hb0 = hrow(8 * fh), hz = hrow(0);
-  int dl[9];
-#pragma unroll
-  for (int u = 0; u < 9; ++u) {
-    const int nt = nq * 9 + u, t = nt >> 2;
-    const int ty = t / 3, tx = t - ty * 3;
-    dl[u] = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
-  }
-  v4f acc[2][9];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int u = 0; u < 9; ++u) acc[i][u] = v4f{0.f, 0.f, 0.f, 0.f};
-  const bool bias_on = a.wgb != nullptr && blockIdx.x == 0 && nq == 0;
-  const v4i ones = {0x3F803F80, 0x3F803F80, 0x3F803F80, 0x3F803F80};   // bf16 1.0 pairs
-  v4f accb[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
-
-  const int ntl = t_end - t_begin, nst = ntl * 4;
-  const int pro = min(DS - 1, nst);                  // dy stages issued in the prologue
-  // issue bookkeeping (per wave, wave-uniform): I(st) = DMA instructions issued before stage st's wait
-  auto issued_before = [&](int st) {
-    return HPW + pro + HPW * min(ntl - 1, (st + 3) >> 2) + min(st, max(0, nst - DS + 1));
-  };
-  auto pos_dy = [&](int s) {                         // issue position (1-based) of dy(s)
-    if (s < pro) return HPW + s + 1;
-    const int s1 = s - DS + 1;
-    const int h = ((s1 & 3) == 0 && (s1 >> 2) + 1 < ntl) ? HPW : 0;
-    return issued_before(s1) + h + 1;
-  };
-  auto pos_halo = [&](int tl) { return tl == 0 ? HPW : issued_before(4 * (tl - 1)) + HPW; };
-
-  halo_issue(t_begin, lds);
-  for (int q = 0; q < pro; ++q) dy_issue(q);
-  for (int st = 0; st < nst; ++st) {
-    const int tl = st >> 2, k = st & 3;
-    int need = pos_dy(st);
-    if (k == 0) need = max(need, pos_halo(tl));
-    wait_vm_upto16(issued_before(st) - need);
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("" ::: "memory");
-    // every wave is past stage st-1: its dy slot and (k == 0) the halo buffer of tile tl-1 are free
-    if (k == 0 && tl + 1 < ntl) halo_issue(t_begin + tl + 1, lds + ((tl + 1) & 1) * HB);
-    if (st + DS - 1 < nst) dy_issue(st + DS - 1);
-    const char* X = lds + (tl & 1) * HB;
-    const char* D = dring + (st % DS) * DB;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int j = k * 2 + ks;                      // 32-pixel group inside the tile
-      const int hj = __builtin_amdgcn_readfirstlane(hrow(32 * j) - hz);
-      v4i fa[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = tr_frag<128, false>(D, ks * 32 + 8 * fh, ch * 2 + i);
-      v4i fb = tr_frag<128, false>(X, hb0 + hj + dl[0], (nq * 9) & 3);
-#pragma unroll
-      for (int u = 0; u < 9; ++u) {
-        v4i fn = fb;
-        if (u + 1 < 9) fn = tr_frag<128, false>(X, hb0 + hj + dl[u + 1], (nq * 9 + u + 1) & 3);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) acc[i][u] = mma16<T>(acc[i][u], fa[i], fb);
-        if (u + 1 < 9) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the next tile's reads
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // this tile's MFMAs
-        }
-        fb = fn;
-      }
-      if (bias_on) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) accb[i] = mma16<T>(accb[i], fa[i], ones);
-      }
-    }
-  }
-  const int Cpad = (a.Cout + 127) / 128 * 128;       // the slab layout of the other halo wgrad kernels
-  if (bias_on && (lane & 15) == 0) {                 // column 0: rows co = co0 + 16 (2 ch + i) + 4 fh + e
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int co = co0 + (ch * 2 + i) * 16 + fh * 4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (co + e < a.Cout) a.wgb[(size_t)blockIdx.z * Cpad + co + e] = accb[i][e];
-    }
-  }
-  const int KK = 9 * a.Kc;
-  float* out = slab + (size_t)blockIdx.z * Cpad * KK;
-  const int fr = lane & 15;
-#pragma unroll
-  for (int u = 0; u < 9; ++u) {
-    const int nt = nq * 9 + u, t = nt >> 2;
-    const int kk = t * a.Kc + c0 + (nt & 3) * 16 + fr;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int co = co0 + (ch * 2 + i) * 16 + fh * 4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (co + e < Cpad) out[(size_t)(co + e) * KK + kk] = acc[i][u][e];
-    }
-  }
-}
-
 // Weight gradient of a 1x1 stride-1 conv / Linear (bf16; the DiT linears, the UNet's 1x1 convs):
 // dW[co][ci] = sum_p dy[p][co] * x[p][ci]. Block = 128 co x 128 ci over a pixel range (split-K over grid.z); 4
 // waves, 2 (co halves) x 2 (ci halves) of 64 x 64. Both operands stream as SPX-pixel x 128-channel stages DMA'd
 // straight into LDS (buffer_load ... lds; no register staging, no ds_write), 32-byte segments XOR-swizzled on the
 // source column (the dy image of wgrad3x3_halo_kernel), read transposed (ds_read_b64_tr_b16). STAGES-deep ring,
 // one barrier per stage. Requires M % SPX == 0 and whole-stage split ranges (the planner checks).
-template <int SPX, int STAGES, bool TAPS = false>
+template <int SPX, int STAGES>
 __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char* dy, int ld_dy, int dy_bytes,
                                                             float* slab, int KK, int pix_per_split, int nci, int nco,
                                                             int xcd) {
@@ -2723,9 +2323,7 @@ __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char*
   const int p_begin = zb * pix_per_split;
   const int p_end = min(a.M, p_begin + pix_per_split);
   const int nst = (p_end - p_begin) / SPX;
-  // TAPS: the block's 128 kk columns lie in one tap (Kc % 128 == 0): kk = tap * Kc + channel
-  const int tap = TAPS ? ci0 / a.Kc : 0;
-  const int cc0 = TAPS ? ci0 - tap * a.Kc : ci0;
+  const int cc0 = ci0;
   const bool first = cc0 < a.C1;
   const char* xsrc = first ? a.x1 : a.x2;
   const int xbytes = first ? a.x1_bytes : a.x2_bytes;
@@ -2738,27 +2336,14 @@ __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char*
     const int pc = lane & 15;
     const int col = ((((pc >> 1) ^ swz_dy(row)) << 1) | (pc & 1)) * 8;
     od[j] = co0 + col < a.Cout ? ((unsigned)row * ld_dy + co0 + col) * 2u : kOOB;
-    ox[j] = xc0 + col < xcn ? ((unsigned)(TAPS ? 0 : row) * xld + xc0 + col) * 2u : kOOB;
+    ox[j] = xc0 + col < xcn ? ((unsigned)row * xld + xc0 + col) * 2u : kOOB;
   }
   // (kOOB + a stage offset < 2^31 stays past the buffer's num_records: still a zero read)
-  unsigned oxs[PW];   // TAPS: per-stage source offsets of the x rows (the tap's source pixel, or kOOB = zero)
   auto issue = [&](int st) {
     char* base = lds + (st % STAGES) * SB;
     const unsigned p0 = (unsigned)(p_begin + st * SPX);
     dma_pieces<PW>(dy, dy_bytes, base + wave * PW * 1024, od, p0 * (unsigned)ld_dy * 2u, 0, PW);
-    if constexpr (TAPS) {
-#pragma unroll
-      for (int j = 0; j < PW; ++j) {
-        const int pix = (int)p0 + (wave * PW + j) * 4 + (lane >> 4);
-        const int n = pix / a.OHW, rem = pix - n * a.OHW;
-        const int oy = rem / a.OW, oxx = rem - oy * a.OW;
-        const int sp = src_pixel(a, n, oy, oxx, tap);
-        oxs[j] = (sp >= 0 && ox[j] != kOOB) ? (unsigned)sp * (unsigned)xld * 2u + ox[j] : kOOB;
-      }
-      dma_pieces<PW>(xsrc, xbytes, base + OPB + wave * PW * 1024, oxs, 0u, 0, PW);
-    } else {
-      dma_pieces<PW>(xsrc, xbytes, base + OPB + wave * PW * 1024, ox, p0 * (unsigned)xld * 2u, 0, PW);
-    }
+    dma_pieces<PW>(xsrc, xbytes, base + OPB + wave * PW * 1024, ox, p0 * (unsigned)xld * 2u, 0, PW);
   };
 
   v4f acc[4][4];
@@ -3061,19 +2646,6 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
     DMC_REQUIRE(ok, "conv: taps must form a regular grid");
   }
   k.prologue = d->prologue; k.psc = d->pro_scale; k.psh = d->pro_shift; k.ldp = d->ld_pro;
-  k.pro_part = 0; k.pG = 0; k.peps = 0.f; k.pgam = nullptr; k.pbet = nullptr;
-  if (d->prologue == DMC_PRO_GN_SILU) {
-    const int C = d->C1 + d->C2, HW = d->H * d->W;
-    DMC_REQUIRE(d->pro_gn && d->pro_scale && (d->C2 == 0 || d->pro_shift), "conv: DMC_PRO_GN_SILU needs pro_gn and "
-                "the partials of every source");
-    const int G = d->pro_gn->G;
-    DMC_REQUIRE(G > 0 && C % G == 0 && (C / G) % 8 == 0 && C / G >= 16 && d->C1 % 8 == 0 && d->C2 % 8 == 0 && HW % 64 == 0 &&
-                    (HW / 64) * (C / G / 8) <= 128 && d->drop_thresh == 0,
-                "conv: DMC_PRO_GN_SILU: G %d over %d channels, H*W %d", G, C, HW);
-    k.prologue = DMC_PRO_AFFINE_SILU;
-    k.pro_part = 1; k.pG = G; k.peps = d->pro_gn->eps; k.pgam = d->pro_gn->gamma; k.pbet = d->pro_gn->beta;
-    k.ldp = C;   // (no scale / shift rows: keeps halo2_pro_plan's row check satisfied)
-  }
   k.dseed = d->drop_seed; k.dthresh = d->drop_thresh; k.dscale = d->drop_scale; k.dld = d->drop_ld;
   k.dseed_base = d->drop_seed_base;
   k.bias = d->bias; k.addvec = d->addvec; k.ld_add = d->ld_add; k.resid = (const char*)d->resid; k.ld_res = d->ld_res;
@@ -3088,13 +2660,9 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
   DMC_REQUIRE(d->act != DMC_ACT_DGELU || d->y_pre, "conv: DGELU reads the pre-activation y_pre");
   k.act = d->act; k.ypre = (char*)d->y_pre; k.ldpre = d->ld_pre;
   k.gst = nullptr;   // set by dmc_conv2d when the chosen kernel emits the GroupNorm partials
-  k.gb_on = 0;       // likewise for the GroupNorm-backward partials
   k.wgb = nullptr;   // set by dmc_conv2d_wgrad when the bias gradient is requested
   k.gsk = nullptr; k.gsk_done = nullptr;
-  k.fin_on = 0;      // set by dmc_conv2d with gst
   k.reg_epi = (int)dmc::opt(dmc::OPT_REG_EPI);
-  k.fin = d->gn_fin ? *d->gn_fin : dmc_gn_fin{};
-  k.stamp = (unsigned long long*)dmc::opt(dmc::OPT_STAMP_PTR);   // 0 unless a DMC_STAMP probe sets it
   k.M = d->N * d->OH * d->OW; k.OHW = d->OH * d->OW;
   k.sk = nullptr; k.sk_per = 0;
   {
@@ -3191,12 +2759,6 @@ template <bool PRO>
 void launch_halo2(const ConvK& k, int hp, int R, int nimg, hipStream_t s) {
   const dim3 g = dmc::opt(dmc::OPT_NO_XCD) ? dim3(k.M / 128, dmc::cdiv(k.Cout, 128))
                                           : dim3(k.M / 128 * dmc::cdiv(k.Cout, 128));
-  if (dmc::opt(dmc::OPT_HALO_NOSCHED)) {   // A/B: the compiler's own fragment-read schedule
-    if (hp == 6) conv3x3_halo2_kernel<6, 3, PRO, false><<<g, 256, 0, s>>>(k, R, nimg);
-    else if (hp == 7) conv3x3_halo2_kernel<7, 3, PRO, false><<<g, 256, 0, s>>>(k, R, nimg);
-    else conv3x3_halo2_kernel<9, 2, PRO, false><<<g, 256, 0, s>>>(k, R, nimg);
-    return;
-  }
   if (hp == 6) conv3x3_halo2_kernel<6, 3, PRO><<<g, 256, 0, s>>>(k, R, nimg);
   else if (hp == 7) conv3x3_halo2_kernel<7, 3, PRO><<<g, 256, 0, s>>>(k, R, nimg);
   else conv3x3_halo2_kernel<9, 2, PRO><<<g, 256, 0, s>>>(k, R, nimg);
@@ -3206,14 +2768,8 @@ template <bool BUF>
 void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
   if (p.splits > 1) {
     const dim3 gs(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128), p.splits);
-    if (dmc::opt(dmc::OPT_SK_2B))   // A/B: the 2-stage ring, two split blocks per CU
-      conv_fwd_glds_kernel<2, 2, BUF, 2><<<gs, 256, 0, s>>>(k);
-    else if (dmc::opt(dmc::OPT_SK_STAGES) == 5)   // A/B: 4 stages in flight (160 KB ring): a split's stages at once
-      conv_fwd_glds_kernel<2, 2, BUF, 5><<<gs, 256, 0, s>>>(k);
-    else if (dmc::opt(dmc::OPT_SK_STAGES) == 4)
-      conv_fwd_glds_kernel<2, 2, BUF, 4><<<gs, 256, 0, s>>>(k);
-    else
-      conv_fwd_glds_kernel<2, 2, BUF><<<dim3(dmc::cdiv(k.M, 128), dmc::cdiv(k.Cout, 128), p.splits), 256, 0, s>>>(k);
+    // (a 2-stage ring with two split blocks per CU and deeper 4 / 5-stage rings measured neutral or slower, round 4)
+    conv_fwd_glds_kernel<2, 2, BUF><<<gs, 256, 0, s>>>(k);
     const int Cpad = dmc::cdiv(k.Cout, 128) * 128;
     if (k.gsk && k.M % 64 == 0 && k.Cout % 8 == 0 && !k.out_f32 && !k.out_nchw && k.Csplit == k.Cout) {
       launch_splitk_epi_gn(k, p.splits, Cpad, s);
@@ -3228,12 +2784,12 @@ void launch_glds(ConvK k, const FwdPlan& p, hipStream_t s) {
     const int bm = p.cfg == 0 ? 256 : p.cfg == 1 ? 128 : 64;
     const int nb = dmc::cdiv(k.Cout, 128);
     const dim3 g = dmc::opt(dmc::OPT_NO_XCD) ? dim3(dmc::cdiv(k.M, bm), nb) : dim3(dmc::cdiv(k.M, bm) * nb);
-    if (p.cfg == 0 && (dmc::opt(dmc::OPT_GLDS_2B) & 1)) {
-      // A/B: 128x128 tiles, 2-stage ring, two blocks per CU
+    if (p.cfg == 0) {
+      // 128x128 tiles, 2-stage ring, two blocks per CU (the 8-wave 256x128 tile with a 3-stage ring, one block per
+      // CU, measured slower: round 2)
       const dim3 g2 = dmc::opt(dmc::OPT_NO_XCD) ? dim3(dmc::cdiv(k.M, 128), nb) : dim3(dmc::cdiv(k.M, 128) * nb);
       conv_fwd_glds_kernel<2, 2, BUF, 2><<<g2, 256, 0, s>>>(k);
-    } else if (p.cfg == 0) conv_fwd_glds_kernel<4, 2, BUF><<<g, 512, 0, s>>>(k);
-    else if (p.cfg == 1 && (dmc::opt(dmc::OPT_GLDS_2B) & 2) && (long)dmc::cdiv(k.M, 128) * nb > 256)
+    } else if (p.cfg == 1 && (long)dmc::cdiv(k.M, 128) * nb > 256)
       // more 128x128 tiles than CUs: the 2-stage ring fits two blocks per CU (one round instead of two; the
       // 8x8 attention qkv GEMM: 384 tiles)
       conv_fwd_glds_kernel<2, 2, BUF, 2><<<g, 256, 0, s>>>(k);
@@ -3265,48 +2821,6 @@ __global__ __launch_bounds__(256) void gn_part_kernel(const char* y, int ldy, in
   if (lane == 0) { out[w * 2] = m; out[w * 2 + 1] = q; }
 }
 
-// GroupNorm-backward partials of a stored input gradient g for the paths whose epilogue does not emit them: one
-// wave per (64-pixel segment, 8-channel chunk), the sums over the segment's pixels per channel.
-template <typename T>
-__global__ __launch_bounds__(256) void gn_bwd_part_kernel(const char* gy, int ldy, int nseg, int C, int OHW,
-                                                          dmc_gn_bwd_epi gb) {
-  const int lane = threadIdx.x & 63;
-  const int nch = C / 8;
-  const long w = blockIdx.x * 4L + (threadIdx.x >> 6);
-  if (w >= (long)nseg * nch) return;
-  const int seg = (int)(w / nch), ch = (int)(w - (long)seg * nch);
-  const int pix = seg * 64 + lane, c0 = ch * 8;
-  const int n = pix / OHW, cpg = C / gb.G, grp = c0 / cpg;
-  const float mean = gb.mean_rstd[((size_t)n * gb.G + grp) * 2], rstd = gb.mean_rstd[((size_t)n * gb.G + grp) * 2 + 1];
-  const bool in1 = c0 < gb.C1;
-  const char* xb = in1 ? (const char*)gb.x1 : (const char*)gb.x2;
-  const int xld = in1 ? gb.ld1 : gb.ld2, xc = in1 ? c0 : c0 - gb.C1;
-  float gv[8], xv[8];
-  load4<T>(gy, (size_t)pix * ldy + c0, gv, false);
-  load4<T>(gy, (size_t)pix * ldy + c0 + 4, gv + 4, false);
-  load4<T>(xb, (size_t)pix * xld + xc, xv, false);
-  load4<T>(xb, (size_t)pix * xld + xc + 4, xv + 4, false);
-  const uint32_t seed = gb.drop_thresh ? gb.drop_seed + (gb.drop_seed_base ? *gb.drop_seed_base : 0u) : 0u;
-  float s1[8], s2[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    float g = gv[e];
-    if (gb.drop_thresh) g = drop_keep((uint64_t)pix * C + c0 + e, seed, gb.drop_thresh) ? g * gb.drop_scale : 0.f;
-    const float gm = gb.gamma ? gb.gamma[c0 + e] : 1.f, bt = gb.beta ? gb.beta[c0 + e] : 0.f;
-    float xh;
-    const float dz = gnb_dz(xv[e], g, mean, rstd, gm, bt, xh, gb.silu);
-    s1[e] = wave_sum(dz);
-    s2[e] = wave_sum(dz * xh);
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      gb.part[((size_t)seg * C + c0 + e) * 2] = s1[e];
-      gb.part[((size_t)seg * C + c0 + e) * 2 + 1] = s2[e];
-    }
-  }
-}
-
 // Whether dmc_conv2d's chosen kernel emits the GroupNorm partials in its epilogue (tile_epilogue8: bf16, one NHWC
 // output, 128-channel tiles, 64-pixel partial segments). The kernels that can: conv3x3_halo2_kernel (128-pixel
 // tiles, with or without the halo prologue) and the non-split LDS-DMA kernel (128- or 256-pixel tiles). M % 256 is
@@ -3332,19 +2846,6 @@ bool epi_stats_ok(const ConvK& k, const void* ws, size_t ws_bytes) {
   return p.splits == 1 || ws == nullptr || ws_bytes < p.ws || dmc::opt(dmc::OPT_NO_SPLITK);
 }
 
-// ... and the GroupNorm-backward sums: only the 4-wave tiles have the LDS for their cross-wave reduction (the
-// halo2 kernel, the 128x128 / 64x128 LDS-DMA tiles), never with a prologue (input-gradient convs have none).
-bool epi_gnb_ok(const ConvK& k, const void* ws, size_t ws_bytes) {
-  if (k.prologue != DMC_PRO_NONE || !epi_stats_ok(k, ws, ws_bytes)) return false;
-  const bool buf = k.C1 % 64 == 0 && k.C2 % 64 == 0 && k.Kc == k.C1 + k.C2 && k.x1_bytes > 0 &&
-                   (k.C2 == 0 || k.x2_bytes > 0) && k.w_bytes > 0 && !dmc::opt(dmc::OPT_NO_BUFLDS);
-  const FwdPlan p = plan_glds(k);
-  const bool split = p.splits > 1 && !(ws == nullptr || ws_bytes < p.ws || dmc::opt(dmc::OPT_NO_SPLITK));
-  if (split) return false;
-  int R, nimg;
-  if (buf && !dmc::opt(dmc::OPT_NO_HALO) && halo2_plan(k, &R, &nimg)) return true;
-  return p.splits > 1 || p.cfg != 0 || (dmc::opt(dmc::OPT_GLDS_2B) & 1);
-}
 
 // The persistent 1x1 GEMM applies (bf16 1x1 stride-1, 64-aligned channel sources, plain bias epilogue, whole
 // 128x128 tiles, enough tiles to give every CU one block): returns the tiles per block, or 0.
@@ -3354,12 +2855,12 @@ int gemm1x1_plan(const ConvK& k) {
     return 0;
   if (k.C1 % 64 || k.C2 % 64 || k.Kc != k.C1 + k.C2 || k.x1_bytes == 0 || (k.C2 && k.x2_bytes == 0) || k.w_bytes == 0)
     return 0;
-  if (k.addvec || k.resid || k.silu_pre || k.gst || k.gsk || k.gb_on || k.fin_on || k.act != DMC_ACT_NONE || k.sk ||
+  if (k.addvec || k.resid || k.silu_pre || k.gst || k.gsk || k.act != DMC_ACT_NONE || k.sk ||
       k.Csplit != k.Cout || k.out_f32 || k.out_nchw || (k.ldy1 & 3) || k.M % 128 || k.Cout % 128 || k.Cout > 1024)
     return 0;
   const long ntiles = (long)(k.M / 128) * (k.Cout / 128);
   if (ntiles < 128) return 0;
-  const long blocks = dmc::opt(dmc::OPT_GEMM1X1) == 2 ? 512 : 256;   // 2: the 2-slot ring, two blocks per CU
+  const long blocks = 512;   // the 2-slot ring, two blocks per CU (the 4-slot one-block form: +1 % only, round 4)
   return (int)((ntiles + blocks - 1) / blocks);
 }
 
@@ -3400,10 +2901,7 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     const int tpb = gemm1x1_plan(k);
     if (tpb) {
       const int NB = k.Cout / 128, ntiles = (k.M / 128) * NB;
-      if (dmc::opt(dmc::OPT_GEMM1X1) == 2)
-        gemm1x1_persist_kernel<2><<<dmc::cdiv(ntiles, tpb), 256, 0, s>>>(k, ntiles, NB, tpb);
-      else
-        gemm1x1_persist_kernel<4><<<dmc::cdiv(ntiles, tpb), 256, 0, s>>>(k, ntiles, NB, tpb);
+      gemm1x1_persist_kernel<2><<<dmc::cdiv(ntiles, tpb), 256, 0, s>>>(k, ntiles, NB, tpb);
       return dmc::check_launch("dmc_conv2d");
     }
   }
@@ -3412,7 +2910,6 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
     const int hp2 = halo2_pro_plan(k, &R, &nimg);
     if (hp2) { launch_halo2<true>(k, hp2, R, nimg, s); return dmc::check_launch("dmc_conv2d"); }
   }
-  DMC_REQUIRE(!k.pro_part, "conv: DMC_PRO_GN_SILU runs only on the halo prologue kernel (dmc_conv_halo_prologue)");
   if (sizeof(T) == 2 && k.prologue == DMC_PRO_NONE && !dmc::opt(dmc::OPT_NO_GLDS)) {
     // bf16, plain operands: LDS-DMA pipelined kernel
     FwdPlan p = plan_glds(k);
@@ -3460,17 +2957,8 @@ int wgrad_splits(const dmc_conv_desc* d, int* pps) {
   const long minpix = dmc::opt(dmc::OPT_WG_MINPIX) > 4 * sp ? dmc::opt(dmc::OPT_WG_MINPIX) : 4 * sp;
   const long max_splits = (M + minpix - 1) / minpix;
   if (splits > max_splits) splits = max_splits;
-  // the fp32 slab (splits x KK x Cout) against the operands (dy + x): on the small maps the split count that fills
-  // the chip writes and re-reads ~10x the operand bytes. DMC_WG_SLAB_RATIO caps the ratio (0 = no cap, the
-  // default): measured, every cap is slower (same box, B=128 train: no cap 9069/9070 img/s, 8: 9011/9028,
-  // 4: 8749/8763, 2: 8164/8157) -- the blocks the cap removes cost more than the slab bytes it saves
-  const long ratio = dmc::opt(dmc::OPT_WG_SLAB_RATIO);
-  if (ratio > 0) {
-    const long eb = d->dtype == DMC_F32 ? 4 : 2;
-    const long opnd = M * (d->Cout + (long)(d->C1 + d->C2) * d->stride * d->stride) * eb;
-    const long per_split = KK * d->Cout * 4;
-    while (splits > 1 && splits * per_split > ratio * opnd) splits = (splits + 1) / 2;
-  }
+  // (a cap on the slab against the operand bytes measured slower at every ratio, round 4: no cap 9069 img/s,
+  // 8x 9011, 4x 8749, 2x 8164 -- the blocks a cap removes cost more than the slab bytes it saves)
   if (splits < 1) splits = 1;
   long per = (M + splits - 1) / splits;
   per = (per + sp - 1) / sp * sp;
@@ -3495,8 +2983,7 @@ extern "C" int dmc_conv2d_fused_epilogue(const dmc_conv_desc* d, size_t ws_bytes
   // the planners only ask whether a workspace of ws_bytes is present
   const void* ws = ws_bytes ? (const void*)d : nullptr;
   int f = 0;
-  if (k.OHW % 64 == 0 && k.Cout % 8 == 0 && epi_stats_ok(k, ws, ws_bytes)) f |= DMC_FUSED_GN_STATS | DMC_FUSED_GN_FIN;
-  if (k.OHW % 64 == 0 && k.Cout % 8 == 0 && epi_gnb_ok(k, ws, ws_bytes)) f |= DMC_FUSED_GN_BWD;
+  if (k.OHW % 64 == 0 && k.Cout % 8 == 0 && epi_stats_ok(k, ws, ws_bytes)) f |= DMC_FUSED_GN_STATS;
   return f;
 }
 
@@ -3506,27 +2993,11 @@ extern "C" int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2
   if (fill_convk(d, x1, x2, w, y1, y2, k)) return 1;
   hipStream_t s = dmc::as_stream(stream);
   if (k.M == 0 || k.Cout == 0) return 0;
-  if (d->gnb) {
-    DMC_REQUIRE(k.OHW % 64 == 0 && k.Cout % 8 == 0 && k.Csplit == k.Cout && !k.out_nchw && !k.out_f32 &&
-                    d->gnb->G > 0 && (k.Cout / d->gnb->G) % 8 == 0 && d->gnb->part,
-                "conv: GroupNorm-backward partials need OH*OW %% 64 == 0, one NHWC output, 8-channel chunks per group");
-    k.gb = *d->gnb;
-    k.gb_on = epi_gnb_ok(k, workspace, ws_bytes) ? 1 : 0;
-  }
   float* const part = d->gn_part;
   if (part) {
     DMC_REQUIRE(k.OHW % 64 == 0 && k.Cout % 8 == 0 && k.Csplit == k.Cout && !k.out_nchw && k.ldy1 % 4 == 0,
                 "conv: GroupNorm partials need OH*OW %% 64 == 0, Cout %% 8 == 0 and one NHWC output");
     k.gst = epi_stats_ok(k, workspace, ws_bytes) ? part : nullptr;
-  }
-  if (d->gn_fin) {
-    const dmc_gn_fin& f = *d->gn_fin;
-    const int C = k.Cout + f.C2;
-    DMC_REQUIRE(k.gst != nullptr, "conv: gn_fin needs gn_part from a kernel that emits it (DMC_FUSED_GN_FIN)");
-    DMC_REQUIRE(f.counters && f.G > 0 && C % f.G == 0 && (C / f.G) % 8 == 0 && f.C2 % 8 == 0 && (f.C2 == 0 || f.part2) &&
-                    f.scale && f.shift,
-                "conv: gn_fin: G %d over %d channels (8-channel chunks inside groups), counters and outputs", f.G, C);
-    k.fin_on = 1;
   }
   // split-K launches: the split-K epilogue emits the partials in its pass (DMC_NO_SKGN=1: a separate pass)
   int gsk_done = 0;
@@ -3534,16 +3005,6 @@ extern "C" int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2
   const int rc = d->dtype == DMC_F32 ? launch_fwd<float>(k, workspace, ws_bytes, s)
                                      : launch_fwd<bf16_t>(k, workspace, ws_bytes, s);
   if (rc) return rc;
-  if (d->gnb && !k.gb_on) {   // the chosen kernel's epilogue does not emit them: one pass over (g, x)
-    const int nseg = k.M / 64, nch = k.Cout / 8;
-    const int blocks = (int)(((long)nseg * nch + 3) / 4);
-    if (d->dtype == DMC_F32)
-      gn_bwd_part_kernel<float><<<blocks, 256, 0, s>>>(k.y1, k.ldy1, nseg, k.Cout, k.OHW, *d->gnb);
-    else
-      gn_bwd_part_kernel<bf16_t><<<blocks, 256, 0, s>>>(k.y1, k.ldy1, nseg, k.Cout, k.OHW, *d->gnb);
-    const int rc2 = dmc::check_launch("dmc_conv2d (GroupNorm-backward partials)");
-    if (rc2) return rc2;
-  }
   if (!part || k.gst || gsk_done) return 0;
   // the chosen kernel's epilogue does not emit them: one pass over the stored output
   const int nseg = k.M / 64, nch = k.Cout / 8;
@@ -3560,44 +3021,25 @@ extern "C" int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2
 struct WgHaloPlan {
   bool ok;
   int R, nimg, splits, tps, hp;
-  bool v3;   // wgrad3x3_halo3_kernel (one 8-wave block per CU): splits for ~256 blocks
 };
 
 WgHaloPlan wgrad_halo_plan(const dmc_conv_desc* d) {
-  WgHaloPlan p{false, 0, 0, 1, 0, 0, false};
+  WgHaloPlan p{false, 0, 0, 1, 0, 0};
   if (d->dtype != DMC_BF16 || dmc::opt(dmc::OPT_NO_HALO)) return p;
   ConvK k;
   if (fill_convk(d, nullptr, nullptr, nullptr, nullptr, nullptr, k)) return p;
   if (k.C1 % 64 || k.C2 % 64 || k.Kc != k.C1 + k.C2 || k.x1_bytes == 0 || (k.C2 && k.x2_bytes == 0)) return p;
-  // DMC_WG_HALO9: also the 4x4 maps (16 whole images per 256-pixel tile, a 576-pixel halo: 9 pieces per wave,
-  // 96 KB of LDS, one block per CU)
-  p.hp = halo_plan(k, &p.R, &p.nimg, dmc::opt(dmc::OPT_WG_HALO9) ? 9 : 7);
+  p.hp = halo_plan(k, &p.R, &p.nimg, 7);
   if (!p.hp) return p;
   const int ntiles = k.M / 256;
   const int base = (k.Kc / 64) * dmc::cdiv(k.Cout, 128);
   const int target = (int)dmc::opt(dmc::OPT_WG_HALO_TARGET);   // blocks of 128 co (the 64-co kernel runs twice as many)
   int sp = (target + base - 1) / base;
   if (sp > ntiles) sp = ntiles;
-  {  // slab cap (see wgrad_splits): splits x 9 Kc x Cout fp32 against dy + x
-    const long ratio = dmc::opt(dmc::OPT_WG_SLAB_RATIO);
-    const long opnd = (long)k.M * (k.Cout + k.C1 + k.C2) * 2;
-    const long per_split = 9L * k.Kc * dmc::cdiv(k.Cout, 128) * 128 * 4;
-    while (ratio > 0 && sp > 1 && sp * per_split > ratio * opnd) sp = (sp + 1) / 2;
-  }
   if (sp < 1) sp = 1;
   p.tps = (ntiles + sp - 1) / sp;
   p.splits = (ntiles + p.tps - 1) / p.tps;
   p.ok = true;
-  if (dmc::opt(dmc::OPT_WG_HALO3) && p.hp != 9) {
-    // one block per CU: ~256 blocks of (64 ci, 64 co, tile range)
-    const int base3 = (k.Kc / 64) * dmc::cdiv(k.Cout, 64);
-    int sp3 = (256 + base3 - 1) / base3;
-    if (sp3 > ntiles) sp3 = ntiles;
-    if (sp3 < 1) sp3 = 1;
-    p.tps = (ntiles + sp3 - 1) / sp3;
-    p.splits = (ntiles + p.tps - 1) / p.tps;
-    p.v3 = true;
-  }
   return p;
 }
 
@@ -3617,7 +3059,6 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   if (fill_convk(d, x1, x2, nullptr, nullptr, nullptr, k)) return 1;
   const int epc = d->dtype == DMC_F32 ? 4 : 8;
   DMC_REQUIRE(ld_dy % epc == 0, "wgrad: ld_dy %d alignment", ld_dy);
-  DMC_REQUIRE(!k.pro_part, "wgrad: no DMC_PRO_GN_SILU prologue");
   hipStream_t s = dmc::as_stream(stream);
   int pps;
   int splits = wgrad_splits(d, &pps);
@@ -3629,14 +3070,10 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   if (halo) splits = hp.splits;
   // 1x1 stride-1 bf16 (Linear-shaped): both operands DMA'd into LDS (wgrad1x1_glds_kernel); splits are whole
   // SPX-pixel stages, never more than wgrad_splits() counted (the workspace query's bound)
-  const long w1 = halo ? 0 : dmc::opt(dmc::OPT_WG_1X1);
   const bool direct = d->ntaps == 1 && k.stride == 1 && k.mode == DMC_MODE_NORMAL && k.tdy0 == 0 && k.tdx0 == 0 &&
                       k.H == k.OH && k.W == k.OW && k.prologue == DMC_PRO_NONE;
-  const int spx = (w1 == 2 && direct) ? 32 : 64;
-  // any tap grid / stride / upsample mode (TAPS): a 128-wide kk block must stay inside one tap
-  const bool wtaps = !direct && w1 != 0 && k.prologue == DMC_PRO_NONE && d->Kc % 128 == 0 &&
-                     dmc::opt(dmc::OPT_WG_TAPS);
-  const bool w1x1 = w1 != 0 && d->dtype == DMC_BF16 && (direct || wtaps) && k.M % spx == 0 && d->Cout % 8 == 0 &&
+  constexpr int spx = 64;
+  const bool w1x1 = !halo && d->dtype == DMC_BF16 && direct && k.M % spx == 0 && d->Cout % 8 == 0 &&
                     ld_dy % 8 == 0 && k.C1 % 8 == 0 && k.C2 % 8 == 0 && (k.C2 == 0 || k.C1 % 128 == 0) &&
                     k.ld1 % 8 == 0 && (k.C2 == 0 || k.ld2 % 8 == 0) && k.x1_bytes > 0 && (k.C2 == 0 || k.x2_bytes > 0) &&
                     dyb < 0x7fff0000u;
@@ -3652,36 +3089,17 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   if (halo) {
     // two blocks per CU: 64-co blocks, the same split count (twice the co tiles, half the block target's share)
     g = dim3(d->Kc / 64, dmc::cdiv(d->Cout, 64), splits);
-    if (hp.v3) {
-      if (hp.hp == 6)
-        wgrad3x3_halo3_kernel<6, 8><<<g, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R,
-                                                      hp.nimg, hp.tps);
-      else
-        wgrad3x3_halo3_kernel<7, 6><<<g, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R,
-                                                      hp.nimg, hp.tps);
-    } else if (hp.hp == 6)
+    if (hp.hp == 6)
       wgrad3x3_halo2_kernel<6><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
-    else if (hp.hp == 7)
-      wgrad3x3_halo2_kernel<7><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
     else
-      wgrad3x3_halo2_kernel<9><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
+      wgrad3x3_halo2_kernel<7><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, hp.R, hp.nimg, hp.tps);
     g.y = dmc::cdiv(d->Cout, 128);   // the reduce's slab pitch: Cout rounded to 128
   } else if (w1x1) {
     g.z = splits;
     const dim3 g1(g.x * g.y * g.z);
-    const int xcd = (dmc::opt(dmc::OPT_NO_XCD) || w1 == 4) ? 0 : 1;   // DMC_WG_1X1=4: variant 1 without the XCD order
-    if (!direct)
-      wgrad1x1_glds_kernel<64, 2, true><<<g1, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK,
-                                                          pps1, (int)g.x, (int)g.y, xcd);
-    else if (w1 == 2)
-      wgrad1x1_glds_kernel<32, 4><<<g1, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1,
-                                                    (int)g.x, (int)g.y, xcd);
-    else if (w1 == 3)
-      wgrad1x1_glds_kernel<64, 3><<<g1, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1,
-                                                    (int)g.x, (int)g.y, xcd);
-    else
-      wgrad1x1_glds_kernel<64, 2><<<g1, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1,
-                                                    (int)g.x, (int)g.y, xcd);
+    const int xcd = dmc::opt(dmc::OPT_NO_XCD) ? 0 : 1;
+    wgrad1x1_glds_kernel<64, 2><<<g1, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1,
+                                                  (int)g.x, (int)g.y, xcd);
   } else if (d->dtype == DMC_F32)
     conv_wgrad_kernel<float><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (float*)workspace, KK, pps);
   else

@@ -34,16 +34,13 @@ struct OptDef {
 };
 // name (= environment variable), default
 constexpr OptDef kOpts[OPT_COUNT] = {
-    {"DMC_NO_NARROW", 0},  {"DMC_NO_GLDS", 0},        {"DMC_NO_SPLITK", 0},          {"DMC_NO_BUFLDS", 0},
-    {"DMC_NO_HALO", 0},    {"DMC_HALO_PRO", 1},
-    {"DMC_GN_STATS_SPLIT", 0}, {"DMC_GN_BWD_SPLIT", 0}, {"DMC_ATTN_STAGED", 0},    {"DMC_ATTN_HG", 0},
-    {"DMC_WG_BLOCKS", 512}, {"DMC_GN_STATS_ONE_MAX", 1l << 20}, {"DMC_GN_BWD_ONE_MAX", 65536},
-    {"DMC_NO_XCD", 0}, {"DMC_NO_EPI_STATS", 0}, {"DMC_HALO_NOSCHED", 0}, {"DMC_GLDS_2B", 3}, {"DMC_WG_MINPIX", 0},
-    {"DMC_WG_1X1", 1}, {"DMC_GN_BWD_SLICES", 2},
-    {"DMC_WG_TAPS", 0}, {"DMC_NO_SKGN", 0},
-    {"DMC_WG_HALO_TARGET", 256},
-    {"DMC_STAMP_PTR", 0},
-    {"DMC_SK_TARGET", 240}, {"DMC_SK_MAX", 8}, {"DMC_NO_SMALL", 0}, {"DMC_NO_NHALO", 0}, {"DMC_SMALL_MASK", 1}, {"DMC_WG_HALO3", 0}, {"DMC_GN_BWD_FUSED", 4}, {"DMC_WG_SLAB_RATIO", 0}, {"DMC_GEMM1X1", 2}, {"DMC_SK_2B", 0}, {"DMC_GN_BWD_FUSED_MAXHW", 1l << 30}, {"DMC_GN_BWD_NT", 1024}, {"DMC_REG_EPI", 3}, {"DMC_SK_STAGES", 0}, {"DMC_GN_BWD_IPB", 1}, {"DMC_WG_HALO9", 0},
+    {"DMC_NO_NARROW", 0}, {"DMC_NO_GLDS", 0}, {"DMC_NO_SPLITK", 0}, {"DMC_NO_BUFLDS", 0}, {"DMC_NO_HALO", 0},
+    {"DMC_HALO_PRO", 1}, {"DMC_GN_STATS_SPLIT", 0}, {"DMC_GN_BWD_SPLIT", 0}, {"DMC_ATTN_STAGED", 0},
+    {"DMC_ATTN_HG", 0}, {"DMC_WG_BLOCKS", 512}, {"DMC_GN_STATS_ONE_MAX", 1l << 20}, {"DMC_GN_BWD_ONE_MAX", 65536},
+    {"DMC_NO_XCD", 0}, {"DMC_NO_EPI_STATS", 0}, {"DMC_WG_MINPIX", 0}, {"DMC_GN_BWD_SLICES", 2}, {"DMC_NO_SKGN", 0},
+    {"DMC_WG_HALO_TARGET", 256}, {"DMC_SK_TARGET", 240}, {"DMC_SK_MAX", 8}, {"DMC_NO_SMALL", 0}, {"DMC_NO_NHALO", 0},
+    {"DMC_SMALL_MASK", 1}, {"DMC_GN_BWD_FUSED", 4}, {"DMC_GN_BWD_FUSED_MAXHW", 1l << 30}, {"DMC_GN_BWD_NT", 1024},
+    {"DMC_REG_EPI", 3}, {"DMC_GEMM1X1", 1},
 };
 struct OptTable {
   long v[OPT_COUNT];

@@ -24,11 +24,11 @@ inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 // dmc_reset_options() change it. The planners read plain fields, never the environment.
 namespace dmc {
 enum Opt {
-  OPT_NO_NARROW, OPT_NO_GLDS, OPT_NO_SPLITK, OPT_NO_BUFLDS, OPT_NO_HALO, OPT_HALO_PRO,
-  OPT_GN_STATS_SPLIT, OPT_GN_BWD_SPLIT, OPT_ATTN_STAGED, OPT_ATTN_HG, OPT_WG_BLOCKS, OPT_GN_STATS_ONE_MAX,
-  OPT_GN_BWD_ONE_MAX, OPT_NO_XCD, OPT_NO_EPI_STATS, OPT_HALO_NOSCHED, OPT_GLDS_2B, OPT_WG_MINPIX,
-  OPT_WG_1X1, OPT_GN_BWD_SLICES, OPT_WG_TAPS, OPT_NO_SKGN, OPT_WG_HALO_TARGET, OPT_STAMP_PTR,
-  OPT_SK_TARGET, OPT_SK_MAX, OPT_NO_SMALL, OPT_NO_NHALO, OPT_SMALL_MASK, OPT_WG_HALO3, OPT_GN_BWD_FUSED, OPT_WG_SLAB_RATIO, OPT_GEMM1X1, OPT_SK_2B, OPT_GN_BWD_FUSED_MAXHW, OPT_GN_BWD_NT, OPT_REG_EPI, OPT_SK_STAGES, OPT_GN_BWD_IPB, OPT_WG_HALO9, OPT_COUNT
+  OPT_NO_NARROW, OPT_NO_GLDS, OPT_NO_SPLITK, OPT_NO_BUFLDS, OPT_NO_HALO, OPT_HALO_PRO, OPT_GN_STATS_SPLIT,
+  OPT_GN_BWD_SPLIT, OPT_ATTN_STAGED, OPT_ATTN_HG, OPT_WG_BLOCKS, OPT_GN_STATS_ONE_MAX, OPT_GN_BWD_ONE_MAX,
+  OPT_NO_XCD, OPT_NO_EPI_STATS, OPT_WG_MINPIX, OPT_GN_BWD_SLICES, OPT_NO_SKGN, OPT_WG_HALO_TARGET, OPT_SK_TARGET,
+  OPT_SK_MAX, OPT_NO_SMALL, OPT_NO_NHALO, OPT_SMALL_MASK, OPT_GN_BWD_FUSED, OPT_GN_BWD_FUSED_MAXHW, OPT_GN_BWD_NT,
+  OPT_REG_EPI, OPT_GEMM1X1, OPT_COUNT
 };
 long opt(Opt o);
 }  // namespace dmc

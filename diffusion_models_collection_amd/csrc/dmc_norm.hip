@@ -553,116 +553,6 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(Src2 s, int HW, const flo
   }
 }
 
-// gn_apply_kernel with the GroupNorm statistics finalised in the same launch from the producing convs' epilogue
-// partials (dmc_conv_desc.gn_part): every block combines the partials of its image (one wave per group, exactly
-// gn_finalize_group's order: bitwise the dmc_gn_finalize statistics) while its first pixel rows are in flight, keeps
-// mean / rstd in LDS and folds scale / shift for its channels; the blocks of the first pixel split also store
-// mean_rstd (the GroupNorm backward reads it) and scale / shift. Replaces the finalize launch (~5 us + a dependent
-// kernel boundary per GroupNorm) at the price of a 2-4 KB L2 read per block.
-struct GnPart {
-  const float* p1; const float* p2; int nch1, nch2, G; float eps;
-  const float* gamma; const float* beta; float* mean_rstd; float* scale; float* shift;
-};
-template <typename T>
-__global__ __launch_bounds__(256) void gn_apply_fin_kernel(Src2 s, int HW, GnPart gp, int silu, uint32_t seed0,
-                                                           const uint32_t* seed_base, uint32_t thresh, float dscale,
-                                                           char* out, int ldo, int splits) {
-  __shared__ float smr[64][2];
-  const uint32_t seed = drop_seed(seed0, seed_base);
-  constexpr int EPC = TT<T>::KPL;
-  const int C = s.C1 + s.C2, CPR = C / EPC;
-  const int rpi = 256 / CPR;
-  const int col = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
-  const bool active = r0 < rpi;
-  const int n = blockIdx.x;
-  const int per = (HW + splits - 1) / splits;
-  const int pb = blockIdx.y * per, pe = min(HW, pb + per);
-  const int c0 = col * EPC;
-  v4i buf[UNR];
-  auto issue = [&](int p0) {
-#pragma unroll
-    for (int u = 0; u < UNR; ++u)
-      if (p0 + u * rpi < pe) buf[u] = load_chunk2<T>(s, n * HW + p0 + u * rpi, c0);
-  };
-  // The partials are loaded FIRST (their values return ahead of the pixel rows: the combine never waits behind the
-  // rows), every group at once: LG = the group's partial count rounded up to a power of two lanes, 64 / LG groups per
-  // wave. The butterfly over LG lanes is gn_group_stats' 64-lane tree with its identity rounds (empty lanes) left
-  // out, so the statistics stay bitwise those of dmc_gn_finalize.
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int spi = HW / 64, Cp = 8 * (gp.nch1 + gp.nch2), kpg = Cp / gp.G / 8, np = spi * kpg;
-  int LG = 1;
-  while (LG < np && LG < 64) LG <<= 1;
-  const int gpw = 64 / LG;                     // groups per wave per pass
-  const int npass = (gp.G + 4 * gpw - 1) / (4 * gpw);
-  v2f pv[2][2];   // [pass][k]: this lane's partials t = lane % LG + 64 k (np <= 128)
-#pragma unroll
-  for (int ps = 0; ps < 2; ++ps)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      pv[ps][k] = v2f{0.f, 0.f};
-      const int g = (ps * 4 + wave) * gpw + lane / LG, t = lane % LG + 64 * k;
-      if (ps < npass && g < gp.G && t < np) {
-        const int sg = n * spi + t / kpg, kc = g * kpg + t % kpg;
-        const float* pp = kc < gp.nch1 ? gp.p1 + ((size_t)sg * gp.nch1 + kc) * 2
-                                       : gp.p2 + ((size_t)sg * gp.nch2 + (kc - gp.nch1)) * 2;
-        pv[ps][k] = *(const v2f*)pp;
-      }
-    }
-  if (active && pb + r0 < pe) issue(pb + r0);   // the first pixel rows, in flight while the statistics combine
-  for (int ps = 0; ps < npass && ps < 2; ++ps) {
-    float c_ = 0.f, m_ = 0.f, q_ = 0.f;
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-      if (lane % LG + 64 * k < np) gn_chan(c_, m_, q_, 512.f, pv[ps][k][0], pv[ps][k][1]);
-    for (int sh = 1; sh < LG; sh <<= 1) {
-      const float nb = __shfl_xor(c_, sh), mb = __shfl_xor(m_, sh), qb = __shfl_xor(q_, sh);
-      if ((lane & sh) == 0) gn_chan(c_, m_, q_, nb, mb, qb);
-      else { float n2 = nb, m2 = mb, q2 = qb; gn_chan(n2, m2, q2, c_, m_, q_); c_ = n2; m_ = m2; q_ = q2; }
-    }
-    const int g = (ps * 4 + wave) * gpw + lane / LG;
-    if (g < gp.G && lane % LG == 0) {
-      float mean, rstd;
-      gn_mean_rstd(c_, m_, q_, gp.eps, mean, rstd);
-      smr[g][0] = mean;
-      smr[g][1] = rstd;
-      if (blockIdx.y == 0 && gp.mean_rstd) {
-        gp.mean_rstd[((size_t)n * gp.G + g) * 2] = mean;
-        gp.mean_rstd[((size_t)n * gp.G + g) * 2 + 1] = rstd;
-      }
-    }
-  }
-  __syncthreads();
-  if (!active) return;
-  const int cpg = C / gp.G;
-  float sc[EPC], sh[EPC];
-#pragma unroll
-  for (int e = 0; e < EPC; ++e) {
-    const int c = c0 + e, g = c / cpg;
-    gn_fold(smr[g][0], smr[g][1], gp.gamma ? gp.gamma[c] : 1.f, gp.beta ? gp.beta[c] : 0.f, sc[e], sh[e]);
-    if (blockIdx.y == 0 && r0 == 0 && gp.scale) {
-      gp.scale[(size_t)n * C + c] = sc[e];
-      gp.shift[(size_t)n * C + c] = sh[e];
-    }
-  }
-  for (int p0 = pb + r0; p0 < pe; p0 += UNR * rpi) {
-    if (p0 != pb + r0) issue(p0);
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      if (p0 + u * rpi >= pe) break;
-      const int pix = n * HW + p0 + u * rpi;
-      float f[EPC];
-      Chunk<T>::unpack(buf[u], f);
-#pragma unroll
-      for (int e = 0; e < EPC; ++e) {
-        float v = fmaf(f[e], sc[e], sh[e]);
-        if (silu) v = silu_f(v);
-        if (thresh) v = drop_keep((uint64_t)pix * C + c0 + e, seed, thresh) ? v * dscale : 0.f;
-        f[e] = v;
-      }
-      *(v4i*)(out + ((size_t)pix * ldo + c0) * sizeof(T)) = Chunk<T>::pack(f);
-    }
-  }
-}
 
 // dx = ka*dz + u*(x - mean) + w per element with the per-(n, c) coefficients of gn_bwd_final (vector loads).
 // Grid (N, pixel splits) like gn_apply_kernel: a thread owns one 16-byte channel chunk column of one
@@ -822,10 +712,8 @@ __global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* cf, ch
 // the registers with gn_bwd_apply's formula -- one HBM pass over x and g instead of two and one launch instead of
 // two. The per-(n, c) pixel sums of the stored dx (bias / time-embedding gradients) are reduced in-block and
 // written directly; dgamma / dbeta and the per-c sums are column sums over n (gn_bwd_finish_kernel).
-// IPB = 2 (DMC_GN_BWD_IPB): a block runs two samples, the second one's x / g rows DMA'd into registers with the
-// first's, so they land while the first sample's reductions and dx stores run (with one sample per block the whole
-// grid loads, then reduces, then stores in lockstep); the per-sample arithmetic is unchanged (bitwise).
-template <int NR, int NT, int IPB = 1>
+// (two samples per block, the second one's rows loaded with the first's, measured slower: round 4, -3 %)
+template <int NR, int NT>
 __global__ __launch_bounds__(NT) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]*/, char* dx1, char* dx2, int ld1,
                                                      int ld2, int acc1, int acc2, float* sums /*[N][C]*/,
                                                      float* out_nc, int ld_nc) {
@@ -980,18 +868,10 @@ __global__ __launch_bounds__(NT) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]
       if (out_nc) out_nc[(size_t)n * ld_nc + cb + cl] = v;
     }
   };
-  const int nb = (int)blockIdx.x * IPB;
+  const int nb = (int)blockIdx.x;
   v4i bx0[NR], bg0[NR], bp0[NR];
   load_item(nb, bx0, bg0, bp0);
-  if constexpr (IPB == 1) {
-    run_item(nb, bx0, bg0, bp0);
-  } else {
-    v4i bx1[NR], bg1[NR], bp1[NR];
-    load_item(nb + 1, bx1, bg1, bp1);
-    run_item(nb, bx0, bg0, bp0);
-    __syncthreads();   // the LDS reduction buffers are reused
-    run_item(nb + 1, bx1, bg1, bp1);
-  }
+  run_item(nb, bx0, bg0, bp0);
 }
 
 // dgamma / dbeta (column sums of A over n) and, when asked, the per-c sums of dx (column sums of gn_bwd_fused's
@@ -1182,12 +1062,12 @@ int gn_silu_bwd_impl(int dtype, const void* g, int ld_g, const void* x1, const v
   if (!part && dtype != DMC_F32 && N >= 64 && fused_max > 0 && !dmc::opt(dmc::OPT_GN_BWD_SPLIT) &&
       HW <= dmc::opt(dmc::OPT_GN_BWD_FUSED_MAXHW)) {
     // DMC_GN_BWD_NT: threads per block (1024, or 512: two blocks per CU, twice the channel slices)
-    // (two samples per block, DMC_GN_BWD_IPB = 2, runs 512-thread blocks: with 1024 threads the second sample's rows
-    // do not fit the 128-VGPR budget at 4 chunks per thread)
-    const bool want2 = dmc::opt(dmc::OPT_GN_BWD_IPB) == 2;
-    const int NT = (dmc::opt(dmc::OPT_GN_BWD_NT) == 512 || want2) ? 512 : 1024;
+    const int NT = dmc::opt(dmc::OPT_GN_BWD_NT) == 512 ? 512 : 1024;
     auto rows = [&](int s_) { const int rp = NT / (C / s_ / epc); return rp > 0 ? (HW + rp - 1) / rp : 1 << 30; };
-    auto ok = [&](int s_) { return C % s_ == 0 && (C / s_) % (C / G) == 0 && (C / s_) % epc == 0 && C / s_ <= NT; };
+    // a thread's 8-channel chunk takes ONE group's (mean, rstd): channels per group must be whole chunks
+    auto ok = [&](int s_) {
+      return (C / G) % epc == 0 && C % s_ == 0 && (C / s_) % (C / G) == 0 && (C / s_) % epc == 0 && C / s_ <= NT;
+    };
     int S = 1;
     const int Smax = NT == 512 ? 16 : 8;
     while ((N * S < 256 * 1024 / NT || rows(S) > fused_max) && S < Smax && ok(S * 2)) S *= 2;
@@ -1197,13 +1077,9 @@ int gn_silu_bwd_impl(int dtype, const void* g, int ld_g, const void* x1, const v
       const bool defer = A_keep && (!dx_sum_c || sums_keep);
       if (defer) A = A_keep;
       float* ssum = want_sums ? (defer && sums_keep ? sums_keep : sums) : nullptr;
-      // DMC_GN_BWD_IPB = 2: two samples per block (needs N even and at least 256 blocks left)
-      const bool ipb2 = want2 && N % 2 == 0 && (N / 2) * S >= 256;
-      const dim3 gf(ipb2 ? N / 2 : N, S);
+      const dim3 gf(N, S);
 #define DMC_GNBF(NR_) do { \
-        if (ipb2) gn_bwd_fused<NR_, 512, 2><<<gf, 512, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
-                                                             accumulate1, accumulate2, ssum, dx_sum_nc, ld_sum_nc); \
-        else if (NT == 512) gn_bwd_fused<NR_, 512><<<gf, 512, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
+        if (NT == 512) gn_bwd_fused<NR_, 512><<<gf, 512, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
                                                            accumulate1, accumulate2, ssum, dx_sum_nc, ld_sum_nc); \
         else gn_bwd_fused<NR_, 1024><<<gf, 1024, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
                                                      accumulate1, accumulate2, ssum, dx_sum_nc, ld_sum_nc); \
@@ -1329,34 +1205,6 @@ extern "C" int dmc_channel_sum(int dtype, const void* dy, int N, int HW, int C, 
   else chsum_partial<bf16_t><<<g, 256, 0, s>>>((const char*)dy, HW, C, ld, splits, partial);
   chsum_finish(s, N, C, splits, partial, out_nc, ld_out, out_c, scale);
   return dmc::check_launch("dmc_channel_sum");
-}
-
-extern "C" int dmc_gn_apply_fin(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1,
-                                int ld2, const float* part1, const float* part2, int G, float eps, const float* gamma,
-                                const float* beta, float* mean_rstd, float* scale, float* shift, int silu,
-                                uint32_t drop_seed, const uint32_t* drop_seed_base, uint32_t drop_thresh,
-                                float drop_scale, void* out, int ld_out, void* stream) {
-  const int C = C1 + C2;
-  DMC_REQUIRE(dtype == DMC_BF16, "gn_apply_fin: bf16 (the conv-epilogue partials exist in bf16 mode only)");
-  {  // the kernel combines every group in at most two passes of 4 waves x (64 / LG) groups
-    const int np = HW / 64 * ((C1 + C2) / G / 8);
-    int LG = 1;
-    while (LG < np && LG < 64) LG <<= 1;
-    DMC_REQUIRE(G <= 8 * (64 / LG) && np <= 128, "gn_apply_fin: G %d with %d partials per group", G, np);
-  }
-  DMC_REQUIRE(HW % 64 == 0 && C1 % 8 == 0 && C2 % 8 == 0 && G > 0 && G <= 64 && C % G == 0 && (C / G) % 8 == 0 &&
-                  (C2 == 0 || part2) && part1 && ld_out % 8 == 0 && C / 8 <= 256,
-              "gn_apply_fin: HW %d, C1 %d, C2 %d, G %d (64-pixel segments, 8-channel chunks inside groups)", HW, C1, C2,
-              G);
-  const int cpr = C / 8, rpi = 256 / cpr;
-  int splits = (2048 + N - 1) / N;
-  const int maxs = (HW + rpi - 1) / rpi;
-  splits = splits < maxs ? splits : maxs;
-  Src2 src{(const char*)x1, (const char*)x2, C1, C2, ld1, ld2};
-  GnPart gp{part1, part2, C1 / 8, C2 / 8, G, eps, gamma, beta, mean_rstd, scale, shift};
-  gn_apply_fin_kernel<bf16_t><<<dim3(N, splits), 256, 0, dmc::as_stream(stream)>>>(
-      src, HW, gp, silu, drop_seed, drop_seed_base, drop_thresh, drop_scale, (char*)out, ld_out, splits);
-  return dmc::check_launch("dmc_gn_apply_fin");
 }
 
 extern "C" int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1, int ld2,

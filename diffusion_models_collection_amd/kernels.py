@@ -72,25 +72,11 @@ def set_prologue(d, kind=L.PRO_NONE, scale=None, shift=None, ld=0, drop=None, dr
     d.drop_ld = drop_ld if drop is not None else 0
 
 
-def set_prologue_gn(d, part1, part2, G, eps, gamma, beta, ld=0):
-    """Prologue DMC_PRO_GN_SILU: SiLU(GroupNorm) with the statistics combined in the conv from the producing convs'
-    partials (part1 / part2 of the two sources, dmc_conv_desc.gn_part layout); include/dmc.h."""
-    f = L.GnFin()
-    f.G, f.eps, f.gamma, f.beta = G, eps, ptr(gamma), ptr(beta)
-    d.prologue = L.PRO_GN_SILU
-    d._keep_pro = (part1, part2, gamma, beta, f)
-    d.pro_scale, d.pro_shift, d.ld_pro = ptr(part1), ptr(part2), ld
-    d.pro_gn = ctypes.addressof(f)
-    d.drop_seed, d.drop_seed_base, d.drop_thresh, d.drop_scale = 0, None, 0, 1.0
-    d.drop_ld = 0
-
-
 def set_epilogue(d, bias=None, addvec=None, ld_add=0, resid=None, ld_res=0, silu_pre=None, ld_silu=0,
                  ldy1=0, ldy2=0, Csplit=None, out_f32=False, out_nchw=False, act=L.ACT_NONE, y_pre=None, ld_pre=0,
-                 gn_part=None, gnb=None):
-    d._keep_epi = (bias, addvec, resid, silu_pre, y_pre, gn_part, gnb)   # keep what the raw pointers point at alive
+                 gn_part=None):
+    d._keep_epi = (bias, addvec, resid, silu_pre, y_pre, gn_part)   # keep what the raw pointers point at alive
     d.gn_part = ptr(gn_part)
-    d.gnb = None if gnb is None else ctypes.addressof(gnb)
     d.act = act
     d.y_pre = ptr(y_pre)
     d.ld_pre = ld_pre
@@ -273,31 +259,11 @@ def gn_apply(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, scale, shift, silu=True, dr
     return out
 
 
-def gn_apply_fin(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, p1, p2, G, eps, gamma, beta, silu=True, drop=None,
-                 out=None, stats=None):
-    """gn_finalize + gn_apply in one launch (bitwise equal to the pair). stats: (scale, shift, mean_rstd) buffers
-    to fill, allocated if None. Returns (out, (scale, shift, mean_rstd))."""
-    C = C1 + C2
-    dev = x1.device
-    if stats is None:
-        stats = (torch.empty(N * C, dtype=torch.float32, device=dev),
-                 torch.empty(N * C, dtype=torch.float32, device=dev),
-                 torch.empty(N * G * 2, dtype=torch.float32, device=dev))
-    sc, sh, mr = stats
-    if out is None:
-        out = torch.empty(N * HW * C, dtype=dtype, device=dev)
-    seed, base, thresh, dscale = drop_args(drop)
-    check(LIB.dmc_gn_apply_fin(L.dtype_code(dtype), ptr(x1), ptr(x2), N, HW, C1, C2, ld1, ld2, ptr(p1), ptr(p2), G,
-                               eps, ptr(gamma), ptr(beta), ptr(mr), ptr(sc), ptr(sh), int(silu), seed, base, thresh,
-                               dscale, ptr(out), C, L.stream()), "dmc_gn_apply_fin")
-    return out, stats
-
-
 def gn_bwd(dtype, g, ld_g, x1, x2, N, HW, C1, C2, ld1, ld2, G, mr, gamma, beta, silu, drop, dx1, dx2, ld_dx1,
            ld_dx2, acc1, acc2, dgamma, dbeta, dx_sum_nc=None, ld_sum_nc=0, dx_sum_c=None, part=None, defer=None):
     """GroupNorm(+SiLU+dropout) backward; optionally also the per-(n,c) / per-c pixel sums of dx (the bias and
-    time-embedding gradients of the layer that produced x), fused into the dx pass. part: the (sum dz,
-    sum dz*xhat) partials the input-gradient conv that produced g wrote (gn_bwd_epi), skipping the reduction."""
+    time-embedding gradients of the layer that produced x), fused into the dx pass. part: (sum dz, sum dz*xhat)
+    partials from an earlier pass ([N*HW/64][C][2]), skipping the reduction."""
     ws = SCRATCH.get(LIB.dmc_gn_workspace(N, C1 + C2, G, HW), g.device)
     seed, base, thresh, scale = drop_args(drop)
     if defer is not None:
@@ -333,20 +299,6 @@ def colsum_batch(jobs):
             arr[j].out0, arr[j].out1, arr[j].scale = ptr(o0), ptr(o1), 1.0
         check(LIB.dmc_colsum_batch(arr, len(chunk), L.stream()), "dmc_colsum_batch")
     jobs.clear()
-
-
-def gn_bwd_epi(x1, x2, C1, ld1, ld2, mr, gamma, beta, G, silu, drop, M, C):
-    """The dmc_gn_bwd_epi of an input-gradient conv whose output feeds gn_bwd: returns (struct, partials tensor
-    [M/64][C][2]); pass the struct to set_epilogue(gnb=...) and the tensor to gn_bwd(part=...)."""
-    part = torch.empty(M // 64 * C * 2, dtype=torch.float32, device=x1.device)
-    e = L.GnBwdEpi()
-    seed, base, thresh, scale = drop_args(drop)
-    e.x1, e.x2, e.C1, e.ld1, e.ld2 = ptr(x1), ptr(x2), C1, ld1, ld2
-    e.mean_rstd, e.gamma, e.beta, e.G, e.silu = ptr(mr), ptr(gamma), ptr(beta), G, int(silu)
-    e.drop_seed, e.drop_seed_base, e.drop_thresh, e.drop_scale = seed, base, thresh, scale
-    e.part = ptr(part)
-    e._keep = (x1, x2, mr, gamma, beta, part)
-    return e, part
 
 
 def channel_sum(dtype, dy, N, HW, C, ld, out_nc=None, ld_out=0, out_c=None, scale=1.0):

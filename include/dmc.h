@@ -25,14 +25,7 @@ extern "C" {
 
 enum { DMC_F32 = 0, DMC_BF16 = 1 };
 enum { DMC_MODE_NORMAL = 0, DMC_MODE_UPSAMPLE = 1, DMC_MODE_DILATE = 2 };
-enum { DMC_PRO_NONE = 0, DMC_PRO_AFFINE_SILU = 1, DMC_PRO_SILU = 2, DMC_PRO_AFFINE = 3, DMC_PRO_GN_SILU = 4 };
-/* DMC_PRO_GN_SILU: SiLU(GroupNorm(x)) with the statistics combined in the conv itself from the producing convs'
- * partials (dmc_conv_desc.gn_part layout, [N*H*W/64][C/8][2]): pro_scale = the partials of x1 (C1 channels),
- * pro_shift = those of x2 (C2) or NULL, pro_gn = the GroupNorm's G, eps, gamma, beta (its other fields unused).
- * Every block combines its image's groups exactly as dmc_gn_finalize does, so the output is bitwise that of
- * DMC_PRO_AFFINE_SILU with dmc_gn_finalize's scale / shift -- without the finalize launch (models/unet.py:33-35 at
- * inference). Only on the halo prologue kernel (dmc_conv_halo_prologue(d) == 1; dmc_conv2d fails otherwise);
- * needs H*W % 64 == 0, C / G a multiple of 8 and >= 16, (H*W / 64) * (C / G / 8) <= 128 and no dropout. */
+enum { DMC_PRO_NONE = 0, DMC_PRO_AFFINE_SILU = 1, DMC_PRO_SILU = 2, DMC_PRO_AFFINE = 3 };
 enum { DMC_LOSS_L1 = 0, DMC_LOSS_L2 = 1, DMC_LOSS_HUBER = 2 };
 enum { DMC_PACK_FWD = 0, DMC_PACK_DGRAD = 1, DMC_PACK_UPDGRAD = 2 };
 
@@ -54,44 +47,6 @@ void dmc_reset_options(int from_env);
  * then mode UPSAMPLE: valid in [0,2H) and >>1 (nearest x2); DILATE: valid iff even, /2 (the
  * transposed stride-2 conv of a dgrad); NORMAL: valid in [0,H). Invalid taps read zero.
  */
-/* GroupNorm-backward partials from an input-gradient conv (models/unet.py:35/:51, the backward of
- * dropout(SiLU(GroupNorm(x)))): the conv's output y1 is g = dL/d(GN+SiLU output); per 64-pixel segment and channel
- * the epilogue (or one pass over y1 where the kernel has no such epilogue) writes part[seg][c] = (sum dz,
- * sum dz * xhat), dz = dL/dz recomputed from x exactly as dmc_gn_silu_bwd does; dmc_gn_silu_bwd(..., part, ...)
- * then skips its own reduction pass over (g, x). */
-typedef struct dmc_gn_bwd_epi {
-  const void* x1;            /* GroupNorm input x (virtual concat x1 | x2), same dtype as the conv */
-  const void* x2;
-  int C1, ld1, ld2;
-  const float* mean_rstd;    /* forward statistics [N][G][2] */
-  const float* gamma;
-  const float* beta;
-  int G, silu;
-  uint32_t drop_seed;        /* dropout after the SiLU (the forward's mask, index pix * C + c) */
-  const uint32_t* drop_seed_base;
-  uint32_t drop_thresh;
-  float drop_scale;
-  float* part;               /* out: [M/64][Cout][2] */
-} dmc_gn_bwd_epi;
-
-/* GroupNorm statistics finalised by the conv that produces the GroupNorm's (last) input, in its own launch
- * (dmc_conv_desc.gn_fin): the blocks hand their epilogue partials (gn_part) off through per-image arrival counters and
- * the last block of each image combines them -- with the second source's partials for a virtual-concat GroupNorm
- * -- exactly as dmc_gn_finalize does (bitwise), so the finalize launch disappears. Needs gn_part and a kernel that
- * emits the partials in its epilogue (dmc_conv2d_fused_epilogue & DMC_FUSED_GN_FIN). */
-typedef struct dmc_gn_fin {
-  unsigned* counters;        /* [N] arrival counters, zero before the launch (one fresh set per launch) */
-  const float* part2;        /* partials of the second GroupNorm source [N*OH*OW/64][C2/8][2], or NULL */
-  int C2;                    /* its channels (the GroupNorm covers Cout + C2 channels) */
-  int G;
-  float eps;
-  const float* gamma;        /* [Cout + C2] or NULL */
-  const float* beta;
-  float* mean_rstd;          /* out: [N][G][2], as dmc_gn_finalize */
-  float* scale;              /* out: [N][Cout + C2] */
-  float* shift;
-} dmc_gn_fin;
-
 typedef struct dmc_conv_desc {
   int dtype;
   int N, H, W;               /* source batch and spatial size */
@@ -123,15 +78,12 @@ typedef struct dmc_conv_desc {
   int act;                   /* DMC_ACT_*: activation applied last (after bias / addvec / resid) */
   void* y_pre;               /* with act: the pre-activation value is also stored here ([pix][ld_pre], output dtype) */
   int ld_pre;
-  const struct dmc_gn_bwd_epi* gnb;  /* if set: GroupNorm-backward partial sums of the stored output (see below) */
   float* gn_part;            /* if set: GroupNorm partial statistics of the stored output y1 (the input of the next
                               * GroupNorm, models/unet.py:34/:84), [M/64][Cout/8][2] = (mean, M2) over 64 pixels x 8
                               * channels, from the kernel's epilogue where it can, else one pass over y1. Needs
                               * OH*OW % 64 == 0, Cout % 8 == 0, one NHWC output. Finalised by dmc_gn_finalize. */
   float* wg_bias;            /* dmc_conv2d_wgrad only: if set, also the bias gradient wg_bias[co] = scale * sum over
                               * pixels of dy[pix][co] (nn.Conv2d bias), from the same pass over dy */
-  const struct dmc_gn_fin* gn_fin;   /* if set (with gn_part): finalise the next GroupNorm's statistics in this launch */
-  const struct dmc_gn_fin* pro_gn;   /* prologue DMC_PRO_GN_SILU: the GroupNorm (G, eps, gamma, beta) it applies */
 } dmc_conv_desc;
 enum { DMC_ACT_NONE = 0, DMC_ACT_GELU = 1, DMC_ACT_GELU_DROP = 2, DMC_ACT_DGELU = 3 };
 /* DGELU: the backward of GELU_DROP / GELU on an input-gradient conv: out = round(acc) * mask * scale * gelu'(u) with
@@ -153,11 +105,9 @@ size_t dmc_conv2d_workspace(const dmc_conv_desc* d);
  * epilogue the activation is not read before this conv at all. */
 int dmc_conv_halo_prologue(const dmc_conv_desc* d);
 /* Which of the optional outputs dmc_conv2d(d, ..., ws_bytes) produces inside its kernel's epilogue (bit mask), as
- * opposed to one extra pass over the stored output: DMC_FUSED_GN_STATS (gn_part), DMC_FUSED_GN_BWD (gnb). The
- * executor asks before it records a layer, and asks for the GroupNorm-backward sums only where they come fused
- * (the extra pass costs more than dmc_gn_silu_bwd's own reduction). */
+ * opposed to one extra pass over the stored output: DMC_FUSED_GN_STATS (gn_part). */
 int dmc_conv2d_fused_epilogue(const dmc_conv_desc* d, size_t ws_bytes);
-enum { DMC_FUSED_GN_STATS = 1, DMC_FUSED_GN_BWD = 2, DMC_FUSED_GN_FIN = 4 };
+enum { DMC_FUSED_GN_STATS = 1 };
 int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2, const void* w,
                void* y1, void* y2, void* workspace, size_t ws_bytes, void* stream);
 
@@ -209,21 +159,14 @@ int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C
                  const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* out, int ld_out,
                  void* stream);
 
-/* dmc_gn_finalize + dmc_gn_apply in one launch: every block combines its image's partials (bitwise the
- * dmc_gn_finalize statistics) while its first rows load; mean_rstd / scale / shift (may be NULL) are stored too.
- * bf16 only (the conv-epilogue partials exist in bf16 mode). */
-int dmc_gn_apply_fin(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1, int ld2,
-                     const float* part1, const float* part2, int G, float eps, const float* gamma, const float* beta,
-                     float* mean_rstd, float* scale, float* shift, int silu, uint32_t drop_seed,
-                     const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* out, int ld_out,
-                     void* stream);
-
 /* Backward of a = dropout(SiLU(GroupNorm(x))) (silu=1) or a = GroupNorm(x) (silu=0, AttentionBlock
  * norm :80): g = dL/da (dtype, [pix][ld_g]); writes
  * dx (split into dx1/dx2 by channel like the sources; accumulate_k: add into existing),
  * dgamma/dbeta (fp32 [C], overwritten) and, if dx_sum_nc / dx_sum_c are not NULL (single source
  * only), the pixel sums of the stored dx per (n,c) ([N][ld_sum_nc]) / per c -- the bias and
- * time-embedding gradients of the layer that produced x (models/unet.py:64), fused into the dx pass. */
+ * time-embedding gradients of the layer that produced x (models/unet.py:64), fused into the dx pass.
+ * part (may be NULL): the per-(64-pixel segment, channel) sums (sum dz, sum dz * xhat) [N*HW/64][C][2] from an
+ * earlier pass; the call then skips its own reduction over (g, x). */
 int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x1, const void* x2, int N,
                     int HW, int C1, int C2, int ld1, int ld2, int G, const float* mean_rstd,
                     const float* gamma, const float* beta, int silu, uint32_t drop_seed,

@@ -220,3 +220,30 @@ def test_launch_option_table():
             L.set_option("DMC_NOT_AN_OPTION", 1)
     finally:
         L.reset_options(from_env=False)
+
+
+def test_integration_lists_every_option():
+    """INTEGRATION.md §3 documents the complete launch-option table: every option the library knows (the kOpts table
+    of csrc/dmc_elem.hip) is listed there with its default, and every listed launch option is one the library
+    accepts (dmc_get_option != -1). The executor switches are the DMC_* names the Python package reads."""
+    import re
+    _ensure_lib()
+    from diffusion_models_collection_amd import _lib as L
+    src = (ROOT / "diffusion_models_collection_amd" / "csrc" / "dmc_elem.hip").read_text()
+    table = src[src.index("constexpr OptDef kOpts"):]
+    table = table[:table.index("};")]
+    lib_opts = set(re.findall(r'"(DMC_[A-Z0-9_]+)"', table))
+    doc = (ROOT / "INTEGRATION.md").read_text()
+    launch = doc[doc.index("Launch options (measurement A/B only"):doc.index("Executor and package switches")]
+    exec_ = doc[doc.index("Executor and package switches"):doc.index("Fused epilogue activation")]
+    doc_launch = set(re.findall(r"^\| `(DMC_[A-Z0-9_]+)`", launch, re.M))
+    doc_exec = set(re.findall(r"^\| `(DMC_[A-Z0-9_]+)`", exec_, re.M))
+    assert doc_launch == lib_opts, (sorted(lib_opts - doc_launch), sorted(doc_launch - lib_opts))
+    for name in lib_opts:
+        assert L.get_option(name) != -1, name
+    py_read = set()
+    for f in (ROOT / "diffusion_models_collection_amd").rglob("*.py"):
+        py_read |= set(re.findall(r'environ\.get\("(DMC_[A-Z0-9_]+)"', f.read_text()))
+        py_read |= set(re.findall(r'environ\["(DMC_[A-Z0-9_]+)"\]', f.read_text()))
+    assert py_read <= doc_exec, sorted(py_read - doc_exec)
+    assert len(doc_launch | doc_exec) <= 45

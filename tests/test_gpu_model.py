@@ -318,35 +318,6 @@ def test_bf16_training_step_finite_and_dropout_deterministic():
     assert res[0][0] == res[1][0] and torch.equal(res[0][1], res[1][1])
 
 
-def test_bf16_train_step_with_fused_groupnorm_backward_sums(monkeypatch):
-    """The opt-in DMC_GNB_PARTIALS path (the input-gradient convs' epilogues emit the GroupNorm-backward sums, with
-    dropout 0.1) gives the gradients of the default path up to summation order: every parameter gradient within
-    rel 2e-2 and cosine > 0.9999 (bf16 activations; B=64 so the 32x32 layers take the halo kernel)."""
-    from diffusion_models_collection_amd.models import UNet, _unet_exec as X
-    from diffusion_models_collection_amd.diffusion import DDPM
-    torch.manual_seed(0)
-    m = UNet(compute_dtype="bf16", dropout=0.1).to(DEV).train()
-    ddpm = DDPM(device=DEV)
-    x = torch.rand(64, 3, 32, 32, device=DEV) * 2 - 1
-    t = torch.randint(0, 1000, (64,), device=DEV)
-    n = torch.randn_like(x)
-    grads = []
-    for on in (False, True):
-        monkeypatch.setattr(X, "_GNB_PARTIALS", on)
-        torch.manual_seed(123)
-        m.zero_grad(set_to_none=True)
-        loss = ddpm.p_losses(m, x, t, noise=n)
-        loss.backward()
-        grads.append([p.grad.float().clone() for p in m.parameters()])
-    for (name, _), a, b in zip(m.named_parameters(), *grads):
-        if b.norm() == 0:
-            assert a.norm() == 0, name
-            continue
-        err = (a - b).norm() / b.norm()
-        cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0)
-        assert err < 2e-2 and cos > 0.9999, (name, err.item(), cos.item())
-
-
 def test_flat_adamw_trainer_matches_torch_optimizer_path(tmp_path, monkeypatch):
     """The trainer's fused flat step (clip + AdamW + EMA in one kernel, packs refreshed in one launch) gives
     the same parameters, optimizer state and EMA as the reference path (clip_grad_norm_, AdamW.step,
@@ -734,107 +705,3 @@ def test_ema_sampling_sees_unfused_ema_updates(tmp_path):
     third = ddim.sample(fresh, (2, 3, 16, 16), None, x_T=xT)
     assert not torch.equal(first, second)
     assert torch.equal(second, third)
-
-
-@pytest.mark.parametrize("mode", ["eval", "train"])
-def test_groupnorm_finalize_in_producing_conv_bitwise(mode, monkeypatch, dmc_opt):
-    """The GroupNorm statistics finalised by the conv that produces the GroupNorm's input (dmc_gn_fin: per-image
-    arrival counters, the last block combines the epilogue partials with gn_finalize_group) instead of a
-    dmc_gn_finalize launch: the bf16 CIFAR UNet at B=128 gives BITWISE the same output (eval) / loss and every
-    gradient (train, dropout 0), and the finalize launches are gone (only GroupNorms whose producer cannot emit the
-    partials keep one)."""
-    from diffusion_models_collection_amd.models import UNet, _unet_exec as UE
-    from diffusion_models_collection_amd import kernels as K
-    cfg = dict(image_size=(32, 32), in_channels=3, model_channels=128, out_channels=3, num_res_blocks=2,
-               attention_resolutions=(16, 8), dropout=0.0, channel_mult=(1, 2, 2, 2), num_classes=None,
-               use_attention=True)
-    torch.manual_seed(42)
-    m = UNet(**cfg, compute_dtype="bf16").to(DEV)
-    m.train() if mode == "train" else m.eval()
-    gen = torch.Generator().manual_seed(3)
-    x = torch.randn(128, 3, 32, 32, generator=gen).to(DEV)
-    t = torch.randint(0, 1000, (128,), generator=gen).to(DEV)
-    calls = {"n": 0}
-    orig = K.gn_finalize
-
-    def counted(*a, **kw):
-        calls["n"] += 1
-        return orig(*a, **kw)
-
-    monkeypatch.setattr(K, "gn_finalize", counted)
-    monkeypatch.setattr(UE, "_GN_APPLY_FIN", False)
-    # the producer-side finalize runs with the LDS-staged epilogue's partials (the halo conv's epilogue from the
-    # accumulators, DMC_REG_EPI, folds them in another order): compare both arms on that epilogue
-    dmc_opt("DMC_REG_EPI", 0)
-    res = []
-    for on in (True, False):
-        monkeypatch.setattr(UE, "_GN_FIN", on)
-        calls["n"] = 0
-        m.zero_grad(set_to_none=True)
-        if mode == "train":
-            out = m(x.clone().requires_grad_(True), t)
-            (out.float() ** 2).mean().backward()
-            res.append((out.detach().clone(), {k: p.grad.clone() for k, p in m.named_parameters()}, calls["n"]))
-        else:
-            with torch.no_grad():
-                res.append((m(x, t).clone(), {}, calls["n"]))
-    (o1, g1, n1), (o0, g0, n0) = res
-    print(f"{mode}: gn_finalize launches {n1} (fused) vs {n0}")
-    assert n0 > 20 and n1 <= n0 // 4, (n1, n0)
-    assert torch.equal(o1, o0)
-    for k in g0:
-        assert torch.equal(g1[k], g0[k]), k
-
-
-@pytest.mark.parametrize("mode", ["eval", "train"])
-def test_groupnorm_finalize_in_apply_bitwise(mode, monkeypatch):
-    """The GroupNorm statistics finalised inside the apply launch (dmc_gn_apply_fin, every block combines its
-    image's epilogue partials) instead of a dmc_gn_finalize launch before dmc_gn_apply: the bf16 CIFAR UNet at
-    B=128 gives BITWISE the same output (eval) / loss and every gradient (train, dropout 0). In training every
-    finalize launch whose GroupNorm is materialised disappears; in eval the halo-prologue convs still finalise."""
-    from diffusion_models_collection_amd.models import UNet, _unet_exec as UE
-    from diffusion_models_collection_amd import kernels as K
-    cfg = dict(image_size=(32, 32), in_channels=3, model_channels=128, out_channels=3, num_res_blocks=2,
-               attention_resolutions=(16, 8), dropout=0.0, channel_mult=(1, 2, 2, 2), num_classes=None,
-               use_attention=True)
-    torch.manual_seed(42)
-    m = UNet(**cfg, compute_dtype="bf16").to(DEV)
-    m.train() if mode == "train" else m.eval()
-    gen = torch.Generator().manual_seed(5)
-    x = torch.randn(128, 3, 32, 32, generator=gen).to(DEV)
-    t = torch.randint(0, 1000, (128,), generator=gen).to(DEV)
-    calls = {"fin": 0, "apply_fin": 0}
-    orig_f, orig_a = K.gn_finalize, K.gn_apply_fin
-
-    def cf(*a, **kw):
-        calls["fin"] += 1
-        return orig_f(*a, **kw)
-
-    def ca(*a, **kw):
-        calls["apply_fin"] += 1
-        return orig_a(*a, **kw)
-
-    monkeypatch.setattr(K, "gn_finalize", cf)
-    monkeypatch.setattr(K, "gn_apply_fin", ca)
-    monkeypatch.setattr(UE, "_GN_FIN", False)
-    res = []
-    for on in (True, False):
-        monkeypatch.setattr(UE, "_GN_APPLY_FIN", on)
-        calls.update(fin=0, apply_fin=0)
-        m.zero_grad(set_to_none=True)
-        if mode == "train":
-            out = m(x.clone().requires_grad_(True), t)
-            (out.float() ** 2).mean().backward()
-            res.append((out.detach().clone(), {k: p.grad.clone() for k, p in m.named_parameters()}, dict(calls)))
-        else:
-            with torch.no_grad():
-                res.append((m(x, t).clone(), {}, dict(calls)))
-    (o1, g1, c1), (o0, g0, c0) = res
-    print(f"{mode}: fused {c1} vs separate {c0}")
-    assert c0["apply_fin"] == 0 and c1["apply_fin"] > 0
-    assert c1["fin"] + c1["apply_fin"] == c0["fin"], (c1, c0)
-    if mode == "train":
-        assert c1["fin"] == 0, c1
-    assert torch.equal(o1, o0)
-    for k in g0:
-        assert torch.equal(g1[k], g0[k]), k
