@@ -179,8 +179,20 @@ def cpu_cores():
     return n
 
 
-def cpu_baseline(B=32, warm=1, steps=3):
-    """The CPU oracle (a port of the reference path, fp32) doing the same train step on the host cores."""
+def cpu_model():
+    """The host CPU's model string (/proc/cpuinfo), reported beside the core count."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(B=32, warm=3, steps=5):
+    """The CPU oracle (a port of the reference path, fp32) doing the same train step on the host cores, with
+    BASELINE.md §3's protocol: B=32, 3 warm-up + 5 timed steps."""
     from oracle.unet_oracle import make_oracle
     from oracle import diffusion_oracle as DO
     from diffusion_models_collection_amd.models import UNet
@@ -212,15 +224,15 @@ def cpu_baseline(B=32, warm=1, steps=3):
         step()
     dt = time.perf_counter() - t0
     return {"value": round(B * steps / dt, 3), "unit": "img/s", "cores": threads, "os_cpu_count": os.cpu_count(),
-            "kind": "port",
-            "sample": f"oracle fp32 train step (q_sample, UNet fwd+bwd, clip, AdamW, EMA), B={B}, {steps} timed "
-                      f"steps after {warm} warm-up, torch CPU with {threads} threads (the cores available to the "
-                      f"process: affinity and cgroup quota)"}
+            "cpu_model": cpu_model(), "kind": "port",
+            "sample": f"BASELINE.md §3 protocol: oracle fp32 train step (q_sample, UNet fwd+bwd, clip, AdamW, EMA), "
+                      f"B={B}, {steps} timed steps after {warm} warm-up steps, torch CPU with {threads} threads "
+                      f"(the cores available to the process: affinity and cgroup quota)"}
 
 
-def cpu_ddim_baseline(B=16, steps=5, S=50):
-    """DDIM-50 sampling on the CPU oracle (B=16): `steps` of the 50 DDIM steps timed (a DDIM step is
-    one UNet forward + the update, identical work at every step), img/s extrapolated to the full 50-step loop."""
+def cpu_ddim_baseline(B=16, S=50):
+    """DDIM-50 sampling on the CPU oracle with BASELINE.md §3's protocol: B=16, one warm-up forward, then one
+    whole S-step loop (UNet forward + DDIM update per step, diffusion/ddim.py:210-249) timed."""
     from oracle.unet_oracle import make_oracle
     from oracle import diffusion_oracle as DO
     from diffusion_models_collection_amd.models import UNet
@@ -232,16 +244,14 @@ def cpu_ddim_baseline(B=16, steps=5, S=50):
     ts = DO.ddim_timesteps(1000, S)
     img = torch.randn(B, 3, 32, 32)
     with torch.no_grad():
-        t = torch.full((B,), int(ts[0]))
-        orc.forward(img, t, None)          # warm-up
+        orc.forward(img, torch.full((B,), int(ts[0])), None)          # warm-up forward
         t0 = time.perf_counter()
-        for i in range(steps):
-            t = torch.full((B,), int(ts[i]))
-            tn = torch.full((B,), int(ts[i + 1]))
-            img = DO.ddim_step(ac, img, orc.forward(img, t, None), t, tn)
+        img = DO.ddim_sample(lambda x, t, y: orc.forward(x, t, y), ac, ts, img)
         dt = time.perf_counter() - t0
-    return {"value": round(B / (dt / steps * S), 4), "unit": "img/s", "cores": threads, "kind": "port",
-            "sample": f"oracle fp32 DDIM, B={B}, {steps} of {S} steps timed, img/s for the {S}-step loop"}
+    assert torch.isfinite(img).all()
+    return {"value": round(B / dt, 4), "unit": "img/s", "cores": threads, "cpu_model": cpu_model(), "kind": "port",
+            "sample": f"BASELINE.md §3 protocol: oracle fp32 DDIM-{S}, B={B}, one warm-up forward, then the whole "
+                      f"{S}-step loop timed ({dt:.2f} s)"}
 
 
 def train_rate(trainer, pool, steps, warmup, world):

@@ -649,3 +649,78 @@ def test_cifar_unet_b128_rows_match_oracle(dtype, mode):
         assert e < 1e-4 and le < 1e-4, (e, le)
     else:
         assert e < 5e-2 and c > 0.999 and le < 2e-2, (e, c, le)
+
+
+@pytest.fixture(scope="module")
+def cifar_b128_oracle_grads():
+    """The oracle's fp32 CPU forward + backward (models/unet.py:243-292 restated, autograd) of one p_losses on a
+    B=128 batch (diffusion/ddpm.py:106-140: q_sample, forward, MSE mean over all elements) for the seed-42 CIFAR
+    UNet: (x0, t, noise, loss, {name: grad}). Computed once for the two dtype cases (~5-10 s on the host)."""
+    from diffusion_models_collection_amd.models import UNet
+    from oracle.unet_oracle import make_oracle
+    from oracle import diffusion_oracle as DO
+    torch.manual_seed(42)
+    m = UNet(**CIFAR)
+    gen = torch.Generator().manual_seed(23)
+    x0 = torch.rand(128, 3, 32, 32, generator=gen) * 2 - 1
+    t = torch.randint(0, 1000, (128,), generator=gen)
+    noise = torch.randn(128, 3, 32, 32, generator=gen)
+    orc, sd = make_oracle(m.state_dict(), CIFAR, requires_grad=True)
+    xt = DO.q_sample(DO.schedule(), x0, t, noise)
+    out = orc.forward(xt, t, None, training=True)           # dropout 0: deterministic
+    loss = ((out - noise) ** 2).mean()
+    loss.backward()
+    grads = {k: v.grad.detach().clone() for k, v in sd.items()}
+    return x0, t, noise, loss.item(), grads
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_cifar_unet_b128_grads_match_oracle(dtype, cifar_b128_oracle_grads):
+    """the benchmarked configuration's BACKWARD pinned to the oracle directly at B=128. One p_losses
+    + backward of the configs/cifar10_unet.py network (dropout 0) through the default launch plans of the bench
+    (bf16: the halo weight gradients with their B=128 pixel split and deterministic split reduction, the one-pass
+    GroupNorm backward on its B=128 grid, the deferred column sums, the split-K small-map convs; fp32: the
+    register-staged kernels) against the oracle's fp32 forward + backward of the same batch on the host.
+    Tolerances: fp32 -- loss within 1e-5 relative, every gradient within 5e-4 of its absmax; bf16 (the stated
+    north_star bf16 tolerance) -- loss within 1e-3 relative, per tensor rel < 5e-2 and cosine >
+    0.999 for every gradient with a non-negligible norm (>= 1e-3 of the largest; the rest cosine > 0.99), the
+    global gradient norm within 2e-3."""
+    from diffusion_models_collection_amd.models import UNet
+    from diffusion_models_collection_amd.diffusion import DDPM
+    x0, t, noise, lref, gref = cifar_b128_oracle_grads
+    torch.manual_seed(42)
+    m = UNet(**CIFAR, compute_dtype=dtype).to(DEV).train()
+    ddpm = DDPM(device=DEV)
+    loss = ddpm.p_losses(m, x0.to(DEV), t.to(DEV), noise=noise.to(DEV))
+    loss.backward()
+    got = {k: p.grad.detach().float().cpu() for k, p in m.named_parameters()}
+    assert set(got) == set(gref)
+    lrel = abs(loss.item() - lref) / abs(lref)
+    norms = {k: v.norm().item() for k, v in gref.items()}
+    big = max(norms.values())
+    worst = (0.0, "")
+    worst_rel, worst_cos = 0.0, 1.0
+    for k, g in gref.items():
+        if dtype == "fp32":
+            e = (got[k] - g).abs().max().item() / max(g.abs().max().item(), 1e-30)
+            worst = max(worst, (e, k))
+            assert e < 5e-4, (k, e)
+        else:
+            c = cos(got[k], g)
+            r = (got[k] - g).norm().item() / max(norms[k], 1e-30)
+            if norms[k] >= 1e-3 * big:
+                worst_rel, worst_cos = max(worst_rel, r), min(worst_cos, c)
+                assert c > 0.999 and r < 0.05, (k, c, r)
+            else:
+                assert c > 0.99, (k, c, r)
+    tot_r = sum(n * n for n in norms.values()) ** 0.5
+    tot_g = sum(v.norm().item() ** 2 for v in got.values()) ** 0.5
+    print(f"B=128 {dtype} vs oracle: loss {loss.item():.7f} vs {lref:.7f} (rel {lrel:.2e}); "
+          + (f"worst grad err/absmax {worst[0]:.2e} ({worst[1]})" if dtype == "fp32" else
+             f"worst rel {worst_rel:.3e}, worst cos {worst_cos:.6f}")
+          + f"; grad norm {tot_g:.6f} vs {tot_r:.6f}")
+    if dtype == "fp32":
+        assert lrel < 1e-5, lrel
+    else:
+        assert lrel < 1e-3, lrel
+        assert abs(tot_g - tot_r) < 2e-3 * tot_r
