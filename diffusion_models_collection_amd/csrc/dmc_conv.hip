@@ -2064,8 +2064,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvK a, const char* dy
       __syncthreads();
     }
   }
-  // slab [z][Cpad][KK], Cpad = Cout rounded up to 128 (co is the row of C: co = 4h+i, kk = col r):
-  // for each register i, 16 lanes store 16 consecutive kk of one co row (64-byte segments)
+  // slab [z][KK][Cpad], Cpad = Cout rounded up to 128 (co is the row of C: co = 4h+i, kk = col r): a lane's
+  // 4 consecutive co of one kk are one 16-byte store
   const int Cpad = gridDim.y * 128;
   if (bias_on) {   // fixed order: rows within a thread, lanes of the same chunk (xor CPR ...), then the 4 waves
 #pragma unroll
@@ -2089,11 +2089,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvK a, const char* dy
     const int k = kk0 + wn * 64 + j * 16 + fr;
     if (k >= KK) continue;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int co = co0 + wm * 64 + i * 16 + fh * 4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) out[(size_t)(co + e) * KK + k] = acc[i][j][e];
-    }
+    for (int i = 0; i < 4; ++i) *(v4f*)(out + (size_t)k * Cpad + co0 + wm * 64 + i * 16 + fh * 4) = acc[i][j];
   }
 }
 
@@ -2276,19 +2272,292 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_halo2_kernel(ConvK a, const c
       if (co + e < a.Cout) a.wgb[(size_t)blockIdx.z * Cpad + co + e] = accb[e];
   }
   const int KK = 9 * a.Kc;
-  float* out = slab + (size_t)blockIdx.z * Cpad * KK;
+  float* out = slab + (size_t)blockIdx.z * Cpad * KK;   // [z][kk][Cpad]
   const int fr = lane & 15;
 #pragma unroll
   for (int u = 0; u < 9; ++u) {
     const int nt = wq * 9 + u, t = nt >> 2;
     const int kk = t * a.Kc + c0 + (nt & 3) * 16 + fr;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int co = co0 + i * 16 + fh * 4;
+    for (int i = 0; i < 4; ++i) *(v4f*)(out + (size_t)kk * Cpad + co0 + i * 16 + fh * 4) = acc[i][u];
+  }
+}
+
+// Pipelined 3x3 weight gradient (round 5). The round-4 kernel above spends most of its issue slots on LDS address
+// arithmetic (each transposed x fragment recomputed its row, XOR swizzle and byte offset: ~9 VALU per
+// ds_read_b64_tr, ~170 VALU per 36-MFMA k-step, more than the MFMAs leave room for) and drains the DMA queue at every
+// tile to reload its single halo buffer. Here:
+//   * the swizzle of the x halo depends only on the halo COLUMN (and, for 8-wide maps, the parity of the halo row),
+//     so moving to the next 32-pixel k-step shifts every fragment row by a whole number of halo rows without
+//     changing its swizzle: a lane's 18 x-fragment addresses and 8 dy-fragment addresses are computed once, and
+//     each k-step's shift is the ds_read instruction's immediate offset (the geometry is a template argument) --
+//     no VALU in the fragment reads;
+//   * 128-pixel tiles whose halos (<= 224 pixels x 64 channels = 28 KB) are double-buffered: tile t+1's halo is
+//     DMA'd while tile t computes, every wait is a counted vmcnt of the wave's own issue order;
+//   * the partial sums leave as 16-byte stores into a [split][kk][co] slab (wgrad_reduce_t_kernel).
+// Block = (64-channel x chunk, 64 output channels, a range of 128-pixel tiles); 4 waves, each 64 co x 144 n (9 of
+// the 36 16-wide n tiles: the nine taps of the wave's 16-channel column segment). LDS: 2 x 28 KB + 3 x 8 KB =
+// 80 KB: two blocks per CU. Geometry: OW = 32 / 16 (R = 128 / OW rows of one image) or 8 (two whole 8x8 images).
+template <int OW>
+struct WgPipeGeo {
+  static constexpr int R = OW >= 16 ? 128 / OW : 8;          // image rows per tile
+  static constexpr int NIMG = OW >= 16 ? 1 : 128 / (8 * OW);  // whole images per tile (8x8 maps: 2)
+  static constexpr int HW = OW + 2;                          // halo row pitch (pixels)
+  static constexpr int SEGP = (R + 2) * HW;                  // halo pixels per image
+  static constexpr int NPIX = NIMG * SEGP;                   // <= 224
+  static constexpr int HPW = (NPIX + 31) / 32;               // halo DMA pieces (8 pixels) per wave
+  static constexpr int HB = HPW * 4 * 1024;                  // bytes of one halo buffer
+  // halo index of tile pixel p (before the tap shift)
+  static constexpr int hrow(int p) {
+    return (p / (R * OW)) * SEGP + ((p % (R * OW)) / OW + 1) * HW + (p % OW) + 1;
+  }
+  // shift of k-step j (pixels 32j..32j+31) in halo rows x 128 bytes: an ds_read immediate offset
+  static constexpr int koff(int j) { return (hrow(32 * j) - hrow(0)) * 128; }
+};
+// x halo swizzle: the 32-byte segment of halo pixel h is stored at seg ^ swz_h(h). Bit 0 = bit 1 of the halo
+// column; bit 1 = bit 3 of the column (maps >= 16 wide) or the parity of the halo row (8 wide: a fragment's two
+// 8-pixel row groups are one image row apart, at the same columns). Conflict-free ds_read_b64_tr_b16 for every tap
+// (checked by brute force, scripts/swizzle_check.py) and invariant under each k-step's whole-row shift.
+template <int OW>
+DMC_DEV int swz_h(int h) {
+  constexpr int HW = OW + 2;
+  const int hc = h % HW;
+  return ((hc >> 1) & 1) | ((OW >= 16 ? (hc >> 3) & 1 : (h / HW) & 1) << 1);
+}
+
+DMC_DEV v4i tr2(const char* pa, const char* pb) {
+  v4s ra = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS v4s*)(uintptr_t)pa);
+  v4s rb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS v4s*)(uintptr_t)pb);
+  v2i ia = __builtin_bit_cast(v2i, ra), ib = __builtin_bit_cast(v2i, rb);
+  v4i r; r[0] = ia[0]; r[1] = ia[1]; r[2] = ib[0]; r[3] = ib[1];
+  return r;
+}
+
+template <int OW>
+__global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const char* dy, int ld_dy, int dy_bytes,
+                                                             float* slab, int tiles_per_split, int ncb, int nob,
+                                                             int Cpad) {
+  using T = bf16_t;
+  using G = WgPipeGeo<OW>;
+  constexpr int HPW = G::HPW, HB = G::HB;
+  constexpr int DB = 64 * 128;                       // dy stage: 64 pixels x 64 co
+  constexpr int HALF = 2 * HB + 3 * DB;              // LDS of one half: two halo buffers + the dy ring (<= 80 KB)
+  constexpr int RED = 4 * 36 * 64 * 16;              // the second half's partial sums at the end (144 KB)
+  constexpr int REDB = RED + 4 * 64 * 16;            // ... and its bias partials
+  __shared__ __attribute__((aligned(16))) char lds[2 * HALF > REDB ? 2 * HALF : REDB];
+
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int hv = wv >> 2, wq = wv & 3;               // half, wave within the half
+  char* const base = lds + hv * HALF;
+  // 1-D grid over (ci chunk, co tile, split), ci fastest; XCD-aware: block b takes tile (b mod 8) * (n / 8) + b / 8
+  // (blocks are dealt to the 8 XCDs round-robin), so an XCD works on a contiguous range and the blocks that share a
+  // dy slice (same co tile and split) or an x slice (same ci chunk and split) read it through one L2
+  const int nblk = (int)gridDim.x, per8 = nblk >> 3, bid = (int)blockIdx.x;
+  const int lin = bid < (per8 << 3) ? (bid & 7) * per8 + (bid >> 3) : bid;
+  const int zb = lin / (ncb * nob), rem = lin - zb * ncb * nob;
+  const int cob = rem / ncb, cib = rem - cob * ncb;
+  const int c0 = cib * 64, co0 = cob * 64;
+  const int ntiles = a.M / 128;
+  // the split's tiles: the first half of them to half 0, the rest to half 1 (both run nt stages pairs: the barriers
+  // are the block's; a half with fewer tiles idles through the last pair)
+  const int s_begin = zb * tiles_per_split, s_end = min(ntiles, s_begin + tiles_per_split);
+  const int nh0 = (s_end - s_begin + 1) / 2;
+  const int t_begin = hv ? s_begin + nh0 : s_begin;
+  const int my_nt = hv ? (s_end - s_begin - nh0) : nh0;
+  const int nt = nh0, nst = 2 * nt;                  // the block's loop length (half 0 has the most tiles)
+  const bool first = c0 < a.C1;
+  const int cs = first ? c0 : c0 - a.C1;
+  const int ldx = first ? a.ld1 : a.ld2;
+  const char* const xsrc = first ? a.x1 : a.x2;
+  const int xbytes = first ? a.x1_bytes : a.x2_bytes;
+
+  // dy DMA: 2 pieces per wave per stage, piece = 8 pixel rows x 128 B; chunk-level source swizzle swz_x(row)
+  unsigned od[2];
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (co + e < Cpad) out[(size_t)(co + e) * KK + kk] = acc[i][u][e];
+  for (int j = 0; j < 2; ++j) {
+    const int row = (wq * 2 + j) * 8 + (lane >> 3);
+    const int pc = lane & 7;
+    const int lc = (((pc >> 1) ^ swz_x(row)) << 1) | (pc & 1);
+    const int co = co0 + lc * 8;
+    od[j] = co < a.Cout ? ((unsigned)row * ld_dy + co) * 2u : kOOB;
+  }
+  auto dy_issue = [&](int st) {   // stage st of this half -> pixels [st*64, st*64+64) of its tile range
+    const unsigned off = (unsigned)(t_begin * 128 + st * 64) * (unsigned)ld_dy * 2u;
+    dma_pieces<2>(dy, dy_bytes, base + 2 * HB + (st % 3) * DB + wq * 2 * 1024, od, off, 0, 2);
+  };
+  auto halo_issue = [&](int tl) {   // tile tl of this half -> halo buffer tl & 1
+    const int m0 = (t_begin + tl) * 128;
+    const int n_first = m0 / a.OHW;
+    const int r0 = (m0 - n_first * a.OHW) / OW;
+    // the per-piece geometry is tile-invariant, but keeping it across the tile loop costs ~30 registers: recompute
+    int lv = lane;
+    asm volatile("" : "+v"(lv));
+    unsigned hx[HPW];
+#pragma unroll
+    for (int p = 0; p < HPW; ++p) {
+      const int h = (wq * HPW + p) * 8 + (lv >> 3);
+      hx[p] = kOOB;
+      if (h < G::NPIX) {
+        const int img = h / G::SEGP, hrem = h - img * G::SEGP;
+        const int hr = hrem / G::HW, hc = hrem - hr * G::HW;
+        const int iy = r0 + hr - 1, ix = hc - 1;
+        const int lc = ((((lv & 7) >> 1) ^ swz_h<OW>(h)) << 1) | (lv & 1);
+        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+          hx[p] = ((unsigned)(((n_first + img) * a.H + iy) * a.W + ix) * ldx + cs + lc * 8) * 2u;
+      }
     }
+    dma_pieces<HPW>(xsrc, xbytes, base + (tl & 1) * HB + wq * HPW * 1024, hx, 0u, 0, HPW);
+  };
+
+  // fragment addresses (bytes into the LDS array): lane rows r = 8 fh + 4 half + q of a k-step, 8-byte column group
+  // p of the 32-byte segment. They are rotated in place when the dy ring slot / halo buffer changes (8 / 6-12 VALU
+  // per stage / tile), so every read is lds + address + an immediate
+  const int fh = lane >> 4, q = (lane >> 2) & 3, pcol = lane & 3;
+  const unsigned hb = (unsigned)(hv * HALF);
+  unsigned da[4][2];   // dy: segment i (16 co), half; ring slot 0; k-step 1 adds 32 rows (immediate)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int row = 8 * fh + 4 * hf + q;
+      da[i][hf] = hb + (unsigned)(2 * HB + row * 128 + ((i ^ swz_x(row)) << 5) + pcol * 8);
+    }
+  // x: wave wq owns the 16-column segment wq of the 64-channel chunk for all nine taps (n tile = tap). A tap's row
+  // shift ty * HW keeps the swizzle of maps >= 16 wide (it depends on the column only): one address per (tap column
+  // tx, half) and the row part in the immediate. 8-wide maps swizzle on the row parity too: a second set for odd ty.
+  constexpr int NXA = OW >= 16 ? 1 : 2;
+  unsigned xa[NXA][3][2];
+#pragma unroll
+  for (int py = 0; py < NXA; ++py)
+#pragma unroll
+    for (int tx = 0; tx < 3; ++tx)
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int dl = (py - 1) * G::HW + (tx - 1);   // forward taps (kh - 1, kw - 1): the planner checks
+        const int h = G::hrow(8 * fh + 4 * hf) + q + dl;
+        xa[py][tx][hf] = hb + (unsigned)(h * 128 + ((wq ^ swz_h<OW>(h)) << 5) + pcol * 8);
+      }
+  // LDS offset of tap row ty relative to the address set it reads (compile-time: an immediate)
+  auto tap_row_off = [](int ty) { return (OW >= 16 ? ty : (ty & ~1)) * G::HW * 128; };
+
+  v4f acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int u = 0; u < 9; ++u) acc[i][u] = v4f{0.f, 0.f, 0.f, 0.f};
+  const bool bias_on = a.wgb != nullptr && cib == 0;
+  const v4i ones = {0x3F803F80, 0x3F803F80, 0x3F803F80, 0x3F803F80};   // bf16 1.0 pairs
+  v4f accb = {0.f, 0.f, 0.f, 0.f};
+
+  const int mst = 2 * my_nt;   // this half's stages
+  if (my_nt > 0) {
+    halo_issue(0);
+    dy_issue(0);
+    dy_issue(1);
+  }
+#pragma unroll 1
+  for (int tl = 0; tl < nt; ++tl) {
+    if (tl > 0) {   // halo buffer tl & 1
+      const unsigned dx = (tl & 1) ? (unsigned)HB : (unsigned)-HB;
+#pragma unroll
+      for (int py = 0; py < NXA; ++py)
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx) { xa[py][tx][0] += dx; xa[py][tx][1] += dx; }
+    }
+    const bool live = tl < my_nt;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int st = 2 * tl + k;
+      if (st > 0) {   // dy ring slot st % 3
+        const unsigned dd = (st % 3 == 0) ? (unsigned)(-2 * DB) : (unsigned)DB;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { da[i][0] += dd; da[i][1] += dd; }
+      }
+      // counted waits of this wave's issue order: k = 0 needs dy(st) and halo(tl), only dy(st+1) may
+      // be in flight; k = 1 needs dy(st), dy(st+1) and halo(tl+1) may be in flight
+      if (live) wait_vm_dyn((st + 1 < mst ? 2 : 0) + (k == 1 && tl + 1 < my_nt ? HPW : 0));
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("" ::: "memory");
+      if (!live) continue;
+      if (st + 2 < mst) dy_issue(st + 2);
+      if (k == 0 && tl + 1 < my_nt) halo_issue(tl + 1);   // into the buffer tile tl-1 used (every wave is past it)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int ko = G::koff(2 * k + ks);
+        // (tap row ty of k-step j reads the rows of tap row ty - 1 of k-step j + 1: left visible, the compiler keeps
+        // those sums -- and fragments -- in registers across k-steps. Opaque per k-step, each read folds its row
+        // shift into the instruction's immediate offset.)
+#pragma unroll
+        for (int py = 0; py < NXA; ++py)
+#pragma unroll
+          for (int tx = 0; tx < 3; ++tx) asm volatile("" : "+v"(xa[py][tx][0]), "+v"(xa[py][tx][1]));
+        v4i fa[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = tr2(lds + da[i][0] + ks * 4096, lds + da[i][1] + ks * 4096);
+        // x fragment of tap u (ty = u / 3, tx = u % 3)
+        auto xfrag = [&](int u) __attribute__((always_inline)) {
+          const int ty = u / 3, tx = u - 3 * (u / 3), py = OW >= 16 ? 0 : (ty & 1);
+          const int o = ko + tap_row_off(ty);
+          return tr2(lds + xa[py][tx][0] + o, lds + xa[py][tx][1] + o);
+        };
+        v4i fb = xfrag(0);
+#pragma unroll
+        for (int u = 0; u < 9; ++u) {
+          v4i fn = fb;
+          if (u + 1 < 9) fn = xfrag(u + 1);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i][u] = mma16<T>(acc[i][u], fa[i], fb);
+          if (u + 1 < 9) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the next fragment's reads
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // this fragment's MFMAs
+          }
+          fb = fn;
+        }
+        if (bias_on) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (i == wq) accb = mma16<T>(accb, fa[i], ones);
+        }
+      }
+    }
+  }
+  // the two halves' partial sums combined in LDS (half 1 -> LDS, half 0 adds): one slab row per block instead of two
+  __syncthreads();   // every LDS read of the loop is done (and the DMA: every wave waited for all it issued)
+  v4f* const red = (v4f*)lds;
+  v4f* const redb = (v4f*)(lds + RED);   // the bias partials past the accumulators
+  if (hv == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int u = 0; u < 9; ++u) red[(wq * 36 + i * 9 + u) * 64 + lane] = acc[i][u];
+    redb[wq * 64 + lane] = accb;
+  }
+  __syncthreads();
+  if (hv == 1) return;
+  accb += redb[wq * 64 + lane];
+  const int fr = lane & 15;
+  if (bias_on && fr == 0) {   // column 0 of the all-ones product: rows co = 4 fh + e of dy fragment wq
+    const int co = co0 + wq * 16 + fh * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (co + e < a.Cout) a.wgb[(size_t)zb * Cpad + co + e] = accb[e];
+  }
+  // partial dW (half 0 + half 1) -> slab [z][kk][Cpad]: lane (fr, fh) holds C[co = 4 fh + e][kk = fr] of each tile:
+  // one 16-byte store; one tap at a time (the scheduling barrier keeps the LDS loads from all being hoisted ahead of
+  // the stores, which would need 144 more registers)
+  const int KK = 9 * a.Kc;
+  float* const out = slab + (size_t)zb * KK * Cpad;
+#pragma unroll
+  for (int u = 0; u < 9; ++u) {   // n tile (tap u, segment wq)
+    const int kk = u * a.Kc + c0 + wq * 16 + fr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *(v4f*)(out + (size_t)kk * Cpad + co0 + i * 16 + fh * 4) = acc[i][u] + red[(wq * 36 + i * 9 + u) * 64 + lane];
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -2396,29 +2665,21 @@ __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char*
       for (int e = 0; e < 4; ++e) a.wgb[(size_t)zb * Cpad + co + e] = accb[u][e];
     }
   }
-  // partial dW -> slab [z][Cpad][KK]: C[co = 4 fh + e][ci = fr]
+  // partial dW -> slab [z][KK][Cpad]: C[co = 4 fh + e][ci = fr], 16-byte stores
   float* out = slab + (size_t)zb * KK * Cpad;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int k = ci0 + wn * 64 + j * 16 + fr;
     if (k >= KK) continue;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int co = co0 + wm * 64 + i * 16 + fh * 4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) out[(size_t)(co + e) * KK + k] = acc[i][j][e];
-    }
+    for (int i = 0; i < 4; ++i) *(v4f*)(out + (size_t)k * Cpad + co0 + wm * 64 + i * 16 + fh * 4) = acc[i][j];
   }
 }
 
-// dw[co][c][t] = scale * sum_z slab[z][co][t*Kc + c]; threads walk the slab contiguously (k fastest)
-// ... and with bslab: dbias[co] = scale * sum_z bslab[z][co], one wave per co in the blocks past wblocks (lanes
-// take z = lane, lane + 64, ...; fixed xor tree: deterministic)
-// Sum of the per-split fp32 slabs [split][Cpad][KK] into the reference-layout weight gradient dw[co][c][t] (x scale),
-// plus the bias gradient from the per-split bias slab (one wave per channel, blocks past wblocks). A thread owns 4
-// consecutive (co, k) outputs (16-byte slab loads, 16 in flight) and adds the splits in ascending order, one fp32
-// add per split and output: the same sums, bit for bit, as one output per thread (the round-1/2 form), at a quarter
-// of the load instructions and 8x the bytes in flight per thread (the reduce was latency-bound at 1.3-2.7 TB/s).
+// Sum of the per-split fp32 slabs [split][KK][Cpad] into the reference-layout weight gradient dw[co][c][t] (x scale),
+// plus the bias gradient from the per-split bias slab (one wave per channel, blocks past wblocks; lanes take z = lane,
+// lane + 64, ..., fixed xor tree: deterministic). A thread owns 4 consecutive co of one kk (16-byte slab loads, up to
+// 16 in flight) and adds the splits in ascending order, one fp32 add per split and output.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slab, int splits, int KK, int Cpad, int Cout,
                                                            int Ctot, int ntaps, int Kc, float scale, float* dw,
                                                            const float* bslab, float* dbias, int wblocks) {
@@ -2431,37 +2692,37 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slab, in
     if ((threadIdx.x & 63) == 0) dbias[co] = s * scale;
     return;
   }
-  const int total4 = Cout * KK / 4;   // KK = ntaps * Kc, Kc a multiple of 32: 4 | KK
-  const size_t zs = (size_t)Cpad * KK / 4;
+  const int cq = (Cout + 3) / 4, total4 = KK * cq;
+  const size_t zs = (size_t)KK * Cpad / 4;
   const v4f* s4 = (const v4f*)slab;
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < total4; q += wblocks * blockDim.x) {
-    const int o = q * 4;
-    const int co = o / KK;
-    const int k = o - co * KK;
-    const int t = k / Kc, c = k - t * Kc;   // 4 | Kc: the 4 outputs share co and t
+    const int k = q / cq, co = (q - k * cq) * 4;
+    const int t = k / Kc, c = k - t * Kc;
     if (c >= Ctot) continue;
+    const size_t o = ((size_t)k * Cpad + co) / 4;
     v4f s = {0.f, 0.f, 0.f, 0.f};
     int z = 0;
     for (; z + 16 <= splits; z += 16) {
       v4f v[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = s4[(size_t)(z + u) * zs + q];
+      for (int u = 0; u < 16; ++u) v[u] = s4[(size_t)(z + u) * zs + o];
 #pragma unroll
       for (int u = 0; u < 16; ++u) s += v[u];
     }
     if (z + 8 <= splits) {
       v4f v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = s4[(size_t)(z + u) * zs + q];
+      for (int u = 0; u < 8; ++u) v[u] = s4[(size_t)(z + u) * zs + o];
 #pragma unroll
       for (int u = 0; u < 8; ++u) s += v[u];
       z += 8;
     }
-    for (; z < splits; ++z) s += s4[(size_t)z * zs + q];
+    for (; z < splits; ++z) s += s4[(size_t)z * zs + o];
     float* d = dw + ((size_t)co * Ctot + c) * ntaps + t;
+    const size_t cs = (size_t)Ctot * ntaps;
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-      if (c + e < Ctot) d[(size_t)e * ntaps] = s[e] * scale;
+      if (co + e < Cout) d[e * cs] = s[e] * scale;
   }
 }
 
@@ -3043,11 +3304,47 @@ WgHaloPlan wgrad_halo_plan(const dmc_conv_desc* d) {
   return p;
 }
 
+// Pipelined weight-gradient plan (wgrad3x3_pipe_kernel): bf16 3x3 stride-1 convs on halo2_plan's 128-pixel geometry
+// with 32- or 16-wide maps (rows of one image) or 8x8 maps (two images per tile), 64-aligned channel sources, no
+// prologue, Cout % 8 == 0. Returns OW (the template argument) or 0; splits the tiles so that ~DMC_WG_HALO_TARGET x 2
+// blocks of 64 x 64 run.
+struct WgPipePlan {
+  int ow, splits, tps;
+};
+WgPipePlan wgrad_pipe_plan(const dmc_conv_desc* d, int ld_dy) {
+  WgPipePlan p{0, 1, 0};
+  if (d->dtype != DMC_BF16 || dmc::opt(dmc::OPT_NO_HALO) || dmc::opt(dmc::OPT_WG_PIPE) == 0) return p;
+  ConvK k;
+  if (fill_convk(d, nullptr, nullptr, nullptr, nullptr, nullptr, k)) return p;
+  if (k.C1 % 64 || k.C2 % 64 || k.Kc != k.C1 + k.C2 || k.x1_bytes == 0 || (k.C2 && k.x2_bytes == 0)) return p;
+  if (k.prologue != DMC_PRO_NONE || k.Cout % 8 || ld_dy % 8 || k.M % 128) return p;
+  if ((size_t)k.M * ld_dy * 2 >= 0x7fff0000u) return p;
+  int R, nimg;
+  if (!halo2_plan(k, &R, &nimg)) return p;
+  if (k.tdy0 != -1 || k.tsy != 1 || k.tdx0 != -1 || k.tsx != 1) return p;   // the forward taps (weight gradient)
+  const bool ok = ((k.OW == 32 || k.OW == 16) && nimg == 1) || (k.OW == 8 && k.OH == 8 && nimg == 2);
+  if (!ok) return p;
+  const int ntiles = k.M / 128;
+  const long base = (long)(k.Kc / 64) * dmc::cdiv(k.Cout, 64);
+  // 512-thread blocks (two 64 x 64 halves): one per CU, never more than one round of them (264 blocks for 256 CUs
+  // measured 1.4x slower than 192)
+  const long target = dmc::opt(dmc::OPT_WG_HALO_TARGET);
+  long sp = target / base;
+  if (sp > ntiles) sp = ntiles;
+  if (sp < 1) sp = 1;
+  p.tps = (int)((ntiles + sp - 1) / sp);
+  p.splits = (ntiles + p.tps - 1) / p.tps;
+  p.ow = k.OW;
+  return p;
+}
+
 extern "C" size_t dmc_conv2d_wgrad_workspace(const dmc_conv_desc* d) {
   int pps;
   int splits = wgrad_splits(d, &pps);
   const WgHaloPlan hp = wgrad_halo_plan(d);
   if (hp.ok && hp.splits > splits) splits = hp.splits;
+  const WgPipePlan pp = wgrad_pipe_plan(d, ((d->Cout + 7) / 8) * 8);
+  if (pp.ow && pp.splits > splits) splits = pp.splits;
   const size_t KK = (size_t)d->ntaps * d->Kc;
   const size_t Cpad = (size_t)dmc::cdiv(d->Cout, 128) * 128;
   return (size_t)splits * (KK + 1) * Cpad * sizeof(float);   // + the bias partials [splits][Cpad]
@@ -3066,8 +3363,10 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   dim3 g(dmc::cdiv(KK, 128), dmc::cdiv(d->Cout, 128), splits);
   const WgHaloPlan hp = wgrad_halo_plan(d);
   const size_t dyb = (size_t)k.M * ld_dy * 2;
-  const bool halo = hp.ok && dyb < 0x7fff0000u;
+  const WgPipePlan pp = wgrad_pipe_plan(d, ld_dy);
+  const bool halo = !pp.ow && hp.ok && dyb < 0x7fff0000u;
   if (halo) splits = hp.splits;
+  if (pp.ow) splits = pp.splits;
   // 1x1 stride-1 bf16 (Linear-shaped): both operands DMA'd into LDS (wgrad1x1_glds_kernel); splits are whole
   // SPX-pixel stages, never more than wgrad_splits() counted (the workspace query's bound)
   const bool direct = d->ntaps == 1 && k.stride == 1 && k.mode == DMC_MODE_NORMAL && k.tdy0 == 0 && k.tdx0 == 0 &&
@@ -3086,7 +3385,21 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   // bias partials after the weight slab (dmc_conv2d_wgrad_workspace sized for the larger split count)
   float* const bslab = d->wg_bias ? (float*)workspace + (size_t)splits * KK * Cpad : nullptr;
   k.wgb = bslab;
-  if (halo) {
+  if (pp.ow) {
+    const int ncb = d->Kc / 64, nob = dmc::cdiv(d->Cout, 64);
+    const dim3 g1(ncb * nob * splits);
+    const int Cp = (int)Cpad;
+    if (pp.ow == 32)
+      wgrad3x3_pipe_kernel<32><<<g1, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, pp.tps, ncb,
+                                                  nob, Cp);
+    else if (pp.ow == 16)
+      wgrad3x3_pipe_kernel<16><<<g1, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, pp.tps, ncb,
+                                                  nob, Cp);
+    else
+      wgrad3x3_pipe_kernel<8><<<g1, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, pp.tps, ncb,
+                                                 nob, Cp);
+    g.y = dmc::cdiv(d->Cout, 128);   // the reduce's slab pitch: Cout rounded to 128
+  } else if (halo) {
     // two blocks per CU: 64-co blocks, the same split count (twice the co tiles, half the block target's share)
     g = dim3(d->Kc / 64, dmc::cdiv(d->Cout, 64), splits);
     if (hp.hp == 6)
@@ -3106,7 +3419,7 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
     conv_wgrad_kernel<bf16_t><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (float*)workspace, KK, pps);
   if (dmc::check_launch("dmc_conv2d_wgrad")) return 2;
   const int Ctot = d->C1 + d->C2;
-  const long total = (long)d->Cout * KK / 4;   // 4 outputs per thread
+  const long total = (long)KK * ((d->Cout + 3) / 4);   // 4 outputs per thread
   const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
   const int bblocks = d->wg_bias ? dmc::cdiv(d->Cout, 4) : 0;   // one wave per bias channel
   wgrad_reduce_kernel<<<blocks + bblocks, 256, 0, s>>>((const float*)workspace, splits, KK, (int)g.y * 128, d->Cout,

@@ -1060,3 +1060,38 @@ def test_wgrad_small_maps_and_taps(case):
     torch.cuda.synchronize()
     assert rel_err(dw.cpu(), w.grad) < 1e-5
     assert rel_err(db.cpu(), g.float().sum((0, 2, 3))) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(128, 32, 32, 128, 0, 128), (64, 32, 32, 128, 128, 128), (128, 16, 16, 256, 0, 256),
+                                   (32, 16, 16, 256, 128, 256), (128, 8, 8, 256, 256, 256), (6, 8, 8, 128, 64, 192),
+                                   (3, 16, 16, 128, 0, 200)])
+def test_wgrad_pipe_kernel(shape, dmc_opt):
+    """The pipelined 3x3 weight gradient (wgrad3x3_pipe_kernel: x-fragment addresses fixed per lane with the k-step
+    and tap row shifts as immediates, double-buffered 128-pixel halos, [split][kk][co] slab) against the round-4 halo
+    kernel (DMC_WG_PIPE=0) and an fp32 torch reference of the same bf16 operands: weight and bias gradients, two
+    sources (virtual concat), ragged Cout, the B=128 split plans; and bitwise reproducible run to run."""
+    from diffusion_models_collection_amd import _lib as L, kernels as K
+    N, H, W, C1, C2, Cout = shape
+    gen = torch.Generator().manual_seed(N + H + C1 + C2 + Cout)
+    dt = torch.bfloat16
+    x = torch.randn(N, H, W, C1 + C2, generator=gen).to(dt)
+    g = torch.randn(N, H, W, Cout, generator=gen).to(dt)
+    x1d = x[..., :C1].contiguous().to(DEV)
+    x2d = x[..., C1:].contiguous().to(DEV) if C2 else None
+    gd = g.to(DEV)
+    d = K.make_desc(dt, N, H, W, C1, C2, C1, C2, L.kc_for(C1 + C2, dt), H, W, Cout, K.TAPS3)
+    res = []
+    for pipe in (1, 1, 0):
+        dmc_opt("DMC_WG_PIPE", pipe)
+        dw = torch.full((Cout, C1 + C2, 3, 3), float("nan"), device=DEV)
+        db = torch.full((Cout,), float("nan"), device=DEV)
+        K.wgrad(d, gd, Cout, x1d, x2d, dw, dbias=db)
+        torch.cuda.synchronize()
+        res.append((dw.cpu(), db.cpu()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])   # deterministic
+    xr = x.permute(0, 3, 1, 2).float()
+    gr = g.permute(0, 3, 1, 2).float()
+    wr = torch.nn.grad.conv2d_weight(xr, (Cout, C1 + C2, 3, 3), gr, padding=1)
+    assert rel_err(res[0][0], wr) < 1e-5, rel_err(res[0][0], wr)
+    assert rel_err(res[0][0], res[2][0]) < 1e-5
+    assert rel_err(res[0][1], gr.sum((0, 2, 3))) < 1e-5
