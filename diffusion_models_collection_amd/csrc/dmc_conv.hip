@@ -2300,13 +2300,19 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_halo2_kernel(ConvK a, const c
 // 80 KB: two blocks per CU. Geometry: OW = 32 / 16 (R = 128 / OW rows of one image) or 8 (two whole 8x8 images).
 template <int OW>
 struct WgPipeGeo {
-  static constexpr int R = OW >= 16 ? 128 / OW : 8;          // image rows per tile
-  static constexpr int NIMG = OW >= 16 ? 1 : 128 / (8 * OW);  // whole images per tile (8x8 maps: 2)
-  static constexpr int HW = OW + 2;                          // halo row pitch (pixels)
-  static constexpr int SEGP = (R + 2) * HW;                  // halo pixels per image
-  static constexpr int NPIX = NIMG * SEGP;                   // <= 224
-  static constexpr int HPW = (NPIX + 31) / 32;               // halo DMA pieces (8 pixels) per wave
-  static constexpr int HB = HPW * 4 * 1024;                  // bytes of one halo buffer
+  static constexpr int TILE = OW >= 8 ? 128 : 64;             // output pixels per tile (4x4 maps: 64)
+  static constexpr int SPT = TILE / 64;                        // 64-pixel dy stages per tile
+  static constexpr int R = OW >= 16 ? 128 / OW : OW;          // image rows per tile (small maps: whole images)
+  static constexpr int NIMG = OW >= 16 ? 1 : TILE / (OW * OW); // whole images per tile (8x8: 2, 4x4: 4)
+  static constexpr int HW = OW + 2;                            // halo row pitch (pixels)
+  static constexpr int SEGP = (R + 2) * HW;                    // halo pixels per image
+  static constexpr int NPIX = NIMG * SEGP;                     // <= 224
+  static constexpr int HPW = (NPIX + 31) / 32;                 // halo DMA pieces (8 pixels) per wave
+  static constexpr int HB = HPW * 4 * 1024;                    // bytes of one halo buffer
+  // x-fragment address sets: the tap rows a set serves by a whole-row shift that keeps its swizzle (below)
+  static constexpr int NXA = OW >= 16 ? 1 : OW == 8 ? 2 : 3;
+  static constexpr int set_of(int ty) { return OW >= 16 ? 0 : OW == 8 ? (ty & 1) : ty; }
+  static constexpr int row_off(int ty) { return ty - set_of(ty); }   // halo rows added to the set's base row
   // halo index of tile pixel p (before the tap shift)
   static constexpr int hrow(int p) {
     return (p / (R * OW)) * SEGP + ((p % (R * OW)) / OW + 1) * HW + (p % OW) + 1;
@@ -2314,15 +2320,16 @@ struct WgPipeGeo {
   // shift of k-step j (pixels 32j..32j+31) in halo rows x 128 bytes: an ds_read immediate offset
   static constexpr int koff(int j) { return (hrow(32 * j) - hrow(0)) * 128; }
 };
-// x halo swizzle: the 32-byte segment of halo pixel h is stored at seg ^ swz_h(h). Bit 0 = bit 1 of the halo
-// column; bit 1 = bit 3 of the column (maps >= 16 wide) or the parity of the halo row (8 wide: a fragment's two
-// 8-pixel row groups are one image row apart, at the same columns). Conflict-free ds_read_b64_tr_b16 for every tap
-// (checked by brute force, scripts/swizzle_check.py) and invariant under each k-step's whole-row shift.
+// x halo swizzle: the 32-byte segment of halo pixel h (halo row hr = h / HW, column hc = h % HW) is stored at
+// seg ^ swz_h(h). Bit 0 = bit 1 of hc; bit 1 = bit 3 of hc (maps >= 16 wide: a fragment's two 8-pixel groups are 8
+// columns apart), bit 0 of hr (8 wide: one image row apart, same columns) or bit 1 of hr (4 wide: two rows apart).
+// Conflict-free ds_read_b64_tr_b16 for every tap and k-step, and unchanged by each k-step's whole-row shift and by
+// the row shift between the taps of one address set (scripts/swizzle_check.py checks both by brute force).
 template <int OW>
-DMC_DEV int swz_h(int h) {
+DMC_DEV constexpr int swz_h(int h) {
   constexpr int HW = OW + 2;
-  const int hc = h % HW;
-  return ((hc >> 1) & 1) | ((OW >= 16 ? (hc >> 3) & 1 : (h / HW) & 1) << 1);
+  const int hc = h % HW, hr = h / HW;
+  return ((hc >> 1) & 1) | ((OW >= 16 ? (hc >> 3) & 1 : OW == 8 ? hr & 1 : (hr >> 1) & 1) << 1);
 }
 
 DMC_DEV v4i tr2(const char* pa, const char* pb) {
@@ -2339,7 +2346,7 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
                                                              int Cpad) {
   using T = bf16_t;
   using G = WgPipeGeo<OW>;
-  constexpr int HPW = G::HPW, HB = G::HB;
+  constexpr int HPW = G::HPW, HB = G::HB, SPT = G::SPT, TILE = G::TILE;
   constexpr int DB = 64 * 128;                       // dy stage: 64 pixels x 64 co
   constexpr int HALF = 2 * HB + 3 * DB;              // LDS of one half: two halo buffers + the dy ring (<= 80 KB)
   constexpr int RED = 4 * 36 * 64 * 16;              // the second half's partial sums at the end (144 KB)
@@ -2358,14 +2365,14 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
   const int zb = lin / (ncb * nob), rem = lin - zb * ncb * nob;
   const int cob = rem / ncb, cib = rem - cob * ncb;
   const int c0 = cib * 64, co0 = cob * 64;
-  const int ntiles = a.M / 128;
+  const int ntiles = a.M / TILE;
   // the split's tiles: the first half of them to half 0, the rest to half 1 (both run nt stages pairs: the barriers
   // are the block's; a half with fewer tiles idles through the last pair)
   const int s_begin = zb * tiles_per_split, s_end = min(ntiles, s_begin + tiles_per_split);
   const int nh0 = (s_end - s_begin + 1) / 2;
   const int t_begin = hv ? s_begin + nh0 : s_begin;
   const int my_nt = hv ? (s_end - s_begin - nh0) : nh0;
-  const int nt = nh0, nst = 2 * nt;                  // the block's loop length (half 0 has the most tiles)
+  const int nt = nh0;                                // the block's loop length (half 0 has the most tiles)
   const bool first = c0 < a.C1;
   const int cs = first ? c0 : c0 - a.C1;
   const int ldx = first ? a.ld1 : a.ld2;
@@ -2383,11 +2390,11 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
     od[j] = co < a.Cout ? ((unsigned)row * ld_dy + co) * 2u : kOOB;
   }
   auto dy_issue = [&](int st) {   // stage st of this half -> pixels [st*64, st*64+64) of its tile range
-    const unsigned off = (unsigned)(t_begin * 128 + st * 64) * (unsigned)ld_dy * 2u;
+    const unsigned off = (unsigned)(t_begin * TILE + st * 64) * (unsigned)ld_dy * 2u;
     dma_pieces<2>(dy, dy_bytes, base + 2 * HB + (st % 3) * DB + wq * 2 * 1024, od, off, 0, 2);
   };
   auto halo_issue = [&](int tl) {   // tile tl of this half -> halo buffer tl & 1
-    const int m0 = (t_begin + tl) * 128;
+    const int m0 = (t_begin + tl) * TILE;
     const int n_first = m0 / a.OHW;
     const int r0 = (m0 - n_first * a.OHW) / OW;
     // the per-piece geometry is tile-invariant, but keeping it across the tile loop costs ~30 registers: recompute
@@ -2424,9 +2431,9 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
       da[i][hf] = hb + (unsigned)(2 * HB + row * 128 + ((i ^ swz_x(row)) << 5) + pcol * 8);
     }
   // x: wave wq owns the 16-column segment wq of the 64-channel chunk for all nine taps (n tile = tap). A tap's row
-  // shift ty * HW keeps the swizzle of maps >= 16 wide (it depends on the column only): one address per (tap column
-  // tx, half) and the row part in the immediate. 8-wide maps swizzle on the row parity too: a second set for odd ty.
-  constexpr int NXA = OW >= 16 ? 1 : 2;
+  // shift keeps the swizzle of maps >= 16 wide (it depends on the column only): one address per (tap column tx, half)
+  // and the row part in the immediate. Small maps swizzle on the row too: a set per row class (G::set_of).
+  constexpr int NXA = G::NXA;
   unsigned xa[NXA][3][2];
 #pragma unroll
   for (int py = 0; py < NXA; ++py)
@@ -2439,7 +2446,7 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
         xa[py][tx][hf] = hb + (unsigned)(h * 128 + ((wq ^ swz_h<OW>(h)) << 5) + pcol * 8);
       }
   // LDS offset of tap row ty relative to the address set it reads (compile-time: an immediate)
-  auto tap_row_off = [](int ty) { return (OW >= 16 ? ty : (ty & ~1)) * G::HW * 128; };
+  auto tap_row_off = [](int ty) { return G::row_off(ty) * G::HW * 128; };
 
   v4f acc[4][9];
 #pragma unroll
@@ -2450,7 +2457,7 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
   const v4i ones = {0x3F803F80, 0x3F803F80, 0x3F803F80, 0x3F803F80};   // bf16 1.0 pairs
   v4f accb = {0.f, 0.f, 0.f, 0.f};
 
-  const int mst = 2 * my_nt;   // this half's stages
+  const int mst = SPT * my_nt;   // this half's stages
   if (my_nt > 0) {
     halo_issue(0);
     dy_issue(0);
@@ -2467,15 +2474,16 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
     }
     const bool live = tl < my_nt;
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int st = 2 * tl + k;
+    for (int k = 0; k < SPT; ++k) {
+      const int st = SPT * tl + k;
       if (st > 0) {   // dy ring slot st % 3
         const unsigned dd = (st % 3 == 0) ? (unsigned)(-2 * DB) : (unsigned)DB;
 #pragma unroll
         for (int i = 0; i < 4; ++i) { da[i][0] += dd; da[i][1] += dd; }
       }
-      // counted waits of this wave's issue order: k = 0 needs dy(st) and halo(tl), only dy(st+1) may
-      // be in flight; k = 1 needs dy(st), dy(st+1) and halo(tl+1) may be in flight
+      // counted waits of this wave's issue order (a stage issues halo(tl+1) at k = 0, then dy(st+2)):
+      // k = 0 needs dy(st) and halo(tl), only dy(st+1) may be in flight; k = 1 needs dy(st), and halo(tl+1) and
+      // dy(st+1) may be in flight
       if (live) wait_vm_dyn((st + 1 < mst ? 2 : 0) + (k == 1 && tl + 1 < my_nt ? HPW : 0));
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
@@ -2483,45 +2491,43 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("" ::: "memory");
       if (!live) continue;
-      if (st + 2 < mst) dy_issue(st + 2);
       if (k == 0 && tl + 1 < my_nt) halo_issue(tl + 1);   // into the buffer tile tl-1 used (every wave is past it)
+      if (st + 2 < mst) dy_issue(st + 2);
+      // the stage's two k-steps as one stream of 18 fragment groups (k-step ks, tap u): the x fragment of group g + 2 is
+      // read while group g's 4 MFMAs issue (three rotating fragment buffers), the dy fragments of both k-steps up front.
+      // Each read's base register is made opaque right before it: equal address sums of different groups are not
+      // merged (left visible, the compiler keeps them -- and fragments -- live across groups), so every row shift
+      // (k-step, tap row) folds into the instruction's immediate offset.
+      auto xfrag = [&](int g) __attribute__((always_inline)) {
+        const int ks = g / 9, u = g - 9 * (g / 9), ty = u / 3, tx = u - 3 * (u / 3), py = G::set_of(ty);
+        const int o = G::koff(2 * k + ks) + tap_row_off(ty);
+        asm volatile("" : "+v"(xa[py][tx][0]), "+v"(xa[py][tx][1]));
+        return tr2(lds + xa[py][tx][0] + o, lds + xa[py][tx][1] + o);
+      };
+      v4i fa[2][4], xf[3];
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int ko = G::koff(2 * k + ks);
-        // (tap row ty of k-step j reads the rows of tap row ty - 1 of k-step j + 1: left visible, the compiler keeps
-        // those sums -- and fragments -- in registers across k-steps. Opaque per k-step, each read folds its row
-        // shift into the instruction's immediate offset.)
+      for (int i = 0; i < 4; ++i) fa[0][i] = tr2(lds + da[i][0], lds + da[i][1]);
+      xf[0] = xfrag(0);
+      xf[1] = xfrag(1);
 #pragma unroll
-        for (int py = 0; py < NXA; ++py)
+      for (int i = 0; i < 4; ++i) fa[1][i] = tr2(lds + da[i][0] + 4096, lds + da[i][1] + 4096);
 #pragma unroll
-          for (int tx = 0; tx < 3; ++tx) asm volatile("" : "+v"(xa[py][tx][0]), "+v"(xa[py][tx][1]));
-        v4i fa[4];
+      for (int g = 0; g < 18; ++g) {
+        const int ks = g / 9, u = g - 9 * (g / 9);
+        if (g + 2 < 18) xf[(g + 2) % 3] = xfrag(g + 2);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = tr2(lds + da[i][0] + ks * 4096, lds + da[i][1] + ks * 4096);
-        // x fragment of tap u (ty = u / 3, tx = u % 3)
-        auto xfrag = [&](int u) __attribute__((always_inline)) {
-          const int ty = u / 3, tx = u - 3 * (u / 3), py = OW >= 16 ? 0 : (ty & 1);
-          const int o = ko + tap_row_off(ty);
-          return tr2(lds + xa[py][tx][0] + o, lds + xa[py][tx][1] + o);
-        };
-        v4i fb = xfrag(0);
-#pragma unroll
-        for (int u = 0; u < 9; ++u) {
-          v4i fn = fb;
-          if (u + 1 < 9) fn = xfrag(u + 1);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[i][u] = mma16<T>(acc[i][u], fa[i], fb);
-          if (u + 1 < 9) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the next fragment's reads
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // this fragment's MFMAs
-          }
-          fb = fn;
+        for (int i = 0; i < 4; ++i) acc[i][u] = mma16<T>(acc[i][u], fa[ks][i], xf[g % 3]);
+        if (g + 2 < 18) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the reads of group g + 2
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // this group's MFMAs
         }
-        if (bias_on) {
+      }
+      if (bias_on) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            if (i == wq) accb = mma16<T>(accb, fa[i], ones);
-        }
+            if (i == wq) accb = mma16<T>(accb, fa[ks][i], ones);
       }
     }
   }
@@ -3317,14 +3323,15 @@ WgPipePlan wgrad_pipe_plan(const dmc_conv_desc* d, int ld_dy) {
   ConvK k;
   if (fill_convk(d, nullptr, nullptr, nullptr, nullptr, nullptr, k)) return p;
   if (k.C1 % 64 || k.C2 % 64 || k.Kc != k.C1 + k.C2 || k.x1_bytes == 0 || (k.C2 && k.x2_bytes == 0)) return p;
-  if (k.prologue != DMC_PRO_NONE || k.Cout % 8 || ld_dy % 8 || k.M % 128) return p;
+  if (k.prologue != DMC_PRO_NONE || k.Cout % 8 || ld_dy % 8) return p;
   if ((size_t)k.M * ld_dy * 2 >= 0x7fff0000u) return p;
-  int R, nimg;
-  if (!halo2_plan(k, &R, &nimg)) return p;
+  if (k.mode != DMC_MODE_NORMAL || k.stride != 1 || k.ntaps != 9 || k.tkw != 3 || k.OH != k.H || k.OW != k.W) return p;
   if (k.tdy0 != -1 || k.tsy != 1 || k.tdx0 != -1 || k.tsx != 1) return p;   // the forward taps (weight gradient)
-  const bool ok = ((k.OW == 32 || k.OW == 16) && nimg == 1) || (k.OW == 8 && k.OH == 8 && nimg == 2);
+  // WgPipeGeo: rows of one image (32 / 16 wide, whole 128-pixel tiles per image), two 8x8 or four 4x4 images per tile
+  const bool ok = ((k.OW == 32 || k.OW == 16) && k.OH % (128 / k.OW) == 0) || (k.OW == 8 && k.OH == 8 && k.N % 2 == 0) ||
+                  (k.OW == 4 && k.OH == 4 && k.N % 4 == 0);
   if (!ok) return p;
-  const int ntiles = k.M / 128;
+  const int ntiles = k.M / (k.OW == 4 ? 64 : 128);
   const long base = (long)(k.Kc / 64) * dmc::cdiv(k.Cout, 64);
   // 512-thread blocks (two 64 x 64 halves): one per CU, never more than one round of them (264 blocks for 256 CUs
   // measured 1.4x slower than 192)
@@ -3395,8 +3402,11 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
     else if (pp.ow == 16)
       wgrad3x3_pipe_kernel<16><<<g1, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, pp.tps, ncb,
                                                   nob, Cp);
-    else
+    else if (pp.ow == 8)
       wgrad3x3_pipe_kernel<8><<<g1, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, pp.tps, ncb,
+                                                 nob, Cp);
+    else
+      wgrad3x3_pipe_kernel<4><<<g1, 512, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, pp.tps, ncb,
                                                  nob, Cp);
     g.y = dmc::cdiv(d->Cout, 128);   // the reduce's slab pitch: Cout rounded to 128
   } else if (halo) {

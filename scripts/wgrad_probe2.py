@@ -22,6 +22,8 @@ SHAPES = {   # name: (B, H, W, C1, C2, Cout, count per train step)
     "16 128-256": (128, 16, 16, 128, 0, 256, 1),
     "8 256-256": (128, 8, 8, 256, 0, 256, 8),
     "8 512-256": (128, 8, 8, 256, 256, 256, 3),
+    "4 256-256": (128, 4, 4, 256, 0, 256, 11),
+    "4 512-256": (128, 4, 4, 256, 256, 256, 3),
 }
 
 
@@ -32,7 +34,9 @@ def main():
     ap.add_argument("--only", default="", help="one setting name (e.g. pipe)")
     a = ap.parse_args()
     settings = [("r4 halo", {"DMC_WG_PIPE": 0}), ("pipe", {}), ("pipe t128", {"DMC_WG_HALO_TARGET": 128}),
-                ("pipe t192", {"DMC_WG_HALO_TARGET": 192}), ("pipe t384", {"DMC_WG_HALO_TARGET": 384})]
+                ("pipe t192", {"DMC_WG_HALO_TARGET": 192}), ("pipe t384", {"DMC_WG_HALO_TARGET": 384}),
+                ("pipe t16", {"DMC_WG_HALO_TARGET": 16}), ("pipe t32", {"DMC_WG_HALO_TARGET": 32}),
+                ("pipe t64", {"DMC_WG_HALO_TARGET": 64})]
     if a.only:
         settings = [s_ for s_ in settings if s_[0] == a.only]
     tot = {n: 0.0 for n, _ in settings}

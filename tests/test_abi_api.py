@@ -247,3 +247,13 @@ def test_integration_lists_every_option():
         py_read |= set(re.findall(r'environ\["(DMC_[A-Z0-9_]+)"\]', f.read_text()))
     assert py_read <= doc_exec, sorted(py_read - doc_exec)
     assert len(doc_launch | doc_exec) <= 45
+
+
+def test_wgrad_pipe_lds_swizzle_conflict_free():
+    """scripts/swizzle_check.py: the x-halo and dy images of wgrad3x3_pipe_kernel are bank-conflict free for every
+    tap / k-step / lane group of ds_read_b64_tr_b16, and every fragment address is its set's base + an immediate."""
+    import runpy
+    mod = runpy.run_path(str(ROOT / "scripts" / "swizzle_check.py"))
+    for ow in (32, 16, 8, 4):
+        assert mod["check_x"](ow) == 0, ow
+    assert mod["check_dy"]() == 0

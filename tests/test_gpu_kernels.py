@@ -1064,7 +1064,8 @@ def test_wgrad_small_maps_and_taps(case):
 
 @pytest.mark.parametrize("shape", [(128, 32, 32, 128, 0, 128), (64, 32, 32, 128, 128, 128), (128, 16, 16, 256, 0, 256),
                                    (32, 16, 16, 256, 128, 256), (128, 8, 8, 256, 256, 256), (6, 8, 8, 128, 64, 192),
-                                   (3, 16, 16, 128, 0, 200)])
+                                   (3, 16, 16, 128, 0, 200), (128, 4, 4, 256, 0, 256), (32, 4, 4, 256, 256, 256),
+                                   (4, 4, 4, 128, 64, 64)])
 def test_wgrad_pipe_kernel(shape, dmc_opt):
     """The pipelined 3x3 weight gradient (wgrad3x3_pipe_kernel: x-fragment addresses fixed per lane with the k-step
     and tap row shifts as immediates, double-buffered 128-pixel halos, [split][kk][co] slab) against the round-4 halo
