@@ -2684,8 +2684,10 @@ __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char*
 
 // Sum of the per-split fp32 slabs [split][KK][Cpad] into the reference-layout weight gradient dw[co][c][t] (x scale),
 // plus the bias gradient from the per-split bias slab (one wave per channel, blocks past wblocks; lanes take z = lane,
-// lane + 64, ..., fixed xor tree: deterministic). A thread owns 4 consecutive co of one kk (16-byte slab loads, up to
-// 16 in flight) and adds the splits in ascending order, one fp32 add per split and output.
+// lane + 64, ..., fixed xor tree: deterministic). A block owns 256 / G output quads (4 consecutive co of one kk each)
+// and G groups of its threads take contiguous ranges of the splits (G = 4 from 64 splits, 2 from 32; 16-byte slab
+// loads, up to 16 in flight per lane); each group adds its splits in ascending order, then group 0 adds the other
+// groups' sums in group order through LDS -- a fixed summation order, so the result is bitwise reproducible.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slab, int splits, int KK, int Cpad, int Cout,
                                                            int Ctot, int ntaps, int Kc, float scale, float* dw,
                                                            const float* bslab, float* dbias, int wblocks) {
@@ -2698,37 +2700,54 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slab, in
     if ((threadIdx.x & 63) == 0) dbias[co] = s * scale;
     return;
   }
+  __shared__ v4f part[192];
   const int cq = (Cout + 3) / 4, total4 = KK * cq;
   const size_t zs = (size_t)KK * Cpad / 4;
   const v4f* s4 = (const v4f*)slab;
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < total4; q += wblocks * blockDim.x) {
-    const int k = q / cq, co = (q - k * cq) * 4;
-    const int t = k / Kc, c = k - t * Kc;
-    if (c >= Ctot) continue;
+  // G split groups of 4 / G waves (>= 16 splits per group where there are that many): QB quads per block
+  const int G = splits >= 64 ? 4 : splits >= 32 ? 2 : 1, QB = 256 / G;
+  const int g = (int)threadIdx.x / QB, lane = (int)threadIdx.x - g * QB;
+  const int zpg = (splits + G - 1) / G;
+  const int zb = min(splits, g * zpg), ze = min(splits, zb + zpg);
+  for (int q0 = blockIdx.x * QB; q0 < total4; q0 += wblocks * QB) {
+    const int q = q0 + lane;
+    const bool on = q < total4;
+    const int k = on ? q / cq : 0, co = on ? (q - k * cq) * 4 : 0;
     const size_t o = ((size_t)k * Cpad + co) / 4;
     v4f s = {0.f, 0.f, 0.f, 0.f};
-    int z = 0;
-    for (; z + 16 <= splits; z += 16) {
-      v4f v[16];
+    if (on) {
+      int z = zb;
+      for (; z + 16 <= ze; z += 16) {
+        v4f v[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = s4[(size_t)(z + u) * zs + o];
+        for (int u = 0; u < 16; ++u) v[u] = s4[(size_t)(z + u) * zs + o];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) s += v[u];
+        for (int u = 0; u < 16; ++u) s += v[u];
+      }
+      if (z + 8 <= ze) {
+        v4f v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = s4[(size_t)(z + u) * zs + o];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+        z += 8;
+      }
+      for (; z < ze; ++z) s += s4[(size_t)z * zs + o];
     }
-    if (z + 8 <= splits) {
-      v4f v[8];
+    if (g) part[(g - 1) * QB + lane] = s;
+    __syncthreads();
+    if (g == 0 && on) {
+      for (int u = 0; u + 1 < G; ++u) s += part[u * QB + lane];
+      const int t = k / Kc, c = k - t * Kc;
+      if (c < Ctot) {
+        float* d = dw + ((size_t)co * Ctot + c) * ntaps + t;
+        const size_t cs = (size_t)Ctot * ntaps;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = s4[(size_t)(z + u) * zs + o];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
-      z += 8;
+        for (int e = 0; e < 4; ++e)
+          if (co + e < Cout) d[e * cs] = s[e] * scale;
+      }
     }
-    for (; z < splits; ++z) s += s4[(size_t)z * zs + o];
-    float* d = dw + ((size_t)co * Ctot + c) * ntaps + t;
-    const size_t cs = (size_t)Ctot * ntaps;
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (co + e < Cout) d[e * cs] = s[e] * scale;
+    __syncthreads();
   }
 }
 
@@ -3429,8 +3448,9 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
     conv_wgrad_kernel<bf16_t><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (float*)workspace, KK, pps);
   if (dmc::check_launch("dmc_conv2d_wgrad")) return 2;
   const int Ctot = d->C1 + d->C2;
-  const long total = (long)KK * ((d->Cout + 3) / 4);   // 4 outputs per thread
-  const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  const long total = (long)KK * ((d->Cout + 3) / 4);   // output quads, 256 / G per block (wgrad_reduce_kernel)
+  const int qb = splits >= 64 ? 64 : splits >= 32 ? 128 : 256;
+  const int blocks = (int)((total + qb - 1) / qb < 16384 ? (total + qb - 1) / qb : 16384);
   const int bblocks = d->wg_bias ? dmc::cdiv(d->Cout, 4) : 0;   // one wave per bias channel
   wgrad_reduce_kernel<<<blocks + bblocks, 256, 0, s>>>((const float*)workspace, splits, KK, (int)g.y * 128, d->Cout,
                                                        Ctot, d->ntaps, d->Kc, scale, dw, bslab, d->wg_bias, blocks);
