@@ -43,6 +43,14 @@ class ConvDesc(ctypes.Structure):
     ]
 
 
+class WgradJob(ctypes.Structure):
+    """include/dmc.h dmc_wgrad_job"""
+    _fields_ = [("slab", ctypes.c_void_p), ("bslab", ctypes.c_void_p), ("dw", ctypes.c_void_p),
+                ("dbias", ctypes.c_void_p), ("splits", ctypes.c_int), ("KK", ctypes.c_int), ("Cpad", ctypes.c_int),
+                ("Cout", ctypes.c_int), ("Ctot", ctypes.c_int), ("ntaps", ctypes.c_int), ("Kc", ctypes.c_int),
+                ("scale", ctypes.c_float), ("layout", ctypes.c_int)]
+
+
 class ColsumJob(ctypes.Structure):
     """include/dmc.h dmc_colsum_job"""
     _fields_ = [("in_", ctypes.c_void_p), ("R", ctypes.c_int), ("C", ctypes.c_int), ("ld", ctypes.c_long),
@@ -77,6 +85,9 @@ def _load():
         "dmc_conv2d": (_c_int, [ctypes.POINTER(ConvDesc), _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_size, _c_p]),
         "dmc_conv2d_wgrad_workspace": (_c_size, [ctypes.POINTER(ConvDesc)]),
         "dmc_conv2d_wgrad": (_c_int, [ctypes.POINTER(ConvDesc), _c_p, _c_int, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p]),
+        "dmc_conv2d_wgrad_partial": (_c_int, [ctypes.POINTER(ConvDesc), _c_p, _c_int, _c_p, _c_p, _c_p, _c_p, _c_f,
+                                              ctypes.POINTER(WgradJob), _c_p]),
+        "dmc_wgrad_reduce_batch": (_c_int, [ctypes.POINTER(WgradJob), _c_int, _c_p]),
         "dmc_pack_weight": (_c_int, [_c_int, _c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p]),
         "dmc_pack_tiles": (_c_int, [ctypes.POINTER(PackJob), _c_int, _c_p, _c_int]),
         "dmc_pack_weights": (_c_int, [_c_p, _c_p, _c_int, _c_p]),

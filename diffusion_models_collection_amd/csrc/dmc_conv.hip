@@ -2294,7 +2294,8 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_halo2_kernel(ConvK a, const c
 //     no VALU in the fragment reads;
 //   * 128-pixel tiles whose halos (<= 224 pixels x 64 channels = 28 KB) are double-buffered: tile t+1's halo is
 //     DMA'd while tile t computes, every wait is a counted vmcnt of the wave's own issue order;
-//   * the partial sums leave as 16-byte stores into a [split][kk][co] slab (wgrad_reduce_t_kernel).
+//   * the two halves' partial sums are combined in LDS and leave as coalesced rows of a dw-shaped slab
+//     [split][Cout][Ctot][9] (dmc_wgrad_job layout 1: the reduction is a plain sum over the splits).
 // Block = (64-channel x chunk, 64 output channels, a range of 128-pixel tiles); 4 waves, each 64 co x 144 n (9 of
 // the 36 16-wide n tiles: the nine taps of the wave's 16-channel column segment). LDS: 2 x 28 KB + 3 x 8 KB =
 // 80 KB: two blocks per CU. Geometry: OW = 32 / 16 (R = 128 / OW rows of one image) or 8 (two whole 8x8 images).
@@ -2340,6 +2341,10 @@ DMC_DEV v4i tr2(const char* pa, const char* pb) {
   return r;
 }
 
+#ifndef WG_ABL
+#define WG_ABL 0   // timing ablations of wgrad3x3_pipe_kernel (scripts/build_variant.sh; results wrong): 1 no stage
+                   // barrier, 2 no x-fragment reads in the stream, 4 no DMA
+#endif
 template <int OW>
 __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const char* dy, int ld_dy, int dy_bytes,
                                                              float* slab, int tiles_per_split, int ncb, int nob,
@@ -2349,8 +2354,7 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
   constexpr int HPW = G::HPW, HB = G::HB, SPT = G::SPT, TILE = G::TILE;
   constexpr int DB = 64 * 128;                       // dy stage: 64 pixels x 64 co
   constexpr int HALF = 2 * HB + 3 * DB;              // LDS of one half: two halo buffers + the dy ring (<= 80 KB)
-  constexpr int RED = 4 * 36 * 64 * 16;              // the second half's partial sums at the end (144 KB)
-  constexpr int REDB = RED + 4 * 64 * 16;            // ... and its bias partials
+  constexpr int REDB = 64 * 580 * 4 + 4 * 64 * 16;   // the [64 co][580] combine tile at the end + bias partials
   __shared__ __attribute__((aligned(16))) char lds[2 * HALF > REDB ? 2 * HALF : REDB];
 
   const int lane = threadIdx.x & 63;
@@ -2484,15 +2488,15 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
       // counted waits of this wave's issue order (a stage issues halo(tl+1) at k = 0, then dy(st+2)):
       // k = 0 needs dy(st) and halo(tl), only dy(st+1) may be in flight; k = 1 needs dy(st), and halo(tl+1) and
       // dy(st+1) may be in flight
-      if (live) wait_vm_dyn((st + 1 < mst ? 2 : 0) + (k == 1 && tl + 1 < my_nt ? HPW : 0));
+      if (!(WG_ABL & 4) && live) wait_vm_dyn((st + 1 < mst ? 2 : 0) + (k == 1 && tl + 1 < my_nt ? HPW : 0));
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
+      if (!(WG_ABL & 1)) __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("" ::: "memory");
       if (!live) continue;
-      if (k == 0 && tl + 1 < my_nt) halo_issue(tl + 1);   // into the buffer tile tl-1 used (every wave is past it)
-      if (st + 2 < mst) dy_issue(st + 2);
+      if (!(WG_ABL & 4) && k == 0 && tl + 1 < my_nt) halo_issue(tl + 1);   // into the buffer tile tl-1 used (every wave is past it)
+      if (!(WG_ABL & 4) && st + 2 < mst) dy_issue(st + 2);
       // the stage's two k-steps as one stream of 18 fragment groups (k-step ks, tap u): the x fragment of group g + 2 is
       // read while group g's 4 MFMAs issue (three rotating fragment buffers), the dy fragments of both k-steps up front.
       // Each read's base register is made opaque right before it: equal address sums of different groups are not
@@ -2514,7 +2518,8 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
 #pragma unroll
       for (int g = 0; g < 18; ++g) {
         const int ks = g / 9, u = g - 9 * (g / 9);
-        if (g + 2 < 18) xf[(g + 2) % 3] = xfrag(g + 2);
+        if (!(WG_ABL & 2) && g + 2 < 18) xf[(g + 2) % 3] = xfrag(g + 2);
+        if ((WG_ABL & 2) && g == 0) xf[2] = xf[0];
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i][u] = mma16<T>(acc[i][u], fa[ks][i], xf[g % 3]);
         if (g + 2 < 18) {
@@ -2531,39 +2536,50 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
       }
     }
   }
-  // the two halves' partial sums combined in LDS (half 1 -> LDS, half 0 adds): one slab row per block instead of two
+  // the two halves' partial sums combined in LDS, in the reference layout [co][c][tap] (half 1 stores, half 0 adds),
+  // then the block's 64 rows of 64 x 9 consecutive floats leave as coalesced 16-byte stores into the split's
+  // dw-shaped slab [z][Cout][Ctot][9] (the reduction is then a plain sum over z)
   __syncthreads();   // every LDS read of the loop is done (and the DMA: every wave waited for all it issued)
-  v4f* const red = (v4f*)lds;
-  v4f* const redb = (v4f*)(lds + RED);   // the bias partials past the accumulators
+  float* const TL = (float*)lds;   // [64 co][TP]: row pitch TP = 580 floats (conflict-free fragment stores)
+  constexpr int TP = 580;
+  v4f* const redb = (v4f*)(lds + 64 * TP * 4);   // the bias partials past the tile
+  const int fr = lane & 15;
+  // lane (fr, fh) holds C[co = 16 i + 4 fh + e][c = 16 wq + fr] of tap u
+  auto tix = [&](int i, int u, int e) { return (i * 16 + fh * 4 + e) * TP + (wq * 16 + fr) * 9 + u; };
   if (hv == 1) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int u = 0; u < 9; ++u) red[(wq * 36 + i * 9 + u) * 64 + lane] = acc[i][u];
+      for (int u = 0; u < 9; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) TL[tix(i, u, e)] = acc[i][u][e];
     redb[wq * 64 + lane] = accb;
   }
   __syncthreads();
-  if (hv == 1) return;
-  accb += redb[wq * 64 + lane];
-  const int fr = lane & 15;
-  if (bias_on && fr == 0) {   // column 0 of the all-ones product: rows co = 4 fh + e of dy fragment wq
-    const int co = co0 + wq * 16 + fh * 4;
+  if (hv == 0) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (co + e < a.Cout) a.wgb[(size_t)zb * Cpad + co + e] = accb[e];
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int u = 0; u < 9; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) TL[tix(i, u, e)] += acc[i][u][e];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    accb += redb[wq * 64 + lane];
+    if (bias_on && fr == 0) {   // column 0 of the all-ones product: rows co = 4 fh + e of dy fragment wq
+      const int co = co0 + wq * 16 + fh * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (co + e < a.Cout) a.wgb[(size_t)zb * Cpad + co + e] = accb[e];
+    }
   }
-  // partial dW (half 0 + half 1) -> slab [z][kk][Cpad]: lane (fr, fh) holds C[co = 4 fh + e][kk = fr] of each tile:
-  // one 16-byte store; one tap at a time (the scheduling barrier keeps the LDS loads from all being hoisted ahead of
-  // the stores, which would need 144 more registers)
-  const int KK = 9 * a.Kc;
-  float* const out = slab + (size_t)zb * KK * Cpad;
-#pragma unroll
-  for (int u = 0; u < 9; ++u) {   // n tile (tap u, segment wq)
-    const int kk = u * a.Kc + c0 + wq * 16 + fr;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *(v4f*)(out + (size_t)kk * Cpad + co0 + i * 16 + fh * 4) = acc[i][u] + red[(wq * 36 + i * 9 + u) * 64 + lane];
-    __builtin_amdgcn_sched_barrier(0);
+  __syncthreads();
+  const int Ctot = a.C1 + a.C2;
+  float* const out = slab + ((size_t)zb * a.Cout + co0) * Ctot * 9 + (size_t)c0 * 9;
+  const int nrow = min(64, a.Cout - co0);
+  for (int idx = (int)threadIdx.x; idx < nrow * 144; idx += 512) {
+    const int r = idx / 144, qd = idx - r * 144;
+    *(v4f*)(out + (size_t)r * Ctot * 9 + qd * 4) = *(const v4f*)(TL + r * TP + qd * 4);
   }
 }
 
@@ -2573,6 +2589,10 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
 // straight into LDS (buffer_load ... lds; no register staging, no ds_write), 32-byte segments XOR-swizzled on the
 // source column (the dy image of wgrad3x3_halo_kernel), read transposed (ds_read_b64_tr_b16). STAGES-deep ring,
 // one barrier per stage. Requires M % SPX == 0 and whole-stage split ranges (the planner checks).
+#ifndef W1_SPX
+#define W1_SPX 64      // wgrad1x1_glds_kernel stage pixels / ring depth (variant builds: scripts/build_variant.sh)
+#define W1_STAGES 2
+#endif
 template <int SPX, int STAGES>
 __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char* dy, int ld_dy, int dy_bytes,
                                                             float* slab, int KK, int pix_per_split, int nci, int nco,
@@ -2583,6 +2603,7 @@ __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char*
   constexpr int PW = SPX / 16;             // DMA pieces (4 rows x 256 B) per wave per operand per stage
   constexpr int KS = SPX / 32;             // MFMA k-steps per stage
   __shared__ __attribute__((aligned(16))) char lds[STAGES * SB];
+  static_assert(STAGES * SB >= 128 * 128 * 4, "the epilogue's [128][128] fp32 tile reuses the ring");
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2671,84 +2692,190 @@ __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char*
       for (int e = 0; e < 4; ++e) a.wgb[(size_t)zb * Cpad + co + e] = accb[u][e];
     }
   }
-  // partial dW -> slab [z][KK][Cpad]: C[co = 4 fh + e][ci = fr], 16-byte stores
-  float* out = slab + (size_t)zb * KK * Cpad;
+  // partial dW -> dw-shaped slab [z][Cout][Ctot] through LDS (the ring is dead): lane (fr, fh) holds
+  // C[co = 4 fh + e][ci = fr] of each 16 x 16 tile; [128 co][128 ci] fp32 = 64 KB (2-way bank conflicts on the
+  // b32 stores cost nothing), then 128-float row segments leave as coalesced 16-byte stores
+  __syncthreads();
+  float* const TL = (float*)lds;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int k = ci0 + wn * 64 + j * 16 + fr;
-    if (k >= KK) continue;
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *(v4f*)(out + (size_t)k * Cpad + co0 + wm * 64 + i * 16 + fh * 4) = acc[i][j];
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) TL[(wm * 64 + i * 16 + fh * 4 + e) * 128 + wn * 64 + j * 16 + fr] = acc[i][j][e];
+  __syncthreads();
+  const int Ctot = a.C1 + a.C2;
+  const int nrow = min(128, a.Cout - co0), ncol = min(128, Ctot - ci0);   // ncol % 4 == 0 (Ctot % 8: the planner)
+  float* const out = slab + ((size_t)zb * a.Cout + co0) * Ctot + ci0;
+  for (int idx = (int)threadIdx.x; idx < nrow * 32; idx += 256) {
+    const int r = idx >> 5, qd = idx & 31;
+    if (qd * 4 < ncol) *(v4f*)(out + (size_t)r * Ctot + qd * 4) = *(const v4f*)(TL + r * 128 + qd * 4);
   }
 }
 
 // Sum of the per-split fp32 slabs [split][KK][Cpad] into the reference-layout weight gradient dw[co][c][t] (x scale),
-// plus the bias gradient from the per-split bias slab (one wave per channel, blocks past wblocks; lanes take z = lane,
-// lane + 64, ..., fixed xor tree: deterministic). A block owns 256 / G output quads (4 consecutive co of one kk each)
-// and G groups of its threads take contiguous ranges of the splits (G = 4 from 64 splits, 2 from 32; 16-byte slab
-// loads, up to 16 in flight per lane); each group adds its splits in ascending order, then group 0 adds the other
-// groups' sums in group order through LDS -- a fixed summation order, so the result is bitwise reproducible.
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slab, int splits, int KK, int Cpad, int Cout,
-                                                           int Ctot, int ntaps, int Kc, float scale, float* dw,
-                                                           const float* bslab, float* dbias, int wblocks) {
-  if ((int)blockIdx.x >= wblocks) {
-    const int co = ((int)blockIdx.x - wblocks) * (blockDim.x / 64) + (int)(threadIdx.x >> 6);
+// plus the bias gradient from the per-split bias slab (one wave per channel, blocks past the weight blocks; lanes take
+// z = lane, lane + 64, ..., fixed xor tree: deterministic). A 1024-thread block owns a tile of 16 output channels x
+// CT input channels x all ntaps taps (CT = 64 / ntaps: 7 for 3x3, 64 for 1x1) and its 4 groups of 256 threads take
+// contiguous quarters of the splits: a thread loads the 16-byte quads (4 co) of one slab row kk = t * Kc + c, adds its
+// splits in ascending order, group 0 adds the other groups' sums in group order (bitwise reproducible), and the tile
+// goes out through LDS as 16 contiguous dw rows of CT * ntaps floats (one quad per thread, scattered 4-byte stores
+// along co, ran the reduction at half the rate).
+// One launch serves up to kWgJobs reductions (dmc_wgrad_reduce_batch): the weight gradients a backward segment left
+// behind (dmc_conv2d_wgrad_partial) in one grid instead of one small launch after each weight-gradient kernel.
+constexpr int kWgJobs = 32;
+constexpr int kWgCoT = 16;
+struct WgBatch {
+  int njobs;
+  int first[kWgJobs + 1];   // first block of each job
+  int wblocks[kWgJobs];     // weight blocks of each job (bias blocks follow)
+  dmc_wgrad_job j[kWgJobs];
+};
+// layout-1 blocks: G groups over the splits (4 from 64 splits, 2 from 32, else 1) of 1024 / G threads, a thread
+// summing QPT quads (2 below 16 splits): >= 16 loads in flight per thread where the split count allows
+__host__ __device__ constexpr int wg_groups(int splits) { return splits >= 64 ? 4 : splits >= 32 ? 2 : 1; }
+__host__ __device__ constexpr int wg_qpt(int splits) { return splits < 16 ? 2 : 1; }
+inline int wg_reduce_blocks(const dmc_wgrad_job& J) {
+  if (J.layout == 1)
+    return (int)dmc::cdiv((long)J.Cout * J.Ctot * J.ntaps / 4, (long)(1024 / wg_groups(J.splits)) * wg_qpt(J.splits));
+  const int CT = 64 / J.ntaps;
+  return dmc::cdiv(J.Cout, kWgCoT) * dmc::cdiv(J.Ctot, CT);
+}
+
+// Sum over the splits of one 16-byte quad per thread, the 4 thread groups of the block taking contiguous quarters of
+// the splits (ascending inside a group; group 0 adds the others in group order). Returns the total in group 0.
+DMC_DEV v4f wg_split_sum(const v4f* p, size_t zs, int splits, bool on, v4f (*part)[256]) {
+  const int g = (int)threadIdx.x >> 8, lt = (int)threadIdx.x & 255;
+  const int zpg = (splits + 3) >> 2;
+  const int zb = min(splits, g * zpg), ze = min(splits, zb + zpg);
+  v4f s = {0.f, 0.f, 0.f, 0.f};
+  if (on) {
+    int z = zb;
+    for (; z + 16 <= ze; z += 16) {
+      v4f v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = p[(size_t)(z + u) * zs];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += v[u];
+    }
+    if (z + 8 <= ze) {
+      v4f v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(z + u) * zs];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+      z += 8;
+    }
+    for (; z < ze; ++z) s += p[(size_t)z * zs];
+  }
+  if (g) part[g - 1][lt] = s;
+  __syncthreads();
+  if (g == 0) {
+    s += part[0][lt];
+    s += part[1][lt];
+    s += part[2][lt];
+  }
+  return s;
+}
+
+__global__ __launch_bounds__(1024) void wgrad_reduce_batch_kernel(WgBatch b) {
+  const int bid = (int)blockIdx.x;
+  int jb = 0;
+  while (jb + 1 < b.njobs && bid >= b.first[jb + 1]) ++jb;
+  const dmc_wgrad_job& J = b.j[jb];
+  const int blk = bid - b.first[jb];
+  const int splits = J.splits, Cpad = J.Cpad, Cout = J.Cout;
+  const int tid = (int)threadIdx.x;
+  if (blk >= b.wblocks[jb]) {
+    const int co = (blk - b.wblocks[jb]) * 16 + (tid >> 6);
     if (co >= Cout) return;
     float s = 0.f;
-    for (int z = threadIdx.x & 63; z < splits; z += 64) s += bslab[(size_t)z * Cpad + co];
+    for (int z = tid & 63; z < splits; z += 64) s += J.bslab[(size_t)z * Cpad + co];
     s = wave_sum(s);
-    if ((threadIdx.x & 63) == 0) dbias[co] = s * scale;
+    if ((tid & 63) == 0) J.dbias[co] = s * J.scale;
     return;
   }
-  __shared__ v4f part[192];
-  const int cq = (Cout + 3) / 4, total4 = KK * cq;
-  const size_t zs = (size_t)KK * Cpad / 4;
-  const v4f* s4 = (const v4f*)slab;
-  // G split groups of 4 / G waves (>= 16 splits per group where there are that many): QB quads per block
-  const int G = splits >= 64 ? 4 : splits >= 32 ? 2 : 1, QB = 256 / G;
-  const int g = (int)threadIdx.x / QB, lane = (int)threadIdx.x - g * QB;
-  const int zpg = (splits + G - 1) / G;
-  const int zb = min(splits, g * zpg), ze = min(splits, zb + zpg);
-  for (int q0 = blockIdx.x * QB; q0 < total4; q0 += wblocks * QB) {
-    const int q = q0 + lane;
-    const bool on = q < total4;
-    const int k = on ? q / cq : 0, co = on ? (q - k * cq) * 4 : 0;
-    const size_t o = ((size_t)k * Cpad + co) / 4;
-    v4f s = {0.f, 0.f, 0.f, 0.f};
-    if (on) {
-      int z = zb;
-      for (; z + 16 <= ze; z += 16) {
-        v4f v[16];
+  __shared__ v4f part[3][256];
+  __shared__ float tile[kWgCoT][65];
+  if (J.layout == 1) {   // [split][Cout][Ctot][ntaps]: the slab rows are dw's own layout -- a plain sum
+    const long nq = (long)Cout * J.Ctot * J.ntaps / 4;
+    const int G = wg_groups(splits), TPG = 1024 / G, QPT = wg_qpt(splits);
+    const int g = tid / TPG, lt = tid - g * TPG;
+    const int zpg = (splits + G - 1) / G;
+    const int zb = min(splits, g * zpg), ze = min(splits, zb + zpg);
+    const v4f* p = (const v4f*)J.slab;
+    v4f* pf = (v4f*)part;   // [G - 1][TPG * QPT]
+    long q[2];
+    bool on[2];
+    v4f s[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = s4[(size_t)(z + u) * zs + o];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) s += v[u];
-      }
-      if (z + 8 <= ze) {
-        v4f v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = s4[(size_t)(z + u) * zs + o];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) s += v[u];
-        z += 8;
-      }
-      for (; z < ze; ++z) s += s4[(size_t)z * zs + o];
+    for (int u = 0; u < 2; ++u) {
+      q[u] = ((long)blk * QPT + u) * TPG + lt;
+      on[u] = u < QPT && q[u] < nq;
     }
-    if (g) part[(g - 1) * QB + lane] = s;
-    __syncthreads();
-    if (g == 0 && on) {
-      for (int u = 0; u + 1 < G; ++u) s += part[u * QB + lane];
-      const int t = k / Kc, c = k - t * Kc;
-      if (c < Ctot) {
-        float* d = dw + ((size_t)co * Ctot + c) * ntaps + t;
-        const size_t cs = (size_t)Ctot * ntaps;
+    int z = zb;
+    for (; z + 8 <= ze; z += 8) {
+      v4f v[2][8];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (co + e < Cout) d[e * cs] = s[e] * scale;
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int w = 0; w < 8; ++w)
+          if (on[u]) v[u][w] = p[(size_t)(z + w) * nq + q[u]];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int w = 0; w < 8; ++w)
+          if (on[u]) s[u] += v[u][w];
+    }
+    for (; z < ze; ++z)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (on[u]) s[u] += p[(size_t)z * nq + q[u]];
+    if (G > 1) {
+      if (g) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          if (u < QPT) pf[(g - 1) * TPG * QPT + u * TPG + lt] = s[u];
+      }
+      __syncthreads();
+      if (g) return;
+      for (int k = 1; k < G; ++k)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          if (u < QPT) s[u] += pf[(k - 1) * TPG * QPT + u * TPG + lt];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (!on[u]) continue;
+      float* d = J.dw + q[u] * 4;
+      if (((uintptr_t)J.dw & 15) == 0) {
+        *(v4f*)d = s[u] * J.scale;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d[e] = s[u][e] * J.scale;
       }
     }
-    __syncthreads();
+    return;
   }
+  const int ntaps = J.ntaps, Kc = J.Kc, Ctot = J.Ctot, CT = 64 / ntaps;
+  const int nct = (Ctot + CT - 1) / CT;
+  const int cot = blk / nct, c0 = (blk - cot * nct) * CT, co0 = cot * kWgCoT;
+  const int g = tid >> 8, lt = tid & 255, qi = lt & 3, j = lt >> 2;
+  const int cl = j / ntaps, t = j - cl * ntaps;
+  const int co = co0 + 4 * qi;
+  const bool on = cl < CT && c0 + cl < Ctot && co < Cout;
+  const size_t zs = (size_t)J.KK * Cpad / 4;
+  const v4f s = wg_split_sum((const v4f*)J.slab + (on ? ((size_t)(t * Kc + c0 + cl) * Cpad + co) / 4 : 0), zs, splits,
+                             on, part);
+  if (g == 0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tile[4 * qi + e][j] = s[e] * J.scale;
+  }
+  __syncthreads();
+  // row r = co0 + r of dw: the tile's CT * ntaps floats are contiguous ((co * Ctot + c0) * ntaps + j)
+  const int r = tid >> 6, f = tid & 63;
+  const int nf = min(CT, Ctot - c0) * ntaps;
+  if (co0 + r < Cout && f < nf) J.dw[((size_t)(co0 + r) * Ctot + c0) * ntaps + f] = tile[r][f];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -3376,8 +3503,10 @@ extern "C" size_t dmc_conv2d_wgrad_workspace(const dmc_conv_desc* d) {
   return (size_t)splits * (KK + 1) * Cpad * sizeof(float);   // + the bias partials [splits][Cpad]
 }
 
-extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_dy, const void* x1, const void* x2,
-                                void* workspace, float* dw, float scale, void* stream) {
+// Launches the weight-gradient kernel of `d` (partial sums into the workspace slab) and describes the reduction
+// that finishes it in *job (dmc_conv2d_wgrad runs it at once, dmc_conv2d_wgrad_partial leaves it to the caller).
+static int wgrad_partial(const dmc_conv_desc* d, const void* dy, int ld_dy, const void* x1, const void* x2,
+                         void* workspace, float* dw, float scale, dmc_wgrad_job* job, void* stream) {
   ConvK k;
   if (fill_convk(d, x1, x2, nullptr, nullptr, nullptr, k)) return 1;
   const int epc = d->dtype == DMC_F32 ? 4 : 8;
@@ -3397,7 +3526,7 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   // SPX-pixel stages, never more than wgrad_splits() counted (the workspace query's bound)
   const bool direct = d->ntaps == 1 && k.stride == 1 && k.mode == DMC_MODE_NORMAL && k.tdy0 == 0 && k.tdx0 == 0 &&
                       k.H == k.OH && k.W == k.OW && k.prologue == DMC_PRO_NONE;
-  constexpr int spx = 64;
+  constexpr int spx = W1_SPX;
   const bool w1x1 = !halo && d->dtype == DMC_BF16 && direct && k.M % spx == 0 && d->Cout % 8 == 0 &&
                     ld_dy % 8 == 0 && k.C1 % 8 == 0 && k.C2 % 8 == 0 && (k.C2 == 0 || k.C1 % 128 == 0) &&
                     k.ld1 % 8 == 0 && (k.C2 == 0 || k.ld2 % 8 == 0) && k.x1_bytes > 0 && (k.C2 == 0 || k.x2_bytes > 0) &&
@@ -3440,21 +3569,64 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
     g.z = splits;
     const dim3 g1(g.x * g.y * g.z);
     const int xcd = dmc::opt(dmc::OPT_NO_XCD) ? 0 : 1;
-    wgrad1x1_glds_kernel<64, 2><<<g1, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1,
+    wgrad1x1_glds_kernel<W1_SPX, W1_STAGES><<<g1, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1,
                                                   (int)g.x, (int)g.y, xcd);
   } else if (d->dtype == DMC_F32)
     conv_wgrad_kernel<float><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (float*)workspace, KK, pps);
   else
     conv_wgrad_kernel<bf16_t><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (float*)workspace, KK, pps);
   if (dmc::check_launch("dmc_conv2d_wgrad")) return 2;
-  const int Ctot = d->C1 + d->C2;
-  const long total = (long)KK * ((d->Cout + 3) / 4);   // output quads, 256 / G per block (wgrad_reduce_kernel)
-  const int qb = splits >= 64 ? 64 : splits >= 32 ? 128 : 256;
-  const int blocks = (int)((total + qb - 1) / qb < 16384 ? (total + qb - 1) / qb : 16384);
-  const int bblocks = d->wg_bias ? dmc::cdiv(d->Cout, 4) : 0;   // one wave per bias channel
-  wgrad_reduce_kernel<<<blocks + bblocks, 256, 0, s>>>((const float*)workspace, splits, KK, (int)g.y * 128, d->Cout,
-                                                       Ctot, d->ntaps, d->Kc, scale, dw, bslab, d->wg_bias, blocks);
-  return dmc::check_launch("dmc_conv2d_wgrad reduce");
+  job->slab = (const float*)workspace;
+  job->bslab = bslab;
+  job->dw = dw;
+  job->dbias = d->wg_bias;
+  job->splits = splits;
+  job->KK = KK;
+  job->Cpad = (int)g.y * 128;
+  job->Cout = d->Cout;
+  job->Ctot = d->C1 + d->C2;
+  job->ntaps = d->ntaps;
+  job->Kc = d->Kc;
+  job->scale = scale;
+  job->layout = (pp.ow || w1x1) ? 1 : 0;   // the pipelined 3x3 and the 1x1 kernels write dw-shaped slabs
+  return 0;
+}
+
+extern "C" int dmc_conv2d_wgrad_partial(const dmc_conv_desc* d, const void* dy, int ld_dy, const void* x1,
+                                        const void* x2, void* workspace, float* dw, float scale, dmc_wgrad_job* job,
+                                        void* stream) {
+  DMC_REQUIRE(job != nullptr, "wgrad_partial: job");
+  return wgrad_partial(d, dy, ld_dy, x1, x2, workspace, dw, scale, job, stream);
+}
+
+extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_dy, const void* x1, const void* x2,
+                                void* workspace, float* dw, float scale, void* stream) {
+  dmc_wgrad_job job;
+  const int r = wgrad_partial(d, dy, ld_dy, x1, x2, workspace, dw, scale, &job, stream);
+  return r ? r : dmc_wgrad_reduce_batch(&job, 1, stream);
+}
+
+extern "C" int dmc_wgrad_reduce_batch(const dmc_wgrad_job* jobs, int njobs, void* stream) {
+  DMC_REQUIRE(njobs >= 0 && njobs <= kWgJobs, "wgrad_reduce_batch: %d jobs (at most %d)", njobs, kWgJobs);
+  if (njobs == 0) return 0;
+  WgBatch b;
+  b.njobs = njobs;
+  long nb = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const dmc_wgrad_job& J = jobs[i];
+    DMC_REQUIRE(J.slab && J.dw && J.splits > 0 && J.KK > 0 && J.Cout > 0 && J.Cpad >= J.Cout && J.Kc > 0 &&
+                    J.ntaps > 0 && (J.dbias == nullptr || J.bslab != nullptr),
+                "wgrad_reduce_batch: job %d", i);
+    DMC_REQUIRE(J.ntaps <= 64 && J.KK >= J.ntaps * J.Ctot && J.Kc >= J.Ctot, "wgrad_reduce_batch: job %d taps", i);
+    b.first[i] = (int)nb;
+    b.wblocks[i] = wg_reduce_blocks(J);
+    b.j[i] = J;
+    nb += b.wblocks[i] + (J.dbias ? dmc::cdiv(J.Cout, 16) : 0);   // + one wave per bias channel
+  }
+  DMC_REQUIRE(nb < (1L << 30), "wgrad_reduce_batch: %ld blocks", nb);
+  b.first[njobs] = (int)nb;
+  wgrad_reduce_batch_kernel<<<(int)nb, 1024, 0, dmc::as_stream(stream)>>>(b);
+  return dmc::check_launch("dmc_wgrad_reduce_batch");
 }
 
 extern "C" int dmc_pack_weight(int pack_mode, int dtype, const float* w, int Cout, int Cin, int kh, int kw, int Kc,

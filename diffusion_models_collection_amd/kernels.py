@@ -162,11 +162,65 @@ def conv_halo_prologue(d):
     return bool(LIB.dmc_conv_halo_prologue(ctypes.byref(d)))
 
 
-def wgrad(d, dy, ld_dy, x1, x2, dw, scale=1.0, dbias=None):
-    """dmc_conv2d_wgrad: dw (and with dbias the bias gradient, the pixel sums of dy) from one pass over dy."""
+class WgradDefer:
+    """Weight-gradient reductions deferred to one dmc_wgrad_reduce_batch per backward segment (wgrad(defer=...)).
+
+    Each deferred call's fp32 partial sums get their own slice of a grow-only device arena and stay there until
+    flush() reduces every pending job (<= 32 per launch) and recycles the arena. When a segment needs more than
+    the arena holds, the pending jobs are flushed early and a larger arena is allocated for the following
+    segments; every arena ever allocated stays referenced (a captured HIP graph keeps using its addresses)."""
+
+    def __init__(self):
+        self.arenas = []
+        self.buf = None
+        self.off = 0
+        self.demand = 0     # bytes the current segment asked for so far (sizes the next arena)
+        self.jobs = []
+
+    def alloc(self, nbytes, device):
+        nbytes = (max(int(nbytes), 256) + 255) // 256 * 256
+        self.demand += nbytes
+        if self.buf is None or self.buf.device != device or self.off + nbytes > self.buf.numel():
+            self.flush()
+            if self.buf is None or self.buf.device != device or nbytes > self.buf.numel():
+                self.buf = torch.empty(max(nbytes, int(self.demand * 1.25)), dtype=torch.uint8, device=device)
+                self.arenas.append(self.buf)
+        ws = self.buf[self.off:self.off + nbytes]
+        self.off += nbytes
+        return ws
+
+    def flush(self):
+        for k in range(0, len(self.jobs), 32):
+            chunk = self.jobs[k:k + 32]
+            arr = (L.WgradJob * len(chunk))(*chunk)
+            check(LIB.dmc_wgrad_reduce_batch(arr, len(chunk), L.stream()), "dmc_wgrad_reduce_batch")
+        self.jobs = []
+        self.off = 0
+
+    def end_segment(self):
+        """flush() and, if this segment outgrew the arena, size the next one for it."""
+        self.flush()
+        if self.buf is not None and self.demand > self.buf.numel():
+            self.buf = torch.empty(int(self.demand * 1.25), dtype=torch.uint8, device=self.buf.device)
+            self.arenas.append(self.buf)
+        self.demand = 0
+
+
+def wgrad(d, dy, ld_dy, x1, x2, dw, scale=1.0, dbias=None, defer=None):
+    """dmc_conv2d_wgrad: dw (and with dbias the bias gradient, the pixel sums of dy) from one pass over dy. With
+    defer (a WgradDefer) only the partial-sum kernel runs now (dmc_conv2d_wgrad_partial); the reduction joins
+    defer's batch."""
     d.wg_bias = ptr(dbias)
     d._keep_wgb = dbias
     nbytes = LIB.dmc_conv2d_wgrad_workspace(ctypes.byref(d))
+    if defer is not None:
+        ws = defer.alloc(nbytes, dy.device)
+        job = L.WgradJob()
+        PROF.wrap("wgrad", d, lambda: check(LIB.dmc_conv2d_wgrad_partial(
+            ctypes.byref(d), ptr(dy), ld_dy, ptr(x1), ptr(x2), ptr(ws), ptr(dw), scale, ctypes.byref(job), L.stream()),
+            "dmc_conv2d_wgrad_partial"))
+        defer.jobs.append(job)
+        return
     ws = SCRATCH.get(nbytes, dy.device)
     PROF.wrap("wgrad", d, lambda: check(LIB.dmc_conv2d_wgrad(ctypes.byref(d), ptr(dy), ld_dy, ptr(x1), ptr(x2), ptr(ws),
                                                              ptr(dw), scale, L.stream()), "dmc_conv2d_wgrad"))

@@ -45,6 +45,9 @@ _GN_PARTIALS = os.environ.get("DMC_GN_PARTIALS", "1") not in ("", "0")
 # The GroupNorm backward's parameter column sums deferred to one dmc_colsum_batch per gradient segment (A/B switch
 # DMC_GN_DEFER=0: one finish launch per GroupNorm)
 _GN_DEFER = os.environ.get("DMC_GN_DEFER", "1") not in ("", "0")
+# The weight-gradient slab reductions deferred to one dmc_wgrad_reduce_batch per gradient segment (A/B switch
+# DMC_WG_DEFER=0: one reduce launch after each weight-gradient kernel)
+_WG_DEFER = os.environ.get("DMC_WG_DEFER", "1") not in ("", "0")
 
 
 def _seed_from_torch():
@@ -187,7 +190,8 @@ class ExecCore:
                         OH, OW, Cout, taps, mode, stride)
         if pro is not None:
             K.set_prologue(d, pro[0], pro[1], pro[2], C1 + C2, drop, C1 + C2)
-        K.wgrad(d, dy, ld_dy, a.t, srcs[1].t if len(srcs) > 1 else None, dw, self.training_grad_scale, dbias=dbias)
+        K.wgrad(d, dy, ld_dy, a.t, srcs[1].t if len(srcs) > 1 else None, dw, self.training_grad_scale, dbias=dbias,
+                defer=getattr(self, "_wg_defer", None))
 
     def _new(self, N, H, W, C, dtype=None):
         return Act(torch.empty(N, H, W, C, dtype=dtype or self.dt, device=self.device), H, W, C)
@@ -563,6 +567,10 @@ class UNetExecutor(ExecCore):
         dx = None
         hook = self.grad_hook
         self._gn_defer = [] if _GN_DEFER else None
+        if _WG_DEFER:
+            if getattr(self, "_wg_arena", None) is None:
+                self._wg_arena = K.WgradDefer()
+            self._wg_defer = self._wg_arena
         if hook is not None:
             order = sorted(range(len(self.params)), key=lambda i: self.goff[i])
             final = [False] * len(self.params)
@@ -588,10 +596,11 @@ class UNetExecutor(ExecCore):
                     cursor += 1
                 hi = self.goff[order[cursor]] if cursor < len(order) else self.gtotal
                 if getattr(hook, "wants", None) is None or hook.wants(hi, last):
-                    self._flush_gn()       # the deferred GroupNorm parameter sums of that prefix
+                    self._flush_gn()       # the deferred GroupNorm parameter sums and weight-gradient reductions
                 hook(flat, hi, last)
         self._flush_gn()
         self._gn_defer = None
+        self._wg_defer = None
         self.daddvec = None
         grads = [self._gview(flat, p) for p in self.params]
         return dx, grads
@@ -761,6 +770,8 @@ class UNetExecutor(ExecCore):
     def _flush_gn(self):
         if getattr(self, "_gn_defer", None):
             K.colsum_batch(self._gn_defer)
+        if getattr(self, "_wg_defer", None) is not None:
+            self._wg_defer.end_segment()
 
     def _scatter_add_concat(self, tmp, b1, acc1, b2, acc2, C1, C2):
         t1 = tmp[..., :C1].contiguous()

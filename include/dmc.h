@@ -117,6 +117,24 @@ int dmc_conv2d(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
 size_t dmc_conv2d_wgrad_workspace(const dmc_conv_desc* d);
 int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_dy, const void* x1,
                      const void* x2, void* workspace, float* dw, float scale, void* stream);
+/* The same weight gradient in two parts: dmc_conv2d_wgrad_partial launches only the kernel that writes the per-split
+ * fp32 partial sums into `workspace` and fills *job (a HOST struct) with the reduction that finishes dw (and
+ * d->wg_bias); dmc_wgrad_reduce_batch then runs up to 32 such reductions in ONE launch (jobs: HOST array; each
+ * job's workspace must stay untouched until it ran). Bitwise what dmc_conv2d_wgrad computes -- which is exactly
+ * partial + a one-job batch. The executor batches a backward segment's weight gradients this way (the per-layer
+ * reduce launches of the CIFAR step: 90 -> 3). */
+typedef struct dmc_wgrad_job {
+  const float* slab;         /* layout 0: [splits][KK][Cpad] partial sums; layout 1: [splits][Cout][Ctot][ntaps] */
+  const float* bslab;        /* [splits][Cpad] bias partials (NULL: no bias gradient) */
+  float* dw;                 /* fp32 [Cout][Ctot][ntaps] */
+  float* dbias;              /* fp32 [Cout] or NULL */
+  int splits, KK, Cpad, Cout, Ctot, ntaps, Kc;
+  float scale;
+  int layout;                /* the slab layout the weight-gradient kernel wrote (library-internal choice) */
+} dmc_wgrad_job;
+int dmc_conv2d_wgrad_partial(const dmc_conv_desc* d, const void* dy, int ld_dy, const void* x1, const void* x2,
+                             void* workspace, float* dw, float scale, dmc_wgrad_job* job, void* stream);
+int dmc_wgrad_reduce_batch(const dmc_wgrad_job* jobs, int njobs, void* stream);
 
 /* Repack an fp32 nn.Conv2d / nn.Linear weight [Cout][Cin][kh][kw] into the kernel layout:
  * FWD [Cout][t][Kc], DGRAD [Cin][t][Kc>=Cout], UPDGRAD [Cin][16][Kc] (nearest-x2 + 3x3 folded

@@ -1062,6 +1062,50 @@ def test_wgrad_small_maps_and_taps(case):
     assert rel_err(db.cpu(), g.float().sum((0, 2, 3))) < 1e-5
 
 
+def test_wgrad_partial_reduce_batch_bitwise():
+    """dmc_conv2d_wgrad_partial + ONE dmc_wgrad_reduce_batch over the jobs of several layers (the pipelined 3x3 kernel
+    with its bias, a two-source 1x1, the generic kernel on a stride-2 conv, an fp32 Linear-shaped 1x1), partial sums in
+    slices of one arena (K.WgradDefer), equal dmc_conv2d_wgrad of each layer bitwise; an arena too small for the
+    segment flushes early and grows, with the same results."""
+    from diffusion_models_collection_amd import _lib as L, kernels as K
+    gen = torch.Generator().manual_seed(11)
+    bf, f32 = torch.bfloat16, torch.float32
+    # (dtype, N, H, W, C1, C2, Cout, taps, stride, bias)
+    cases = [(bf, 16, 32, 32, 128, 0, 128, K.TAPS3, 1, True), (bf, 8, 8, 8, 256, 128, 256, K.TAPS1, 1, True),
+             (bf, 4, 16, 16, 128, 0, 128, K.TAPS3, 2, False), (f32, 128, 1, 1, 512, 0, 256, K.TAPS1, 1, True)]
+    layers = []
+    for dt, N, H, W, C1, C2, Cout, taps, stride, bias in cases:
+        OH, OW = (H - 1) // stride + 1, (W - 1) // stride + 1
+        x1 = torch.randn(N, H, W, C1, generator=gen).to(dt).to(DEV)
+        x2 = torch.randn(N, H, W, C2, generator=gen).to(dt).to(DEV) if C2 else None
+        dy = torch.randn(N, OH, OW, Cout, generator=gen).to(dt).to(DEV)
+        kh = 3 if len(taps) == 9 else 1
+        d = K.make_desc(dt, N, H, W, C1, C2, C1, C2, L.kc_for(C1 + C2, dt), OH, OW, Cout, taps, L.MODE_NORMAL, stride)
+        layers.append((d, dy, Cout, x1, x2, (Cout, C1 + C2, kh, kh), bias))
+
+    def run(defer):
+        outs = []
+        for d, dy, Cout, x1, x2, wshape, bias in layers:
+            dw = torch.full(wshape, float("nan"), device=DEV)
+            db = torch.full((Cout,), float("nan"), device=DEV) if bias else None
+            K.wgrad(d, dy, Cout, x1, x2, dw, 0.5, dbias=db, defer=defer)
+            outs.append((dw, db))
+        if defer is not None:
+            defer.end_segment()
+        torch.cuda.synchronize()
+        return outs
+
+    ref = run(None)
+    small = K.WgradDefer()
+    small.buf = torch.empty(1 << 20, dtype=torch.uint8, device=DEV)   # forces early flushes and a regrow
+    for defer in (K.WgradDefer(), small, small):
+        got = run(defer)
+        for (a, ab), (b, bb) in zip(ref, got):
+            assert torch.equal(a, b)
+            assert ab is None or torch.equal(ab, bb)
+    assert small.buf.numel() > (1 << 20)
+
+
 @pytest.mark.parametrize("shape", [(128, 32, 32, 128, 0, 128), (64, 32, 32, 128, 128, 128), (128, 16, 16, 256, 0, 256),
                                    (32, 16, 16, 256, 128, 256), (128, 8, 8, 256, 256, 256), (6, 8, 8, 128, 64, 192),
                                    (3, 16, 16, 128, 0, 200), (128, 4, 4, 256, 0, 256), (32, 4, 4, 256, 256, 256),
