@@ -2398,25 +2398,22 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
     dma_pieces<2>(dy, dy_bytes, base + 2 * HB + (st % 3) * DB + wq * 2 * 1024, od, off, 0, 2);
   };
   auto halo_issue = [&](int tl) {   // tile tl of this half -> halo buffer tl & 1
-    const int m0 = (t_begin + tl) * TILE;
-    const int n_first = m0 / a.OHW;
-    const int r0 = (m0 - n_first * a.OHW) / OW;
-    // the per-piece geometry is tile-invariant, but keeping it across the tile loop costs ~30 registers: recompute
+    const int m0 = (t_begin + tl) * TILE;   // first pixel of the tile (a row start: W == OW)
+    const int r0 = (m0 % a.OHW) / OW;       // its image row (0 for the small maps' whole images)
+    // the per-piece geometry is tile-invariant, but keeping it across the tile loop costs ~30 registers: recompute,
+    // branch-free with compile-time divisors (halo pixel h -> image, halo row, halo column)
     int lv = lane;
     asm volatile("" : "+v"(lv));
     unsigned hx[HPW];
 #pragma unroll
     for (int p = 0; p < HPW; ++p) {
       const int h = (wq * HPW + p) * 8 + (lv >> 3);
-      hx[p] = kOOB;
-      if (h < G::NPIX) {
-        const int img = h / G::SEGP, hrem = h - img * G::SEGP;
-        const int hr = hrem / G::HW, hc = hrem - hr * G::HW;
-        const int iy = r0 + hr - 1, ix = hc - 1;
-        const int lc = ((((lv & 7) >> 1) ^ swz_h<OW>(h)) << 1) | (lv & 1);
-        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-          hx[p] = ((unsigned)(((n_first + img) * a.H + iy) * a.W + ix) * ldx + cs + lc * 8) * 2u;
-      }
+      const int img = h / G::SEGP, hrem = h - img * G::SEGP;
+      const int hr = hrem / G::HW, hc = hrem - hr * G::HW;
+      const int lc = ((((lv & 7) >> 1) ^ swz_h<OW>(h)) << 1) | (lv & 1);
+      const bool ok = h < G::NPIX && (unsigned)(r0 + hr - 1) < (unsigned)a.H && (unsigned)(hc - 1) < (unsigned)OW;
+      const int pix = m0 + img * OW * OW + (hr - 1) * OW + (hc - 1);   // img > 0 only for whole OW x OW images
+      hx[p] = ok ? ((unsigned)pix * (unsigned)ldx + (unsigned)(cs + lc * 8)) * 2u : kOOB;
     }
     dma_pieces<HPW>(xsrc, xbytes, base + (tl & 1) * HB + wq * HPW * 1024, hx, 0u, 0, HPW);
   };
