@@ -3455,7 +3455,7 @@ WgHaloPlan wgrad_halo_plan(const dmc_conv_desc* d) {
 
 // Pipelined weight-gradient plan (wgrad3x3_pipe_kernel): bf16 3x3 stride-1 convs on halo2_plan's 128-pixel geometry
 // with 32- or 16-wide maps (rows of one image) or 8x8 maps (two images per tile), 64-aligned channel sources, no
-// prologue, Cout % 8 == 0. Returns OW (the template argument) or 0; splits the tiles so that ~DMC_WG_HALO_TARGET x 2
+// prologue, ld_dy % 8 == 0. Returns OW (the template argument) or 0; splits the tiles so that ~DMC_WG_HALO_TARGET x 2
 // blocks of 64 x 64 run.
 struct WgPipePlan {
   int ow, splits, tps;
@@ -3466,7 +3466,9 @@ WgPipePlan wgrad_pipe_plan(const dmc_conv_desc* d, int ld_dy) {
   ConvK k;
   if (fill_convk(d, nullptr, nullptr, nullptr, nullptr, nullptr, k)) return p;
   if (k.C1 % 64 || k.C2 % 64 || k.Kc != k.C1 + k.C2 || k.x1_bytes == 0 || (k.C2 && k.x2_bytes == 0)) return p;
-  if (k.prologue != DMC_PRO_NONE || k.Cout % 8 || ld_dy % 8) return p;
+  // any Cout with an 8-aligned dy pitch: the dy DMA reads whole 16-byte chunks, so the pitch padding of a narrow dy
+  // (the output conv's 3 channels in a pitch of 8) lands in accumulator rows co >= Cout, which are never stored
+  if (k.prologue != DMC_PRO_NONE || ld_dy % 8) return p;
   if ((size_t)k.M * ld_dy * 2 >= 0x7fff0000u) return p;
   if (k.mode != DMC_MODE_NORMAL || k.stride != 1 || k.ntaps != 9 || k.tkw != 3 || k.OH != k.H || k.OW != k.W) return p;
   if (k.tdy0 != -1 || k.tsy != 1 || k.tdx0 != -1 || k.tsx != 1) return p;   // the forward taps (weight gradient)

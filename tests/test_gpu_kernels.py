@@ -1062,6 +1062,29 @@ def test_wgrad_small_maps_and_taps(case):
     assert rel_err(db.cpu(), g.float().sum((0, 2, 3))) < 1e-5
 
 
+def test_wgrad_pipe_narrow_output_padded_dy():
+    """The pipelined 3x3 weight gradient of the UNet's output conv (Cout = 3, dy in a pitch of 8): the dy pitch
+    padding holds NaN here, and must not reach the weight or bias gradients (it feeds only accumulator rows that are
+    never stored). Against an fp32 torch reference of the same bf16 operands."""
+    from diffusion_models_collection_amd import _lib as L, kernels as K
+    N, H, W, Cin, Cout = 16, 32, 32, 128, 3
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn(N, H, W, Cin, generator=gen).to(torch.bfloat16)
+    g = torch.randn(N, H, W, Cout, generator=gen).to(torch.bfloat16)
+    gp = torch.full((N, H, W, 8), float("nan"), dtype=torch.bfloat16)
+    gp[..., :Cout] = g
+    d = K.make_desc(torch.bfloat16, N, H, W, Cin, 0, Cin, 0, L.kc_for(Cin, torch.bfloat16), H, W, Cout, K.TAPS3)
+    dw = torch.full((Cout, Cin, 3, 3), float("nan"), device=DEV)
+    db = torch.full((Cout,), float("nan"), device=DEV)
+    K.wgrad(d, gp.to(DEV), 8, x.to(DEV), None, dw, dbias=db)
+    torch.cuda.synchronize()
+    xr, gr = x.permute(0, 3, 1, 2).float(), g.permute(0, 3, 1, 2).float()
+    wr = torch.nn.grad.conv2d_weight(xr, (Cout, Cin, 3, 3), gr, padding=1)
+    assert torch.isfinite(dw).all() and torch.isfinite(db).all()
+    assert rel_err(dw.cpu(), wr) < 1e-5
+    assert rel_err(db.cpu(), gr.sum((0, 2, 3))) < 1e-5
+
+
 def test_wgrad_partial_reduce_batch_bitwise():
     """dmc_conv2d_wgrad_partial + ONE dmc_wgrad_reduce_batch over the jobs of several layers (the pipelined 3x3 kernel
     with its bias, a two-source 1x1, the generic kernel on a stride-2 conv, an fp32 Linear-shaped 1x1), partial sums in
@@ -1098,7 +1121,9 @@ def test_wgrad_partial_reduce_batch_bitwise():
     ref = run(None)
     small = K.WgradDefer()
     small.buf = torch.empty(1 << 20, dtype=torch.uint8, device=DEV)   # forces early flushes and a regrow
-    for defer in (K.WgradDefer(), small, small):
+    one_batch = K.WgradDefer()
+    one_batch.every = 0                                                 # all four jobs in one launch
+    for defer in (one_batch, K.WgradDefer(), small, small):
         got = run(defer)
         for (a, ab), (b, bb) in zip(ref, got):
             assert torch.equal(a, b)
