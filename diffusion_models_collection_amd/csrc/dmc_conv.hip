@@ -2341,10 +2341,6 @@ DMC_DEV v4i tr2(const char* pa, const char* pb) {
   return r;
 }
 
-#ifndef WG_ABL
-#define WG_ABL 0   // timing ablations of wgrad3x3_pipe_kernel (scripts/build_variant.sh; results wrong): 1 no stage
-                   // barrier, 2 no x-fragment reads in the stream, 4 no DMA
-#endif
 template <int OW>
 __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const char* dy, int ld_dy, int dy_bytes,
                                                              float* slab, int tiles_per_split, int ncb, int nob,
@@ -2485,15 +2481,15 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
       // counted waits of this wave's issue order (a stage issues halo(tl+1) at k = 0, then dy(st+2)):
       // k = 0 needs dy(st) and halo(tl), only dy(st+1) may be in flight; k = 1 needs dy(st), and halo(tl+1) and
       // dy(st+1) may be in flight
-      if (!(WG_ABL & 4) && live) wait_vm_dyn((st + 1 < mst ? 2 : 0) + (k == 1 && tl + 1 < my_nt ? HPW : 0));
+      if (live) wait_vm_dyn((st + 1 < mst ? 2 : 0) + (k == 1 && tl + 1 < my_nt ? HPW : 0));
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      if (!(WG_ABL & 1)) __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("" ::: "memory");
       if (!live) continue;
-      if (!(WG_ABL & 4) && k == 0 && tl + 1 < my_nt) halo_issue(tl + 1);   // into the buffer tile tl-1 used (every wave is past it)
-      if (!(WG_ABL & 4) && st + 2 < mst) dy_issue(st + 2);
+      if (k == 0 && tl + 1 < my_nt) halo_issue(tl + 1);   // into the buffer tile tl-1 used (every wave is past it)
+      if (st + 2 < mst) dy_issue(st + 2);
       // the stage's two k-steps as one stream of 18 fragment groups (k-step ks, tap u): the x fragment of group g + 2 is
       // read while group g's 4 MFMAs issue (three rotating fragment buffers), the dy fragments of both k-steps up front.
       // Each read's base register is made opaque right before it: equal address sums of different groups are not
@@ -2515,8 +2511,7 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
 #pragma unroll
       for (int g = 0; g < 18; ++g) {
         const int ks = g / 9, u = g - 9 * (g / 9);
-        if (!(WG_ABL & 2) && g + 2 < 18) xf[(g + 2) % 3] = xfrag(g + 2);
-        if ((WG_ABL & 2) && g == 0) xf[2] = xf[0];
+        if (g + 2 < 18) xf[(g + 2) % 3] = xfrag(g + 2);
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i][u] = mma16<T>(acc[i][u], fa[ks][i], xf[g % 3]);
         if (g + 2 < 18) {
@@ -2586,10 +2581,6 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_pipe_kernel(ConvK a, const ch
 // straight into LDS (buffer_load ... lds; no register staging, no ds_write), 32-byte segments XOR-swizzled on the
 // source column (the dy image of wgrad3x3_halo_kernel), read transposed (ds_read_b64_tr_b16). STAGES-deep ring,
 // one barrier per stage. Requires M % SPX == 0 and whole-stage split ranges (the planner checks).
-#ifndef W1_SPX
-#define W1_SPX 64      // wgrad1x1_glds_kernel stage pixels / ring depth (variant builds: scripts/build_variant.sh)
-#define W1_STAGES 2
-#endif
 template <int SPX, int STAGES>
 __global__ __launch_bounds__(256) void wgrad1x1_glds_kernel(ConvK a, const char* dy, int ld_dy, int dy_bytes,
                                                             float* slab, int KK, int pix_per_split, int nci, int nco,
@@ -3525,7 +3516,7 @@ static int wgrad_partial(const dmc_conv_desc* d, const void* dy, int ld_dy, cons
   // SPX-pixel stages, never more than wgrad_splits() counted (the workspace query's bound)
   const bool direct = d->ntaps == 1 && k.stride == 1 && k.mode == DMC_MODE_NORMAL && k.tdy0 == 0 && k.tdx0 == 0 &&
                       k.H == k.OH && k.W == k.OW && k.prologue == DMC_PRO_NONE;
-  constexpr int spx = W1_SPX;
+  constexpr int spx = 64;
   const bool w1x1 = !halo && d->dtype == DMC_BF16 && direct && k.M % spx == 0 && d->Cout % 8 == 0 &&
                     ld_dy % 8 == 0 && k.C1 % 8 == 0 && k.C2 % 8 == 0 && (k.C2 == 0 || k.C1 % 128 == 0) &&
                     k.ld1 % 8 == 0 && (k.C2 == 0 || k.ld2 % 8 == 0) && k.x1_bytes > 0 && (k.C2 == 0 || k.x2_bytes > 0) &&
@@ -3568,7 +3559,7 @@ static int wgrad_partial(const dmc_conv_desc* d, const void* dy, int ld_dy, cons
     g.z = splits;
     const dim3 g1(g.x * g.y * g.z);
     const int xcd = dmc::opt(dmc::OPT_NO_XCD) ? 0 : 1;
-    wgrad1x1_glds_kernel<W1_SPX, W1_STAGES><<<g1, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1,
+    wgrad1x1_glds_kernel<64, 2><<<g1, 256, 0, s>>>(k, (const char*)dy, ld_dy, (int)dyb, (float*)workspace, KK, pps1,
                                                   (int)g.x, (int)g.y, xcd);
   } else if (d->dtype == DMC_F32)
     conv_wgrad_kernel<float><<<g, 256, 0, s>>>(k, (const char*)dy, ld_dy, (float*)workspace, KK, pps);
