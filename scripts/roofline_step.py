@@ -48,7 +48,7 @@ def a_conv(d, x1, x2, w, y1, y2=None):
     return f, b, f"N{d.N} {d.H}x{d.W}x{Cin}->{d.OH}x{d.OW}x{d.Cout} t{d.ntaps} m{d.mode}"
 
 
-def a_wgrad(d, dy, ld_dy, x1, x2, dw, scale=1.0, dbias=None):
+def a_wgrad(d, dy, ld_dy, x1, x2, dw, scale=1.0, dbias=None, defer=None):
     M, Cin, e = d.N * d.OH * d.OW, d.C1 + d.C2, _esz(d.dtype)
     f = 2.0 * M * d.Cout * d.ntaps * Cin
     return f, M * d.Cout * e + d.N * d.H * d.W * Cin * e + d.Cout * d.ntaps * Cin * 4, \
@@ -107,7 +107,9 @@ def a_gn_none(*a, **k):
 
 
 def wrap(mod, name, alg):
-    fn = getattr(mod, name)
+    fn = getattr(mod, name, None)
+    if fn is None:
+        return
 
     def w(*a, **kw):
         f, b, shp = alg(*a, **kw)
@@ -127,6 +129,7 @@ for nm, alg in [("conv", a_conv), ("wgrad", a_wgrad), ("gn_stats", a_gn_stats), 
                 ("loss_fwd", a_gn_none), ("loss_bwd", a_gn_none), ("add_", a_gn_none), ("upsample2x", a_gn_none),
                 ("channel_sum", a_gn_none), ("colsum_batch", a_gn_none), ("time_embed", a_gn_none), ("unpack_output", a_gn_none)]:
     wrap(K, nm, alg)
+wrap(K.WgradDefer, "flush", lambda self: (0.0, 0.0, f"jobs{len(self.jobs)}"))   # the batched slab reductions
 _launch = K.PackBatch.launch
 
 
