@@ -136,6 +136,27 @@ DMC_DEV void onecta_chan_totals(const float (*red)[2 * EPC], int C, int CPR, int
   if (c < C && q == 0) { out[c][0] = b1; out[c][1] = b2; }
 }
 
+// onecta_chan_totals over a row-padded partial array (row pitch RP = 2 * EPC + 1 floats: the tpc lanes of one channel
+// read rows CPR apart, which a 16-float pitch put on one bank -- 16-way conflicts). The totals go to `out` after a
+// barrier, so `out` may alias `red`. Same summation order as onecta_chan_totals.
+template <int EPC, int NT, int RP>
+DMC_DEV void chan_totals_padded(const float* red, int C, int CPR, int rpi, float (*out)[2]) {
+  int tpc = 1;
+  while (tpc * 2 * C <= NT && tpc < 16) tpc *= 2;
+  const int c = threadIdx.x / tpc, q = threadIdx.x % tpc;
+  float b1 = 0.f, b2 = 0.f;
+  if (c < C) {
+    const int cc = c / EPC, e = c % EPC;
+    for (int r = q; r < rpi; r += tpc) {
+      b1 += red[(r * CPR + cc) * RP + 2 * e];
+      b2 += red[(r * CPR + cc) * RP + 2 * e + 1];
+    }
+  }
+  for (int o = tpc / 2; o > 0; o >>= 1) { b1 += __shfl_xor(b1, o, 64); b2 += __shfl_xor(b2, o, 64); }
+  __syncthreads();
+  if (c < C && q == 0) { out[c][0] = b1; out[c][1] = b2; }
+}
+
 // Statistics of one sample per 1024-thread block, finalised in the same launch (no partial buffer, no second
 // kernel): used at training/sampling batch sizes, where N blocks fill the chip. Same shifted sums and fixed
 // reduction order as gn_stats_partial + gn_stats_final with splits = 1. Replaces a ~5 us dependent launch per
@@ -727,8 +748,9 @@ __global__ __launch_bounds__(NT) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]
   const int rows = rpi < HW ? rpi : HW;   // row-threads that hold pixels (the rest only add zeros)
   const int tid = threadIdx.x, col = tid % CPR, r0 = tid / CPR;
   const bool active = r0 < rows;
-  __shared__ float red[NT][2 * EPC];
-  __shared__ float sA[1024][2];
+  constexpr int RP = 2 * EPC + 1;   // padded partial rows (chan_totals_padded)
+  __shared__ float red[NT * RP];
+  float (*const sA)[2] = (float (*)[2])red;   // the channel totals overwrite the partials (Cs <= NT * RP / 2)
   __shared__ float sm[64][2];
   __shared__ float sG[1024];
   const int c0 = cb + col * EPC;
@@ -783,9 +805,12 @@ __global__ __launch_bounds__(NT) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]
       }
     }
 #pragma unroll
-    for (int e = 0; e < EPC; ++e) { red[tid][2 * e] = active ? a1[e] : 0.f; red[tid][2 * e + 1] = active ? a2[e] : 0.f; }
+    for (int e = 0; e < EPC; ++e) {
+      red[tid * RP + 2 * e] = active ? a1[e] : 0.f;
+      red[tid * RP + 2 * e + 1] = active ? a2[e] : 0.f;
+    }
     __syncthreads();
-    onecta_chan_totals<EPC, NT>(red, Cs, CPR, rows, sA);   // sA[c - cb] (rows past `rows` held zeros)
+    chan_totals_padded<EPC, NT, RP>(red, Cs, CPR, rows, sA);   // sA[c - cb] (rows past `rows` held zeros)
     __syncthreads();
     for (int c = tid; c < Cs; c += NT) {
       A[((size_t)n * C + cb + c) * 2] = sA[c][0];
@@ -856,11 +881,10 @@ __global__ __launch_bounds__(NT) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]
       }
     }
     if (!sums) return;
-    float (*red1)[2 * EPC] = red;
 #pragma unroll
-    for (int e = 0; e < EPC; ++e) { red1[tid][2 * e] = active ? sum[e] : 0.f; red1[tid][2 * e + 1] = 0.f; }
+    for (int e = 0; e < EPC; ++e) { red[tid * RP + 2 * e] = active ? sum[e] : 0.f; red[tid * RP + 2 * e + 1] = 0.f; }
     __syncthreads();
-    onecta_chan_totals<EPC, NT>(red, Cs, CPR, rows, sA);   // the same fixed-order lane-parallel channel totals
+    chan_totals_padded<EPC, NT, RP>(red, Cs, CPR, rows, sA);   // the same fixed-order lane-parallel channel totals
     __syncthreads();
     for (int cl = tid; cl < Cs; cl += NT) {
       const float v = sA[cl][0];
