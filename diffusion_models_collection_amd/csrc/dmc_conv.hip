@@ -3523,7 +3523,14 @@ static int wgrad_partial(const dmc_conv_desc* d, const void* dy, int ld_dy, cons
                     dyb < 0x7fff0000u;
   int pps1 = 0;
   if (w1x1) {
-    pps1 = dmc::cdiv(dmc::cdiv(k.M, splits), spx) * spx;
+    // one round of blocks (two per CU: <= 512, e.g. 504 not 516 for the 16x16 qkv's 12 tiles -- a 4-block second
+    // round cost 24 %) and >= 256 pixels per block (fewer, longer splits on the 8x8 / 4x4 maps): the block-count
+    // sweep's per-shape optimum within ~4 % (scripts/wgrad_sweep.py --only 1x1, round 5)
+    const long tiles = (long)g.x * g.y;
+    long sp = std::min(512 / tiles, (long)k.M / 256);
+    if (sp > splits) sp = splits;   // never above the workspace query's split count
+    if (sp < 1) sp = 1;
+    pps1 = dmc::cdiv(dmc::cdiv(k.M, (int)sp), spx) * spx;
     splits = dmc::cdiv(k.M, pps1);
   }
   const size_t Cpad = (size_t)dmc::cdiv(d->Cout, 128) * 128;
