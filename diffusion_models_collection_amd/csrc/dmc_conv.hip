@@ -647,22 +647,39 @@ DMC_DEV void reg_epilogue(const ConvK& a, v4f (&acc)[4][4], int m0, int n0, int 
   // lane the whole chunk of pixel j0 and the odd lane that of pixel j1 (8-byte stores are store-issue bound).
   const int lane = threadIdx.x & 63, fr = lane & 15, fh = lane >> 4;
   const bool odd = fh & 1;
+  // every global operand of the epilogue (residual chunks, bias and time-embedding rows) is loaded up front: issued
+  // between the output stores, each load waited for its own round trip (the stores may alias them) -- eight to
+  // twelve serialised L2/HBM latencies per tile (the 32x32 conv's epilogue took a third of the kernel)
+  v4i rra[4][2];
+  v4f ba[4], eva[4];
+  const int img0 = (m0 + wm * 64) / a.OHW;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int co = n0 + wn * 64 + i * 16 + fh * 4;
+    const int cc = co - (odd ? 4 : 0);
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      rra[i][jp] = v4i{0, 0, 0, 0};
+      if (a.resid) {   // 16 bytes of the chunk: pixel j0 (even lane) or j1 (odd lane)
+        const int px = m0 + wm * 64 + (2 * jp + (odd ? 1 : 0)) * 16 + fr;
+        rra[i][jp] = *(const v4i*)(a.resid + ((size_t)px * a.ld_res + cc) * 2);
+      }
+    }
+    ba[i] = a.bias ? *(const v4f*)(a.bias + co) : v4f{0.f, 0.f, 0.f, 0.f};
+    eva[i] = a.addvec ? *(const v4f*)(a.addvec + (size_t)img0 * a.ld_add + co) : v4f{0.f, 0.f, 0.f, 0.f};
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int co = n0 + wn * 64 + i * 16 + fh * 4;
     const int cc = co - (odd ? 4 : 0);   // first channel of the lane pair's 8-channel chunk
-    const v4f b = a.bias ? *(const v4f*)(a.bias + co) : v4f{0.f, 0.f, 0.f, 0.f};
+    const v4f b = ba[i];
     float gm = 0.f, gq = 0.f;
-    int nimg = -1;
-    v4f ev = {0.f, 0.f, 0.f, 0.f};
+    int nimg = img0;
+    v4f ev = eva[i];
 #pragma unroll
     for (int jp = 0; jp < 2; ++jp) {
       v2i o[2];
-      v4i rr = {0, 0, 0, 0};
-      if (a.resid) {   // 16 bytes of the chunk: pixel j0 (even lane) or j1 (odd lane)
-        const int px = m0 + wm * 64 + (2 * jp + (odd ? 1 : 0)) * 16 + fr;
-        rr = *(const v4i*)(a.resid + ((size_t)px * a.ld_res + cc) * 2);
-      }
+      const v4i rr = rra[i][jp];
       // the other pixel's residual half: even lanes need their 4 channels of pixel j1, odd lanes of pixel j0
       v2i rs;
       rs[0] = __shfl_xor(odd ? rr[0] : rr[2], 16);
