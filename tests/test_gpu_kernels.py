@@ -1165,3 +1165,45 @@ def test_wgrad_pipe_kernel(shape, dmc_opt):
     assert rel_err(res[0][0], wr) < 1e-5, rel_err(res[0][0], wr)
     assert rel_err(res[0][0], res[2][0]) < 1e-5
     assert rel_err(res[0][1], gr.sum((0, 2, 3))) < 1e-5
+
+
+@pytest.mark.parametrize("case", ["halo2_32", "halo2_16", "glds_up"])
+@pytest.mark.parametrize("shared_t", [False, True])
+def test_reg_epilogue_bitwise_lds_staged(case, shared_t, dmc_opt):
+    """The register epilogue (DMC_REG_EPI=3, default: bias, time-embedding row, residual and the GroupNorm partials
+    straight from the accumulators, lane-pair exchanges for 16-byte stores) against the LDS-staged epilogue
+    (DMC_REG_EPI=0) on the halo conv (32x32 and 16x16 tiles) and the LDS-DMA GEMM (the nearest-x2 upsample conv),
+    with bias, a per-image or shared (ld_add = 0) time-embedding row and a residual: the stored outputs are bitwise
+    equal (same additions in the same order), the GroupNorm partials equal up to their fp32 combine order."""
+    from diffusion_models_collection_amd import _lib as L, kernels as K
+    dt = torch.bfloat16
+    # batch sizes that give the non-split plans (>= 240 tiles of 256 x 128), whose epilogues these are
+    N, H, W, Cin, Cout, mode = {"halo2_32": (64, 32, 32, 128, 128, L.MODE_NORMAL),
+                                "halo2_16": (128, 16, 16, 256, 256, L.MODE_NORMAL),
+                                "glds_up": (64, 16, 16, 128, 128, L.MODE_UPSAMPLE)}[case]
+    OH, OW = (2 * H, 2 * W) if mode == L.MODE_UPSAMPLE else (H, W)
+    gen = torch.Generator().manual_seed(21)
+    x = torch.randn(N, H, W, Cin, generator=gen).to(dt).to(DEV)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=gen) * 0.03).to(DEV)
+    Kc = L.kc_for(Cin, dt)
+    wp = K.pack_weight(L.PACK_FWD, dt, w, Kc)
+    bias = torch.randn(Cout, generator=gen).to(DEV)
+    tv = torch.randn(1 if shared_t else N, Cout, generator=gen).to(DEV)
+    resid = torch.randn(N, OH, OW, Cout, generator=gen).to(dt).to(DEV)
+    outs = {}
+    for reg in (3, 0):
+        dmc_opt("DMC_REG_EPI", reg)
+        d = K.make_desc(dt, N, H, W, Cin, 0, Cin, 0, Kc, OH, OW, Cout, K.TAPS3, mode)
+        y = torch.full((N, OH, OW, Cout), float("nan"), dtype=dt, device=DEV)
+        part = torch.full((N * OH * OW // 64 * (Cout // 8) * 2,), float("nan"), device=DEV)
+        K.set_epilogue(d, bias=bias, addvec=tv, ld_add=0 if shared_t else Cout, resid=resid, ld_res=Cout,
+                       ldy1=Cout, gn_part=part)
+        K.conv(d, x, None, wp, y)
+        torch.cuda.synchronize()
+        fused = K.conv_fused(d) & L.FUSED_GN_STATS
+        outs[reg] = (y.cpu(), part.cpu(), fused)
+    (y3, p3, f3), (y0, p0, f0) = outs[3], outs[0]
+    assert torch.isfinite(y3.float()).all()
+    assert torch.equal(y3, y0)
+    if f3 and f0:   # both epilogues emitted the partials
+        assert torch.isfinite(p3).all() and torch.allclose(p3, p0, rtol=1e-5, atol=1e-6)
