@@ -22,7 +22,7 @@ LIB = PKG / "libdmc.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("DMC_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["dmc_conv.hip", "dmc_norm.hip", "dmc_attn.hip", "dmc_elem.hip", "dmc_dit.hip", "dmc_data.hip"]
+SOURCES = ["dmc_conv.hip", "dmc_wgrad.hip", "dmc_norm.hip", "dmc_attn.hip", "dmc_elem.hip", "dmc_dit.hip", "dmc_data.hip"]
 # the element-wise and data files restate torch op sequences: no FMA contraction there
 EXTRA = {"dmc_elem.hip": ["-ffp-contract=off"], "dmc_data.hip": ["-ffp-contract=off"]}
 COMMON = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",

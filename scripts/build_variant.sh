@@ -10,7 +10,7 @@ mkdir -p $R/build/var_$N
   -I $R/include -I $R/diffusion_models_collection_amd/csrc -c $R/diffusion_models_collection_amd/csrc/dmc_conv.hip \
   -o $R/build/var_$N/dmc_conv.o
 O=""
-for f in dmc_norm dmc_attn dmc_elem dmc_dit dmc_data; do O="$O $R/build/$f.o"; done
+for f in dmc_wgrad dmc_norm dmc_attn dmc_elem dmc_dit dmc_data; do O="$O $R/build/$f.o"; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/diffusion_models_collection_amd/libdmc_$N.so \
   $R/build/var_$N/dmc_conv.o $O
 echo built libdmc_$N.so
