@@ -565,9 +565,11 @@ class DiffusionTrainer:
 
     # ------------------------------------------------------------------------------------------
     def _make_grad_sync(self, config, process_group=None, force_avg=False):
-        # bucket size: the reference's DDP default (25 MB); 'ddp_bucket_mb' (not a reference key) overrides.
-        # 'ddp_force_avg' (not a reference key): ReduceOp.AVG even on a one-rank RCCL group (GradSync)
-        bmb = float((config or {}).get('ddp_bucket_mb', 25))
+        # bucket size: the reference's DDP default (25 MB); 'ddp_bucket_mb' (not a reference key) or the
+        # DMC_DDP_BUCKET_MB environment variable overrides. 'ddp_force_avg' (not a reference key): ReduceOp.AVG
+        # even on a one-rank RCCL group (GradSync)
+        import os
+        bmb = float((config or {}).get('ddp_bucket_mb', os.environ.get('DMC_DDP_BUCKET_MB', 25)))
         force_avg = force_avg or bool((config or {}).get('ddp_force_avg', False))
         return GradSync(self.model.executor, process_group=process_group, bucket_bytes=int(bmb * 1024 * 1024),
                         force_avg=force_avg)
