@@ -1046,7 +1046,9 @@ WgPipePlan wgrad_pipe_plan(const dmc_conv_desc* d, int ld_dy) {
   const long base = (long)(k.Kc / 64) * dmc::cdiv(k.Cout, 64);
   // 512-thread blocks (two 64 x 64 halves): one per CU, never more than one round of them (264 blocks for 256 CUs
   // measured 1.4x slower than 192)
-  const long target = dmc::opt(dmc::OPT_WG_HALO_TARGET);
+  // 4x4 maps: half the blocks (each half-block two 64-pixel tiles instead of one; half the slab): 28.5 vs 31.1 us
+  // per 256 -> 256 layer (scripts/wgrad_probe2.py, round 5)
+  const long target = dmc::opt(dmc::OPT_WG_HALO_TARGET) / (k.OW == 4 ? 2 : 1);
   long sp = target / base;
   if (sp > ntiles) sp = ntiles;
   if (sp < 1) sp = 1;
