@@ -54,6 +54,10 @@ def run(name, iters, epi="bias", cold=False):
         resid = torch.randn(B, H, W, Cout, device=dev).to(dt)
         K.set_epilogue(d, bias=torch.randn(Cout, device=dev), addvec=torch.randn(B, Cout, device=dev), ld_add=Cout,
                        resid=resid, ld_res=Cout, ldy1=Cout)
+    elif epi in ("temb", "gn"):   # conv1 epilogue: bias + time embedding (+ the next GroupNorm's partials: bench roofline)
+        part = torch.empty(B * H * W // 64 * (Cout // 8) * 2, device=dev) if epi == "gn" else None
+        K.set_epilogue(d, bias=torch.randn(Cout, device=dev), addvec=torch.randn(B, Cout, device=dev), ld_add=Cout,
+                       ldy1=Cout, gn_part=part)
     else:
         K.set_epilogue(d, bias=torch.randn(Cout, device=dev), ldy1=Cout)
     ws = L.LIB.dmc_conv2d_workspace(ctypes.byref(d))
@@ -90,7 +94,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="all")
     ap.add_argument("--iters", type=int, default=50)
-    ap.add_argument("--epi", default="bias", choices=["bias", "full"])
+    ap.add_argument("--epi", default="bias", choices=["bias", "full", "temb", "gn"])
     ap.add_argument("--cold", default="", choices=["", "cold", "hot1"],
                     help="time launches one at a time, with L2 / MALL evicted before each (cold) or not (hot1)")
     a = ap.parse_args()
