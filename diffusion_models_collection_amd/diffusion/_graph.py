@@ -6,51 +6,92 @@ utils/trainer.py:303-312). The step function is captured once with static input 
 new inputs in (device copies), launches the graph, and returns the static output (the next step copies it
 back in, so the output buffer is never read and written by the same replay). Random draws happen OUTSIDE the
 graph, eagerly and in the eager loop's order (`buf.normal_()` is what `torch.randn_like` does), so a graphed
-loop computes bitwise what the eager loop computes (tests/test_gpu_model.py). A graph lives for one sample()
-call: the weights may change between calls.
+loop computes bitwise what the eager loop computes (tests/test_gpu_model.py).
+
+A loop whose step reads nothing but its inputs, the sampler's tables and the model's weights may keep its graph
+on the model's executor across sample() calls (`cache=`): the key holds the sampler's settings, the input shapes
+and every parameter's (version, pointer) plus the executor's weight generation (bumped by the fused optimizer /
+EMA kernels that write the parameters behind torch's back), so any weight update recaptures. Without a cache
+key a graph lives for one call.
 """
+import collections
 import os
 
 import torch
 
 
 class StepGraph:
-    def __init__(self, fn, *inputs):
+    def __init__(self, fn, *inputs, const=()):
+        """const: positions of inputs that stay the same tensor through a loop (class labels): copied only when
+        a different tensor, or a new torch version of it, is handed in."""
         self.static = [x.clone() for x in inputs]
+        self.const = frozenset(const)
+        self.seen = [(x, x._version) for x in inputs]
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):   # see utils/trainer.py begin()
             self.out = fn(*self.static)
 
     def step(self, *inputs):
-        for s, x in zip(self.static, inputs):
-            if x is not None and x is not s:
-                s.copy_(x)
+        for i, (s, x) in enumerate(zip(self.static, inputs)):
+            if x is None or x is s:
+                continue
+            if i in self.const and self.seen[i][0] is x and self.seen[i][1] == x._version:
+                continue
+            s.copy_(x)
+            self.seen[i] = (x, x._version)
         self.graph.replay()
         return self.out
 
     @staticmethod
     def eligible(model, x, deterministic, return_all):
-        """DMC_GRAPH=0 / 1 turns the replay off / on; by default it is used for batches of <= 32, where the
-        step's host enqueue exceeds its GPU time (at B=128 the step is GPU-bound and a per-call capture only
-        adds its own cost: 569 vs 602 img/s measured for DDIM-50)."""
+        """DMC_GRAPH=0 / 1 turns the replay off / on; by default it is used for batches of <= 64, where the
+        step's host enqueue (~2.8-3.1 ms for the CIFAR UNet) is at or above its GPU time. Measured DDIM-50 on one
+        MI355X (scripts/ddim_probe.py, ms per call, eager / graphed / graph kept across calls): B=16 172 / 116 /
+        110, B=64 155 / 143 / 134, B=128 178 / 187 / 179 -- at B=128 the step is GPU-bound and a replay runs no
+        faster than the eager loop, so the first call's capture would only add its cost."""
         mode = os.environ.get("DMC_GRAPH")
         if mode == "0" or not deterministic or return_all or not x.is_cuda:
             return False
         if getattr(model, "executor", None) is None or model.training:
             return False
-        return mode == "1" or x.shape[0] <= 32
+        return mode == "1" or x.shape[0] <= 64
+
+    @staticmethod
+    def weights_key(model):
+        ex = getattr(model, "executor", None)
+        return (getattr(ex, "wgen", None),) + tuple((p._version, p.data_ptr()) for p in model.parameters())
 
 
-def run_loop(x, nsteps, make_inputs, fn, use_graph, record=None):
+_CACHE_MAX = 2      # graphs kept per executor (each holds its activation pool)
+
+
+def cache_for(model, tag, owner, x):
+    """(store, key, owner) for run_loop(cache=...): owner = the sampler whose tables the step reads (kept alive by
+    the entry, so its id cannot be reused while the graph is). None for a model without an executor."""
+    ex = getattr(model, "executor", None)
+    if ex is None:
+        return None
+    store = ex.__dict__.setdefault("_step_graphs", collections.OrderedDict())
+    return store, (tag, id(owner), tuple(x.shape), x.dtype, x.device, StepGraph.weights_key(model)), owner
+
+
+def run_loop(x, nsteps, make_inputs, fn, use_graph, record=None, cache=None, const=()):
     """for i in range(nsteps): x = fn(*make_inputs(i, x)); eager for step 0 (caches and weight packs are then
-    in place) and graphed afterwards when use_graph. make_inputs(i, x) -> tuple of tensors, x first."""
+    in place) and graphed afterwards when use_graph. make_inputs(i, x) -> tuple of tensors, x first. With a
+    cache (cache_for) a graph from an earlier call with the same key replays from step 0."""
     graph = None
+    if use_graph and cache is not None:
+        store, key, _ = cache
+        hit = store.get(key)
+        if hit is not None:
+            store.move_to_end(key)
+            graph = hit[1]
     for i in range(nsteps):
         args = make_inputs(i, x)
         if graph is None and use_graph and i >= 1:
             prev = torch.cuda.current_stream()
             try:
-                graph = StepGraph(fn, *args)
+                graph = StepGraph(fn, *args, const=const)
             except Exception as e:   # noqa: BLE001
                 # loud, as the training step's capture (utils/trainer.py GraphCaptureError): the stream a failed
                 # capture ran on may be poisoned, so the loop does not silently carry on eagerly on it. A failure in
@@ -58,6 +99,11 @@ def run_loop(x, nsteps, make_inputs, fn, use_graph, record=None):
                 torch.cuda.set_stream(prev)
                 from ..utils.trainer import GraphCaptureError
                 raise GraphCaptureError(f"sampling step capture failed at step {i}: {e!r}") from e
+            if cache is not None:
+                store, key, owner = cache
+                store[key] = (owner, graph)
+                while len(store) > _CACHE_MAX:
+                    store.popitem(last=False)
         x = graph.step(*args) if graph is not None else fn(*args)
         if record is not None:
             record(i, x)

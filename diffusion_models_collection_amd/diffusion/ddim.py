@@ -18,7 +18,7 @@ from tqdm import tqdm
 
 from .. import kernels as K
 from . import _schedule
-from ._graph import StepGraph, run_loop
+from ._graph import StepGraph, cache_for, run_loop
 from .ddpm import DDPM, _require_cuda, diffusion_loss, make_betas
 
 
@@ -112,25 +112,35 @@ class DDIM:
         S = len(self.inference_timesteps)
         bar = tqdm(total=S, desc='DDIM Sampling')
 
+        if y is not None:
+            y = y.to(img.device)
+        has_y, has_z = y is not None, self.eta > 0
+
         def inputs(i, x):
+            # the labels are a step input (not captured by fn), so a graph kept across calls reads the new ones
             z = self._noise(noise, i, x)
-            return (x, tab[i], tab[i + 1]) + ((z,) if z is not None else ())
+            return (x, tab[i], tab[i + 1]) + ((y,) if has_y else ()) + ((z,) if z is not None else ())
 
         # every sample shares the step's timestep: a model that takes a length-1 t (UNet.shared_timestep) runs its
         # time-embedding MLPs once per step instead of once per image
         shared_t = (y is None and getattr(model, "shared_timestep", False)
                     and os.environ.get("DMC_SHARED_T", "1") != "0")   # A/B switch
 
-        def fn(x, t, tn, z=None):
+        def fn(x, t, tn, *rest):
+            yy = rest[0] if has_y else None
+            z = rest[-1] if len(rest) > has_y else None
             eps = model(x, t[:1], None) if shared_t else None
-            return self.p_sample(model, x, t, tn, y, eps=eps, noise=z)
+            return self.p_sample(model, x, t, tn, yy, eps=eps, noise=z)
 
         def record(i, x):
             bar.update(1)
             if return_all_timesteps:
                 imgs.append(x.cpu())
 
-        img = run_loop(img, S, inputs, fn, StepGraph.eligible(model, img, True, False), record)
+        cache = None if return_all_timesteps else cache_for(
+            model, ("ddim", self.eta, shared_t, has_y, has_z, self.alphas_cumprod.data_ptr()), self, img)
+        img = run_loop(img, S, inputs, fn, StepGraph.eligible(model, img, True, False),
+                       record, cache=cache, const=(3,) if has_y else ())
         bar.close()
         if return_all_timesteps:
             return torch.stack(imgs, dim=0)
@@ -155,12 +165,14 @@ class DDIM:
         S = len(self.inference_timesteps)
         bar = tqdm(total=S, desc=f"DDIM sampling with CFG scale {cfg_scale}")
 
+        has_z = self.eta > 0
+
         def inputs(i, x):
             z = self._noise(noise, i, x)
-            return (x, tab[i], tab[i + 1]) + ((z,) if z is not None else ())
+            return (x, tab[i], tab[i + 1], y) + ((z,) if z is not None else ())
 
-        def fn(x, t, tn, z=None):
-            eps_c, eps_u = DDPM._cfg_eps(model, x, t, y)
+        def fn(x, t, tn, yy, z=None):
+            eps_c, eps_u = DDPM._cfg_eps(model, x, t, yy)
             eps_g, x0 = K.cfg_x0(x.contiguous(), eps_c.contiguous(), eps_u.contiguous(), cfg_scale, t, ac, None, 0,
                                  p_threshold)
             return self.p_sample(model, x, t, tn, y=None, clip_denoised=False, eps=eps_g, x0_pred=x0, noise=z)
@@ -170,7 +182,10 @@ class DDIM:
             if return_all_timesteps:
                 imgs.append(x.cpu())
 
-        img = run_loop(img, S, inputs, fn, StepGraph.eligible(model, img, True, False), record)
+        cache = None if return_all_timesteps else cache_for(
+            model, ("ddim_cfg", self.eta, has_z, float(cfg_scale), p_threshold, ac.data_ptr()), self, img)
+        img = run_loop(img, S, inputs, fn, StepGraph.eligible(model, img, True, False),
+                       record, cache=cache, const=(3,))
         bar.close()
         if return_all_timesteps:
             return torch.stack(imgs, dim=0)

@@ -440,6 +440,53 @@ def test_ddim_sample_graph_matches_eager(dtype, monkeypatch):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
+def test_ddim_step_graph_kept_across_calls(monkeypatch):
+    """The DDIM step graph is kept on the executor across sample() calls (diffusion/_graph.py cache_for): a second
+    call replays it from step 0, new class labels reach it as an input, and an in-place weight update or a weight
+    generation bump (the fused optimizer / EMA kernels) recaptures -- every output bitwise the eager loop's."""
+    from diffusion_models_collection_amd.models import UNet
+    from diffusion_models_collection_amd.diffusion import DDIM
+    torch.manual_seed(5)
+    m = UNet(image_size=(16, 16), in_channels=3, model_channels=32, out_channels=3, num_res_blocks=1,
+             attention_resolutions=(8,), dropout=0.1, channel_mult=(1, 2), num_classes=10,
+             compute_dtype="bf16").to(DEV).eval()
+    ddim = DDIM(1000, 6, device=DEV)
+    xT = torch.randn(4, 3, 16, 16, device=DEV)
+    ya, yb = torch.tensor([1, 2, 3, 4], device=DEV), torch.tensor([7, 0, 9, 5], device=DEV)
+
+    def run(graph):
+        monkeypatch.setenv("DMC_GRAPH", graph)
+        with torch.no_grad():
+            return [ddim.sample(m, tuple(xT.shape), ya, x_T=xT), ddim.sample(m, tuple(xT.shape), yb, x_T=xT),
+                    ddim.sample_with_cfg(m, tuple(xT.shape), ya, x_T=xT),
+                    ddim.sample_with_cfg(m, tuple(xT.shape), yb, x_T=xT)]
+
+    m.executor.__dict__.pop("_step_graphs", None)
+    eager = run("0")
+    assert not m.executor.__dict__.get("_step_graphs")
+    graphed = run("1")
+    store = m.executor._step_graphs
+    assert len(store) == 2                                  # one DDIM and one CFG graph, reused by the second calls
+    graphs = [e[1] for e in store.values()]
+    again = run("1")
+    assert [e[1] for e in store.values()] == graphs          # replayed, not recaptured
+    for a, b, c in zip(eager, graphed, again):
+        assert torch.equal(a, b) and torch.equal(a, c)
+    assert not torch.equal(eager[0], eager[1])               # the labels did change the samples
+    with torch.no_grad():
+        next(m.parameters()).mul_(1.01)                       # torch version bump
+    eager2 = run("0")
+    graphed2 = run("1")
+    assert all(g not in graphs for g in (e[1] for e in store.values()))
+    for a, b in zip(eager2, graphed2):
+        assert torch.equal(a, b)
+    assert not torch.equal(eager[0], eager2[0])
+    m.executor.wgen += 1                                      # weights rewritten behind torch's back
+    keys = list(store.keys())
+    run("1")
+    assert all(k not in keys for k in store.keys())
+
+
 # ------------------------------------------------------------------------------------------------------------
 # round 2: DDPM sampling loops, BASELINE config #1 / #5 shapes, bf16 at the benchmarked size, checkpoints
 # ------------------------------------------------------------------------------------------------------------
