@@ -96,6 +96,10 @@ def _load():
                                   _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
         "dmc_gn_finalize": (_c_int, [_c_p, _c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_f, _c_p, _c_p, _c_p, _c_p,
                                      _c_p, _c_p]),
+        "dmc_gn_stats_apply_ok": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_int]),
+        "dmc_gn_stats_apply": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                                        _c_f, _c_p, _c_p, _c_p, _c_p, _c_p, _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p,
+                                        _c_int, _c_p]),
         "dmc_gn_apply": (_c_int, [_c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p,
                                   _c_int, _c_u32, _c_p, _c_u32, _c_f, _c_p, _c_int, _c_p]),
         "dmc_gn_silu_bwd": (_c_int, [_c_int, _c_p, _c_int, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_int,

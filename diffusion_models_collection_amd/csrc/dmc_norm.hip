@@ -157,13 +157,25 @@ DMC_DEV void chan_totals_padded(const float* red, int C, int CPR, int rpi, float
   if (c < C && q == 0) { out[c][0] = b1; out[c][1] = b2; }
 }
 
+// dropout seed: the host seed plus the device-side per-step base (graph replays), if any
+DMC_DEV uint32_t drop_seed(uint32_t seed, const uint32_t* base) { return seed + (base ? *base : 0u); }
+
+// The apply half of gn_stats_one<T, true> (dmc_gn_stats_apply): gn_apply_kernel's arguments.
+struct GnApplyArgs {
+  int silu; uint32_t seed0; const uint32_t* seed_base; uint32_t thresh; float dscale; char* out; int ldo;
+};
+
 // Statistics of one sample per 1024-thread block, finalised in the same launch (no partial buffer, no second
 // kernel): used at training/sampling batch sizes, where N blocks fill the chip. Same shifted sums and fixed
 // reduction order as gn_stats_partial + gn_stats_final with splits = 1. Replaces a ~5 us dependent launch per
 // GroupNorm; the per-element work (unpack, sub, add, fma) keeps one CU's walk memory-bound.
-template <typename T>
+// APPLY: the block then also writes the sample's a = drop(silu(x * scale + shift)) with gn_apply_kernel's
+// arithmetic and the scale / shift it just stored (bitwise dmc_gn_stats + dmc_gn_apply): for the 4x4 levels, where
+// a sample is a few KB and the separate apply launch costs more than re-reading it from L2.
+template <typename T, bool APPLY = false>
 __global__ __launch_bounds__(1024) void gn_stats_one(Src2 s, int HW, int G, float eps, const float* gamma,
-                                                     const float* beta, float* mean_rstd, float* scale, float* shift) {
+                                                     const float* beta, float* mean_rstd, float* scale, float* shift,
+                                                     GnApplyArgs ap = {}) {
   constexpr int EPC = TT<T>::KPL;
   const int n = blockIdx.x;
   const int C = s.C1 + s.C2, cpg = C / G;
@@ -224,13 +236,37 @@ __global__ __launch_bounds__(1024) void gn_stats_one(Src2 s, int HW, int G, floa
     if (mean_rstd) { mean_rstd[((size_t)n * G + g) * 2] = mean; mean_rstd[((size_t)n * G + g) * 2 + 1] = rstd; }
   }
   __syncthreads();
+  float* const ssc = &red[0][0];          // APPLY: this sample's scale / shift (red is free after the totals)
+  float* const ssh = ssc + 1024;
   for (int c = tid; c < C; c += 1024) {
     const int g = c / cpg;
     const float mean = gstat[g][0], rstd = gstat[g][1];
     const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-    const float sc = rstd * gm;
+    const float sc = rstd * gm, sh = bt - mean * sc;
     scale[(size_t)n * C + c] = sc;
-    shift[(size_t)n * C + c] = bt - mean * sc;
+    shift[(size_t)n * C + c] = sh;
+    if constexpr (APPLY) { ssc[c] = sc; ssh[c] = sh; }
+  }
+  if constexpr (APPLY) {
+    __syncthreads();
+    if (!active) return;
+    const uint32_t seed = drop_seed(ap.seed0, ap.seed_base);
+    float sc[EPC], sh[EPC];
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) { sc[e] = ssc[c0 + e]; sh[e] = ssh[c0 + e]; }
+    for (int p = r0; p < HW; p += rpi) {
+      const int pix = n * HW + p;
+      float f[EPC];
+      Chunk<T>::unpack(load_chunk2<T>(s, pix, c0), f);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        float v = fmaf(f[e], sc[e], sh[e]);
+        if (ap.silu) v = silu_f(v);
+        if (ap.thresh) v = drop_keep((uint64_t)pix * C + c0 + e, seed, ap.thresh) ? v * ap.dscale : 0.f;
+        f[e] = v;
+      }
+      *(v4i*)(ap.out + ((size_t)pix * ap.ldo + c0) * sizeof(T)) = Chunk<T>::pack(f);
+    }
   }
 }
 
@@ -245,7 +281,6 @@ struct GnBwd {
   int silu;
 };
 
-DMC_DEV uint32_t drop_seed(uint32_t seed, const uint32_t* base) { return seed + (base ? *base : 0u); }
 
 // dz for one element (recomputes the forward)
 DMC_DEV float gn_dz(float x, float gv, float mean, float rstd, float gm, float bt, float& xhat, int silu) {
@@ -1229,6 +1264,27 @@ extern "C" int dmc_channel_sum(int dtype, const void* dy, int N, int HW, int C, 
   else chsum_partial<bf16_t><<<g, 256, 0, s>>>((const char*)dy, HW, C, ld, splits, partial);
   chsum_finish(s, N, C, splits, partial, out_nc, ld_out, out_c, scale);
   return dmc::check_launch("dmc_channel_sum");
+}
+
+extern "C" int dmc_gn_stats_apply_ok(int dtype, int N, int HW, int C1, int C2, int G) {
+  const int C = C1 + C2;
+  return dtype != DMC_F32 && !dmc::opt(dmc::OPT_GN_STATS_SPLIT) && N >= 64 && G <= 64 && C % G == 0 && C1 % 8 == 0 &&
+         C2 % 8 == 0 && C <= 1024 && (long)HW * C <= 8192;
+}
+
+extern "C" int dmc_gn_stats_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1,
+                                  int ld2, int G, float eps, const float* gamma, const float* beta, float* mean_rstd,
+                                  float* scale, float* shift, int silu, uint32_t drop_seed,
+                                  const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* out,
+                                  int ld_out, void* stream) {
+  DMC_REQUIRE(dmc_gn_stats_apply_ok(dtype, N, HW, C1, C2, G), "gn_stats_apply: dtype %d N %d HW %d C %d+%d G %d",
+              dtype, N, HW, C1, C2, G);
+  DMC_REQUIRE(ld1 % 8 == 0 && (C2 == 0 || ld2 % 8 == 0) && ld_out % 8 == 0, "gn_stats_apply: pitch alignment");
+  Src2 src{(const char*)x1, (const char*)x2, C1, C2, ld1, ld2};
+  GnApplyArgs ap{silu, drop_seed, drop_seed_base, drop_thresh, drop_scale, (char*)out, ld_out};
+  gn_stats_one<bf16_t, true><<<N, 1024, 0, dmc::as_stream(stream)>>>(src, HW, G, eps, gamma, beta, mean_rstd, scale,
+                                                                     shift, ap);
+  return dmc::check_launch("dmc_gn_stats_apply");
 }
 
 extern "C" int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1, int ld2,

@@ -306,6 +306,25 @@ def gn_finalize(p1, C1, p2, C2, N, HW, G, eps, gamma, beta, out=None):
     return sc, sh, mr
 
 
+def gn_stats_apply_ok(dtype, N, HW, C1, C2, G):
+    return bool(LIB.dmc_gn_stats_apply_ok(L.dtype_code(dtype), N, HW, C1, C2, G))
+
+
+def gn_stats_apply(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, G, eps, gamma, beta, silu=True, drop=None):
+    """gn_stats + gn_apply in one launch (small samples, gn_stats_apply_ok): ((scale, shift, mean_rstd), a)."""
+    C = C1 + C2
+    dev = x1.device
+    mr = torch.empty(N * G * 2, dtype=torch.float32, device=dev)
+    sc = torch.empty(N * C, dtype=torch.float32, device=dev)
+    sh = torch.empty(N * C, dtype=torch.float32, device=dev)
+    out = torch.empty(N * HW * C, dtype=dtype, device=dev)
+    seed, base, thresh, dscale = drop_args(drop)
+    check(LIB.dmc_gn_stats_apply(L.dtype_code(dtype), ptr(x1), ptr(x2), N, HW, C1, C2, ld1, ld2, G, eps, ptr(gamma),
+                                 ptr(beta), ptr(mr), ptr(sc), ptr(sh), int(silu), seed, base, thresh, dscale, ptr(out),
+                                 C, L.stream()), "dmc_gn_stats_apply")
+    return (sc, sh, mr), out
+
+
 def gn_apply(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, scale, shift, silu=True, drop=None, out=None):
     """a = dropout(silu(x*scale + shift)) materialised as [N*HW][C1+C2] (dtype)."""
     C = C1 + C2

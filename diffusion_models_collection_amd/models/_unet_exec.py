@@ -48,6 +48,9 @@ _GN_DEFER = os.environ.get("DMC_GN_DEFER", "1") not in ("", "0")
 # The weight-gradient slab reductions deferred to one dmc_wgrad_reduce_batch per gradient segment (A/B switch
 # DMC_WG_DEFER=0: one reduce launch after each weight-gradient kernel)
 _WG_DEFER = os.environ.get("DMC_WG_DEFER", "1") not in ("", "0")
+# GroupNorm statistics + apply in one launch where a sample is a few KB (dmc_gn_stats_apply: the 4x4 levels);
+# a module switch for same-box A/Bs (scripts/r5_gsa.sh), not an option
+_GN_SMALL_FUSE = True
 
 
 def _seed_from_torch():
@@ -205,6 +208,7 @@ class UNetExecutor(ExecCore):
         self.cdt = L.dtype_code(self.dt)
         self.chunk = L.chunk_for(self.dt)
         self._halo_pro_cache = {}   # shape -> dmc_conv_halo_prologue verdict
+        self._gsa_cache = {}        # shape -> dmc_gn_stats_apply_ok verdict
         self.wgen = 0               # weight generation: bumped when a fused step rewrote the parameters
         self.packs = _PackCache(self)
         self.params = list(model.parameters())
@@ -335,6 +339,25 @@ class UNetExecutor(ExecCore):
                                  gn.eps, gn.weight, gn.bias)
         return K.gn_stats(dtype, a.t, b.t if b else None, N, a.H * a.W, a.C, b.C if b else 0, a.t.shape[-1],
                           b.t.shape[-1] if b else 0, gn.num_groups, gn.eps, gn.weight, gn.bias)
+
+    def _gn_apply_small(self, srcs, gn, silu, drop=None):
+        """(stats, Act) of SiLU(GN(concat(srcs))) from ONE dmc_gn_stats_apply launch (bitwise _gn + _apply) where a
+        sample is small enough for one block (the 4x4 levels); None elsewhere."""
+        if not _GN_SMALL_FUSE or any(s.part is not None for s in srcs):
+            return None
+        a = srcs[0]
+        b = srcs[1] if len(srcs) > 1 else None
+        N, HW, C1, C2 = a.t.shape[0], a.H * a.W, a.C, (b.C if b else 0)
+        key = (self.dt, N, HW, C1, C2, gn.num_groups, L.get_option("DMC_GN_STATS_SPLIT"))
+        ok = self._gsa_cache.get(key)
+        if ok is None:
+            ok = self._gsa_cache[key] = K.gn_stats_apply_ok(self.dt, N, HW, C1, C2, gn.num_groups)
+        if not ok:
+            return None
+        st, out = K.gn_stats_apply(self.dt, a.t, b.t if b else None, N, HW, C1, C2, a.t.shape[-1],
+                                   b.t.shape[-1] if b else 0, gn.num_groups, gn.eps, gn.weight, gn.bias, silu=silu,
+                                   drop=drop)
+        return st, Act(out.view(N, a.H, a.W, C1 + C2), a.H, a.W, C1 + C2)
 
     def _apply(self, srcs, st, silu=True, drop=None):
         """Act of dropout(silu(GN(concat(srcs)))) materialised with dmc_gn_apply."""
@@ -495,10 +518,15 @@ class UNetExecutor(ExecCore):
         # a1 = SiLU(GN1(x)) materialised once (the 3x3 implicit GEMM reads every pixel 9x; the weight
         # gradient re-reads it in backward). Inference (no tape): where the halo kernel takes the conv, it
         # applies GN+SiLU to its LDS-resident halo instead and nothing is materialised.
-        st1 = self._gn(srcs, gn1)
+        fused = self._gn_apply_small(srcs, gn1, True)
+        st1 = fused[0] if fused else self._gn(srcs, gn1)
         h1 = self._new(N, H, W, Cout)
         off = self.temb_off[id(rb)]
-        if tape is None and self._halo_pro_ok(srcs, Cout, st1):
+        if fused:
+            a1 = fused[1]
+            self._conv([a1], conv1, K.TAPS3, H, W, Cout, bias=conv1.bias,
+                       addvec=self.addvec.view(self.addvec.shape[0], -1)[:, off:], ld_add=self._ld_add, out=h1.t, stats=h1)
+        elif tape is None and self._halo_pro_ok(srcs, Cout, st1):
             a1 = None
             self._conv(srcs, conv1, K.TAPS3, H, W, Cout, pro=(L.PRO_AFFINE_SILU, st1[0], st1[1]), bias=conv1.bias,
                        addvec=self.addvec.view(self.addvec.shape[0], -1)[:, off:], ld_add=self._ld_add, out=h1.t, stats=h1)
@@ -506,7 +534,6 @@ class UNetExecutor(ExecCore):
             a1 = self._apply(srcs, st1, silu=True)
             self._conv([a1], conv1, K.TAPS3, H, W, Cout, bias=conv1.bias,
                        addvec=self.addvec.view(self.addvec.shape[0], -1)[:, off:], ld_add=self._ld_add, out=h1.t, stats=h1)
-        st2 = self._gn([h1], gn2)
         if isinstance(rb.shortcut, torch.nn.Conv2d):
             s = torch.empty(N, H, W, Cout, dtype=self.dt, device=self.device)
             self._conv(srcs, rb.shortcut, K.TAPS1, H, W, Cout, bias=rb.shortcut.bias, out=s)
@@ -520,7 +547,12 @@ class UNetExecutor(ExecCore):
                 drop = drop + (self.seed_ptr,)
         self._blk_idx += 1
         out = self._new(N, H, W, Cout)
-        if tape is None and drop is None and self._halo_pro_ok([h1], Cout, st2):
+        fused = self._gn_apply_small([h1], gn2, True, drop)
+        st2 = fused[0] if fused else self._gn([h1], gn2)
+        if fused:
+            a2 = fused[1]
+            self._conv([a2], conv2, K.TAPS3, H, W, Cout, bias=conv2.bias, resid=resid, out=out.t, stats=out)
+        elif tape is None and drop is None and self._halo_pro_ok([h1], Cout, st2):
             a2 = None
             self._conv([h1], conv2, K.TAPS3, H, W, Cout, pro=(L.PRO_AFFINE_SILU, st2[0], st2[1]), bias=conv2.bias,
                        resid=resid, out=out.t, stats=out)
@@ -538,9 +570,13 @@ class UNetExecutor(ExecCore):
         Lq = H * W
         heads = ab.num_heads
         hd = C // heads
-        st = self._gn([a], ab.norm)
         qkv = self._new(N, H, W, 3 * C)
-        an = self._apply([a], st, silu=False)          # GroupNorm output (no SiLU in AttentionBlock, :86)
+        fused = self._gn_apply_small([a], ab.norm, False)
+        if fused:
+            st, an = fused
+        else:
+            st = self._gn([a], ab.norm)
+            an = self._apply([a], st, silu=False)      # GroupNorm output (no SiLU in AttentionBlock, :86)
         self._conv([an], ab.qkv, K.TAPS1, H, W, 3 * C, bias=ab.qkv.bias, out=qkv.t)
         st = (st, an)
         o = self._new(N, H, W, C)

@@ -177,6 +177,15 @@ int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C
                  const uint32_t* drop_seed_base, uint32_t drop_thresh, float drop_scale, void* out, int ld_out,
                  void* stream);
 
+/* dmc_gn_stats then dmc_gn_apply in ONE launch, bitwise the pair: one block per sample computes the statistics
+ * (mean_rstd / scale / shift as dmc_gn_stats writes them) and then writes the sample's a. Only for small samples
+ * (bf16, N >= 64, HW * C <= 8192: the UNet's 4x4 levels); dmc_gn_stats_apply_ok() says whether a shape qualifies. */
+int dmc_gn_stats_apply_ok(int dtype, int N, int HW, int C1, int C2, int G);
+int dmc_gn_stats_apply(int dtype, const void* x1, const void* x2, int N, int HW, int C1, int C2, int ld1, int ld2,
+                       int G, float eps, const float* gamma, const float* beta, float* mean_rstd, float* scale,
+                       float* shift, int silu, uint32_t drop_seed, const uint32_t* drop_seed_base,
+                       uint32_t drop_thresh, float drop_scale, void* out, int ld_out, void* stream);
+
 /* Backward of a = dropout(SiLU(GroupNorm(x))) (silu=1) or a = GroupNorm(x) (silu=0, AttentionBlock
  * norm :80): g = dL/da (dtype, [pix][ld_g]); writes
  * dx (split into dx1/dx2 by channel like the sources; accumulate_k: add into existing),

@@ -445,6 +445,36 @@ def test_groupnorm_stats_one_block_per_sample(shape, monkeypatch, dmc_opt):
         torch.testing.assert_close(a, b, rtol=2e-5, atol=2e-5)
 
 
+@pytest.mark.parametrize("case", [(128, 4, 4, 256, 0, 32, True, 0.0), (64, 4, 4, 256, 256, 32, True, 0.1),
+                                  (128, 4, 4, 512, 0, 32, False, 0.0), (64, 2, 2, 768, 256, 8, True, 0.3)])
+def test_gn_stats_apply_bitwise(case):
+    """dmc_gn_stats_apply (statistics + SiLU / dropout apply of a small sample in one launch, the UNet's 4x4 levels)
+    is BITWISE dmc_gn_stats followed by dmc_gn_apply: scale, shift, mean_rstd and the applied activation; the
+    shape gate rejects samples above 8192 elements and fp32."""
+    L, K = _lib()
+    torch.manual_seed(11)
+    N, H, W, C1, C2, G, silu, p = case
+    C, HW = C1 + C2, H * W
+    x = (torch.randn(N, H, W, C) * 1.3 + 0.4).to(torch.bfloat16).to(DEV)
+    x1, x2 = x[..., :C1].contiguous(), (x[..., C1:].contiguous() if C2 else None)
+    gamma, beta = (torch.rand(C) + 0.5).to(DEV), torch.randn(C).to(DEV)
+    drop = None
+    if p > 0:
+        thresh = int(p * 2 ** 32)
+        drop = (1234567, thresh, 1.0 / (1.0 - p))
+    assert K.gn_stats_apply_ok(torch.bfloat16, N, HW, C1, C2, G)
+    (sc, sh, mr), a = K.gn_stats_apply(torch.bfloat16, x1, x2, N, HW, C1, C2, C1, C2, G, 1e-5, gamma, beta, silu=silu,
+                                       drop=drop)
+    sc0, sh0, mr0 = K.gn_stats(torch.bfloat16, x1, x2, N, HW, C1, C2, C1, C2, G, 1e-5, gamma, beta)
+    a0 = K.gn_apply(torch.bfloat16, x1, x2, N, HW, C1, C2, C1, C2, sc0, sh0, silu=silu, drop=drop)
+    torch.cuda.synchronize()
+    for u, v in ((sc, sc0), (sh, sh0), (mr, mr0), (a, a0)):
+        assert torch.equal(u, v)
+    assert not K.gn_stats_apply_ok(torch.bfloat16, N, 64, 256, 0, 32)
+    assert not K.gn_stats_apply_ok(torch.float32, N, HW, C1, C2, G)
+    assert not K.gn_stats_apply_ok(torch.bfloat16, 32, HW, C1, C2, G)
+
+
 @pytest.mark.parametrize("shape", [(64, 8, 8, 256, 256), (128, 16, 16, 256, 0), (64, 4, 4, 384, 128)])
 def test_groupnorm_backward_one_block_per_sample(shape, monkeypatch, dmc_opt):
     """bf16 at N >= 64 and HW*C <= 64K: the per-channel sums and apply coefficients of a sample in one

@@ -108,6 +108,38 @@ def test_cifar_unet_inference_halo_prologue_bitwise(monkeypatch, dmc_opt):
     assert torch.equal(outs[0], outs[1])
 
 
+def test_cifar_unet_small_map_gn_stats_apply_bitwise(monkeypatch):
+    """The 4x4-level GroupNorms through dmc_gn_stats_apply (statistics + apply in one launch) give bitwise the
+    two-launch path: the bf16 inference output, and the training forward + backward (dropout 0.1) loss and every
+    parameter gradient."""
+    from diffusion_models_collection_amd.models import UNet
+    from diffusion_models_collection_amd.models import _unet_exec as E
+    cfg = dict(image_size=(32, 32), in_channels=3, model_channels=128, out_channels=3, num_res_blocks=2,
+               attention_resolutions=(16, 8), dropout=0.1, channel_mult=(1, 2, 2, 2), num_classes=None,
+               use_attention=True)
+    torch.manual_seed(46)
+    m = UNet(**cfg, compute_dtype="bf16").to(DEV)
+    x = torch.randn(64, 3, 32, 32, device=DEV)
+    t = torch.randint(0, 1000, (64,), device=DEV)
+    res = []
+    for on in (True, False):
+        monkeypatch.setattr(E, "_GN_SMALL_FUSE", on)
+        m.eval()
+        with torch.no_grad():
+            y = m(x, t).clone()
+        m.train()
+        m.zero_grad(set_to_none=True)
+        torch.manual_seed(7)
+        loss = m(x, t).float().square().mean()
+        loss.backward()
+        res.append((y, loss.detach().clone(), [p.grad.clone() for p in m.parameters()]))
+    ex = m.executor
+    assert any(ex._gsa_cache.values()), "dmc_gn_stats_apply never taken"
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    for a, b in zip(res[0][2], res[1][2]):
+        assert torch.equal(a, b)
+
+
 def test_cifar_unet_shared_timestep_broadcast():
     """Inference with a length-1 t (UNet.shared_timestep: the time-embedding MLPs on one row, broadcast by the conv
     epilogues with ld_add = 0) equals the per-image embedding with the same t in every row, within the fp32
