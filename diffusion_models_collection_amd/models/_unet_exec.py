@@ -48,9 +48,10 @@ _GN_DEFER = os.environ.get("DMC_GN_DEFER", "1") not in ("", "0")
 # The weight-gradient slab reductions deferred to one dmc_wgrad_reduce_batch per gradient segment (A/B switch
 # DMC_WG_DEFER=0: one reduce launch after each weight-gradient kernel)
 _WG_DEFER = os.environ.get("DMC_WG_DEFER", "1") not in ("", "0")
-# GroupNorm statistics + apply in one launch where a sample is a few KB (dmc_gn_stats_apply: the 4x4 levels);
-# a module switch for same-box A/Bs (scripts/r5_gsa.sh), not an option
-_GN_SMALL_FUSE = True
+# GroupNorm statistics + apply in one launch where a sample has at most this many elements (dmc_gn_stats_apply: the
+# 4x4 levels); 0 = off. A module switch for same-box A/Bs (scripts/r5_gsa.sh), not an option. 16384 (the 8x8 levels
+# too, in place of the conv-partial finalize + apply) measured neutral to slower
+_GN_SMALL_FUSE = 8192
 
 
 def _seed_from_torch():
@@ -343,11 +344,11 @@ class UNetExecutor(ExecCore):
     def _gn_apply_small(self, srcs, gn, silu, drop=None):
         """(stats, Act) of SiLU(GN(concat(srcs))) from ONE dmc_gn_stats_apply launch (bitwise _gn + _apply) where a
         sample is small enough for one block (the 4x4 levels); None elsewhere."""
-        if not _GN_SMALL_FUSE or any(s.part is not None for s in srcs):
-            return None
         a = srcs[0]
         b = srcs[1] if len(srcs) > 1 else None
         N, HW, C1, C2 = a.t.shape[0], a.H * a.W, a.C, (b.C if b else 0)
+        if HW * (C1 + C2) > _GN_SMALL_FUSE or any(s.part is not None for s in srcs):
+            return None     # (with conv partials the finalize path is taken, as before)
         key = (self.dt, N, HW, C1, C2, gn.num_groups, L.get_option("DMC_GN_STATS_SPLIT"))
         ok = self._gsa_cache.get(key)
         if ok is None:

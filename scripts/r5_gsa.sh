@@ -9,11 +9,11 @@ timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method threa
 tail -2 $O/tests.log
 A="--no-cpu --no-extra --no-dit --no-roofline --no-cfg"
 for r in 1 2; do
-  for on in 1 0; do
+  for on in 16384 8192; do
     timeout -k 10 300 python3 -c "
 import sys, runpy
 import diffusion_models_collection_amd.models._unet_exec as E
-E._GN_SMALL_FUSE = sys.argv[1] == '1'
+E._GN_SMALL_FUSE = int(sys.argv[1])
 sys.argv = ['bench.py'] + sys.argv[2:]
 runpy.run_path('bench.py', run_name='__main__')" $on $A > $O/b$on.json 2> $O/b$on.err || { tail $O/b$on.err; exit 1; }
     python3 -c "import json; d=json.loads(open('$O/b$on.json').read().strip().splitlines()[-1]); print('fuse=$on', d['value'], d['ddim50']['value'])"

@@ -122,7 +122,7 @@ def test_cifar_unet_small_map_gn_stats_apply_bitwise(monkeypatch):
     x = torch.randn(64, 3, 32, 32, device=DEV)
     t = torch.randint(0, 1000, (64,), device=DEV)
     res = []
-    for on in (True, False):
+    for on in (8192, 0):
         monkeypatch.setattr(E, "_GN_SMALL_FUSE", on)
         m.eval()
         with torch.no_grad():
