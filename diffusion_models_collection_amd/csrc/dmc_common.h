@@ -169,8 +169,8 @@ DMC_DEV float wave_max(float v) {
 
 // ---- GroupNorm statistics from conv-epilogue partials (mean, M2 per 64-pixel segment x 8-channel chunk) ----
 // Chan's combination of (n, m, q) with (nb, mb, qb).
-// The fused / unfused steps are spelled out (no contraction left to the compiler): the combine runs in several
-// kernels (dmc_gn_finalize, the producing conv's last block, the GroupNorm-prologue conv) that must agree bitwise.
+// The fused / unfused steps are spelled out (no contraction left to the compiler), so the combine is the same
+// arithmetic wherever it is compiled (round 4 also ran it inside the producing conv and the prologue conv).
 DMC_DEV void gn_chan(float& n, float& m, float& q, float nb, float mb, float qb) {
   const float tot = __fadd_rn(n, nb);
   if (tot == 0.f) return;
@@ -197,40 +197,9 @@ DMC_DEV void gn_group_tree(float cn, float m, float q, float eps, float& mean, f
   }
   gn_mean_rstd(cn, m, q, eps, mean, rstd);
 }
-// gn_group_stats in two halves for a caller that overlaps the loads with other memory traffic (the GroupNorm-prologue
-// halo conv): gn_group_fetch loads the lane's partials (t = lane, lane + 64: np <= 128), gn_group_reduce combines them
-// in gn_group_stats' order -- bitwise its (mean, rstd).
-struct GnLane { float m[2], q[2]; };
-DMC_DEV GnLane gn_group_fetch(const float* p1, int nch1, const float* p2, int nch2, int n, int g, int spi, int G) {
-  const int lane = threadIdx.x & 63;
-  const int C = 8 * (nch1 + nch2), cpg = C / G, kpg = cpg / 8, np = spi * kpg;
-  GnLane v = {{0.f, 0.f}, {0.f, 0.f}};
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int t = lane + 64 * k;
-    if (t < np) {
-      const int sg = n * spi + t / kpg, kc = g * kpg + t % kpg;
-      const float* pp = kc < nch1 ? p1 + ((size_t)sg * nch1 + kc) * 2 : p2 + ((size_t)sg * nch2 + (kc - nch1)) * 2;
-      const v2f w = *(const v2f*)pp;
-      v.m[k] = w[0];
-      v.q[k] = w[1];
-    }
-  }
-  return v;
-}
-DMC_DEV void gn_group_reduce(const GnLane& v, int np, float eps, float& mean, float& rstd) {
-  const int lane = threadIdx.x & 63;
-  float cn = 0.f, m = 0.f, q = 0.f;
-#pragma unroll
-  for (int k = 0; k < 2; ++k)
-    if (lane + 64 * k < np) gn_chan(cn, m, q, 512.f, v.m[k], v.q[k]);
-  gn_group_tree(cn, m, q, eps, mean, rstd);
-}
 // One wave combines GroupNorm group g of image n: lane l takes partials l, l+64, ... (segments outer, the group's
 // chunks inner; p1's chunks, then p2's), the lanes then combine over a fixed xor tree (deterministic). Returns
-// (mean, rstd) in every lane. SC1: the partials of p1 were handed off inside the running launch (write-through
-// stores + an arrival counter): read them with agent-scope (sc1) loads.
-template <bool SC1>
+// (mean, rstd) in every lane.
 DMC_DEV void gn_group_stats(const float* p1, int nch1, const float* p2, int nch2, int n, int g, int spi, int G,
                             float eps, float& mean, float& rstd) {
   const int lane = threadIdx.x & 63;
@@ -239,15 +208,7 @@ DMC_DEV void gn_group_stats(const float* p1, int nch1, const float* p2, int nch2
   for (int t = lane; t < np; t += 64) {
     const int sg = n * spi + t / kpg, kc = g * kpg + t % kpg;
     const float* pp = kc < nch1 ? p1 + ((size_t)sg * nch1 + kc) * 2 : p2 + ((size_t)sg * nch2 + (kc - nch1)) * 2;
-    float pm, pq;
-    if (SC1 && kc < nch1) {
-      pm = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      pq = __hip_atomic_load(pp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      pm = pp[0];
-      pq = pp[1];
-    }
-    gn_chan(cn, m, q, 512.f, pm, pq);
+    gn_chan(cn, m, q, 512.f, pp[0], pp[1]);
   }
   gn_group_tree(cn, m, q, eps, mean, rstd);
 }
@@ -256,9 +217,8 @@ DMC_DEV void gn_fold(float mean, float rstd, float gm, float bt, float& sc, floa
   sc = rstd * gm;
   sh = fmaf(-mean, sc, bt);
 }
-// One wave finalises group g of image n: gn_group_stats, then mean / rstd and the folded per-channel scale / shift.
-// Used by gn_finalize_kernel (dmc_norm.hip) and by the producing conv's last block (dmc_conv.hip): bitwise equal.
-template <bool SC1>
+// One wave finalises group g of image n: gn_group_stats, then mean / rstd and the folded per-channel scale / shift
+// (gn_finalize_kernel, dmc_norm.hip).
 DMC_DEV void gn_finalize_group(const float* p1, int nch1, const float* p2, int nch2, int n, int g, int spi, int G,
                                float eps, const float* gamma, const float* beta, float* mean_rstd, float* scale,
                                float* shift) {
@@ -270,7 +230,7 @@ DMC_DEV void gn_finalize_group(const float* p1, int nch1, const float* p2, int n
   const bool has_first = c_first < (g + 1) * cpg;
   const float gm0 = gamma && has_first ? gamma[c_first] : 1.f, bt0 = beta && has_first ? beta[c_first] : 0.f;
   float mean, rstd;
-  gn_group_stats<SC1>(p1, nch1, p2, nch2, n, g, spi, G, eps, mean, rstd);
+  gn_group_stats(p1, nch1, p2, nch2, n, g, spi, G, eps, mean, rstd);
   const size_t i = (size_t)n * G + g;
   if (lane == 0 && mean_rstd) { mean_rstd[i * 2] = mean; mean_rstd[i * 2 + 1] = rstd; }
   for (int c = c_first; c < (g + 1) * cpg; c += 64) {

@@ -1,9 +1,10 @@
 // GroupNorm statistics / backward and per-channel reductions for gfx950.
 //
 // GroupNorm(8, C, eps=1e-5, affine) of models/unet.py:35, :51, :80, :238 is split in two: the statistics
-// pass below (mean, rstd per (n, group) folded with gamma/beta into a per-(n, c) scale/shift), and the
-// apply, which is fused into the consumer convolution's prologue (dmc_conv.hip). The backward of
-// dropout(SiLU(GroupNorm(x))) is a per-channel reduction pass, a tiny finalize, and an apply pass.
+// pass below (mean, rstd per (n, group) folded with gamma/beta into a per-(n, c) scale/shift; at 32x32 / 16x16 from
+// the producing convs' epilogue partials, dmc_gn_finalize), and the apply: materialised by gn_apply_kernel (training,
+// and the small maps), or on the halo conv's resident tile in bf16 inference (dmc_conv.hip). The backward of
+// dropout(SiLU(GroupNorm(x))) is one pass per channel slice (gn_bwd_fused) or a reduction + finalize + apply.
 //
 // Every reduction is a fixed-order tree (no float atomics), so results are bitwise reproducible.
 // Access pattern: a thread owns one 16-byte chunk column of the NHWC rows and walks pixels, so each
@@ -1067,7 +1068,7 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(const float* p1, int n
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= N * G) return;
   const int n = i / G, g = i - n * G;
-  gn_finalize_group<false>(p1, nch1, p2, nch2, n, g, spi, G, eps, gamma, beta, mean_rstd, scale, shift);
+  gn_finalize_group(p1, nch1, p2, nch2, n, g, spi, G, eps, gamma, beta, mean_rstd, scale, shift);
 }
 }  // namespace
 
