@@ -9,15 +9,34 @@ graph, eagerly and in the eager loop's order (`buf.normal_()` is what `torch.ran
 loop computes bitwise what the eager loop computes (tests/test_gpu_model.py).
 
 A loop whose step reads nothing but its inputs, the sampler's tables and the model's weights may keep its graph
-on the model's executor across sample() calls (`cache=`): the key holds the sampler's settings, the input shapes
-and every parameter's (version, pointer) plus the executor's weight generation (bumped by the fused optimizer /
-EMA kernels that write the parameters behind torch's back), so any weight update recaptures. Without a cache
-key a graph lives for one call.
+on the sampler across sample() calls (`cache=`): the key holds the sampler's settings, the executor, the input
+shapes and every parameter's (version, pointer) plus the executor's weight generation (bumped by the fused
+optimizer / EMA kernels that write the parameters behind torch's back), so any weight update recaptures. The
+entry holds the executor only weakly. (Not on the executor itself: model and executor reference each other, so
+they are freed by the cyclic collector, at whatever moment it runs -- possibly while this thread captures another
+graph, where destroying a graph is illegal.) Without a cache key a graph lives for one call.
 """
 import collections
+import contextlib
+import gc
 import os
+import weakref
 
 import torch
+
+
+@contextlib.contextmanager
+def gc_paused():
+    """No cyclic garbage collection while a graph is captured: a collection can free an unreachable model's HIP
+    graphs and memory, which is illegal on a capturing thread (seen as an abort inside a capture)."""
+    was = gc.isenabled()
+    gc.collect()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 class StepGraph:
@@ -28,7 +47,7 @@ class StepGraph:
         self.const = frozenset(const)
         self.seen = [(x, x._version) for x in inputs]
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):   # see utils/trainer.py begin()
+        with gc_paused(), torch.cuda.graph(self.graph, capture_error_mode="thread_local"):   # see trainer.py begin()
             self.out = fn(*self.static)
 
     def step(self, *inputs):
@@ -66,13 +85,13 @@ _CACHE_MAX = 2      # graphs kept per executor (each holds its activation pool)
 
 
 def cache_for(model, tag, owner, x):
-    """(store, key, owner) for run_loop(cache=...): owner = the sampler whose tables the step reads (kept alive by
-    the entry, so its id cannot be reused while the graph is). None for a model without an executor."""
+    """(store, key, executor) for run_loop(cache=...): the store lives on `owner`, the sampler whose tables the step
+    reads. None for a model without an executor."""
     ex = getattr(model, "executor", None)
     if ex is None:
         return None
-    store = ex.__dict__.setdefault("_step_graphs", collections.OrderedDict())
-    return store, (tag, id(owner), tuple(x.shape), x.dtype, x.device, StepGraph.weights_key(model)), owner
+    store = owner.__dict__.setdefault("_step_graphs", collections.OrderedDict())
+    return store, (tag, id(ex), tuple(x.shape), x.dtype, x.device, StepGraph.weights_key(model)), ex
 
 
 def run_loop(x, nsteps, make_inputs, fn, use_graph, record=None, cache=None, const=()):
@@ -81,9 +100,9 @@ def run_loop(x, nsteps, make_inputs, fn, use_graph, record=None, cache=None, con
     cache (cache_for) a graph from an earlier call with the same key replays from step 0."""
     graph = None
     if use_graph and cache is not None:
-        store, key, _ = cache
+        store, key, ex = cache
         hit = store.get(key)
-        if hit is not None:
+        if hit is not None and hit[0]() is ex:   # the same live executor (an id can be reused after a free)
             store.move_to_end(key)
             graph = hit[1]
     for i in range(nsteps):
@@ -100,8 +119,8 @@ def run_loop(x, nsteps, make_inputs, fn, use_graph, record=None, cache=None, con
                 from ..utils.trainer import GraphCaptureError
                 raise GraphCaptureError(f"sampling step capture failed at step {i}: {e!r}") from e
             if cache is not None:
-                store, key, owner = cache
-                store[key] = (owner, graph)
+                store, key, ex = cache
+                store[key] = (weakref.ref(ex), graph)
                 while len(store) > _CACHE_MAX:
                     store.popitem(last=False)
         x = graph.step(*args) if graph is not None else fn(*args)

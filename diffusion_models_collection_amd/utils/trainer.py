@@ -436,8 +436,10 @@ class GraphedTrainStep:
             if self.graph is not None:
                 return None           # one captured shape (the last, ragged batch of an epoch runs eagerly)
             prev = torch.cuda.current_stream()
+            from ..diffusion._graph import gc_paused
             try:
-                self._capture(images, y)
+                with gc_paused():
+                    self._capture(images, y)
                 self.key = key
             except Exception as e:    # noqa: BLE001
                 # loud: round 3 saw the eager retry of a failed capture fail on the same stream ("operation
