@@ -9,7 +9,7 @@ timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method threa
 tail -2 $O/tests.log
 A="--no-cpu --no-extra --no-dit --no-roofline --no-cfg"
 for r in 1 2; do
-  for on in 16384 8192; do
+  for on in 8192 0; do
     timeout -k 10 300 python3 -c "
 import sys, runpy
 import diffusion_models_collection_amd.models._unet_exec as E
