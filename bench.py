@@ -255,13 +255,18 @@ def cpu_ddim_baseline(B=16, S=50):
 
 
 def train_rate(trainer, pool, steps, warmup, world):
-    """Time `steps` train steps after `warmup`, barrier + synchronize on both sides, max over ranks."""
+    """Time `steps` train steps after `warmup`, barrier + synchronize on both sides, max over ranks. A graphed trainer
+    warms up at least GraphedTrainStep.WARM + 1 steps, so its capture (after WARM eager steps) and first replay are
+    never inside the timed region (trainer._bench_warmup: the warm-up steps actually run)."""
+    g = getattr(trainer, "_graph", None)
+    if g is not None:
+        warmup = max(warmup, g.WARM + 1)
+    trainer._bench_warmup = warmup
     for i in range(warmup):
         trainer.train_step(pool[i % len(pool)], 0)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    g = getattr(trainer, "_graph", None)
     w0 = g.ring_wait_s if g is not None else 0.0
     r0 = g.replays if g is not None else 0
     t0 = time.perf_counter()
@@ -550,6 +555,8 @@ def main():
            "train_tflops_per_gpu": round(value / world * gflop / 1e3, 2)}
     graphed = bool(getattr(trainer, "_bench_graphed", False))
     out["graphed"] = graphed if not args.no_train else None
+    if not args.no_train and trainer._bench_warmup != args.warmup:
+        out["warmup_run"] = trainer._bench_warmup     # raised so that the graph capture is not timed
     if args.no_train:
         out["value"] = None
     elif not graphed and os.environ.get("DMC_GRAPH", "1") != "0":
@@ -607,13 +614,14 @@ def main():
         pool64 = [torch.rand(B, 3, 64, 64, device=dev, generator=gen) * 2 - 1 for _ in range(2)]
         m64.train()
         e64, _ = train_rate(tr64, pool64, 5, 3, world)
+        graphed64 = tr64._bench_graphed
         m64.eval()
         d100 = DDIM(1000, 100, device=dev)
         s64 = sample_rate(lambda: d100.sample(m64, (B, 3, 64, 64)), world)
         gf64 = unet_flops_per_image(m64) / 1e9
         out["celeba64"] = {"train_img_s": round(world * B * 5 / e64, 2), "train_ms_per_step": round(e64 / 5 * 1e3, 3),
                            "ddim100_img_s": round(world * B / s64, 2), "ddim100_seconds": round(s64, 3),
-                           "batch_per_gpu": B, "dtype": args.dtype, "steps_timed": 5,
+                           "batch_per_gpu": B, "dtype": args.dtype, "steps_timed": 5, "graphed": graphed64,
                            "gflop_per_forward_img": round(gf64, 3),
                            "train_tflops_per_gpu": round(B * 5 / e64 * 3 * gf64 / 1e3, 2),
                            "roofline": loop_roofline(B * 5 * 3 * gf64 * 1e9, e64, "64x64 train step (fwd + bwd = 3x "
@@ -624,9 +632,10 @@ def main():
             # the reference's own arithmetic (fp32) on the same step, for comparison with the bf16 headline
             mf, trf = make_trainer(CIFAR, "fp32", dev, rank, world)
             mf.train()
-            ef, _ = train_rate(trf, pool, 5, 2, world)
+            ef, _ = train_rate(trf, pool, 5, 3, world)
             out["fp32"] = {"train_img_s": round(world * B * 5 / ef, 2), "train_ms_per_step": round(ef / 5 * 1e3, 3),
-                           "steps_timed": 5, "note": "exact-fp32 MFMA (v_mfma_f32_16x16x4f32) parity mode"}
+                           "steps_timed": 5, "warmup": trf._bench_warmup, "graphed": trf._bench_graphed,
+                           "note": "exact-fp32 MFMA (v_mfma_f32_16x16x4f32) parity mode"}
             del mf, trf
     if rank == 0 and not args.no_roofline:
         out["roofline"] = conv_roofline(dtype)

@@ -12,9 +12,13 @@ A loop whose step reads nothing but its inputs, the sampler's tables and the mod
 on the sampler across sample() calls (`cache=`): the key holds the sampler's settings, the executor, the input
 shapes and every parameter's (version, pointer) plus the executor's weight generation (bumped by the fused
 optimizer / EMA kernels that write the parameters behind torch's back), so any weight update recaptures. The
-entry holds the executor only weakly. (Not on the executor itself: model and executor reference each other, so
-they are freed by the cyclic collector, at whatever moment it runs -- possibly while this thread captures another
-graph, where destroying a graph is illegal.) Without a cache key a graph lives for one call.
+entry holds the executor only weakly and is dropped once that executor is gone. Without a cache key a graph lives
+for one call.
+
+Destroying a HIP graph while this thread captures another is illegal. Round 5 saw exactly that: a dropped model
+(then tied to its executor by a reference cycle) was freed by a cyclic collection that ran inside a capture. The
+package's objects now hold no cycles (the executor refers to its model weakly), so they are freed at the `del`; as a
+guard for cycles in user code, cyclic collection is paused during every capture (gc_paused).
 """
 import collections
 import contextlib
@@ -27,10 +31,10 @@ import torch
 
 @contextlib.contextmanager
 def gc_paused():
-    """No cyclic garbage collection while a graph is captured: a collection can free an unreachable model's HIP
-    graphs and memory, which is illegal on a capturing thread (seen as an abort inside a capture)."""
+    """No cyclic garbage collection while a graph is captured: a collection can free an unreachable object's HIP
+    graphs and memory, which is illegal on a capturing thread (seen as an abort inside a capture). No collection is
+    forced here either (it would land inside whatever the caller times)."""
     was = gc.isenabled()
-    gc.collect()
     gc.disable()
     try:
         yield
@@ -45,7 +49,9 @@ class StepGraph:
         a different tensor, or a new torch version of it, is handed in."""
         self.static = [x.clone() for x in inputs]
         self.const = frozenset(const)
-        self.seen = [(x, x._version) for x in inputs]
+        # const inputs: (weak reference, version) of the tensor last copied in -- no strong reference to the caller's
+        # tensors outlives the call
+        self.seen = [(weakref.ref(x), x._version) if i in self.const else None for i, x in enumerate(inputs)]
         self.graph = torch.cuda.CUDAGraph()
         with gc_paused(), torch.cuda.graph(self.graph, capture_error_mode="thread_local"):   # see trainer.py begin()
             self.out = fn(*self.static)
@@ -54,10 +60,11 @@ class StepGraph:
         for i, (s, x) in enumerate(zip(self.static, inputs)):
             if x is None or x is s:
                 continue
-            if i in self.const and self.seen[i][0] is x and self.seen[i][1] == x._version:
+            if i in self.const and self.seen[i][0]() is x and self.seen[i][1] == x._version:
                 continue
             s.copy_(x)
-            self.seen[i] = (x, x._version)
+            if i in self.const:
+                self.seen[i] = (weakref.ref(x), x._version)
         self.graph.replay()
         return self.out
 
@@ -91,6 +98,8 @@ def cache_for(model, tag, owner, x):
     if ex is None:
         return None
     store = owner.__dict__.setdefault("_step_graphs", collections.OrderedDict())
+    for k in [k for k, (ref, _) in store.items() if ref() is None]:
+        del store[k]       # a freed executor's graph (and its activation pool) goes with it
     return store, (tag, id(ex), tuple(x.shape), x.dtype, x.device, StepGraph.weights_key(model)), ex
 
 

@@ -209,6 +209,13 @@ class WgradDefer:
     def end_segment(self):
         self.flush()
 
+    def reset(self):
+        """Drop every pending job unreduced and recycle the arena. A backward starts with this: one that
+        raised part-way (an OOM, a capture error the caller survived) leaves jobs holding raw slab / dw pointers that
+        the next backward's first flush would otherwise replay onto reused buffers."""
+        self.jobs = []
+        self.off = 0
+
 
 def wgrad(d, dy, ld_dy, x1, x2, dw, scale=1.0, dbias=None, defer=None):
     """dmc_conv2d_wgrad: dw (and with dbias the bias gradient, the pixel sums of dy) from one pass over dy. With

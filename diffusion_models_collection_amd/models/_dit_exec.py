@@ -48,7 +48,7 @@ class _W:
 
 class DiTExecutor(ExecCore):
     def __init__(self, model):
-        self.m = model
+        self._bind_model(model)
         self.dt = model.compute_dtype
         self.cdt = L.dtype_code(self.dt)
         self.chunk = L.chunk_for(self.dt)

@@ -21,6 +21,7 @@ import contextlib
 import ctypes
 import math
 import os
+import weakref
 from typing import List, Optional
 
 import torch
@@ -70,12 +71,12 @@ class _PackCache:
     """
 
     def __init__(self, owner):
-        self.owner = owner
+        self._owner = weakref.ref(owner)   # the executor owns the cache: no reference cycle back to it
         self.entries = {}
         self._batch = None
 
     def _ver(self, srcs):
-        return (self.owner.wgen,) + tuple((s._version, s.data_ptr()) for s in srcs)
+        return (self._owner().wgen,) + tuple((s._version, s.data_ptr()) for s in srcs)
 
     def get(self, key, srcs, make_buf, make_jobs):
         v = self._ver(srcs)
@@ -110,7 +111,24 @@ class _PackCache:
 class ExecCore:
     """What every backbone executor shares: weight packing through the pack cache, the generic implicit-GEMM conv
     / weight-gradient launchers over 1-2 NHWC sources, activation allocation and views of the flat gradient
-    buffer. Subclasses set self.dt, self.packs, self.device, self.training_grad_scale, self.pindex, self.goff."""
+    buffer. Subclasses set self.dt, self.packs, self.device, self.training_grad_scale, self.pindex, self.goff, and
+    bind their model with _bind_model."""
+
+    def _bind_model(self, model):
+        self._mref = weakref.ref(model)
+
+    @property
+    def m(self):
+        """The backbone, held weakly. model._executor -> executor is the only strong edge between the two (and the
+        executor's pack cache / GradSync / graphed step refer back to it weakly too), so a dropped model frees its
+        executor -- tape arenas, packed weights, flat gradients -- by reference counting at the `del`, never by the
+        cyclic collector at an arbitrary later moment: round 5 saw such a collection free a dropped model's HIP graphs
+        in the middle of another graph's capture and abort the process (tests/test_gpu_model.py
+        test_dropped_model_frees_without_cyclic_gc)."""
+        m = self._mref()
+        if m is None:
+            raise RuntimeError("the model this executor ran has been freed")
+        return m
 
     def _gview(self, flat, p):
         i = self.pindex[id(p)]
@@ -204,7 +222,7 @@ class ExecCore:
 
 class UNetExecutor(ExecCore):
     def __init__(self, model):
-        self.m = model
+        self._bind_model(model)
         self.dt = model.compute_dtype
         self.cdt = L.dtype_code(self.dt)
         self.chunk = L.chunk_for(self.dt)
@@ -607,6 +625,7 @@ class UNetExecutor(ExecCore):
         if _WG_DEFER:
             if getattr(self, "_wg_arena", None) is None:
                 self._wg_arena = K.WgradDefer()
+            self._wg_arena.reset()      # nothing left over from a backward that raised part-way
             self._wg_defer = self._wg_arena
         if hook is not None:
             order = sorted(range(len(self.params)), key=lambda i: self.goff[i])
@@ -619,25 +638,31 @@ class UNetExecutor(ExecCore):
         ci = next(i for i, r in enumerate(recs) if r[0] == "conv_in")
         if ci < ti:
             recs.insert(ci, recs.pop(ti))
-        for ri, rec in enumerate(recs):
-            kind = rec[0]
-            last = ri == len(recs) - 1
-            self._backward_record(rec, dout, gv)
-            if kind == "conv_in" and rec[3]:
-                dx = self._dx
-            if hook is not None:
-                # this record's grads are final: publish the finished prefix of the flat buffer
-                for p in self._record_params(rec):
-                    final[self.pindex[id(p)]] = True
-                while cursor < len(order) and final[order[cursor]]:
-                    cursor += 1
-                hi = self.goff[order[cursor]] if cursor < len(order) else self.gtotal
-                if getattr(hook, "wants", None) is None or hook.wants(hi, last):
-                    self._flush_gn()       # the deferred GroupNorm parameter sums and weight-gradient reductions
-                hook(flat, hi, last)
-        self._flush_gn()
-        self._gn_defer = None
-        self._wg_defer = None
+        try:
+            for ri, rec in enumerate(recs):
+                kind = rec[0]
+                last = ri == len(recs) - 1
+                self._backward_record(rec, dout, gv)
+                if kind == "conv_in" and rec[3]:
+                    dx = self._dx
+                if hook is not None:
+                    # this record's grads are final: publish the finished prefix of the flat buffer
+                    for p in self._record_params(rec):
+                        final[self.pindex[id(p)]] = True
+                    while cursor < len(order) and final[order[cursor]]:
+                        cursor += 1
+                    hi = self.goff[order[cursor]] if cursor < len(order) else self.gtotal
+                    if getattr(hook, "wants", None) is None or hook.wants(hi, last):
+                        self._flush_gn()       # the deferred GroupNorm parameter sums and weight-gradient reductions
+                    hook(flat, hi, last)
+            self._flush_gn()
+        except BaseException:
+            if self._wg_defer is not None:
+                self._wg_defer.reset()  # unflushed jobs point at buffers the caller may free or reuse
+            raise
+        finally:
+            self._gn_defer = None
+            self._wg_defer = None
         self.daddvec = None
         grads = [self._gview(flat, p) for p in self.params]
         return dx, grads

@@ -18,6 +18,7 @@ What changes (MI355X-first):
 """
 import math
 import time
+import weakref
 from pathlib import Path
 
 import torch
@@ -51,7 +52,8 @@ class GradSync:
     """
 
     def __init__(self, executor, process_group=None, bucket_bytes=25 * 1024 * 1024, force_avg=False):
-        self.ex = executor
+        self._ex = weakref.ref(executor)    # the executor holds self.hook: no cycle back to it
+        self.gtotal = executor.gtotal
         self.pg = process_group
         self.bucket = bucket_bytes // 4
         self.works = []
@@ -73,7 +75,7 @@ class GradSync:
 
     def wants(self, hi, final):
         """Whether hook(flat, hi, final) will issue an all-reduce (the executor then joins its side stream)."""
-        return final or self.cut(hi, self.done, self.ex.gtotal, final)
+        return final or self.cut(hi, self.done, self.gtotal, final)
 
     def hook(self, flat, hi, final):
         if self.cut(hi, self.done, flat.numel(), final):
@@ -261,7 +263,7 @@ class GraphedTrainStep:
     RING = 4
 
     def __init__(self, trainer):
-        self.tr = trainer
+        self._tr = weakref.ref(trainer)     # the trainer holds this step (trainer._graph): no cycle back to it
         self.calls = 0
         self.replays = 0
         self.ring_wait_s = 0.0       # host seconds spent waiting for a pinned ring slot (paces the host to the GPU)
@@ -270,6 +272,10 @@ class GraphedTrainStep:
         self.key = None
         self.measure_comm = False
         self.comm_events = []
+
+    @property
+    def tr(self):
+        return self._tr()
 
     @staticmethod
     def supported(trainer):
@@ -438,7 +444,7 @@ class GraphedTrainStep:
             prev = torch.cuda.current_stream()
             from ..diffusion._graph import gc_paused
             try:
-                with gc_paused():
+                with gc_paused():   # a guard: the package's own objects hold no reference cycles
                     self._capture(images, y)
                 self.key = key
             except Exception as e:    # noqa: BLE001

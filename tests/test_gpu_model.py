@@ -83,9 +83,22 @@ def test_cifar_unet_matches_oracle(dtype):
     assert rel(out2, out[:2]) < (1e-5 if dtype == "fp32" else 1e-2)
 
 
-def test_cifar_unet_inference_halo_prologue_bitwise(monkeypatch, dmc_opt):
+@pytest.mark.parametrize("reg_epi", [2, 0, 3])
+def test_cifar_unet_inference_halo_prologue_bitwise(reg_epi, monkeypatch, dmc_opt):
     """bf16 inference at B=128 with DMC_HALO_PRO=1 (the default): the ResBlock convs that take the GN+SiLU
-    prologue on the halo kernel (dmc_conv_halo_prologue) give bitwise the output of the materialised path."""
+    prologue on the halo kernel (dmc_conv_halo_prologue) give bitwise the output of the materialised path when both
+    arms use the same conv epilogue everywhere: DMC_REG_EPI=2 (every eligible tile from the accumulators) and 0
+    (every tile LDS-staged).
+
+    The shipped default DMC_REG_EPI=3 (register epilogue everywhere BUT the prologue halo kernel, measured faster for
+    the sampling loops) cannot be bitwise equal to the materialised path: there the prologue conv's tiles run the
+    LDS-staged epilogue while the materialised arm's plain halo conv runs the register one, and the two fold the
+    GroupNorm partials of the stored output in different fp32 summation orders (per lane over 4 pixels then xor
+    shuffles, vs rows through LDS: dmc_conv.hip reg_epilogue / tile_epilogue8) -- the stored bf16 outputs are
+    identical (test_gpu_kernels.py::test_reg_epilogue_bitwise_lds_staged) but the next GroupNorm's mean / rstd differ
+    in the last fp32 bits, which flips bf16 roundings downstream. For 3 the two arms are therefore compared within
+    a tolerance (5e-3 of max |out|, cosine > 0.99999), and a bitwise comparison is asserted on the FIRST ResBlock's
+    conv1 output, before any such statistic has been consumed."""
     from diffusion_models_collection_amd.models import UNet
     torch.manual_seed(42)
     cfg = dict(image_size=(32, 32), in_channels=3, model_channels=128, out_channels=3, num_res_blocks=2,
@@ -95,9 +108,7 @@ def test_cifar_unet_inference_halo_prologue_bitwise(monkeypatch, dmc_opt):
     x = torch.randn(128, 3, 32, 32, device=DEV)
     t = torch.randint(0, 1000, (128,), device=DEV)
     outs = []
-    # the same epilogue in both arms (the default DMC_REG_EPI=3 keeps the prologue kernel on the LDS-staged one,
-    # whose GroupNorm partials combine in another order)
-    dmc_opt("DMC_REG_EPI", 2)
+    dmc_opt("DMC_REG_EPI", reg_epi)
     for on in ("1", "0"):
         dmc_opt("DMC_HALO_PRO", int(on))
         with torch.no_grad():
@@ -105,7 +116,32 @@ def test_cifar_unet_inference_halo_prologue_bitwise(monkeypatch, dmc_opt):
     ex = m._executor if hasattr(m, "_executor") else None
     if ex is not None:
         assert any(v for k, v in ex._halo_pro_cache.items() if k[-1] == 1), "halo prologue never taken"
-    assert torch.equal(outs[0], outs[1])
+    if reg_epi != 3:
+        assert torch.equal(outs[0], outs[1])
+        return
+    e, c = rel(outs[0], outs[1]), cos(outs[0], outs[1])
+    print(f"DMC_REG_EPI=3: prologue vs materialised out rel {e:.3e} cos {c:.7f}")
+    assert e < 5e-3 and c > 0.99999, (e, c)
+    # the first ResBlock's conv1 output h1 (its input statistics come from the input conv in both arms) is bitwise:
+    # captured as the input of the second GroupNorm the forward computes (models/_unet_exec.py _res_fwd: gn1 on the
+    # input conv's output, then gn2 on h1)
+    from diffusion_models_collection_amd.models import _unet_exec as E
+    seen = []
+    orig = E.UNetExecutor._gn
+
+    def gn_spy(self, srcs, gn, dtype=None):
+        seen.append(srcs[0].t.clone() if len(seen) == 1 else None)
+        return orig(self, srcs, gn, dtype)
+
+    monkeypatch.setattr(E.UNetExecutor, "_gn", gn_spy)
+    h1 = []
+    for on in ("1", "0"):
+        dmc_opt("DMC_HALO_PRO", int(on))
+        seen.clear()
+        with torch.no_grad():
+            m(x, t)
+        h1.append(seen[1])
+    assert torch.equal(h1[0], h1[1])
 
 
 def test_cifar_unet_small_map_gn_stats_apply_bitwise(monkeypatch):
@@ -784,3 +820,107 @@ def test_ema_sampling_sees_unfused_ema_updates(tmp_path):
     third = ddim.sample(fresh, (2, 3, 16, 16), None, x_T=xT)
     assert not torch.equal(first, second)
     assert torch.equal(second, third)
+
+
+# ------------------------------------------------------------------------------------------------------------
+# round 6: object lifetimes around graph captures, a backward that raised part-way
+# ------------------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("backbone", ["unet", "dit"])
+def test_dropped_model_frees_without_cyclic_gc(backbone, tmp_path, monkeypatch):
+    """the precondition of round 5's capture abort, built deterministically. A model whose DDIM step
+    graph is cached on the sampler is dropped with the cyclic collector OFF: the model and its executor must be
+    freed at the `del` (no model <-> executor cycle), the sampler's dead cache entry is pruned at its next lookup,
+    and a training-step graph capture afterwards succeeds and replays (so nothing of the dropped model is left to
+    be freed inside a capture)."""
+    import gc
+    import weakref
+    from diffusion_models_collection_amd.models import UNet, DiT
+    from diffusion_models_collection_amd.diffusion import DDIM, DDPM
+    from diffusion_models_collection_amd.utils.trainer import DiffusionTrainer
+    monkeypatch.setenv("DMC_GRAPH", "1")
+    up = dict(image_size=(16, 16), in_channels=3, model_channels=32, out_channels=3, num_res_blocks=1,
+              attention_resolutions=(8,), dropout=0.1, channel_mult=(1, 2), use_attention=True)
+    dp = dict(img_size=(16, 16), patch_size=2, in_channels=3, hidden_size=64, depth=2, num_heads=2, mlp_ratio=4.0)
+
+    def make():
+        torch.manual_seed(0)
+        return (UNet(**up, compute_dtype="bf16") if backbone == "unet" else DiT(**dp, compute_dtype="bf16")).to(DEV)
+
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        ddim = DDIM(1000, 4, device=DEV)
+        m = make().eval()
+        with torch.no_grad():
+            ddim.sample(m, (4, 3, 16, 16))
+        assert len(ddim._step_graphs) == 1                      # a graph cached on the sampler
+        wm, we = weakref.ref(m), weakref.ref(m.executor)
+        del m
+        assert wm() is None and we() is None, "model / executor not freed by reference counting"
+        m2 = make()
+        opt = torch.optim.AdamW(m2.parameters(), lr=1e-4)
+        cfg = {"epochs": 1, "save_dir": str(tmp_path / "c"), "sample_dir": str(tmp_path / "s"), "loss_type": "l2",
+               "use_ema": True, "ema_decay": 0.99, "model_type": backbone,
+               "model_params": dict(up) if backbone == "unet" else dict(dp)}
+        tr = DiffusionTrainer(m2, DDPM(device=DEV), None, opt, None, device=DEV, config=cfg)
+        m2.train()
+        gen = torch.Generator().manual_seed(3)
+        for i in range(4):
+            loss = tr.train_step((torch.rand(4, 3, 16, 16, generator=gen) * 2 - 1).to(DEV), i)
+        assert tr._graph.graph is not None and not tr._graph.failed and tr._graph.replays >= 1
+        assert torch.isfinite(loss).all()
+        m2.eval()
+        with torch.no_grad():
+            ddim.sample(m2, (4, 3, 16, 16))
+        assert all(ref() is not None for ref, _ in ddim._step_graphs.values())   # the dead entry was pruned
+        wt, wg = weakref.ref(tr), weakref.ref(tr._graph)
+        del tr
+        assert wt() is None and wg() is None, "trainer / graphed step not freed by reference counting"
+    finally:
+        if was:
+            gc.enable()
+
+
+def test_backward_raising_midway_leaves_no_stale_reductions(monkeypatch):
+    """a backward that raises part-way (after some weight gradients deferred their slab reductions) must
+    not leak those pending reductions into the next backward: the next p_losses + backward gives bitwise the
+    gradients of a fresh model that never failed."""
+    from diffusion_models_collection_amd.models import UNet
+    from diffusion_models_collection_amd.models import _unet_exec as E
+    from diffusion_models_collection_amd.diffusion import DDPM
+    mp = dict(image_size=(16, 16), in_channels=3, model_channels=32, out_channels=3, num_res_blocks=1,
+              attention_resolutions=(8,), dropout=0.0, channel_mult=(1, 2), use_attention=True)
+    ddpm = DDPM(device=DEV)
+    gen = torch.Generator().manual_seed(9)
+    x0 = (torch.rand(8, 3, 16, 16, generator=gen) * 2 - 1).to(DEV)
+    t = torch.randint(0, 1000, (8,), generator=gen).to(DEV)
+    noise = torch.randn(8, 3, 16, 16, generator=gen).to(DEV)
+
+    def grads(m):
+        m.zero_grad(set_to_none=True)
+        ddpm.p_losses(m, x0, t, noise=noise).backward()
+        return [p.grad.clone() for p in m.parameters()]
+
+    torch.manual_seed(0)
+    ref = grads(UNet(**mp, compute_dtype="bf16").to(DEV).train())
+    torch.manual_seed(0)
+    m = UNet(**mp, compute_dtype="bf16").to(DEV).train()
+    orig = E.UNetExecutor._backward_record
+    calls = {"n": 0}
+
+    def flaky(self, rec, dout, gv):
+        # fail at the first record boundary with deferred reductions pending (after at least one record)
+        calls["n"] += 1
+        if calls["n"] >= 2 and not calls.get("hit") and self._wg_defer is not None and self._wg_defer.jobs:
+            calls["hit"] = True
+            raise RuntimeError("injected failure mid-backward")
+        return orig(self, rec, dout, gv)
+
+    monkeypatch.setattr(E.UNetExecutor, "_backward_record", flaky)
+    with pytest.raises(RuntimeError, match="injected"):
+        grads(m)
+    monkeypatch.setattr(E.UNetExecutor, "_backward_record", orig)
+    assert m.executor._wg_defer is None and not m.executor._wg_arena.jobs
+    got = grads(m)
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)

@@ -724,3 +724,90 @@ def test_cifar_unet_b128_grads_match_oracle(dtype, cifar_b128_oracle_grads):
     else:
         assert lrel < 1e-3, lrel
         assert abs(tot_g - tot_r) < 2e-3 * tot_r
+
+
+# ----------------------------------------------------------------------------------------------------------
+# BASELINE config #5's sampling plan (64x64, B=128, bf16 inference) pinned
+# ----------------------------------------------------------------------------------------------------------
+def _halo_pro_taken_at(ex, width):
+    """Whether the executor ran a 3x3 conv of `width`-pixel rows with the GN+SiLU prologue on the halo kernel."""
+    return any(v for k, v in ex._halo_pro_cache.items() if k[2] == width and k[-1] == 1)
+
+
+def test_unet_64x64_b128_eval_rows_match_oracle():
+    """BASELINE config #5's inference plan: the CIFAR network at image_size (64, 64), B=128, bf16, eval, default
+    plans -- the 64-pixel-row halo conv with the GroupNorm+SiLU prologue (conv3x3_halo2_kernel<9,2,true>), the
+    default register epilogue (DMC_REG_EPI=3), split-K at 8x8 -- against the oracle (models/unet.py:243-292) run on
+    rows {0, 1, 127} alone, and the per-sample p_losses of those rows (diffusion/ddpm.py:106-140). The bf16
+    tolerance of test_cifar_unet_b128_rows_match_oracle: 5e-2 of max |ref|, cosine > 0.999, per-sample loss 2e-2."""
+    from diffusion_models_collection_amd import _lib as L
+    from diffusion_models_collection_amd.models import UNet
+    from diffusion_models_collection_amd.diffusion import DDPM
+    from oracle.unet_oracle import make_oracle
+    from oracle import diffusion_oracle as DO
+    assert L.get_option("DMC_HALO_PRO") == 1 and L.get_option("DMC_REG_EPI") == 3   # the shipped defaults
+    cfg = dict(CIFAR, image_size=(64, 64), dropout=0.1)
+    torch.manual_seed(42)
+    m = UNet(**cfg, compute_dtype="bf16").to(DEV).eval()
+    orc, _ = make_oracle(m.state_dict(), cfg)
+    gen = torch.Generator().manual_seed(17)
+    x0 = torch.rand(128, 3, 64, 64, generator=gen) * 2 - 1
+    t = torch.randint(0, 1000, (128,), generator=gen)
+    noise = torch.randn(128, 3, 64, 64, generator=gen)
+    ddpm = DDPM(device=DEV)
+    xt = ddpm.q_sample(x0.to(DEV), t.to(DEV), noise.to(DEV))
+    with torch.no_grad():
+        out = m(xt, t.to(DEV)).float().cpu()
+    assert _halo_pro_taken_at(m.executor, 64), "the 64-wide halo prologue plan was not taken"
+    rows = [0, 1, 127]
+    xr = DO.q_sample(DO.schedule(), x0[rows], t[rows], noise[rows])
+    with torch.no_grad():
+        ref = orc.forward(xr, t[rows], None)
+    got = out[rows]
+    lg = ((got - noise[rows]) ** 2).mean(dim=(1, 2, 3))
+    lr = ((ref - noise[rows]) ** 2).mean(dim=(1, 2, 3))
+    e, c, le = rel(got, ref), cos(got, ref), ((lg - lr).abs() / lr.abs()).max().item()
+    print(f"64x64 B=128 bf16 eval: rows {rows} out rel {e:.3e} cos {c:.6f}; per-sample loss rel {le:.3e}")
+    assert e < 5e-2 and c > 0.999 and le < 2e-2, (e, c, le)
+
+
+def test_ddim100_64x64_b128_bf16_trajectory_matches_fp32():
+    """BASELINE config #5's sampling loop (bench.py celeba64.ddim100: the CIFAR network at 64x64, B=128, DDIM-100,
+    eta 0, bf16, the shared-timestep forward the loop takes, default plans with the 64-wide halo prologue) teacher-
+    forced against the fp32 HIP loop (itself pinned to the reference at 64x64 by test_big_unet_matches_reference
+    [unet_64] and to the reference's DDIM by test_diffusion_ops_match_reference), as
+    test_ddim50_b128_bf16_trajectory_matches_fp32 does for config #2: from the fp32 loop's x_i, ONE bf16 step
+    (shared-timestep model forward + fused DDIM update) gives x_{i+1} within relative L2 2e-2 and cosine > 0.9998 of
+    the fp32 loop's, at every one of the 100 steps. The free-running bf16 loop's final cosine is printed (the
+    100-step map of random-init weights is chaotic, see the DDIM-50 test)."""
+    from diffusion_models_collection_amd.models import UNet
+    from diffusion_models_collection_amd.diffusion import DDIM
+    cfg = dict(CIFAR, image_size=(64, 64), dropout=0.1)
+    gen = torch.Generator().manual_seed(37)
+    shape = (128, 3, 64, 64)
+    xT = torch.randn(*shape, generator=gen).to(DEV)
+    ddim = DDIM(1000, 100, device=DEV)
+    ms = {}
+    for dtype in ("fp32", "bf16"):
+        torch.manual_seed(45)
+        ms[dtype] = UNet(**cfg, compute_dtype=dtype).to(DEV).eval()
+    with torch.no_grad():
+        ref = ddim.sample(ms["fp32"], shape, None, return_all_timesteps=True, x_T=xT)     # [100, B, ...] host
+        free = ddim.sample(ms["bf16"], shape, None, x_T=xT).float().cpu()
+    freec = torch.nn.functional.cosine_similarity(free.flatten(1), ref[-1].flatten(1), dim=1)
+    m = ms["bf16"]
+    tab = ddim._ts_table(128, xT.device)
+    worst_rel, worst_cos = 0.0, 1.0
+    with torch.no_grad():
+        for i in range(100):
+            x = xT if i == 0 else ref[i - 1].to(DEV)
+            t, tn = tab[i], tab[i + 1]
+            nxt = ddim.p_sample(m, x, t, tn, None, eps=m(x, t[:1], None))
+            r = ref[i].to(DEV)
+            e = ((nxt - r).norm() / r.norm()).item()
+            c = cos(nxt, r)
+            worst_rel, worst_cos = max(worst_rel, e), min(worst_cos, c)
+            assert e < 2e-2 and c > 0.9998, (i, e, c)
+    assert _halo_pro_taken_at(m.executor, 64), "the 64-wide halo prologue plan was not taken"
+    print(f"DDIM-100 64x64 B=128: teacher-forced worst step rel {worst_rel:.3e} cos {worst_cos:.6f}; free-running "
+          f"final per-image cos min {freec.min().item():.4f} median {freec.median().item():.4f}")
