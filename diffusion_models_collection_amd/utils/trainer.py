@@ -307,31 +307,21 @@ class GraphedTrainStep:
         self.drop_on = drop_on
         ex.wgen += 1                      # the captured forward must contain the weight-pack launch
         ex.seed_ptr = self.h_dev.data_ptr() + 9 * 4
-        if tr.grad_sync is not None:
-            try:
-                self._capture_segmented(ex, f)
-            finally:
-                ex.seed_ptr = None
-            return
-        g = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                loss = tr.diffusion.p_losses(tr.model, self.x_s, self.t_s, self.y_s, noise=self.n_s,
-                                             loss_type=tr.loss_type)
-                loss.backward()
-                grad = f.grads_flat()
-                if grad is None:
-                    raise RuntimeError("gradients are not in the executor's flat buffer")
-                _, coef = K.grad_norm_flat(grad, 1.0)
-                K.adamw_flat_dev(f.flat_p, grad, f.flat_m, f.flat_v, f.flat_e if self.use_ema else None, coef,
-                                 self.h_dev)
+            self._capture_direct(ex, f)
         finally:
             ex.seed_ptr = None
         tr.optimizer.zero_grad()
-        self.graph, self.loss_s = g, loss.detach()
 
-    def _capture_segmented(self, ex, f):
-        """Data-parallel step as a chain of graphs cut at the gradient all-reduce points.
+    def _capture_direct(self, ex, f):
+        """The step captured straight from the executor, without autograd: one graph, or (data parallel) a chain of
+        graphs cut at the gradient all-reduce points.
+
+        No autograd node takes part in a capture. Round 6 found why that matters: a caller that still holds the
+        previous step's loss (the reference loop keeps `loss` alive across iterations, utils/trainer.py:249-268)
+        keeps that step's AccumulateGrad nodes alive, whose stream is the default stream; autograd then syncs the
+        capturing stream with the default stream inside the capture, and hipStreamEndCapture crashed the process
+        (tests/test_gpu_model.py::test_graphed_capture_with_previous_loss_alive).
 
         The step runs without autograd (q_sample -> executor forward -> loss -> executor backward, all on this
         thread) so that the bucket hook of the backward can end the current capture and begin the next one at
@@ -372,7 +362,7 @@ class GraphedTrainStep:
         hook.wants = lambda hi, final: final or gs.cut(hi, state["done"], ex.gtotal, final)
         self.one = torch.ones((), dtype=torch.float32, device=dev)
         old_hook = ex.grad_hook
-        ex.grad_hook = hook
+        ex.grad_hook = hook if gs is not None else None
         try:
             with torch.cuda.stream(stream):
                 begin()
@@ -400,7 +390,7 @@ class GraphedTrainStep:
         finally:
             ex.grad_hook = old_hook
         torch.cuda.current_stream().wait_stream(stream)
-        self.segs, self.graph, self.loss_s = segs, segs[-1][0], loss.detach()
+        self.segs, self.graph, self.loss_s = (segs if gs is not None else None), segs[-1][0], loss.detach()
         self.flat = ex.flat
 
     def _replay(self):
@@ -698,7 +688,7 @@ class DiffusionTrainer:
                 self.optimizer.zero_grad()
                 if self.use_ema:
                     self._update_ema()
-        return loss
+        return loss.detach()    # a caller holding it must not keep this step's autograd graph (and tape) alive
 
     def train_epoch(self, epoch):
         self.model.train()
