@@ -1405,6 +1405,244 @@ void launch_small(const ConvK& k, int mt, hipStream_t s) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Whole-image small-map 3x3 conv (round 6; forward or input gradient, stride 1) for the 4x4 and 8x8 levels
+// (models/unet.py:28-72 at the two deepest resolutions). What bounds these layers is how many bytes each CU must
+// pull in, not the MFMA work (a 4x4 256->256 layer at B = 128 is 2.4 GFLOP: ~1 us of the chip's MFMA): the split-K
+// path's 128 x 128 tiles over K slices load a 128-channel weight slab per block and write an fp32 partial slab
+// (plus an epilogue launch), the round-4 small kernel loads a 64-channel slab of all 2304 taps x channels per block
+// (295 KB). Here a block owns BM = 128 output pixels (whole images: 8 of 4x4 or 2 of 8x8) x BN = 16 / 32 output
+// channels over the FULL K: per 64-channel chunk it DMAs the tile's activations (16 KB, no halo: the zero padding is
+// a per-lane mask at fragment read, every source pixel of a valid tap lies in the tile) and the BN x 9 weight rows
+// (18 / 36 KB) into an NS-slot ring. At 4x4 B = 128 that is 256 blocks of 138 KB (BN 16) instead of slabs of 590 KB
+// or 295 KB per block, no workspace and no second launch. Waves split the pixels (32 each): per k-step BN/16 weight
+// fragments and two activation fragments, BN/16 x 2 MFMAs (v_mfma_f32_16x16x32_bf16). LDS rows are 128 B with the
+// halo kernels' XOR swizzle (16-byte chunk ch of row r at ch ^ (r & 7)). The epilogue runs from the accumulators
+// (conv_store_tile: bias, time embedding, residual, split output); it does not emit GroupNorm partials.
+template <int WP, int AP>
+DMC_DEV void img_issue(const ConvK& a, char* slot, int c, int wave, const unsigned* ao1, const unsigned* ao2,
+                       const unsigned* wo) {
+  const int c0 = c * 64;
+  const bool first = c0 < a.C1;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      first ? (void*)a.x1 : (void*)a.x2, (short)0, first ? a.x1_bytes : a.x2_bytes, 0x00020000);
+  const unsigned c2 = (unsigned)(first ? c0 : c0 - a.C1) * 2u;
+#pragma unroll
+  for (int p = 0; p < AP; ++p)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(slot + (wave * AP + p) * 1024), 16,
+                                             (first ? ao1[p] : ao2[p]) + c2, 0, 0, 0);
+  dma_pieces<WP>(a.w, a.w_bytes, slot + AP * 4 * 1024 + wave * WP * 1024, wo, (unsigned)c0 * 2u, 0, WP);
+}
+
+template <int N>
+DMC_DEV void wait_vm_c() { __builtin_amdgcn_s_waitcnt(waitcnt_vm(N)); }
+
+// BN output channels x BM = 4 * MW pixels per block (MW = 32 / 64 pixels per wave), an NS-slot chunk ring.
+template <int BN, int MW, int NS>
+__global__ __launch_bounds__(256) void conv3x3_img_kernel(ConvK a) {
+  using T = bf16_t;
+  constexpr int BM = 4 * MW, NI = BN / 16, NJ = MW / 16;
+  constexpr int AP = BM / 32;                   // activation DMA pieces (8 pixel rows of 128 B) per wave
+  constexpr int WP = (BN * 9 + 31) / 32;        // weight DMA pieces (8 rows (co, tap) of 128 B) per wave
+  constexpr int AB = BM * 128;                  // activation bytes per ring slot
+  constexpr int SB = AB + WP * 4 * 1024;        // ring slot: activations + weight rows
+  constexpr int PPC = AP + WP;                  // DMA pieces per chunk per wave
+  __shared__ __attribute__((aligned(16))) char lds[NS * SB];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int mb, nb;
+  xcd_tile(a.Cout / BN, mb, nb);                // 1-D grid; the channel slices of one image group share an XCD
+  const int m0 = mb * BM, n0 = nb * BN;
+  const int lrow = lane >> 3, lc = (lane & 7) ^ lrow;
+
+  unsigned ao1[AP], ao2[AP], wo[WP];
+#pragma unroll
+  for (int p = 0; p < AP; ++p) {
+    const unsigned pix = (unsigned)(m0 + (wave * AP + p) * 8 + lrow);
+    ao1[p] = (pix * a.ld1 + lc * 8) * 2u;
+    ao2[p] = (pix * a.ld2 + lc * 8) * 2u;
+  }
+  const unsigned wrow = (unsigned)(a.ntaps * a.Kc);
+#pragma unroll
+  for (int p = 0; p < WP; ++p) {
+    const int r = (wave * WP + p) * 8 + lrow, co = r / 9, t = r - co * 9;
+    wo[p] = co < BN ? ((unsigned)(n0 + co) * wrow + (unsigned)(t * a.Kc + lc * 8)) * 2u : kOOB;
+  }
+  const int nch = a.Kc / 64;
+#pragma unroll
+  for (int q = 0; q < NS - 1; ++q)
+    if (q < nch) img_issue<WP, AP>(a, lds + q * SB, q, wave, ao1, ao2, wo);
+
+  const int fr = lane & 15, fh = lane >> 4;
+  int qrow[NJ], qy[NJ], qx[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    qrow[j] = wave * MW + j * 16 + fr;          // tile row (pixel) of this lane's B-fragment column
+    const int rem = qrow[j] % a.OHW;
+    qy[j] = rem / a.OW;
+    qx[j] = rem - qy[j] * a.OW;
+  }
+  v4f acc[NI][NJ];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  // plain bf16 NHWC epilogue: its operands (bias, time embedding, residual) are loaded during the last chunk
+  const bool fast = !a.out_f32 && !a.out_nchw && !a.silu_pre && !a.act && a.Csplit == a.Cout;
+  v4f eb[NI], ea[NI][NJ];
+  v2i er[NI][NJ];
+
+  for (int c = 0; c < nch; ++c) {
+    // chunk c has landed once at most the chunks issued after it are in flight (this wave's own pieces)
+    const int after = min(nch - 1, c + NS - 2) - c;
+    if (NS >= 4 && after >= 2) wait_vm_c<2 * PPC>();
+    else if (NS >= 3 && after >= 1) wait_vm_c<PPC>();
+    else wait_vm_c<0>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();               // every wave's chunk-c pieces landed; chunk c-1's slot is free
+    asm volatile("" ::: "memory");
+    if (c + NS - 1 < nch) img_issue<WP, AP>(a, lds + ((c + NS - 1) % NS) * SB, c + NS - 1, wave, ao1, ao2, wo);
+    if (c == nch - 1 && fast) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int co = n0 + i * 16 + fh * 4;
+        eb[i] = a.bias ? *(const v4f*)(a.bias + co) : v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int pix = m0 + qrow[j];
+          ea[i][j] = a.addvec ? *(const v4f*)(a.addvec + (size_t)(pix / a.OHW) * a.ld_add + co)
+                              : v4f{0.f, 0.f, 0.f, 0.f};
+          er[i][j] = a.resid ? *(const v2i*)(a.resid + ((size_t)pix * a.ld_res + co) * 2) : v2i{0, 0};
+        }
+      }
+    }
+    const char* A = lds + (c % NS) * SB;
+    const char* Wt = A + AB;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ty = t / 3, tx = t - ty * 3;
+      const int dy = a.tdy0 + a.tsy * ty, dx = a.tdx0 + a.tsx * tx;
+      int src[NJ];
+      bool ok[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        ok[j] = (unsigned)(qy[j] + dy) < (unsigned)a.OH && (unsigned)(qx[j] + dx) < (unsigned)a.OW;
+        src[j] = ok[j] ? qrow[j] + dy * a.OW + dx : qrow[j];
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int cc = ks * 4 + fh;
+        v4i fa[NI], fb[NJ];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const int r = (i * 16 + fr) * 9 + t;
+          fa[i] = *(const v4i*)(Wt + r * 128 + ((cc ^ (r & 7)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const v4i v = *(const v4i*)(A + src[j] * 128 + ((cc ^ (src[j] & 7)) << 4));
+          fb[j] = ok[j] ? v : v4i{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
+      }
+    }
+  }
+  if (fast) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      float gm = 0.f, gq = 0.f;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int co = n0 + i * 16 + fh * 4, pix = m0 + qrow[j];
+        const v4f v = (acc[i][j] + eb[i]) + ea[i][j];
+        const float r0 = bf2f((uint32_t)er[i][j][0] & 0xffffu), r1 = bf2f((uint32_t)er[i][j][0] >> 16);
+        const float r2 = bf2f((uint32_t)er[i][j][1] & 0xffffu), r3 = bf2f((uint32_t)er[i][j][1] >> 16);
+        v2i o;
+        o[0] = (int)f2bf2(v[0] + r0, v[1] + r1);
+        o[1] = (int)f2bf2(v[2] + r2, v[3] + r3);
+        *(v2i*)(a.y1 + ((size_t)pix * a.ldy1 + co) * 2) = o;
+        if (MW == 64 && a.gst) {   // GroupNorm partials of the stored values (reg_epilogue's fold and tree)
+          const float g0 = bf2f((uint32_t)o[0] & 0xffffu), g1 = bf2f((uint32_t)o[0] >> 16);
+          const float g2 = bf2f((uint32_t)o[1] & 0xffffu), g3 = bf2f((uint32_t)o[1] >> 16);
+          const float mb = ((g0 + g1) + (g2 + g3)) * 0.25f;
+          const float qb =
+              fmaf(g3 - mb, g3 - mb, fmaf(g2 - mb, g2 - mb, fmaf(g1 - mb, g1 - mb, (g0 - mb) * (g0 - mb))));
+          if (j == 0) { gm = mb; gq = qb; }
+          else {
+            const float d = mb - gm, nn = 4.f * j;
+            gm += d * (4.f / (nn + 4.f));
+            gq += qb + d * d * (nn * 4.f / (nn + 4.f));
+          }
+        }
+      }
+      if (MW == 64 && a.gst) {   // segment = the wave's 64 pixels (one 8x8 image), chunk = lane groups (fh, fh ^ 1)
+        float cnt = 16.f;
+#pragma unroll
+        for (int sh = 1; sh <= 16; sh <<= 1) {
+          const float mb = __shfl_xor(gm, sh), qb = __shfl_xor(gq, sh);
+          chan_eq(gm, gq, mb, qb, cnt);
+          cnt *= 2.f;
+        }
+        if (fr == 0 && !(fh & 1)) {
+          const size_t o = ((size_t)((m0 + wave * 64) / 64) * (a.Cout / 8) + (n0 + i * 16 + fh * 4) / 8) * 2;
+          a.gst[o] = gm;
+          a.gst[o + 1] = gq;
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) conv_store_tile<T>(a, acc[i][j], m0 + qrow[j], n0 + i * 16 + fh * 4);
+}
+
+// The whole-image small-map kernel applies (bf16 3x3 stride 1 on 4x4 / 8x8 maps, 64-aligned sources, no prologue,
+// DMC_IMG_MASK bit set for the shape: bit 0 4x4 forward, 1 4x4 input gradient, 2 8x8 forward, 3 8x8 input
+// gradient; default 15): returns its channel tile BN (DMC_IMG_BN, 16 or 32), or 0. Same-box A/B of the B = 128 bench
+// (two interleaved runs): mask 0 train 10,481 / 10,458, DDIM-50 728 / 728; mask 3 (4x4) 10,696 / 10,678, 759 / 760;
+// mask 7 10,793 / 10,800, 781 / 788; mask 15 10,797 / 10,813, 780 / 783.
+int img_plan(const ConvK& k) {
+  const long mask = dmc::opt(dmc::OPT_IMG_MASK);
+  if (!mask || k.dtype_bytes != 2 || k.prologue != DMC_PRO_NONE) return 0;
+  if (k.mode != DMC_MODE_NORMAL || k.stride != 1 || k.ntaps != 9 || k.tkw != 3) return 0;
+  if (!((k.tdy0 == -1 && k.tsy == 1) || (k.tdy0 == 1 && k.tsy == -1))) return 0;
+  if (!((k.tdx0 == -1 && k.tsx == 1) || (k.tdx0 == 1 && k.tsx == -1))) return 0;
+  if (k.OH != k.H || k.OW != k.W || !((k.OH == 8 && k.OW == 8) || (k.OH == 4 && k.OW == 4)) || k.M % 128) return 0;
+  if (k.C1 % 64 || k.C2 % 64 || k.Kc != k.C1 + k.C2 || k.x1_bytes == 0 || (k.C2 && k.x2_bytes == 0) || k.w_bytes == 0)
+    return 0;
+  const int bit = (k.OH == 8 ? 2 : 0) + (k.tdy0 == 1 ? 1 : 0);
+  if (!((mask >> bit) & 1)) return 0;
+  // 256-pixel tiles (4 images) at 8x8, 128 (8 images) at 4x4; the channel tile that gives ~256 blocks
+  // (DMC_IMG_BN forces 16 / 32)
+  const int bm = k.OH == 8 ? 256 : 128;
+  if (k.M % bm) return 0;
+  int bn = (long)k.Cout * (k.M / bm) >= 512L * 16 ? 32 : 16;
+  if (dmc::opt(dmc::OPT_IMG_BN) == 16 || dmc::opt(dmc::OPT_IMG_BN) == 32) bn = (int)dmc::opt(dmc::OPT_IMG_BN);
+  if (k.Cout % bn) return 0;
+  // 8x8 maps with more than one round of blocks (the 2B-row CFG forward, the 512-channel input gradients) keep the
+  // halo / split-K plans: measured slower here (d512_8: 38.5 vs 33.7 us; CFG DDIM-50 448 vs 452 img/s)
+  if (k.OH == 8 && (long)(k.M / bm) * (k.Cout / bn) > 256) return 0;
+  return bn;
+}
+
+void launch_img(const ConvK& k, int bn, hipStream_t s) {
+  const int bm = k.OH == 8 ? 256 : 128;
+  const dim3 g(k.M / bm * (k.Cout / bn));
+  if (bm == 256) {
+    if (bn == 16) conv3x3_img_kernel<16, 64, 3><<<g, 256, 0, s>>>(k);
+    else conv3x3_img_kernel<32, 64, 2><<<g, 256, 0, s>>>(k);
+  } else {
+    if (bn == 16) conv3x3_img_kernel<16, 32, 4><<<g, 256, 0, s>>>(k);
+    else conv3x3_img_kernel<32, 32, 3><<<g, 256, 0, s>>>(k);
+  }
+}
+
 // The halo'd narrow kernels (conv3x3_nin_kernel / conv3x3_nout_kernel, below): bf16, 3x3 stride 1 on halo2_plan's
 // 128-pixel geometry. nin: one source of <= 8 channels (one chunk per pixel), Cout a multiple of 128. nout: Cout <=
 // 16, 64-aligned sources of <= 128 channels in all. Return the halo pieces per wave (6/7/9), or 0.
@@ -2087,6 +2325,8 @@ bool epi_stats_ok(const ConvK& k, const void* ws, size_t ws_bytes) {
   }
   if (dmc::opt(dmc::OPT_NO_GLDS) || dmc::opt(dmc::OPT_NO_EPI_STATS))
     return false;
+  if (img_plan(k))   // conv3x3_img_kernel: partials from its plain-epilogue 64-pixel waves (8x8 maps) only
+    return k.OH == 8 && k.act == DMC_ACT_NONE;
   if (small_plan(k) == 8) return true;   // conv3x3_small_kernel: 128-pixel tiles of two 8x8 images
   if (k.prologue == DMC_PRO_AFFINE_SILU) {
     int R, nimg;
@@ -2143,6 +2383,10 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
       conv_narrow_out_kernel<T><<<dmc::cdiv(k.M, 256), 256, 0, s>>>(k);
       return dmc::check_launch("dmc_conv2d");
     }
+  }
+  if (sizeof(T) == 2) {
+    const int bn = img_plan(k);
+    if (bn) { launch_img(k, bn, s); return dmc::check_launch("dmc_conv2d"); }
   }
   if (sizeof(T) == 2) {
     const int mt = small_plan(k);

@@ -1305,3 +1305,61 @@ def test_lds_dma_plain_store_stress_bitwise(case, dmc_opt):
         K.conv(d0, a, None, wp, y0)
         torch.cuda.synchronize()
         assert torch.equal(ref, y0)
+
+
+@pytest.mark.parametrize("bn", [16, 32])
+@pytest.mark.parametrize("case", ["f4", "f4_concat", "d4", "f8", "f8_concat", "d8"])
+def test_conv3x3_img_kernel(case, bn, dmc_opt):
+    """Round 6 whole-image small-map conv (conv3x3_img_kernel, DMC_IMG_MASK): bf16 3x3 stride-1 forward (with the
+    ResBlock conv2 epilogue: bias + time embedding + residual) and input gradient (flipped / transposed pack) at the
+    UNet's 4x4 and 8x8 levels, one and two (virtual concat) sources, BN = 16 / 32 output channels per block, against
+    the fp32 torch reference of the same bf16 operands (models/unet.py:34-60 at the two deepest levels)."""
+    L, K = _lib()
+    dmc_opt("DMC_IMG_MASK", 15)
+    dmc_opt("DMC_IMG_BN", bn)
+    dt = torch.bfloat16
+    torch.manual_seed(31)
+    H = 4 if case.endswith("4") or "4_" in case else 8
+    N = 16 if H == 4 else 4
+    dgrad = case.startswith("d")
+    C1, C2, Cout = {"f": (256, 0, 256), "f_concat": (256, 256, 256), "d": (256, 0, 512)}[
+        case[0] + ("_concat" if "concat" in case else "")]
+    x1 = torch.randn(N, C1, H, H)
+    x2 = torch.randn(N, C2, H, H) if C2 else None
+    xr = q(x1, dt) if x2 is None else torch.cat([q(x1, dt), q(x2, dt)], 1)
+    if dgrad:   # dx = conv_transpose(dy, w) of the forward conv Cout -> C1 (w: [C1, Cout, 3, 3])
+        w = torch.randn(C1, Cout, 3, 3) / math.sqrt(C1 * 9)
+        yr = F.conv_transpose2d(xr, q(w, dt), padding=1)
+    else:
+        w = torch.randn(Cout, C1 + C2, 3, 3) / math.sqrt((C1 + C2) * 9)
+        bias, addv, resid = torch.randn(Cout), torch.randn(N, Cout), torch.randn(N, Cout, H, H)
+        yr = F.conv2d(xr, q(w, dt), bias, padding=1) + addv[:, :, None, None] + q(resid, dt)
+    x1d = nhwc(x1).to(dt).to(DEV)
+    x2d = nhwc(x2).to(dt).to(DEV) if x2 is not None else None
+    Kc = L.kc_for(C1 + C2, dt)
+    wp = K.pack_weight(L.PACK_DGRAD if dgrad else L.PACK_FWD, dt, w.to(DEV), Kc)
+    d = K.make_desc(dt, N, H, H, C1, C2, C1, C2, Kc, H, H, Cout, K.TAPS3_DGRAD if dgrad else K.TAPS3)
+    if dgrad:
+        K.set_epilogue(d, ldy1=Cout)
+    else:   # at 8x8 the epilogue also emits the next GroupNorm's partials (64-pixel segment = one image)
+        part = torch.full((N * H * H // 64 * (Cout // 8) * 2,), float("nan"), device=DEV) if H == 8 else None
+        K.set_epilogue(d, bias=bias.to(DEV), addvec=addv.to(DEV), ld_add=Cout, resid=nhwc(resid).to(dt).to(DEV),
+                       ld_res=Cout, ldy1=Cout, gn_part=part)
+    y = torch.empty(N, H, H, Cout, dtype=dt, device=DEV)
+    K.conv(d, x1d, x2d, wp, y)
+    torch.cuda.synchronize()
+    got = nchw(y.float().cpu())
+    e = rel_err(got, yr)
+    assert e < 1e-2, e
+    if not dgrad and H == 8:   # (mean, M2) of the stored bf16 values per (64-pixel segment, 8-channel chunk)
+        v = y.float().view(N * H * H // 64, 64, Cout // 8, 8).permute(0, 2, 1, 3).reshape(-1, 512)
+        m = v.mean(1)
+        m2 = ((v - m[:, None]) ** 2).sum(1)
+        p2 = part.view(-1, 2)
+        assert torch.allclose(p2[:, 0], m, rtol=1e-4, atol=1e-5)
+        assert torch.allclose(p2[:, 1], m2, rtol=1e-4, atol=1e-3)
+    # the same launch twice: bitwise reproducible
+    y2 = torch.empty_like(y)
+    K.conv(d, x1d, x2d, wp, y2)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2)
