@@ -1447,10 +1447,12 @@ __global__ __launch_bounds__(256) void conv3x3_img_kernel(ConvK a) {
   constexpr int AB = BM * 128;                  // activation bytes per ring slot
   constexpr int SB = AB + WP * 4 * 1024;        // ring slot: activations + weight rows
   constexpr int PPC = AP + WP;                  // DMA pieces per chunk per wave
-  __shared__ __attribute__((aligned(16))) char lds[NS * SB];
+  __shared__ __attribute__((aligned(16))) char lds[NS * SB + 16];
+  char* const zrow = lds + NS * SB;             // 16 zero bytes: the operand of every zero-padding tap
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (threadIdx.x == 0) *(v4i*)zrow = v4i{0, 0, 0, 0};   // visible after the first chunk's barrier
   int mb, nb;
   xcd_tile(a.Cout / BN, mb, nb);                // 1-D grid; the channel slices of one image group share an XCD
   const int m0 = mb * BM, n0 = nb * BN;
@@ -1519,8 +1521,10 @@ __global__ __launch_bounds__(256) void conv3x3_img_kernel(ConvK a) {
     }
     const char* A = lds + (c % NS) * SB;
     const char* Wt = A + AB;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
+    // fragments of tap t + 1 are read (into the other register set) before tap t's MFMAs: one LDS round trip per
+    // chunk is exposed instead of one per k-step (the first form waited for its 3 reads before every 2 MFMAs)
+    v4i fa[2][2][NI], fb[2][2][NJ];
+    auto read_tap = [&](int t, v4i (&ga)[2][NI], v4i (&gb)[2][NJ]) {
       const int ty = t / 3, tx = t - ty * 3;
       const int dy = a.tdy0 + a.tsy * ty, dx = a.tdx0 + a.tsx * tx;
       int src[NJ];
@@ -1533,22 +1537,30 @@ __global__ __launch_bounds__(256) void conv3x3_img_kernel(ConvK a) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const int cc = ks * 4 + fh;
-        v4i fa[NI], fb[NJ];
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
           const int r = (i * 16 + fr) * 9 + t;
-          fa[i] = *(const v4i*)(Wt + r * 128 + ((cc ^ (r & 7)) << 4));
+          ga[ks][i] = *(const v4i*)(Wt + r * 128 + ((cc ^ (r & 7)) << 4));
         }
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const v4i v = *(const v4i*)(A + src[j] * 128 + ((cc ^ (src[j] & 7)) << 4));
-          fb[j] = ok[j] ? v : v4i{0, 0, 0, 0};
-        }
+        for (int j = 0; j < NJ; ++j)   // a padding tap reads the zero row (an address select, no data select)
+          gb[ks][j] = *(const v4i*)(ok[j] ? A + src[j] * 128 + ((cc ^ (src[j] & 7)) << 4) : zrow);
+      }
+    };
+    read_tap(0, fa[0], fb[0]);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * (NI + NJ), 0);   // tap 0's reads
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int cur = t & 1;
+      if (t + 1 < 9) read_tap(t + 1, fa[cur ^ 1], fb[cur ^ 1]);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
-          for (int j = 0; j < NJ; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
-      }
+          for (int j = 0; j < NJ; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[cur][ks][i], fb[cur][ks][j]);
+      if (t + 1 < 9) __builtin_amdgcn_sched_group_barrier(0x100, 2 * (NI + NJ), 0);   // next tap's reads first
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * NI * NJ, 0);                       // then this tap's MFMAs
     }
   }
   if (fast) {
