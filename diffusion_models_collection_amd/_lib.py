@@ -15,7 +15,7 @@ LIB_PATH = Path(os.environ.get("DMC_LIB", _PKG / "libdmc.so"))
 
 DMC_F32, DMC_BF16 = 0, 1
 MODE_NORMAL, MODE_UPSAMPLE, MODE_DILATE = 0, 1, 2
-PRO_NONE, PRO_AFFINE_SILU, PRO_SILU, PRO_AFFINE = 0, 1, 2, 3
+PRO_NONE, PRO_AFFINE_SILU, PRO_SILU, PRO_AFFINE, PRO_GN_SILU = 0, 1, 2, 3, 4
 LOSS = {"l1": 0, "l2": 1, "huber": 2}
 PACK_FWD, PACK_DGRAD, PACK_UPDGRAD = 0, 1, 2
 
@@ -39,7 +39,7 @@ class ConvDesc(ctypes.Structure):
         ("bias", _c_p), ("addvec", _c_p), ("ld_add", _c_int), ("resid", _c_p), ("ld_res", _c_int),
         ("silu_pre", _c_p), ("ld_silu", _c_int), ("Csplit", _c_int), ("ldy1", _c_int), ("ldy2", _c_int),
         ("out_f32", _c_int), ("out_nchw", _c_int), ("act", _c_int), ("y_pre", _c_p), ("ld_pre", _c_int),
-        ("gn_part", _c_p), ("wg_bias", _c_p),
+        ("gn_part", _c_p), ("wg_bias", _c_p), ("pro_groups", _c_int), ("pro_eps", _c_f),
     ]
 
 

@@ -1051,6 +1051,8 @@ DMC_DEV void halo_affine_silu(char* buf, int wave, const unsigned* h1, const v4f
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
+  for (int p = 0; p < HP; ++p) asm volatile("" : "+v"(v[p])::"memory");   // no use before the wait (img_gn_silu)
+#pragma unroll
   for (int p = 0; p < HP; ++p) {
     if (h1[p] == kOOB) continue;
     float f[8];
@@ -1213,197 +1215,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo2_kernel(ConvK a, int R, i
   tile_epilogue<T, BM, BN, NW * 64>(a, lds, EP, m0, n0);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Small-map 3x3 conv (forward or dgrad, stride 1) for the UNet's 8x8 and 4x4 levels (models/unet.py:28-72 at the
-// two deepest resolutions, their up-path concat convs and input gradients). There M is 8192 / 2048 pixels: the
-// 128-pixel x 128-channel tiles of the kernels above give 64-128 blocks for 256 CUs, and split-K to fill the chip
-// leaves every block a handful of K stages behind a fixed prologue / epilogue / slab cost (PMC of the 4x4 split
-// launch: MFMA busy 11 % of a wave's life). Here a block owns a tile of BM = 16 * MT output pixels (two whole
-// images) x 64 output channels over the FULL K, and its four waves split K instead of the tile: wave w takes the
-// input channels [w * CPW, (w + 1) * CPW), CPW = Cin / 4, for all nine taps. So:
-//   * each wave keeps its channel slice of the tile's halo (the images plus their zero border, 64-channel planes
-//     of 128-byte rows, the halo kernels' XOR swizzle) resident in wave-private LDS: loaded once (CPW = 64) or
-//     twice (CPW = 128), never shared, so the K loop has no block barrier at all;
-//   * the weight fragments come straight from global memory (L2) into registers, P k-steps ahead of their
-//     MFMAs (no LDS staging, no DMA issue in the loop);
-//   * the four partial tiles are summed through LDS in a fixed order ((w0 + w2) + (w1 + w3)), then the shared
-//     LDS-staged epilogue (bias, time embedding, residual, GroupNorm partials) runs once: no fp32 slab, no
-//     split-K epilogue launch.
-// Grid: (M / BM) x (Cout / 64) blocks = 256 at B = 128 (512 for 512 output channels). MT = 8 (8x8 maps) or
-// 2 (4x4 maps); HPC = halo DMA pieces (8 pixels) per wave-plane: 2 x 10 x 10 -> 25, 2 x 6 x 6 -> 9.
-template <int MT, int HPC, int NPL, int P>
-__global__ __launch_bounds__(256) void conv3x3_small_kernel(ConvK a) {
-  using T = bf16_t;
-  constexpr int BM = 16 * MT, BN = 64, NT = 256;
-  constexpr int PLB = HPC * 1024;                       // bytes of one wave's halo plane
-  constexpr int EP = BN * 4 + 16;                       // epilogue row pitch (fp32)
-  constexpr int RED = 2 * BM * EP + 4 * (BM / 64 > 0 ? BM / 64 : 1) * 16 * 64;   // 2 partial tiles + stats scratch
-  constexpr int LDS_BYTES = 4 * PLB > RED ? 4 * PLB : RED;
-  constexpr int S = NPL * 18;                           // k32 steps per wave: planes x 9 taps x 2 halves
-  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int NB = a.Cout / BN;
-  const int mb = blockIdx.x / NB, nb = blockIdx.x - mb * NB;
-  const int m0 = mb * BM, n0 = nb * BN;
-  const int OW = a.OW, HW = OW + 2, segpix = (a.OH + 2) * HW, nimg = BM / a.OHW;
-  const int n_first = m0 / a.OHW;
-  const int CPW = NPL * 64, cw0 = wave * CPW;           // this wave's input channels
-  const bool first = cw0 < a.C1;
-  const char* const xs = first ? a.x1 : a.x2;
-  const int xbytes = first ? a.x1_bytes : a.x2_bytes, ldx = first ? a.ld1 : a.ld2, cs = first ? cw0 : cw0 - a.C1;
-  char* const hbuf = lds + wave * PLB;
-  const int lrow = lane >> 3, lc = (lane & 7) ^ lrow;   // DMA piece: lane -> row lrow, logical chunk lc
-
-  // halo DMA of one 64-channel plane (pieces of 8 halo pixels x 128 B; out-of-image pixels read zeros)
-  auto halo_dma = [&](int pl) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)xs, (short)0, xbytes, 0x00020000);
-#pragma unroll
-    for (int p = 0; p < HPC; ++p) {
-      const int h = p * 8 + lrow;
-      unsigned off = kOOB;
-      if (h < nimg * segpix) {
-        const int img = h / segpix, rem = h - img * segpix;
-        const int hr = rem / HW, hc = rem - hr * HW;
-        const int iy = hr - 1, ix = hc - 1;
-        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-          off = ((unsigned)(((n_first + img) * a.H + iy) * a.W + ix) * ldx + cs + pl * 64 + lc * 8) * 2u;
-      }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(hbuf + p * 1024), 16, off, 0, 0, 0);
-    }
-  };
-
-  const int fr = lane & 15, fh = lane >> 4;
-  int hb[MT];
-#pragma unroll
-  for (int j = 0; j < MT; ++j) {
-    const int m = j * 16 + fr;
-    const int img = m / a.OHW, rem = m - img * a.OHW;
-    const int r = rem / OW, col = rem - r * OW;
-    hb[j] = img * segpix + (r + 1) * HW + col + 1;
-  }
-  // weight fragments: packed [Cout][9][Kc]; step s = (plane, tap, half) -> k = tap * Kc + cw0 + plane * 64 + half * 32
-  const char* wb = a.w + ((size_t)(n0 + fr) * (9 * a.Kc) + cw0 + fh * 8) * 2;
-  const size_t wrow16 = (size_t)16 * 9 * a.Kc * 2;      // 16 co rows
-  auto wload = [&](int s, v4i* f) {
-    const int pl = s / 18, rem = s - pl * 18, t = rem >> 1, hf = rem & 1;
-    const char* p = wb + ((size_t)t * a.Kc + pl * 64 + hf * 32) * 2;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) f[i] = *(const v4i*)(p + i * wrow16);
-  };
-
-  v4f acc[4][MT];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < MT; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-  halo_dma(0);
-  // the counted wait below needs the halo DMA issued before the weight loads: keep hipcc from reordering them
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  v4i wq[P][4];
-#pragma unroll
-  for (int q = 0; q < P; ++q) wload(q, wq[q]);
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_waitcnt(waitcnt_vm(4 * P));        // the halo (issued first) has landed
-  asm volatile("" ::: "memory");
-#pragma unroll
-  for (int s = 0; s < S; ++s) {
-    const int pl = s / 18, rem = s - pl * 18, t = rem >> 1, hf = rem & 1;
-    if (pl > 0 && rem == 0) {
-      // next 64-channel plane into the same (wave-private) buffer: this wave's reads of the old plane are done
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      halo_dma(pl);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-      asm volatile("" ::: "memory");
-    }
-    const int ty = t / 3, tx = t - ty * 3;
-    const int delta = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
-    v4i fb[MT];
-#pragma unroll
-    for (int j = 0; j < MT; ++j) {
-      const int h = hb[j] + delta;
-      fb[j] = *(const v4i*)(hbuf + h * 128 + (((hf * 4 + fh) ^ (h & 7)) << 4));
-    }
-    v4i* fa = wq[s % P];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < MT; ++j) acc[i][j] = mma16<T>(acc[i][j], fa[i], fb[j]);
-    if (s + P < S) wload(s + P, wq[s % P]);
-  }
-  // K reduction across the waves: (w0 + w2) + (w1 + w3) in fixed order, into tile 0
-  __syncthreads();
-  float* const t0 = (float*)lds;
-  float* const t1 = (float*)(lds + BM * EP);
-  float* const tw = (wave & 1) ? t1 : t0;
-  const int cfr = (threadIdx.x & 63) & 15;
-  if (wave < 2) {
-#pragma unroll
-    for (int j = 0; j < MT; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        *(v4f*)((char*)tw + (j * 16 + cfr) * EP + (i * 16 + fh * 4) * 4) = acc[i][j];
-  }
-  __syncthreads();
-  if (wave >= 2) {
-#pragma unroll
-    for (int j = 0; j < MT; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        v4f* q = (v4f*)((char*)tw + (j * 16 + cfr) * EP + (i * 16 + fh * 4) * 4);
-        *q = *q + acc[i][j];
-      }
-  }
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < BM * (BN / 4); idx += NT) {
-    const int r = idx / (BN / 4), c4 = idx - r * (BN / 4);
-    v4f* q0 = (v4f*)((char*)t0 + r * EP + c4 * 16);
-    *q0 = *q0 + *(const v4f*)((char*)t1 + r * EP + c4 * 16);
-  }
-  __syncthreads();
-  tile_epilogue<T, BM, BN, NT>(a, lds, EP, m0, n0);
-}
-
-// Whether the small-map kernel takes this conv: bf16 3x3 stride-1 forward / dgrad taps, 8x8 or 4x4 maps (two
-// whole images per tile), Cin a multiple of 256 (4 waves x 64-channel planes, each wave's slice inside one
-// source), Cout a multiple of 64, no prologue. Returns MT (16-pixel m-tiles per block) or 0.
-int small_plan(const ConvK& k) {
-  if (dmc::opt(dmc::OPT_NO_SMALL) || k.dtype_bytes != 2 || k.prologue != DMC_PRO_NONE) return 0;
-  if (k.mode != DMC_MODE_NORMAL || k.stride != 1 || k.ntaps != 9 || k.tkw != 3) return 0;
-  if (!((k.tdy0 == -1 && k.tsy == 1) || (k.tdy0 == 1 && k.tsy == -1))) return 0;
-  if (!((k.tdx0 == -1 && k.tsx == 1) || (k.tdx0 == 1 && k.tsx == -1))) return 0;
-  if (k.OH != k.H || k.OW != k.W || !((k.OH == 8 && k.OW == 8) || (k.OH == 4 && k.OW == 4))) return 0;
-  const int Cin = k.C1 + k.C2, cpw = Cin / 4;
-  // Cin = 256 only: with 512 input channels (two halo planes per wave) it measured slower than the split-K path
-  // (8x8: 93 vs 42 us; 4x4: 25 vs 22 us), with 256 faster (8x8: 23.7 vs 32.5 us; 4x4: 15.2 vs 21.1 us)
-  if (Cin != 256 || k.Kc != Cin || k.C1 % cpw || k.Cout % 64 || k.N % 2) return 0;
-  if (k.x1_bytes == 0 || (k.C2 && k.x2_bytes == 0) || k.w_bytes == 0 || k.silu_pre || k.act) return 0;
-  // DMC_SMALL_MASK: bit 0 8x8 forward, 1 8x8 input gradient, 2 4x4 forward, 3 4x4 input gradient. Default 1: in
-  // the train step / DDIM loop only the 8x8 forward at B = 128 (one round of 256 blocks) measured faster (+0.3 %);
-  // the input gradients (512 output channels: two rounds of 102 KB blocks), the 4x4 shapes and the 2B-row CFG
-  // forward measured neutral to slower than the split-K path (profiles/r4_small_ab.txt)
-  const int bit = (k.OH == 8 ? 0 : 2) + (k.tdy0 == 1 ? 1 : 0);
-  if (!((dmc::opt(dmc::OPT_SMALL_MASK) >> bit) & 1)) return 0;
-  if (k.OH == 8 && k.M / 128 * (k.Cout / 64) > 256 && dmc::opt(dmc::OPT_SMALL_MASK) == 1) return 0;
-  return k.OH == 8 ? 8 : 2;
-}
-
-void launch_small(const ConvK& k, int mt, hipStream_t s) {
-  const int npl = (k.C1 + k.C2) / 256;
-  const dim3 g(k.M / (16 * mt) * (k.Cout / 64));
-  if (mt == 8) {
-    if (npl == 1) conv3x3_small_kernel<8, 25, 1, 4><<<g, 256, 0, s>>>(k);
-    else conv3x3_small_kernel<8, 25, 2, 4><<<g, 256, 0, s>>>(k);
-  } else {
-    if (npl == 1) conv3x3_small_kernel<2, 9, 1, 6><<<g, 256, 0, s>>>(k);
-    else conv3x3_small_kernel<2, 9, 2, 6><<<g, 256, 0, s>>>(k);
-  }
-}
+// (round 6: the round-4 small-map kernel conv3x3_small_kernel is replaced by conv3x3_img_kernel below)
 
 // ---------------------------------------------------------------------------------------------
 // Whole-image small-map 3x3 conv (round 6; forward or input gradient, stride 1) for the 4x4 and 8x8 levels
@@ -1437,8 +1249,83 @@ DMC_DEV void img_issue(const ConvK& a, char* slot, int c, int wave, const unsign
 template <int N>
 DMC_DEV void wait_vm_c() { __builtin_amdgcn_s_waitcnt(waitcnt_vm(N)); }
 
-// BN output channels x BM = 4 * MW pixels per block (MW = 32 / 64 pixels per wave), an NS-slot chunk ring.
-template <int BN, int MW, int NS>
+// DMC_PRO_GN_SILU on a landed chunk (64 channels of BM pixels = whole images) in LDS: every thread owns one 8-channel
+// chunk of RPT consecutive pixel rows of one image, so the GroupNorm sums of a group of one image are a shuffle
+// reduction inside one wave (TPP row threads, then the group's cpg / 8 chunks); two passes (mean, then the sum of
+// squared deviations) over the thread's registers, the reference's biased variance and eps inside the sqrt; then
+// SiLU(x * rstd * gamma + beta - mean * rstd * gamma) (gn_fold) rounded to bf16 and written back in place. LDS accesses
+// are inline asm: plain ones would make hipcc drain the in-flight chunk DMA first (see halo_affine_silu). The values
+// stay packed (RPT x 4 registers) and are unpacked per pass.
+template <int MW>
+DMC_DEV void img_gn_silu(const ConvK& a, char* A, const char* gtab, int c0) {
+  constexpr int OHWC = MW == 32 ? 16 : 64, BM = 4 * MW, NIMG = BM / OHWC, TPP = 256 / (NIMG * 8), RPT = OHWC / TPP;
+  const int t = threadIdx.x, pair = t / TPP, img = pair >> 3, lc8 = pair & 7;
+  const int rb = img * OHWC + (t % TPP) * RPT;
+  const int cpg = (a.C1 + a.C2) / a.gn_G, lw = cpg / 8;
+  v4i v[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = rb + i;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v[i]) : "v"((unsigned)(uintptr_t)(A + r * 128 + ((lc8 ^ (r & 7)) << 4))) : "memory");
+  }
+  v4i gq[4];
+  const char* gp = gtab + (c0 + lc8 * 8) * 4;
+#pragma unroll
+  for (int h = 0; h < 4; ++h)   // gamma[c..c+3], gamma[c+4..], beta[c..], beta[c+4..]
+    asm volatile("ds_read_b128 %0, %1" : "=v"(gq[h]) : "v"((unsigned)(uintptr_t)(gp + (h >> 1) * 2048 + (h & 1) * 16)) : "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // the asm reads complete at the wait; tie every result to it (hipcc would otherwise schedule their uses between the
+  // reads and the wait: it does not know an asm ds_read is asynchronous)
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) asm volatile("" : "+v"(v[i])::"memory");
+#pragma unroll
+  for (int h = 0; h < 4; ++h) asm volatile("" : "+v"(gq[h])::"memory");
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    float f[8];
+    Chunk<bf16_t>::unpack(v[i], f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sum += f[e];
+  }
+#pragma unroll
+  for (int o = 1; o < TPP; o <<= 1) sum += __shfl_xor(sum, o);
+  for (int o = TPP; o < TPP * lw; o <<= 1) sum += __shfl_xor(sum, o);
+  const float n = (float)(OHWC * cpg);
+  const float mean = sum / n;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    float f[8];
+    Chunk<bf16_t>::unpack(v[i], f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { const float d = f[e] - mean; q = fmaf(d, d, q); }
+  }
+#pragma unroll
+  for (int o = 1; o < TPP; o <<= 1) q += __shfl_xor(q, o);
+  for (int o = TPP; o < TPP * lw; o <<= 1) q += __shfl_xor(q, o);
+  const float rstd = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(fmaxf(q / n, 0.f), a.gn_eps)));
+  float sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float gm = __int_as_float(gq[e >> 2][e & 3]), bt = __int_as_float(gq[2 + (e >> 2)][e & 3]);
+    gn_fold(mean, rstd, gm, bt, sc[e], sh[e]);
+  }
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    float f[8];
+    Chunk<bf16_t>::unpack(v[i], f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = silu_f(fmaf(f[e], sc[e], sh[e]));
+    const int r = rb + i;
+    lds_write_b128(A + r * 128 + ((lc8 ^ (r & 7)) << 4), Chunk<bf16_t>::pack(f));
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// BN output channels x BM = 4 * MW pixels per block (MW = 32 / 64 pixels per wave), an NS-slot chunk ring. GNP: the
+// DMC_PRO_GN_SILU prologue (GroupNorm statistics of each landed chunk's images, then affine + SiLU in place).
+template <int BN, int MW, int NS, bool GNP = false>
 __global__ __launch_bounds__(256) void conv3x3_img_kernel(ConvK a) {
   using T = bf16_t;
   constexpr int BM = 4 * MW, NI = BN / 16, NJ = MW / 16;
@@ -1447,8 +1334,15 @@ __global__ __launch_bounds__(256) void conv3x3_img_kernel(ConvK a) {
   constexpr int AB = BM * 128;                  // activation bytes per ring slot
   constexpr int SB = AB + WP * 4 * 1024;        // ring slot: activations + weight rows
   constexpr int PPC = AP + WP;                  // DMA pieces per chunk per wave
-  __shared__ __attribute__((aligned(16))) char lds[NS * SB + 16];
+  constexpr int GT = GNP ? 4096 : 0;            // GNP: gamma [512] and beta [512] fp32 table
+  __shared__ __attribute__((aligned(16))) char lds[NS * SB + 16 + GT];
   char* const zrow = lds + NS * SB;             // 16 zero bytes: the operand of every zero-padding tap
+  char* const gtab = lds + NS * SB + 16;
+  v2f gva = {0.f, 0.f}, bva = {0.f, 0.f};
+  if (GNP && 2 * (int)threadIdx.x < a.C1 + a.C2) {   // loaded before any DMA: landed by chunk 0's counted wait
+    gva = *(const v2f*)(a.psc + 2 * threadIdx.x);
+    bva = *(const v2f*)(a.psh + 2 * threadIdx.x);
+  }
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1492,7 +1386,8 @@ __global__ __launch_bounds__(256) void conv3x3_img_kernel(ConvK a) {
     for (int j = 0; j < NJ; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
   // plain bf16 NHWC epilogue: its operands (bias, time embedding, residual) are loaded during the last chunk
   const bool fast = !a.out_f32 && !a.out_nchw && !a.silu_pre && !a.act && a.Csplit == a.Cout;
-  v4f eb[NI], ea[NI][NJ];
+  constexpr int NJE = MW == 64 ? 1 : NJ;        // time-embedding rows per wave: a 64-pixel wave is one 8x8 image
+  v4f eb[NI], ea[NI][NJE];
   v2i er[NI][NJ];
 
   for (int c = 0; c < nch; ++c) {
@@ -1501,10 +1396,20 @@ __global__ __launch_bounds__(256) void conv3x3_img_kernel(ConvK a) {
     if (NS >= 4 && after >= 2) wait_vm_c<2 * PPC>();
     else if (NS >= 3 && after >= 1) wait_vm_c<PPC>();
     else wait_vm_c<0>();
+    if (GNP && c == 0) {
+      asm volatile("ds_write_b64 %0, %1" ::"v"((unsigned)(uintptr_t)(gtab + threadIdx.x * 8)), "v"(gva) : "memory");
+      asm volatile("ds_write_b64 %0, %1" ::"v"((unsigned)(uintptr_t)(gtab + 2048 + threadIdx.x * 8)), "v"(bva) : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();               // every wave's chunk-c pieces landed; chunk c-1's slot is free
     asm volatile("" ::: "memory");
     if (c + NS - 1 < nch) img_issue<WP, AP>(a, lds + ((c + NS - 1) % NS) * SB, c + NS - 1, wave, ao1, ao2, wo);
+    if (GNP) {
+      img_gn_silu<MW>(a, lds + (c % NS) * SB, gtab, c * 64);
+      __builtin_amdgcn_s_barrier();             // every element of chunk c normalised before any fragment read
+      asm volatile("" ::: "memory");
+    }
     if (c == nch - 1 && fast) {
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
@@ -1513,8 +1418,9 @@ __global__ __launch_bounds__(256) void conv3x3_img_kernel(ConvK a) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const int pix = m0 + qrow[j];
-          ea[i][j] = a.addvec ? *(const v4f*)(a.addvec + (size_t)(pix / a.OHW) * a.ld_add + co)
-                              : v4f{0.f, 0.f, 0.f, 0.f};
+          if (j < NJE)
+            ea[i][j] = a.addvec ? *(const v4f*)(a.addvec + (size_t)(pix / a.OHW) * a.ld_add + co)
+                                : v4f{0.f, 0.f, 0.f, 0.f};
           er[i][j] = a.resid ? *(const v2i*)(a.resid + ((size_t)pix * a.ld_res + co) * 2) : v2i{0, 0};
         }
       }
@@ -1570,7 +1476,7 @@ __global__ __launch_bounds__(256) void conv3x3_img_kernel(ConvK a) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int co = n0 + i * 16 + fh * 4, pix = m0 + qrow[j];
-        const v4f v = (acc[i][j] + eb[i]) + ea[i][j];
+        const v4f v = (acc[i][j] + eb[i]) + ea[i][NJE == 1 ? 0 : j];
         const float r0 = bf2f((uint32_t)er[i][j][0] & 0xffffu), r1 = bf2f((uint32_t)er[i][j][0] >> 16);
         const float r2 = bf2f((uint32_t)er[i][j][1] & 0xffffu), r3 = bf2f((uint32_t)er[i][j][1] >> 16);
         v2i o;
@@ -1616,12 +1522,17 @@ __global__ __launch_bounds__(256) void conv3x3_img_kernel(ConvK a) {
 
 // The whole-image small-map kernel applies (bf16 3x3 stride 1 on 4x4 / 8x8 maps, 64-aligned sources, no prologue,
 // DMC_IMG_MASK bit set for the shape: bit 0 4x4 forward, 1 4x4 input gradient, 2 8x8 forward, 3 8x8 input
-// gradient; default 15): returns its channel tile BN (DMC_IMG_BN, 16 or 32), or 0. Same-box A/B of the B = 128 bench
+// gradient; default 15): returns its channel tile BN (16 or 32), or 0. Same-box A/B of the B = 128 bench
 // (two interleaved runs): mask 0 train 10,481 / 10,458, DDIM-50 728 / 728; mask 3 (4x4) 10,696 / 10,678, 759 / 760;
 // mask 7 10,793 / 10,800, 781 / 788; mask 15 10,797 / 10,813, 780 / 783.
 int img_plan(const ConvK& k) {
   const long mask = dmc::opt(dmc::OPT_IMG_MASK);
-  if (!mask || k.dtype_bytes != 2 || k.prologue != DMC_PRO_NONE) return 0;
+  if (!mask || k.dtype_bytes != 2 || (k.prologue != DMC_PRO_NONE && k.prologue != DMC_PRO_GN_SILU)) return 0;
+  if (k.prologue == DMC_PRO_GN_SILU) {   // forward convs of SiLU(GroupNorm(x)) with whole groups in a 64-channel chunk
+    const int C = k.C1 + k.C2;
+    if (k.tdy0 != -1 || C > 512 || k.gn_G <= 0 || C % k.gn_G || (C / k.gn_G) % 8 || 64 % (C / k.gn_G) || k.dthresh)
+      return 0;
+  }
   if (k.mode != DMC_MODE_NORMAL || k.stride != 1 || k.ntaps != 9 || k.tkw != 3) return 0;
   if (!((k.tdy0 == -1 && k.tsy == 1) || (k.tdy0 == 1 && k.tsy == -1))) return 0;
   if (!((k.tdx0 == -1 && k.tsx == 1) || (k.tdx0 == 1 && k.tsx == -1))) return 0;
@@ -1630,22 +1541,27 @@ int img_plan(const ConvK& k) {
     return 0;
   const int bit = (k.OH == 8 ? 2 : 0) + (k.tdy0 == 1 ? 1 : 0);
   if (!((mask >> bit) & 1)) return 0;
-  // 256-pixel tiles (4 images) at 8x8, 128 (8 images) at 4x4; the channel tile that gives ~256 blocks
-  // (DMC_IMG_BN forces 16 / 32)
+  // 256-pixel tiles (4 images) at 8x8, 128 (8 images) at 4x4; the channel tile (16 / 32) that gives ~256 blocks
   const int bm = k.OH == 8 ? 256 : 128;
   if (k.M % bm) return 0;
-  int bn = (long)k.Cout * (k.M / bm) >= 512L * 16 ? 32 : 16;
-  if (dmc::opt(dmc::OPT_IMG_BN) == 16 || dmc::opt(dmc::OPT_IMG_BN) == 32) bn = (int)dmc::opt(dmc::OPT_IMG_BN);
+  const int bn = (long)k.Cout * (k.M / bm) >= 512L * 16 ? 32 : 16;
   if (k.Cout % bn) return 0;
   // 8x8 maps with more than one round of blocks (the 2B-row CFG forward, the 512-channel input gradients) keep the
   // halo / split-K plans: measured slower here (d512_8: 38.5 vs 33.7 us; CFG DDIM-50 448 vs 452 img/s)
   if (k.OH == 8 && (long)(k.M / bm) * (k.Cout / bn) > 256) return 0;
+  // the GN prologue forms that are compiled: 4x4 with 16-channel tiles, 8x8 with 32 (the LDS holds their gamma table)
+  if (k.prologue == DMC_PRO_GN_SILU && !((k.OH == 4 && bn == 16) || (k.OH == 8 && bn == 32))) return 0;
   return bn;
 }
 
 void launch_img(const ConvK& k, int bn, hipStream_t s) {
   const int bm = k.OH == 8 ? 256 : 128;
   const dim3 g(k.M / bm * (k.Cout / bn));
+  if (k.prologue == DMC_PRO_GN_SILU) {
+    if (bm == 256) conv3x3_img_kernel<32, 64, 2, true><<<g, 256, 0, s>>>(k);
+    else conv3x3_img_kernel<16, 32, 4, true><<<g, 256, 0, s>>>(k);
+    return;
+  }
   if (bm == 256) {
     if (bn == 16) conv3x3_img_kernel<16, 64, 3><<<g, 256, 0, s>>>(k);
     else conv3x3_img_kernel<32, 64, 2><<<g, 256, 0, s>>>(k);
@@ -2339,7 +2255,6 @@ bool epi_stats_ok(const ConvK& k, const void* ws, size_t ws_bytes) {
     return false;
   if (img_plan(k))   // conv3x3_img_kernel: partials from its plain-epilogue 64-pixel waves (8x8 maps) only
     return k.OH == 8 && k.act == DMC_ACT_NONE;
-  if (small_plan(k) == 8) return true;   // conv3x3_small_kernel: 128-pixel tiles of two 8x8 images
   if (k.prologue == DMC_PRO_AFFINE_SILU) {
     int R, nimg;
     return halo2_pro_plan(k, &R, &nimg) != 0;
@@ -2370,6 +2285,8 @@ int gemm1x1_plan(const ConvK& k) {
 template <typename T>
 int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
   constexpr int EPC = TT<T>::KPL;
+  DMC_REQUIRE(k.prologue != DMC_PRO_GN_SILU || img_plan(k),
+              "conv: DMC_PRO_GN_SILU is taken only by the small-map conv (dmc_conv_halo_prologue says when)");
   if (!dmc::opt(dmc::OPT_NO_NARROW) && sizeof(T) == 2) {
     int R, nimg;
     if (k.C2 == 0 && k.C1 <= EPC && k.Cout >= 16 && nin_plan(k, &R, &nimg)) {
@@ -2399,10 +2316,6 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
   if (sizeof(T) == 2) {
     const int bn = img_plan(k);
     if (bn) { launch_img(k, bn, s); return dmc::check_launch("dmc_conv2d"); }
-  }
-  if (sizeof(T) == 2) {
-    const int mt = small_plan(k);
-    if (mt) { launch_small(k, mt, s); return dmc::check_launch("dmc_conv2d"); }
   }
   if (sizeof(T) == 2) {
     const int tpb = gemm1x1_plan(k);
@@ -2525,6 +2438,7 @@ extern "C" int dmc_conv_halo_prologue(const dmc_conv_desc* d) {
   if (d == nullptr || d->dtype != DMC_BF16) return 0;
   ConvK k;
   if (fill_convk(d, nullptr, nullptr, nullptr, nullptr, nullptr, k) != 0) return 0;
+  if (k.prologue == DMC_PRO_GN_SILU) return img_plan(k) ? 1 : 0;
   int R, nimg;
   return halo2_pro_plan(k, &R, &nimg) ? 1 : 0;
 }

@@ -29,6 +29,7 @@ struct ConvK {
   int x1_bytes, x2_bytes, w_bytes;  // operand extents for buffer resources (0: too large / absent)
   int dtype_bytes;  // 4 (fp32) or 2 (bf16) storage
   int reg_epi;      // DMC_REG_EPI: the halo conv's epilogue straight from the accumulators (reg_epilogue)
+  int gn_G; float gn_eps;   // DMC_PRO_GN_SILU: groups, eps (gamma / beta in psc / psh)
 };
 
 // Source pixel of output pixel (n,oy,ox) under tap; returns -1 if it falls in the zero padding.
@@ -191,6 +192,9 @@ int fill_convk(const dmc_conv_desc* d, const void* x1, const void* x2, const voi
     DMC_REQUIRE(ok, "conv: taps must form a regular grid");
   }
   k.prologue = d->prologue; k.psc = d->pro_scale; k.psh = d->pro_shift; k.ldp = d->ld_pro;
+  k.gn_G = d->pro_groups; k.gn_eps = d->pro_eps;
+  DMC_REQUIRE(d->prologue != DMC_PRO_GN_SILU || (d->pro_groups > 0 && d->drop_thresh == 0 && d->pro_scale && d->pro_shift),
+              "conv: DMC_PRO_GN_SILU needs pro_groups, gamma / beta and no dropout");
   k.dseed = d->drop_seed; k.dthresh = d->drop_thresh; k.dscale = d->drop_scale; k.dld = d->drop_ld;
   k.dseed_base = d->drop_seed_base;
   k.bias = d->bias; k.addvec = d->addvec; k.ld_add = d->ld_add; k.resid = (const char*)d->resid; k.ld_res = d->ld_res;

@@ -38,9 +38,9 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"DMC_HALO_PRO", 1}, {"DMC_GN_STATS_SPLIT", 0}, {"DMC_GN_BWD_SPLIT", 0}, {"DMC_ATTN_STAGED", 0},
     {"DMC_ATTN_HG", 0}, {"DMC_WG_BLOCKS", 512}, {"DMC_GN_STATS_ONE_MAX", 1l << 20}, {"DMC_GN_BWD_ONE_MAX", 65536},
     {"DMC_NO_XCD", 0}, {"DMC_NO_EPI_STATS", 0}, {"DMC_WG_MINPIX", 0}, {"DMC_GN_BWD_SLICES", 2}, {"DMC_NO_SKGN", 0},
-    {"DMC_WG_HALO_TARGET", 256}, {"DMC_SK_TARGET", 240}, {"DMC_SK_MAX", 8}, {"DMC_NO_SMALL", 0}, {"DMC_NO_NHALO", 0},
-    {"DMC_SMALL_MASK", 1}, {"DMC_GN_BWD_FUSED", 4}, {"DMC_GN_BWD_FUSED_MAXHW", 1l << 30}, {"DMC_GN_BWD_NT", 1024},
-    {"DMC_REG_EPI", 3}, {"DMC_GEMM1X1", 1}, {"DMC_WG_PIPE", 1}, {"DMC_IMG_MASK", 15}, {"DMC_IMG_BN", 0},
+    {"DMC_WG_HALO_TARGET", 256}, {"DMC_SK_TARGET", 240}, {"DMC_SK_MAX", 8}, {"DMC_NO_NHALO", 0},
+    {"DMC_GN_BWD_FUSED", 4}, {"DMC_GN_BWD_FUSED_MAXHW", 1l << 30}, {"DMC_GN_BWD_NT", 1024},
+    {"DMC_REG_EPI", 3}, {"DMC_GEMM1X1", 1}, {"DMC_WG_PIPE", 1}, {"DMC_IMG_MASK", 15}, {"DMC_IMG_GN", 1},
 };
 struct OptTable {
   long v[OPT_COUNT];

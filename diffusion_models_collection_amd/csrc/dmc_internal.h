@@ -27,8 +27,8 @@ enum Opt {
   OPT_NO_NARROW, OPT_NO_GLDS, OPT_NO_SPLITK, OPT_NO_BUFLDS, OPT_NO_HALO, OPT_HALO_PRO, OPT_GN_STATS_SPLIT,
   OPT_GN_BWD_SPLIT, OPT_ATTN_STAGED, OPT_ATTN_HG, OPT_WG_BLOCKS, OPT_GN_STATS_ONE_MAX, OPT_GN_BWD_ONE_MAX,
   OPT_NO_XCD, OPT_NO_EPI_STATS, OPT_WG_MINPIX, OPT_GN_BWD_SLICES, OPT_NO_SKGN, OPT_WG_HALO_TARGET, OPT_SK_TARGET,
-  OPT_SK_MAX, OPT_NO_SMALL, OPT_NO_NHALO, OPT_SMALL_MASK, OPT_GN_BWD_FUSED, OPT_GN_BWD_FUSED_MAXHW, OPT_GN_BWD_NT,
-  OPT_REG_EPI, OPT_GEMM1X1, OPT_WG_PIPE, OPT_IMG_MASK, OPT_IMG_BN, OPT_COUNT
+  OPT_SK_MAX, OPT_NO_NHALO, OPT_GN_BWD_FUSED, OPT_GN_BWD_FUSED_MAXHW, OPT_GN_BWD_NT,
+  OPT_REG_EPI, OPT_GEMM1X1, OPT_WG_PIPE, OPT_IMG_MASK, OPT_IMG_GN, OPT_COUNT
 };
 long opt(Opt o);
 }  // namespace dmc

@@ -156,9 +156,10 @@ class ExecCore:
               bias=None, addvec=None, ld_add=0, resid=None, out=None, out_f32=False, out_nchw=False,
               dtype=None, packmode=L.PACK_FWD, w=None, Kc=None, silu_pre=None, ld_silu=0, split=None,
               act=L.ACT_NONE, y_pre=None, stats=None):
-        """Generic implicit-GEMM conv over 1-2 NHWC sources. pro = (kind, scale, shift). stats = the output Act:
-        in bf16 mode it gets the GroupNorm partials of the stored output (the next GroupNorm then needs no
-        statistics pass over it, see _gn)."""
+        """Generic implicit-GEMM conv over 1-2 NHWC sources. pro = (kind, scale, shift), or (PRO_GN_SILU, gamma, beta,
+        groups, eps): SiLU(GroupNorm(sources)) with the statistics taken inside the conv. stats = the output Act: in
+        bf16 mode it gets the GroupNorm partials of the stored output (the next GroupNorm then needs no statistics
+        pass over it, see _gn)."""
         dtype = dtype or self.dt
         gn_part = None
         if (stats is not None and _GN_PARTIALS and dtype == torch.bfloat16 and (OH * OW) % 64 == 0 and Cout % 8 == 0
@@ -179,6 +180,8 @@ class ExecCore:
         d = K.make_desc(dtype, N, a.H, a.W, C1, C2, ld1, ld2, Kc, OH, OW, Cout, taps, mode, stride)
         if pro is not None:
             K.set_prologue(d, pro[0], pro[1], pro[2], C1 + C2, drop, C1 + C2)
+            if pro[0] == L.PRO_GN_SILU:
+                d.pro_groups, d.pro_eps = pro[3], pro[4]
         elif drop is not None:
             if act not in (L.ACT_GELU_DROP, L.ACT_DGELU):
                 raise ValueError("dropout needs a prologue (or the GELU-dropout epilogue)")
@@ -407,6 +410,28 @@ class UNetExecutor(ExecCore):
             ok = self._halo_pro_cache[key] = K.conv_halo_prologue(d)
         return ok
 
+    def _img_gn_ok(self, srcs, Cout, gn):
+        """Whether dmc_conv2d runs the 3x3 conv of SiLU(GN(srcs)) on the small-map kernel with the GroupNorm
+        statistics computed inside it (DMC_PRO_GN_SILU: no statistics / finalize / apply launch; bf16 inference at
+        the 4x4 and 8x8 levels). Cached per shape and A/B switch."""
+        if self.dt != torch.bfloat16 or gn.weight is None or gn.bias is None:
+            return False
+        a = srcs[0]
+        b = srcs[1] if len(srcs) > 1 else None
+        N = a.t.shape[0]
+        key = ("gn", N, a.H, a.W, a.C, b.C if b else 0, a.t.shape[-1], b.t.shape[-1] if b else 0, Cout,
+               gn.num_groups, L.get_option("DMC_IMG_MASK"), L.get_option("DMC_IMG_GN"))
+        ok = self._halo_pro_cache.get(key)
+        if ok is None:
+            C1, C2 = a.C, (b.C if b else 0)
+            d = K.make_desc(self.dt, N, a.H, a.W, C1, C2, key[6], key[7], L.kc_for(C1 + C2, self.dt), a.H, a.W, Cout,
+                            K.TAPS3)
+            K.set_prologue(d, L.PRO_GN_SILU, gn.weight, gn.bias, C1 + C2)
+            d.pro_groups, d.pro_eps = gn.num_groups, gn.eps
+            lvl = 0 if a.H <= 4 else 1          # DMC_IMG_GN bit 0: the 4x4 levels, bit 1: the 8x8 levels
+            ok = self._halo_pro_cache[key] = bool((L.get_option("DMC_IMG_GN") >> lvl) & 1) and K.conv_halo_prologue(d)
+        return ok
+
     def _grad_target(self, act):
         """(buffer, accumulate) for writing a gradient contribution into act.grad."""
         if act.grad is None:
@@ -537,11 +562,18 @@ class UNetExecutor(ExecCore):
         # a1 = SiLU(GN1(x)) materialised once (the 3x3 implicit GEMM reads every pixel 9x; the weight
         # gradient re-reads it in backward). Inference (no tape): where the halo kernel takes the conv, it
         # applies GN+SiLU to its LDS-resident halo instead and nothing is materialised.
-        fused = self._gn_apply_small(srcs, gn1, True)
-        st1 = fused[0] if fused else self._gn(srcs, gn1)
         h1 = self._new(N, H, W, Cout)
         off = self.temb_off[id(rb)]
-        if fused:
+        gn_in1 = tape is None and self._img_gn_ok(srcs, Cout, gn1)
+        fused = None if gn_in1 else self._gn_apply_small(srcs, gn1, True)
+        st1 = None if gn_in1 else fused[0] if fused else self._gn(srcs, gn1)
+        if gn_in1:
+            # inference at 4x4 / 8x8: the conv takes GroupNorm statistics, affine and SiLU of its own images
+            a1 = None
+            self._conv(srcs, conv1, K.TAPS3, H, W, Cout, pro=(L.PRO_GN_SILU, gn1.weight, gn1.bias, gn1.num_groups,
+                                                              gn1.eps), bias=conv1.bias,
+                       addvec=self.addvec.view(self.addvec.shape[0], -1)[:, off:], ld_add=self._ld_add, out=h1.t, stats=h1)
+        elif fused:
             a1 = fused[1]
             self._conv([a1], conv1, K.TAPS3, H, W, Cout, bias=conv1.bias,
                        addvec=self.addvec.view(self.addvec.shape[0], -1)[:, off:], ld_add=self._ld_add, out=h1.t, stats=h1)
@@ -566,9 +598,14 @@ class UNetExecutor(ExecCore):
                 drop = drop + (self.seed_ptr,)
         self._blk_idx += 1
         out = self._new(N, H, W, Cout)
-        fused = self._gn_apply_small([h1], gn2, True, drop)
-        st2 = fused[0] if fused else self._gn([h1], gn2)
-        if fused:
+        gn_in2 = tape is None and drop is None and self._img_gn_ok([h1], Cout, gn2)
+        fused = None if gn_in2 else self._gn_apply_small([h1], gn2, True, drop)
+        st2 = None if gn_in2 else fused[0] if fused else self._gn([h1], gn2)
+        if gn_in2:
+            a2 = None
+            self._conv([h1], conv2, K.TAPS3, H, W, Cout, pro=(L.PRO_GN_SILU, gn2.weight, gn2.bias, gn2.num_groups,
+                                                              gn2.eps), bias=conv2.bias, resid=resid, out=out.t, stats=out)
+        elif fused:
             a2 = fused[1]
             self._conv([a2], conv2, K.TAPS3, H, W, Cout, bias=conv2.bias, resid=resid, out=out.t, stats=out)
         elif tape is None and drop is None and self._halo_pro_ok([h1], Cout, st2):

@@ -25,7 +25,11 @@ extern "C" {
 
 enum { DMC_F32 = 0, DMC_BF16 = 1 };
 enum { DMC_MODE_NORMAL = 0, DMC_MODE_UPSAMPLE = 1, DMC_MODE_DILATE = 2 };
-enum { DMC_PRO_NONE = 0, DMC_PRO_AFFINE_SILU = 1, DMC_PRO_SILU = 2, DMC_PRO_AFFINE = 3 };
+enum { DMC_PRO_NONE = 0, DMC_PRO_AFFINE_SILU = 1, DMC_PRO_SILU = 2, DMC_PRO_AFFINE = 3, DMC_PRO_GN_SILU = 4 };
+/* DMC_PRO_GN_SILU (round 6): SiLU(GroupNorm(x)) with the GroupNorm statistics computed inside the conv from the
+ * source images themselves (models/unet.py:35-36 / :51-52 at inference): pro_scale = gamma [C], pro_shift = beta [C],
+ * pro_groups = G, pro_eps = eps; no dropout. Only the whole-image small-map conv (4x4 / 8x8 maps) takes it:
+ * dmc_conv_halo_prologue() says whether a descriptor can be run this way, dmc_conv2d fails otherwise. */
 enum { DMC_LOSS_L1 = 0, DMC_LOSS_L2 = 1, DMC_LOSS_HUBER = 2 };
 enum { DMC_PACK_FWD = 0, DMC_PACK_DGRAD = 1, DMC_PACK_UPDGRAD = 2 };
 
@@ -84,6 +88,8 @@ typedef struct dmc_conv_desc {
                               * OH*OW % 64 == 0, Cout % 8 == 0, one NHWC output. Finalised by dmc_gn_finalize. */
   float* wg_bias;            /* dmc_conv2d_wgrad only: if set, also the bias gradient wg_bias[co] = scale * sum over
                               * pixels of dy[pix][co] (nn.Conv2d bias), from the same pass over dy */
+  int pro_groups;            /* DMC_PRO_GN_SILU: GroupNorm groups G (C / G channels per group) */
+  float pro_eps;             /* DMC_PRO_GN_SILU: GroupNorm eps */
 } dmc_conv_desc;
 enum { DMC_ACT_NONE = 0, DMC_ACT_GELU = 1, DMC_ACT_GELU_DROP = 2, DMC_ACT_DGELU = 3 };
 /* DGELU: the backward of GELU_DROP / GELU on an input-gradient conv: out = round(acc) * mask * scale * gelu'(u) with
@@ -102,7 +108,9 @@ size_t dmc_conv2d_workspace(const dmc_conv_desc* d);
  * GroupNorm output first (inference; replaces the GroupNorm -> SiLU -> Conv2d chain of models/unet.py:34-37,
  * :55-60 without the intermediate tensor). 0 otherwise (dmc_conv2d then uses the register-staged kernel).
  * Default since round 2 (DMC_HALO_PRO=0 turns it off): with the GroupNorm statistics from the producing conv's
- * epilogue the activation is not read before this conv at all. */
+ * epilogue the activation is not read before this conv at all. With prologue DMC_PRO_GN_SILU (round 6): 1 when the
+ * small-map conv takes `d` with the GroupNorm statistics computed in the conv itself (no statistics, finalize or
+ * apply launch before it), 0 when dmc_conv2d would reject it. */
 int dmc_conv_halo_prologue(const dmc_conv_desc* d);
 /* Which of the optional outputs dmc_conv2d(d, ..., ws_bytes) produces inside its kernel's epilogue (bit mask), as
  * opposed to one extra pass over the stored output: DMC_FUSED_GN_STATS (gn_part). */

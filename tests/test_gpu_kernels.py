@@ -358,12 +358,11 @@ def test_conv3x3_narrow_halo_kernels(case, dmc_opt):
 
 @pytest.mark.parametrize("case", ["f8_256", "f8_concat512", "d8_512out", "f4_256", "f4_concat512", "d4_512out"])
 def test_conv3x3_small_kernel(case, dmc_opt):
-    """The small-map 3x3 conv (conv3x3_small_kernel: two whole 8x8 / 4x4 images x 64 output channels per block,
-    K split over the block's four waves, wave-private LDS halos, weight fragments straight from L2, partial tiles
-    summed in LDS) at the UNet's B=128 shapes -- forward (one source and the up path's 256+256 concat) and the
-    input gradient with 512 output channels -- with the full epilogue (bias, time embedding, residual) and, at 8x8,
-    the GroupNorm partials: vs the fp32 torch reference, and vs the split-K LDS-DMA path it replaces
-    (DMC_NO_SMALL=1) on the same inputs."""
+    """The small-map 3x3 conv (round 6: conv3x3_img_kernel, whole-image tiles over the full K; it replaced round 4's
+    conv3x3_small_kernel) at the UNet's B=128 shapes -- forward (one source and the up path's 256+256 concat) and
+    the input gradient with 512 output channels -- with the full epilogue (bias, time embedding, residual) and, at
+    8x8, the GroupNorm partials: vs the fp32 torch reference, and vs the split-K LDS-DMA path (DMC_IMG_MASK=0) on
+    the same inputs."""
     L, K = _lib()
     dt = torch.bfloat16
     torch.manual_seed(9)
@@ -390,8 +389,8 @@ def test_conv3x3_small_kernel(case, dmc_opt):
     x1d, x2d = (xd[..., :C1].contiguous(), xd[..., C1:].contiguous()) if C2 else (xd, None)
     rd = nhwc(resid).to(dt).to(DEV)
     outs, parts = [], []
-    for no_small in (0, 1):
-        dmc_opt("DMC_NO_SMALL", no_small)
+    for mask in (15, 0):
+        dmc_opt("DMC_IMG_MASK", mask)
         d = K.make_desc(dt, N, H, W, C1, C2, C1, C2, L.kc_for(Cin, dt), H, W, Cout, taps)
         part = torch.full((N * H * W // 64 * (Cout // 8) * 2,), float("nan"), device=DEV) if H == 8 else None
         K.set_epilogue(d, bias=bias.to(DEV), addvec=addv.to(DEV), ld_add=Cout, resid=rd, ld_res=Cout, ldy1=Cout,
@@ -1307,20 +1306,22 @@ def test_lds_dma_plain_store_stress_bitwise(case, dmc_opt):
         assert torch.equal(ref, y0)
 
 
-@pytest.mark.parametrize("bn", [16, 32])
+@pytest.mark.parametrize("size", ["bn16", "bn32"])
 @pytest.mark.parametrize("case", ["f4", "f4_concat", "d4", "f8", "f8_concat", "d8"])
-def test_conv3x3_img_kernel(case, bn, dmc_opt):
+def test_conv3x3_img_kernel(case, size, dmc_opt):
     """Round 6 whole-image small-map conv (conv3x3_img_kernel, DMC_IMG_MASK): bf16 3x3 stride-1 forward (with the
     ResBlock conv2 epilogue: bias + time embedding + residual) and input gradient (flipped / transposed pack) at the
-    UNet's 4x4 and 8x8 levels, one and two (virtual concat) sources, BN = 16 / 32 output channels per block, against
-    the fp32 torch reference of the same bf16 operands (models/unet.py:34-60 at the two deepest levels)."""
+    UNet's 4x4 and 8x8 levels, one and two (virtual concat) sources, against the fp32 torch reference of the same
+    bf16 operands (models/unet.py:34-60 at the two deepest levels). The batch picks the channel tile: few images
+    give 16-channel tiles, many 32 (the planner's ~256-block rule)."""
     L, K = _lib()
     dmc_opt("DMC_IMG_MASK", 15)
-    dmc_opt("DMC_IMG_BN", bn)
     dt = torch.bfloat16
     torch.manual_seed(31)
     H = 4 if case.endswith("4") or "4_" in case else 8
-    N = 16 if H == 4 else 4
+    N = (16 if H == 4 else 4) if size == "bn16" else (256 if H == 4 else 128)
+    if size == "bn32" and case == "d8":
+        N = 64   # 8x8 with 512 output channels: one round of 256 blocks (more rounds keep the split-K plan)
     dgrad = case.startswith("d")
     C1, C2, Cout = {"f": (256, 0, 256), "f_concat": (256, 256, 256), "d": (256, 0, 512)}[
         case[0] + ("_concat" if "concat" in case else "")]
@@ -1363,3 +1364,52 @@ def test_conv3x3_img_kernel(case, bn, dmc_opt):
     K.conv(d, x1d, x2d, wp, y2)
     torch.cuda.synchronize()
     assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("case", ["c4", "c4_concat", "c8", "c8_concat"])
+def test_conv3x3_img_gn_silu_prologue(case, dmc_opt):
+    """Round 6: DMC_PRO_GN_SILU on the whole-image small-map conv -- conv(SiLU(GroupNorm(x))) with the GroupNorm
+    statistics of each image computed inside the conv from its LDS chunks (no statistics / finalize / apply launch),
+    the ResBlock inference chain of models/unet.py:34-38 / :50-60 at the 4x4 and 8x8 levels (one source, or the
+    up-path concat whose 512 channels make 64-channel groups), against torch's fp32 group_norm -> silu -> bf16 ->
+    conv2d on the same bf16 operands."""
+    L, K = _lib()
+    dmc_opt("DMC_IMG_MASK", 15)
+    dt = torch.bfloat16
+    torch.manual_seed(41)
+    H = 4 if case.startswith("c4") else 8
+    N = 128
+    C1, C2, Cout, G = (256, 256, 256, 8) if "concat" in case else (256, 0, 256, 8)
+    x1 = torch.randn(N, C1, H, H) * 1.7 + 0.3
+    x2 = torch.randn(N, C2, H, H) * 0.8 - 0.2 if C2 else None
+    xr = q(x1, dt) if x2 is None else torch.cat([q(x1, dt), q(x2, dt)], 1)
+    gamma, beta = torch.rand(C1 + C2) + 0.5, torch.randn(C1 + C2) * 0.3
+    a = q(F.silu(F.group_norm(xr, G, gamma, beta, 1e-5)), dt)
+    w = torch.randn(Cout, C1 + C2, 3, 3) / math.sqrt((C1 + C2) * 9)
+    bias, addv, resid = torch.randn(Cout), torch.randn(N, Cout), torch.randn(N, Cout, H, H)
+    yr = F.conv2d(a, q(w, dt), bias, padding=1) + addv[:, :, None, None] + q(resid, dt)
+    x1d = nhwc(x1).to(dt).to(DEV)
+    x2d = nhwc(x2).to(dt).to(DEV) if x2 is not None else None
+    Kc = L.kc_for(C1 + C2, dt)
+    wp = K.pack_weight(L.PACK_FWD, dt, w.to(DEV), Kc)
+    d = K.make_desc(dt, N, H, H, C1, C2, C1, C2, Kc, H, H, Cout, K.TAPS3)
+    K.set_prologue(d, L.PRO_GN_SILU, gamma.to(DEV), beta.to(DEV), C1 + C2)
+    d.pro_groups, d.pro_eps = G, 1e-5
+    assert K.conv_halo_prologue(d)
+    K.set_epilogue(d, bias=bias.to(DEV), addvec=addv.to(DEV), ld_add=Cout, resid=nhwc(resid).to(dt).to(DEV),
+                   ld_res=Cout, ldy1=Cout)
+    y = torch.empty(N, H, H, Cout, dtype=dt, device=DEV)
+    K.conv(d, x1d, x2d, wp, y)
+    torch.cuda.synchronize()
+    got = nchw(y.float().cpu())
+    e = rel_err(got, yr)
+    assert e < 1e-2, e
+    # a descriptor the small-map kernel cannot take is refused, not silently run another way
+    d2 = K.make_desc(dt, N, 16, 16, 256, 0, 256, 0, L.kc_for(256, dt), 16, 16, 256, K.TAPS3)
+    K.set_prologue(d2, L.PRO_GN_SILU, gamma[:256].to(DEV), beta[:256].to(DEV), 256)
+    d2.pro_groups, d2.pro_eps = G, 1e-5
+    assert not K.conv_halo_prologue(d2)
+    with pytest.raises(RuntimeError):
+        K.conv(d2, torch.zeros(N, 16, 16, 256, dtype=dt, device=DEV), None,
+               K.pack_weight(L.PACK_FWD, dt, torch.zeros(256, 256, 3, 3, device=DEV), L.kc_for(256, dt)),
+               torch.empty(N, 16, 16, 256, dtype=dt, device=DEV))
