@@ -385,8 +385,9 @@ def data_line(trainer, dev, B, steps):
 
 
 def rccl_one_rank_line(args, base_ms):
-    """The data-parallel step (GradSync + the segmented HIP-graph step: graphs cut at the gradient all-reduce
-    points, RCCL all-reduce of each 25 MB bucket issued between the replays) on a world_size-1 'nccl' (RCCL)
+    """The data-parallel step (GradSync + the graphed step: the RCCL all-reduce of each 25 MB bucket captured into the
+    one step graph -- round 6 -- or, if that capture fails, graphs cut at the all-reduce points with the collectives
+    issued between the replays) on a world_size-1 'nccl' (RCCL)
     process group, timed like the headline beside it: what the distributed plumbing costs per step on one GPU
     (segment launches + collective calls + the stream waits), with no inter-GPU traffic. Run as a child process
     (`bench.py --dist-one-rank`): a failure inside RCCL or its watchdog thread aborts that process, never the
@@ -404,10 +405,11 @@ def rccl_one_rank_line(args, base_ms):
     return {"train_img_s": d["value"], "ms_per_step": ms, "overhead_ms_per_step": round(ms - base_ms, 3),
             "graph_segments": d.get("graph_segments"), "steps": args.steps, "batch": d["config"]["per_gpu_batch"],
             "graphed": d.get("graphed"), "reduce_op": d.get("reduce_op"),
+            "comm_in_graph": d.get("comm_in_graph"), "comm_capture_fallback": d.get("comm_capture_fallback"),
             "exposed_comm_ms_per_step": d.get("exposed_comm_ms_per_step"),
             "note": "world_size-1 RCCL group (child process), ReduceOp.AVG forced (the op every multi-rank run takes, "
-                    "with RCCL's averaging kernel): GradSync buckets + segmented graph replay vs the single-graph "
-                    "headline"}
+                    "with RCCL's averaging kernel): GradSync buckets with the all-reduces captured into the one step "
+                    "graph (comm_in_graph; else the segmented graph chain) vs the single-graph headline"}
 
 
 DIT_S2 = dict(img_size=(32, 32), patch_size=2, in_channels=3, hidden_size=384, depth=12, num_heads=6, mlp_ratio=4.0)
@@ -567,6 +569,12 @@ def main():
         out["reduce_op"] = str(trainer.grad_sync.op).split(".")[-1]
         if trainer._graph is not None and trainer._graph.segs:
             out["graph_segments"] = len(trainer._graph.segs)
+        elif trainer._graph is not None and trainer._graph.comm_in_graph:
+            out["graph_segments"] = 1          # the all-reduces are captured inside the one step graph
+        if trainer._graph is not None:
+            out["comm_in_graph"] = bool(trainer._graph.comm_in_graph)
+            if trainer._graph.capture_fallback:
+                out["comm_capture_fallback"] = trainer._graph.capture_fallback
         if not args.no_train:
             # the part of the gradient all-reduce the backward did not hide (measured after the timed region)
             v = exposed_comm(trainer, pool)

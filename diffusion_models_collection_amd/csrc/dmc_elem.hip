@@ -40,7 +40,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"DMC_NO_XCD", 0}, {"DMC_NO_EPI_STATS", 0}, {"DMC_WG_MINPIX", 0}, {"DMC_GN_BWD_SLICES", 2}, {"DMC_NO_SKGN", 0},
     {"DMC_WG_HALO_TARGET", 256}, {"DMC_SK_TARGET", 240}, {"DMC_SK_MAX", 8}, {"DMC_NO_NHALO", 0},
     {"DMC_GN_BWD_FUSED", 4}, {"DMC_GN_BWD_FUSED_MAXHW", 1l << 30}, {"DMC_GN_BWD_NT", 1024},
-    {"DMC_REG_EPI", 3}, {"DMC_GEMM1X1", 1}, {"DMC_WG_PIPE", 1}, {"DMC_IMG_MASK", 15}, {"DMC_IMG_GN", 1},
+    {"DMC_REG_EPI", 3}, {"DMC_GEMM1X1", 1}, {"DMC_WG_PIPE", 1}, {"DMC_IMG_MASK", 15}, {"DMC_IMG_GN", 1}, {"DMC_WG_IMG4", 1},
 };
 struct OptTable {
   long v[OPT_COUNT];

@@ -28,7 +28,7 @@ enum Opt {
   OPT_GN_BWD_SPLIT, OPT_ATTN_STAGED, OPT_ATTN_HG, OPT_WG_BLOCKS, OPT_GN_STATS_ONE_MAX, OPT_GN_BWD_ONE_MAX,
   OPT_NO_XCD, OPT_NO_EPI_STATS, OPT_WG_MINPIX, OPT_GN_BWD_SLICES, OPT_NO_SKGN, OPT_WG_HALO_TARGET, OPT_SK_TARGET,
   OPT_SK_MAX, OPT_NO_NHALO, OPT_GN_BWD_FUSED, OPT_GN_BWD_FUSED_MAXHW, OPT_GN_BWD_NT,
-  OPT_REG_EPI, OPT_GEMM1X1, OPT_WG_PIPE, OPT_IMG_MASK, OPT_IMG_GN, OPT_COUNT
+  OPT_REG_EPI, OPT_GEMM1X1, OPT_WG_PIPE, OPT_IMG_MASK, OPT_IMG_GN, OPT_WG_IMG4, OPT_COUNT
 };
 long opt(Opt o);
 }  // namespace dmc

@@ -1023,6 +1023,222 @@ WgHaloPlan wgrad_halo_plan(const dmc_conv_desc* d) {
 // with 32- or 16-wide maps (rows of one image) or 8x8 maps (two images per tile), 64-aligned channel sources, no
 // prologue, ld_dy % 8 == 0. Returns OW (the template argument) or 0; splits the tiles so that ~DMC_WG_HALO_TARGET x 2
 // blocks of 64 x 64 run.
+// ---------------------------------------------------------------------------------------------
+// Whole-image weight gradient of the 4x4 levels (round 6; models/unet.py:34-60 at the deepest resolution). At B = 128
+// a 4x4 256 -> 256 layer reduces over only M = 2048 pixels, so one block can take ALL of them for its output tile and
+// no slab, split reduction or second launch is needed: a block owns 16 co x 16 ci x 9 taps, streams dy[:, co tile]
+// and x[:, ci tile] (32-byte pixel rows, 64 KB each over the whole batch) through a 3-slot ring of 512-pixel chunks
+// (32 whole images) with LDS-DMA, its 4 waves take 128 pixels of every chunk (4 k-steps of 32) and issue one
+// v_mfma_f32_16x16x32_bf16 per tap per k-step: A = dy^T and B = x shifted by the tap, both read transposed
+// (ds_read_b64_tr_b16). Per lane the tap shift and the zero padding are k-step invariant (chunks are whole images and
+// k-steps 32 pixels = two images), so every read address is precomputed once per chunk; a padding tap reads a zero
+// region. Rows are swizzled (row r at 32 * (r ^ (bit 3 of r) << 2)) so the two 16-lane groups of a transposed read
+// that sit 8 rows apart never share banks. The four waves' partial tiles are summed in LDS in a fixed order
+// ((w0 + w1) + (w2 + w3): deterministic) and stored coalesced as dw[co][ci][t]; the bias gradient (ci tile 0) is a
+// tenth MFMA against a region of bf16 ones.
+constexpr int kWiPch = 512;                  // pixels per chunk
+constexpr int kWiSlot = 2 * kWiPch * 32;     // dy + x rows of one chunk: 32 KB
+constexpr int kWiNs = 4;   // the whole batch's chunks in flight at once at B = 128
+
+DMC_DEV int wi_pos(int r) { return (r ^ (((r >> 3) & 1) << 2)) << 5; }
+
+DMC_DEV void wi_issue(const ConvK& a, const char* dy, int ld_dy, int dyb, char* slot, int chunk, int n0, int c0,
+                      int wave) {
+  // 32 pieces of 1 KB (32 rows x 32 B) per chunk: pieces 0-15 dy, 16-31 x; a wave issues 8. Lane i of a piece fills
+  // LDS bytes [16 i, 16 i + 16): swizzled row i / 2, half i % 2 -> data row r = row ^ (bit 3 << 2)
+  const int lane = threadIdx.x & 63;
+  const int rw = lane >> 1, half = lane & 1;
+  const int rr = rw ^ (((rw >> 3) & 1) << 2);
+  const bool first = c0 < a.C1;
+  const __amdgpu_buffer_rsrc_t rdy = __builtin_amdgcn_make_buffer_rsrc((void*)dy, (short)0, dyb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      first ? (void*)a.x1 : (void*)a.x2, (short)0, first ? a.x1_bytes : a.x2_bytes, 0x00020000);
+  const int ldx = first ? a.ld1 : a.ld2, cx = first ? c0 : c0 - a.C1;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int piece = wave * 8 + j;                     // uniform
+    const int pb = piece & 15;
+    const unsigned pix = (unsigned)(chunk * kWiPch + pb * 32 + rr);
+    char* dst = slot + (piece >= 16 ? kWiPch * 32 : 0) + pb * 1024;
+    if (piece < 16)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rdy, (LDS_AS void*)dst, 16, (pix * ld_dy + n0 + half * 8) * 2u, 0, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (LDS_AS void*)dst, 16, (pix * ldx + cx + half * 8) * 2u, 0, 0, 0);
+  }
+}
+
+// Transposed reads as inline asm: with the builtin, hipcc put an s_waitcnt vmcnt(0) before the first read of every
+// chunk (the reads may alias the in-flight LDS-DMA of the next chunks), draining the whole ring each chunk. The
+// asm reads carry their k-step offset as an immediate; the waits are explicit lgkmcnt counts and every result is
+// tied to its wait (scripts/lds_asm_check.py checks that no use is scheduled before it).
+template <int OFF>
+DMC_DEV v2i wi_tr_asm(unsigned a) {
+  v2i r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF) : "memory");
+  return r;
+}
+// the 2 + 18 (+ 2 with the bias) reads of k-step KS, reads [R0, R1) of them: 0-1 dy^T, 2 + 2t, 3 + 2t tap t, 20-21 ones
+template <int KS, int R0, int R1, bool BIAS>
+DMC_DEV void wi_read(unsigned sdy, int offA, int offB, const unsigned* xa, const unsigned* xb, unsigned ob, int oA,
+                     int oB, v2i (&r)[22]) {
+#pragma unroll
+  for (int i = R0; i < R1; ++i) {
+    if (i == 0) r[i] = wi_tr_asm<KS * 1024>(sdy + offA);
+    else if (i == 1) r[i] = wi_tr_asm<KS * 1024>(sdy + offB);
+    else if (i < 20) r[i] = wi_tr_asm<KS * 1024>(((i & 1) ? xb : xa)[(i - 2) >> 1]);
+    else if (BIAS) r[i] = wi_tr_asm<KS * 1024>(ob + (i == 20 ? oA : oB));
+  }
+}
+DMC_DEV v4i wi_join(const v2i& a, const v2i& b) { v4i r; r[0] = a[0]; r[1] = a[1]; r[2] = b[0]; r[3] = b[1]; return r; }
+
+DMC_DEV v4i wi_tr(unsigned pa, unsigned pb) {
+  v4s ra = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS v4s*)(uintptr_t)pa);
+  v4s rb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS v4s*)(uintptr_t)pb);
+  v2i ia = __builtin_bit_cast(v2i, ra), ib = __builtin_bit_cast(v2i, rb);
+  v4i r; r[0] = ia[0]; r[1] = ia[1]; r[2] = ib[0]; r[3] = ib[1];
+  return r;
+}
+
+template <bool BIAS>
+DMC_DEV void wi_tie(v2i (&r)[22]) {
+#pragma unroll
+  for (int i = 0; i < (BIAS ? 22 : 20); ++i) asm volatile("" : "+v"(r[i])::"memory");
+}
+template <bool BIAS>
+DMC_DEV void wi_mfma(const v2i (&r)[22], v4f (&acc)[10]) {
+  const v4i fa = wi_join(r[0], r[1]);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = mma16<bf16_t>(acc[t], fa, wi_join(r[2 + 2 * t], r[3 + 2 * t]));
+  if (BIAS) acc[9] = mma16<bf16_t>(acc[9], fa, wi_join(r[20], r[21]));
+}
+template <bool BIAS>
+DMC_DEV void wi_kstep_chunk(unsigned sdy, int offA, int offB, const unsigned* xa, const unsigned* xb, unsigned ob,
+                            int oA, int oB, v4f (&acc)[10]) {
+  constexpr int NR = BIAS ? 22 : 20, P1 = 12;
+  v2i r0[22], r1[22];
+  wi_read<0, 0, NR, BIAS>(sdy, offA, offB, xa, xb, ob, oA, oB, r0);
+  wi_read<1, 0, P1, BIAS>(sdy, offA, offB, xa, xb, ob, oA, oB, r1);
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(P1) : "memory");
+  wi_tie<BIAS>(r0);
+  wi_read<1, P1, NR, BIAS>(sdy, offA, offB, xa, xb, ob, oA, oB, r1);
+  wi_mfma<BIAS>(r0, acc);
+  wi_read<2, 0, P1, BIAS>(sdy, offA, offB, xa, xb, ob, oA, oB, r0);
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(P1) : "memory");
+  wi_tie<BIAS>(r1);
+  wi_read<2, P1, NR, BIAS>(sdy, offA, offB, xa, xb, ob, oA, oB, r0);
+  wi_mfma<BIAS>(r1, acc);
+  wi_read<3, 0, P1, BIAS>(sdy, offA, offB, xa, xb, ob, oA, oB, r1);
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(P1) : "memory");
+  wi_tie<BIAS>(r0);
+  wi_read<3, P1, NR, BIAS>(sdy, offA, offB, xa, xb, ob, oA, oB, r1);
+  wi_mfma<BIAS>(r0, acc);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  wi_tie<BIAS>(r1);
+  wi_mfma<BIAS>(r1, acc);
+}
+
+template <bool BIAS>
+__global__ __launch_bounds__(256) void wgrad3x3_img4_kernel(ConvK a, const char* dy, int ld_dy, int dyb, float* dw,
+                                                           float* dbias, float scale) {
+  constexpr int ZB = 4096;                               // zero (then ones) region: every k-step offset of a wave
+  __shared__ __attribute__((aligned(16))) char lds[kWiNs * kWiSlot + 2 * ZB];
+  char* const zero = lds + kWiNs * kWiSlot;
+  char* const ones = zero + ZB;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int Ctot = a.C1 + a.C2, nct = Ctot / 16, nco = a.Cout / 16;
+  // 1-D grid: co tile fastest (the ci tiles of one x slice are spread over the XCDs' L2s anyway)
+  const int co_t = blockIdx.x % nco, ci_t = blockIdx.x / nco;
+  const int n0 = co_t * 16, c0 = ci_t * 16;
+  const bool want_bias = BIAS && ci_t == 0;   // (the bias-less blocks of a BIAS launch run the tenth MFMA idle)
+  for (int i = threadIdx.x; i < ZB / 16; i += 256) {
+    *(v4i*)(zero + i * 16) = v4i{0, 0, 0, 0};
+    *(v4i*)(ones + i * 16) = v4i{0x3f803f80, 0x3f803f80, 0x3f803f80, 0x3f803f80};   // bf16 1.0
+  }
+  const int nchunk = a.M / kWiPch;
+#pragma unroll
+  for (int q = 0; q < kWiNs - 1; ++q)
+    if (q < nchunk) wi_issue(a, dy, ld_dy, dyb, lds + q * kWiSlot, q, n0, c0, wave);
+
+  // lane geometry of a transposed read: rows ka = 8h + q and kb = ka + 4 of a k-step, columns 4p .. 4p + 3
+  const int h = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int ra = 8 * h + q, rb = ra + 4;                 // k-step-local rows (pixel of an image pair)
+  // per tap: byte offset of the shifted row (k-step invariant) or -1 (zero padding)
+  int offa[9], offb[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int dy_ = t / 3 - 1, dx_ = t % 3 - 1;
+    const int ya = (ra >> 2) & 3, xa = ra & 3, yb = (rb >> 2) & 3, xb = rb & 3;
+    const bool va = (unsigned)(ya + dy_) < 4u && (unsigned)(xa + dx_) < 4u;
+    const bool vb = (unsigned)(yb + dy_) < 4u && (unsigned)(xb + dx_) < 4u;
+    offa[t] = va ? wi_pos(ra + dy_ * 4 + dx_) + 8 * p : -1;
+    offb[t] = vb ? wi_pos(rb + dy_ * 4 + dx_) + 8 * p : -1;
+  }
+  const int offA = wi_pos(ra) + 8 * p, offB = wi_pos(rb) + 8 * p;
+  v4f acc[10];
+#pragma unroll
+  for (int t = 0; t < 10; ++t) acc[t] = v4f{0.f, 0.f, 0.f, 0.f};
+  constexpr int PPC = 8;
+  for (int c = 0; c < nchunk; ++c) {
+    const int after = min(nchunk - 1, c + kWiNs - 2) - c;   // chunks issued after c (this wave's pieces)
+    if (after >= 2) __builtin_amdgcn_s_waitcnt(waitcnt_vm(2 * PPC));
+    else if (after == 1) __builtin_amdgcn_s_waitcnt(waitcnt_vm(PPC));
+    else __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (c + kWiNs - 1 < nchunk)
+      wi_issue(a, dy, ld_dy, dyb, lds + ((c + kWiNs - 1) % kWiNs) * kWiSlot, c + kWiNs - 1, n0, c0, wave);
+    const unsigned sdy = (unsigned)(uintptr_t)(lds + (c % kWiNs) * kWiSlot) + wave * 128 * 32;
+    const unsigned sx = sdy + kWiPch * 32;
+    const unsigned zb = (unsigned)(uintptr_t)zero, ob = (unsigned)(uintptr_t)ones;
+    unsigned xa[9], xb[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      xa[t] = offa[t] >= 0 ? sx + offa[t] : zb;
+      xb[t] = offb[t] >= 0 ? sx + offb[t] : zb;
+    }
+    // k-step = 32 pixels: + 1 KB in both images. Zero-padding lanes read the zero region at the same k-step offset
+    // (it spans every offset of a wave). The reads of k-step ks + 1 go out before k-step ks's MFMAs (12 before the
+    // wait for ks's, lgkmcnt counts at most 15, the rest after it), into the other register set.
+    wi_kstep_chunk<BIAS>(sdy, offA, offB, xa, xb, ob, offA % 1024, offB % 1024, acc);
+  }
+  // fixed-order reduction of the four waves' tiles through LDS (the ring is free after this barrier)
+  __syncthreads();
+  float* red = (float*)lds;                              // [wave][10][16 co][16 ci]
+  const int r = lane & 15, hh = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 10; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[((wave * 10 + t) * 16 + hh * 4 + e) * 16 + r] = acc[t][e];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 16 * 16 * 9; i += 256) {  // dw[co][ci][t] order: coalesced rows of 144 floats
+    const int co = i / 144, rem = i - co * 144, ci = rem / 9, t = rem - ci * 9;
+    auto at = [&](int w) { return red[((w * 10 + t) * 16 + co) * 16 + ci]; };
+    const float v = (at(0) + at(1)) + (at(2) + at(3));
+    dw[((size_t)(n0 + co) * Ctot + c0 + ci) * 9 + t] = v * scale;
+  }
+  if (want_bias && threadIdx.x < 16) {
+    const int co = threadIdx.x;
+    auto at = [&](int w) { return red[((w * 10 + 9) * 16 + co) * 16]; };
+    dbias[n0 + co] = ((at(0) + at(1)) + (at(2) + at(3))) * scale;
+  }
+}
+
+// The whole-image 4x4 weight gradient applies (bf16 3x3 stride 1, forward taps, 4x4 maps, whole 512-pixel chunks,
+// 16-aligned channels, DMC_WG_IMG4 = 1).
+bool wgrad_img4_ok(const dmc_conv_desc* d, const ConvK& k, int ld_dy) {
+  if (d->dtype != DMC_BF16 || !dmc::opt(dmc::OPT_WG_IMG4) || k.prologue != DMC_PRO_NONE) return false;
+  if (k.mode != DMC_MODE_NORMAL || k.stride != 1 || k.ntaps != 9 || k.tkw != 3 || k.OH != 4 || k.OW != 4 || k.H != 4 ||
+      k.W != 4)
+    return false;
+  if (k.tdy0 != -1 || k.tsy != 1 || k.tdx0 != -1 || k.tsx != 1) return false;
+  if (k.M % kWiPch || k.M / kWiPch < 1 || k.C1 % 16 || k.C2 % 16 || k.Cout % 16 || ld_dy % 8 || k.ld1 % 8 ||
+      (k.C2 && k.ld2 % 8) || k.x1_bytes == 0 || (k.C2 && k.x2_bytes == 0))
+    return false;
+  return (size_t)k.M * ld_dy * 2 < 0x7fff0000u;
+}
+
 struct WgPipePlan {
   int ow, splits, tps;
 };
@@ -1081,6 +1297,18 @@ static int wgrad_partial(const dmc_conv_desc* d, const void* dy, int ld_dy, cons
   const int epc = d->dtype == DMC_F32 ? 4 : 8;
   DMC_REQUIRE(ld_dy % epc == 0, "wgrad: ld_dy %d alignment", ld_dy);
   hipStream_t s = dmc::as_stream(stream);
+  if (wgrad_img4_ok(d, k, ld_dy)) {
+    // the whole reduction inside the kernel: dw (and the bias gradient) written directly, no job left to reduce
+    const int nb = (d->Cout / 16) * ((k.C1 + k.C2) / 16), dyb = (int)((size_t)k.M * ld_dy * 2);
+    if (d->wg_bias)
+      wgrad3x3_img4_kernel<true><<<nb, 256, 0, s>>>(k, (const char*)dy, ld_dy, dyb, dw, d->wg_bias, scale);
+    else
+      wgrad3x3_img4_kernel<false><<<nb, 256, 0, s>>>(k, (const char*)dy, ld_dy, dyb, dw, nullptr, scale);
+    if (dmc::check_launch("dmc_conv2d_wgrad")) return 2;
+    *job = dmc_wgrad_job{};
+    job->splits = 0;
+    return 0;
+  }
   int pps;
   int splits = wgrad_splits(d, &pps);
   const int KK = d->ntaps * d->Kc;
@@ -1182,8 +1410,13 @@ extern "C" int dmc_conv2d_wgrad(const dmc_conv_desc* d, const void* dy, int ld_d
   return r ? r : dmc_wgrad_reduce_batch(&job, 1, stream);
 }
 
-extern "C" int dmc_wgrad_reduce_batch(const dmc_wgrad_job* jobs, int njobs, void* stream) {
-  DMC_REQUIRE(njobs >= 0 && njobs <= kWgJobs, "wgrad_reduce_batch: %d jobs (at most %d)", njobs, kWgJobs);
+extern "C" int dmc_wgrad_reduce_batch(const dmc_wgrad_job* jobs_in, int njobs_in, void* stream) {
+  DMC_REQUIRE(njobs_in >= 0 && njobs_in <= kWgJobs, "wgrad_reduce_batch: %d jobs (at most %d)", njobs_in, kWgJobs);
+  // jobs with splits == 0 are finished already (a kernel that reduced in-kernel, e.g. wgrad3x3_img4_kernel)
+  dmc_wgrad_job jobs[kWgJobs];
+  int njobs = 0;
+  for (int i = 0; i < njobs_in; ++i)
+    if (jobs_in[i].splits != 0) jobs[njobs++] = jobs_in[i];
   if (njobs == 0) return 0;
   WgBatch b;
   b.njobs = njobs;

@@ -194,6 +194,8 @@ class WgradDefer:
         return ws
 
     def add(self, job):
+        if job.splits == 0:
+            return              # reduced inside the kernel (dmc_conv2d_wgrad_partial wrote dw directly)
         self.jobs.append(job)
         if self.every and len(self.jobs) >= self.every:
             self.flush()

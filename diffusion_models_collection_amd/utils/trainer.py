@@ -17,7 +17,9 @@ What changes (MI355X-first):
     (the reference syncs twice per step via loss.item()).
 """
 import math
+import os
 import time
+import warnings
 import weakref
 from pathlib import Path
 
@@ -272,6 +274,8 @@ class GraphedTrainStep:
         self.key = None
         self.measure_comm = False
         self.comm_events = []
+        self.comm_in_graph = False     # data parallel: the RCCL all-reduces are inside the one step graph
+        self.capture_fallback = None   # why that capture was not possible (the segmented chain runs instead)
 
     @property
     def tr(self):
@@ -308,14 +312,31 @@ class GraphedTrainStep:
         ex.wgen += 1                      # the captured forward must contain the weight-pack launch
         ex.seed_ptr = self.h_dev.data_ptr() + 9 * 4
         try:
-            self._capture_direct(ex, f)
+            gs = tr.grad_sync
+            self.comm_in_graph = False
+            if gs is not None and gs.native_avg and os.environ.get("DMC_DDP_CAPTURE", "1") != "0":
+                # RCCL collectives captured into the one step graph (no graph boundaries, no host-side collective
+                # calls per step); any failure falls back to the segmented chain below
+                try:
+                    self._capture_direct(ex, f, comm_in_graph=True)
+                    self.comm_in_graph = True
+                except Exception as e:   # noqa: BLE001
+                    warnings.warn(f"capturing the RCCL all-reduces into the step graph failed ({e!r}); "
+                                  "using the segmented graph chain")
+                    self.capture_fallback = repr(e)
+                    gs.works, gs.done = [], 0
+                    torch.cuda.synchronize()
+            if not self.comm_in_graph:
+                self._capture_direct(ex, f)
         finally:
             ex.seed_ptr = None
         tr.optimizer.zero_grad()
 
-    def _capture_direct(self, ex, f):
-        """The step captured straight from the executor, without autograd: one graph, or (data parallel) a chain of
-        graphs cut at the gradient all-reduce points.
+    def _capture_direct(self, ex, f, comm_in_graph=False):
+        """The step captured straight from the executor, without autograd: one graph -- with the RCCL all-reduces
+        captured inside it when comm_in_graph (GradSync.hook runs during the capture: the collectives go on RCCL's
+        stream behind event edges from the compute stream, and the optimizer segment waits for them; round 6) --
+        or (gloo, DMC_DDP_CAPTURE=0, or a failed comm capture) a chain of graphs cut at the all-reduce points.
 
         No autograd node takes part in a capture. Round 6 found why that matters: a caller that still holds the
         previous step's loss (the reference loop keeps `loss` alive across iterations, utils/trainer.py:249-268)
@@ -352,6 +373,9 @@ class GraphedTrainStep:
             segs.append((state["g"], bucket))
 
         def hook(flat, hi, final):
+            if comm_in_graph:
+                gs.hook(flat, hi, final)   # async all-reduces (and the final waits) captured into this graph
+                return
             if gs.cut(hi, state["done"], flat.numel(), final):
                 end((state["done"], hi))
                 state["done"] = hi
@@ -359,7 +383,8 @@ class GraphedTrainStep:
 
         # the executor joins its weight-gradient side stream only where a segment ends (True here
         # serialised the side stream after every record of every captured segment)
-        hook.wants = lambda hi, final: final or gs.cut(hi, state["done"], ex.gtotal, final)
+        hook.wants = gs.wants if comm_in_graph else (lambda hi, final: final or gs.cut(hi, state["done"], ex.gtotal,
+                                                                                        final))
         self.one = torch.ones((), dtype=torch.float32, device=dev)
         old_hook = ex.grad_hook
         ex.grad_hook = hook if gs is not None else None
@@ -390,7 +415,8 @@ class GraphedTrainStep:
         finally:
             ex.grad_hook = old_hook
         torch.cuda.current_stream().wait_stream(stream)
-        self.segs, self.graph, self.loss_s = (segs if gs is not None else None), segs[-1][0], loss.detach()
+        self.segs = segs if gs is not None and not comm_in_graph else None
+        self.graph, self.loss_s = segs[-1][0], loss.detach()
         self.flat = ex.flat
 
     def _replay(self):

@@ -20,8 +20,9 @@ def _regs(text):
 
 
 def check(asm_text, window=400):
-    """[(function, read line, offending line)] for every asm ds_read whose destination is read before the next
-    s_waitcnt lgkmcnt(0). Only reads emitted from inline asm (between ;;#ASMSTART / ;;#ASMEND) are checked."""
+    """[(function, read line, offending line)] for every asm ds_read whose destination is read before an
+    s_waitcnt lgkmcnt(N) that covers it (N <= the LDS operations issued after it: LDS completes in order). Only
+    reads emitted from inline asm (between ;;#ASMSTART / ;;#ASMEND) are checked."""
     lines = asm_text.split("\n")
     bad, func, in_asm = [], "?", False
     for n, line in enumerate(lines):
@@ -40,11 +41,17 @@ def check(asm_text, window=400):
         if not mm:
             continue
         dst = _regs(mm.group(1))
+        younger = 0      # LDS operations issued after this read (they complete in order)
         for k in range(n + 1, min(len(lines), n + window)):
             t = lines[k].split(";")[0]
-            if "s_waitcnt" in t and "lgkmcnt(0)" in t:
-                break
-            if not t.strip() or re.match(r"\s*ds_read", t):
+            w = re.search(r"lgkmcnt\((\d+)\)", t) if "s_waitcnt" in t else None
+            if w and int(w.group(1)) <= younger:
+                break    # at most N outstanding and N younger ones exist: this read has completed
+            if re.match(r"\s*ds_", t):
+                younger += 1
+                if re.match(r"\s*ds_read", t):
+                    continue
+            if not t.strip():
                 continue
             ops = t.strip().split(None, 1)
             if len(ops) < 2:

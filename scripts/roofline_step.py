@@ -68,9 +68,10 @@ def a_gn_apply(dtype, x1, x2, N, HW, C1, C2, *a, **k):
     return 0.0, 2 * N * HW * (C1 + C2) * x1.element_size(), f"N{N} HW{HW} C{C1 + C2}"
 
 
-def a_gn_apply_fin(dtype, x1, x2, N, HW, C1, C2, *a, **k):
+def a_gn_stats_apply(dtype, x1, x2, N, HW, C1, C2, *a, **k):
+    # dmc_gn_stats_apply (4x4 levels): the sample read twice (statistics, then apply) + the output written
     C = C1 + C2
-    return 0.0, 2 * N * HW * C * x1.element_size() + N * HW // 64 * C // 8 * 8, f"N{N} HW{HW} C{C}"
+    return 0.0, 3 * N * HW * C * x1.element_size(), f"N{N} HW{HW} C{C}"
 
 
 def a_gn_bwd(dtype, g, ld_g, x1, x2, N, HW, C1, C2, ld1, ld2, G, mr, gamma, beta, silu, drop, dx1, dx2, ld_dx1,
@@ -124,7 +125,7 @@ def wrap(mod, name, alg):
 
 
 for nm, alg in [("conv", a_conv), ("wgrad", a_wgrad), ("gn_stats", a_gn_stats), ("gn_finalize", a_gn_finalize),
-                ("gn_apply", a_gn_apply), ("gn_apply_fin", a_gn_apply_fin), ("gn_bwd", a_gn_bwd), ("attn_fwd", a_attn_fwd), ("attn_bwd", a_attn_bwd),
+                ("gn_apply", a_gn_apply), ("gn_stats_apply", a_gn_stats_apply), ("gn_bwd", a_gn_bwd), ("attn_fwd", a_attn_fwd), ("attn_bwd", a_attn_bwd),
                 ("adamw_flat_dev", a_adamw_dev), ("adamw_flat", a_adamw), ("grad_norm_flat", a_grad_norm), ("pack_input", a_gn_none),
                 ("loss_fwd", a_gn_none), ("loss_bwd", a_gn_none), ("add_", a_gn_none), ("upsample2x", a_gn_none),
                 ("channel_sum", a_gn_none), ("colsum_batch", a_gn_none), ("time_embed", a_gn_none), ("unpack_output", a_gn_none)]:

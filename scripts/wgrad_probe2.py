@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--shape", default="")
     ap.add_argument("--only", default="", help="one setting name (e.g. pipe)")
     a = ap.parse_args()
-    settings = [("r4 halo", {"DMC_WG_PIPE": 0}), ("pipe", {}), ("pipe t128", {"DMC_WG_HALO_TARGET": 128}),
+    settings = [("r4 halo", {"DMC_WG_PIPE": 0}), ("pipe", {"DMC_WG_IMG4": 0}), ("img4", {"DMC_WG_IMG4": 1}), ("pipe t128", {"DMC_WG_HALO_TARGET": 128}),
                 ("pipe t192", {"DMC_WG_HALO_TARGET": 192}), ("pipe t384", {"DMC_WG_HALO_TARGET": 384}),
                 ("pipe t16", {"DMC_WG_HALO_TARGET": 16}), ("pipe t32", {"DMC_WG_HALO_TARGET": 32}),
                 ("pipe t64", {"DMC_WG_HALO_TARGET": 64})]

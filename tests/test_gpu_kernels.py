@@ -1413,3 +1413,45 @@ def test_conv3x3_img_gn_silu_prologue(case, dmc_opt):
         K.conv(d2, torch.zeros(N, 16, 16, 256, dtype=dt, device=DEV), None,
                K.pack_weight(L.PACK_FWD, dt, torch.zeros(256, 256, 3, 3, device=DEV), L.kc_for(256, dt)),
                torch.empty(N, 16, 16, 256, dtype=dt, device=DEV))
+
+
+@pytest.mark.parametrize("shape", [(128, 4, 4, 256, 0, 256), (128, 4, 4, 256, 256, 256), (64, 4, 4, 128, 0, 64)])
+@pytest.mark.parametrize("deferred", [False, True])
+def test_wgrad_img4_kernel(shape, deferred, dmc_opt):
+    """Round 6 whole-image 4x4 weight gradient (wgrad3x3_img4_kernel, DMC_WG_IMG4): every pixel of the batch in one
+    block per 16 co x 16 ci tile, no slab and no reduction job (a deferred call leaves nothing to flush), the bias
+    gradient from a ones-MFMA: against the fp32 torch reference of the same bf16 operands and the pipelined slab
+    kernel (DMC_WG_IMG4=0), one and two (virtual concat) sources, bitwise reproducible run to run
+    (models/unet.py:34-60 conv weights at the 4x4 level)."""
+    from diffusion_models_collection_amd import _lib as L, kernels as K
+    N, H, W, C1, C2, Cout = shape
+    gen = torch.Generator().manual_seed(7 + N + C2)
+    dt = torch.bfloat16
+    x = torch.randn(N, H, W, C1 + C2, generator=gen).to(dt)
+    g = torch.randn(N, H, W, Cout, generator=gen).to(dt)
+    x1d = x[..., :C1].contiguous().to(DEV)
+    x2d = x[..., C1:].contiguous().to(DEV) if C2 else None
+    gd = g.to(DEV)
+    d = K.make_desc(dt, N, H, W, C1, C2, C1, C2, L.kc_for(C1 + C2, dt), H, W, Cout, K.TAPS3)
+    res = []
+    for img in (1, 1, 0):
+        dmc_opt("DMC_WG_IMG4", img)
+        dw = torch.full((Cout, C1 + C2, 3, 3), float("nan"), device=DEV)
+        db = torch.full((Cout,), float("nan"), device=DEV)
+        if deferred:
+            defer = K.WgradDefer()
+            K.wgrad(d, gd, Cout, x1d, x2d, dw, scale=0.5, dbias=db, defer=defer)
+            if img:
+                assert not defer.jobs      # reduced in the kernel: nothing deferred
+            defer.flush()
+        else:
+            K.wgrad(d, gd, Cout, x1d, x2d, dw, scale=0.5, dbias=db)
+        torch.cuda.synchronize()
+        res.append((dw.cpu(), db.cpu()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])   # deterministic
+    xr = x.permute(0, 3, 1, 2).float()
+    gr = g.permute(0, 3, 1, 2).float()
+    wr = 0.5 * torch.nn.grad.conv2d_weight(xr, (Cout, C1 + C2, 3, 3), gr, padding=1)
+    assert rel_err(res[0][0], wr) < 1e-5, rel_err(res[0][0], wr)
+    assert rel_err(res[0][0], res[2][0]) < 1e-5
+    assert rel_err(res[0][1], 0.5 * gr.sum((0, 2, 3))) < 1e-5

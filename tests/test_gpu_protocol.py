@@ -439,8 +439,9 @@ def _free_port():
         return s.getsockname()[1]
 
 
+@pytest.mark.parametrize("capture", ["segmented", "in_graph"])
 @pytest.mark.parametrize("force_avg", [False, True], ids=["sum", "avg"])
-def test_rccl_single_rank_grad_sync_matches_single_process(tmp_path, monkeypatch, force_avg):
+def test_rccl_single_rank_grad_sync_matches_single_process(tmp_path, monkeypatch, force_avg, capture):
     """The RCCL branch never exercised by the 2-rank gloo test (utils/helpers.py:88 backend 'nccl' + the DDP step
     of utils/trainer.py:57-61): a world_size-1 'nccl' process group (RCCL on ROCm), GradSync issued from the
     executor's grad-ready hook on RCCL's stream, and the segmented HIP-graph step (graphs cut at the all-reduce
@@ -448,7 +449,8 @@ def test_rccl_single_rank_grad_sync_matches_single_process(tmp_path, monkeypatch
     nothing); `avg`: ReduceOp.AVG forced (GradSync force_avg) -- ncclAvg with its averaging kernel, the op every
     multi-rank run takes (utils/trainer.py GradSync). Over 5 steps (bf16, dropout 0.1, EMA) the losses,
     parameters and EMA equal the non-distributed graphed step's within 1e-6 (in practice bitwise: the average
-    over one rank is the identity)."""
+    over one rank is the identity). `in_graph` (round 6, the default on RCCL): the all-reduces captured inside the
+    one step graph; `segmented`: DMC_DDP_CAPTURE=0, the chain of graphs cut at the all-reduce points."""
     import torch.distributed as dist
     from diffusion_models_collection_amd.models import UNet
     from diffusion_models_collection_amd.diffusion import DDPM
@@ -456,6 +458,7 @@ def test_rccl_single_rank_grad_sync_matches_single_process(tmp_path, monkeypatch
     mp = dict(image_size=(16, 16), in_channels=3, model_channels=32, out_channels=3, num_res_blocks=1,
               attention_resolutions=(8,), dropout=0.1, channel_mult=(1, 2), use_attention=True)
     monkeypatch.setenv("DMC_GRAPH", "1")
+    monkeypatch.setenv("DMC_DDP_CAPTURE", "1" if capture == "in_graph" else "0")
 
     def run(sync):
         torch.manual_seed(0)
@@ -491,11 +494,14 @@ def test_rccl_single_rank_grad_sync_matches_single_process(tmp_path, monkeypatch
     finally:
         dist.destroy_process_group()
     tr = got[3]
-    assert tr._graph is not None and tr._graph.segs is not None and len(tr._graph.segs) >= 3, "segmented step"
+    if capture == "in_graph":
+        assert tr._graph is not None and tr._graph.comm_in_graph and tr._graph.segs is None, tr._graph.capture_fallback
+    else:
+        assert tr._graph is not None and tr._graph.segs is not None and len(tr._graph.segs) >= 3, "segmented step"
     assert tr._graph.replays == 3, tr._graph.replays          # 5 steps: 2 eager warm-up steps, then replays
     bitwise = torch.equal(got[0], ref[0]) and all(torch.equal(got[1][k], ref[1][k]) for k in ref[1])
-    print(f"RCCL 1-rank segmented step: {len(tr._graph.segs)} segments; bitwise equal to the single-process "
-          f"graph: {bitwise}")
+    print(f"RCCL 1-rank {capture} step: {len(tr._graph.segs) if tr._graph.segs else 1} graph(s); bitwise equal to "
+          f"the single-process graph: {bitwise}")
     assert (got[0] - ref[0]).abs().max().item() <= 1e-6 * ref[0].abs().max().item()
     for k in ref[1]:
         assert (got[1][k] - ref[1][k]).abs().max().item() <= 1e-6 * max(ref[1][k].abs().max().item(), 1.0), k

@@ -3,7 +3,8 @@
 DESIGN.md section 3 "LDS hazards". The halo GroupNorm+SiLU prologue and the small-map conv's in-kernel GroupNorm
 read LDS with inline asm (plain reads would make hipcc drain the in-flight chunk DMA). Round 6 found hipcc
 scheduling uses of such reads before the asm s_waitcnt (all outputs NaN); the fix ties every result to the wait.
-This test compiles dmc_conv.hip for gfx950 to assembly and checks every asm ds_read (scripts/lds_asm_check.py),
+This test compiles dmc_conv.hip and dmc_wgrad.hip (the 4x4 weight gradient's asm transposed reads with partial
+lgkmcnt waits) for gfx950 to assembly and checks every asm ds_read (scripts/lds_asm_check.py),
 and checks the checker on a hand-made bad sequence."""
 import shutil
 import subprocess
@@ -35,8 +36,9 @@ def test_checker_flags_a_premature_use():
 
 
 @pytest.mark.skipif(not Path(HIPCC).exists() and shutil.which("hipcc") is None, reason="hipcc not available")
-def test_conv_kernels_asm_lds_reads_wait_before_use(tmp_path):
-    src = ROOT / "diffusion_models_collection_amd" / "csrc" / "dmc_conv.hip"
+@pytest.mark.parametrize("unit", ["dmc_conv.hip", "dmc_wgrad.hip"])
+def test_conv_kernels_asm_lds_reads_wait_before_use(unit, tmp_path):
+    src = ROOT / "diffusion_models_collection_amd" / "csrc" / unit
     out = tmp_path / "conv.s"
     cmd = [HIPCC if Path(HIPCC).exists() else "hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
            "-I", str(ROOT / "include"), "-I", str(src.parent), "--offload-device-only", "-S", "-o", str(out),
@@ -44,6 +46,6 @@ def test_conv_kernels_asm_lds_reads_wait_before_use(tmp_path):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     text = out.read_text()
-    assert text.count(";;#ASMSTART") > 20 and "ds_read_b128" in text
+    assert text.count(";;#ASMSTART") > 20 and "ds_read_b" in text
     viol = lds_asm_check.check(text)
     assert viol == [], viol[:5]
