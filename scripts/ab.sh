@@ -25,7 +25,7 @@ for rep in $(seq 1 ${REPS:-1}); do
     env $cfg timeout -k 10 300 python -u bench.py $ARGS > "$O/ab$i.json" 2> "$O/ab$i.err" || { tail -30 "$O/ab$i.err"; exit 1; }
     python3 - "$O/ab$i.json" "$cfg" <<'PY'
 import json, sys
-d = json.load(open(sys.argv[1]))
+d = json.loads([l for l in open(sys.argv[1]).read().splitlines() if l.startswith("{")][-1])   # RCCL prints a banner
 parts = [f"train {d['value']}"] if d.get("value") else []
 for k in ("ddim50", "ddim50_cfg"):
     if k in d:

@@ -449,8 +449,8 @@ def test_rccl_single_rank_grad_sync_matches_single_process(tmp_path, monkeypatch
     nothing); `avg`: ReduceOp.AVG forced (GradSync force_avg) -- ncclAvg with its averaging kernel, the op every
     multi-rank run takes (utils/trainer.py GradSync). Over 5 steps (bf16, dropout 0.1, EMA) the losses,
     parameters and EMA equal the non-distributed graphed step's within 1e-6 (in practice bitwise: the average
-    over one rank is the identity). `in_graph` (round 6, the default on RCCL): the all-reduces captured inside the
-    one step graph; `segmented`: DMC_DDP_CAPTURE=0, the chain of graphs cut at the all-reduce points."""
+    over one rank is the identity). `segmented` (the default): the chain of graphs cut at the all-reduce points;
+    `in_graph` (round 6, DMC_DDP_CAPTURE=1): the all-reduces captured inside the one step graph."""
     import torch.distributed as dist
     from diffusion_models_collection_amd.models import UNet
     from diffusion_models_collection_amd.diffusion import DDPM
