@@ -922,6 +922,23 @@ __global__ __launch_bounds__(256, NS <= 2 ? 2 : 1) void gemm1x1_persist_kernel(C
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
+    // residual epilogue (round 6: the attention output projection x + proj(h), the accumulating 1x1 input
+    // gradients): the tile's residual chunks are loaded at its last stage, BEFORE that stage's DMA issue, so the
+    // epilogue waits for them without draining the ring behind them
+    v2i rres[4][4];
+    const bool last = (s + 1) % kst == 0;
+    if (a.resid && last) {
+      const int t = t_begin + s / kst, mb = t / NB, nb = t - mb * NB;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int co = nb * BN + wn * 64 + i * 16 + fh * 4, px = mb * BM + wm * 64 + j * 16 + fr;
+          rres[i][j] = *(const v2i*)(a.resid + ((size_t)px * a.ld_res + co) * 2);
+        }
+      nvm += 16;
+      asm volatile("" ::: "memory");
+    }
     if (s + NS - 1 < total) {
       issue(s + NS - 1);
       nvm += AI + BI;
@@ -972,7 +989,12 @@ __global__ __launch_bounds__(256, NS <= 2 ? 2 : 1) void gemm1x1_persist_kernel(C
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int px = m0 + wm * 64 + j * 16 + fr;
-          const v4f v = acc[i][j] + bv;
+          v4f v = acc[i][j] + bv;
+          if (a.resid) {   // (acc + bias) + residual: conv_store_tile's order
+            const v2i r = rres[i][j];
+            v[0] += bf2f((uint32_t)r[0] & 0xffffu); v[1] += bf2f((uint32_t)r[0] >> 16);
+            v[2] += bf2f((uint32_t)r[1] & 0xffffu); v[3] += bf2f((uint32_t)r[1] >> 16);
+          }
           v2i o;
           o[0] = (int)f2bf2(v[0], v[1]);
           o[1] = (int)f2bf2(v[2], v[3]);
@@ -2273,8 +2295,9 @@ int gemm1x1_plan(const ConvK& k) {
     return 0;
   if (k.C1 % 64 || k.C2 % 64 || k.Kc != k.C1 + k.C2 || k.x1_bytes == 0 || (k.C2 && k.x2_bytes == 0) || k.w_bytes == 0)
     return 0;
-  if (k.addvec || k.resid || k.silu_pre || k.gst || k.gsk || k.act != DMC_ACT_NONE || k.sk ||
-      k.Csplit != k.Cout || k.out_f32 || k.out_nchw || (k.ldy1 & 3) || k.M % 128 || k.Cout % 128 || k.Cout > 1024)
+  if (k.addvec || (k.resid && (k.ld_res & 3)) || k.silu_pre || k.gst || k.gsk ||
+      k.act != DMC_ACT_NONE || k.sk || k.Csplit != k.Cout || k.out_f32 || k.out_nchw || (k.ldy1 & 3) || k.M % 128 ||
+      k.Cout % 128 || k.Cout > 1024)
     return 0;
   const long ntiles = (long)(k.M / 128) * (k.Cout / 128);
   if (ntiles < 128) return 0;

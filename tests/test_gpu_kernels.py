@@ -990,6 +990,42 @@ def test_gemm1x1_persistent_bitwise(N, H, C1, C2, Cout, dmc_opt):
     assert rel_err(outs[0].float().reshape(-1, Cout), ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,C1,Cout,inplace", [(128, 16, 256, 256, False), (128, 8, 256, 256, False),
+                                                  (128, 32, 256, 128, True), (128, 16, 256, 512, True)])
+def test_gemm1x1_persistent_residual_bitwise(N, H, C1, Cout, inplace, dmc_opt):
+    """Round 6: the persistent 1x1 GEMM with the residual epilogue (the attention output projection x + proj(h) of
+    models/unet.py:97-99, and the 1x1 input gradients that accumulate into an existing gradient, the residual then
+    being the output itself) is BITWISE the per-tile LDS-DMA kernel (DMC_GEMM1X1=0: same fragments, same K order,
+    (acc + bias) + residual rounded once) and matches an fp32 torch GEMM. (Same-box A/B of the residual form against
+    the per-tile kernel for these layers: train 10,841 / 10,838 vs 10,865 / 10,836 img/s -- neutral.)"""
+    from diffusion_models_collection_amd import _lib as L, kernels as K
+    gen = torch.Generator().manual_seed(N + H + C1 + Cout + int(inplace))
+    dt = torch.bfloat16
+    x1 = torch.randn(N, H, H, C1, generator=gen).to(dt).to(DEV)
+    w = (torch.randn(Cout, C1, 1, 1, generator=gen) * 0.05).to(DEV)
+    b = torch.randn(Cout, generator=gen).to(DEV)
+    r0 = torch.randn(N, H, H, Cout, generator=gen).to(dt).to(DEV)
+    Kc = L.kc_for(C1, dt)
+    wp = K.pack_weight(L.PACK_FWD, dt, w, Kc)
+    outs = []
+    for on in (1, 0):
+        dmc_opt("DMC_GEMM1X1", on)
+        if inplace:
+            y = r0.clone()
+            res = y
+        else:
+            y = torch.full((N, H, H, Cout), 7.0, device=DEV, dtype=dt)
+            res = r0
+        d = K.make_desc(dt, N, H, H, C1, 0, C1, 0, Kc, H, H, Cout, K.TAPS1)
+        K.set_epilogue(d, bias=b, resid=res, ld_res=Cout, ldy1=Cout)
+        K.conv(d, x1, None, wp, y)
+        outs.append(y)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = x1.float().reshape(-1, C1) @ w.view(Cout, -1).to(dt).float().t() + b + r0.float().reshape(-1, Cout)
+    assert rel_err(outs[0].float().reshape(-1, Cout), ref) < 1e-2
+
+
 @pytest.mark.parametrize("shape", [(32, 32, 32, 256, 0), (64, 16, 16, 128, 128)])
 @pytest.mark.parametrize("silu,dropout", [(True, False), (True, True), (False, False)])
 def test_gn_bwd_with_precomputed_partials(shape, silu, dropout):
