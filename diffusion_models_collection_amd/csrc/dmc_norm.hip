@@ -822,6 +822,16 @@ __global__ __launch_bounds__(NT) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]
     }
 #pragma unroll
     for (int e = 0; e < EPC; ++e) { a1[e] = 0.f; a2[e] = 0.f; }
+    // dz = d(loss)/d(GroupNorm output) is computed ONCE per element (round 6) and kept in registers for the dx pass:
+    // the SiLU' (an exp and a reciprocal) and the dropout hash were evaluated twice per element before, once per pass.
+    // z = x * sc + sh (the forward's folded affine, gn_apply's expression)
+    float sc[EPC], sh[EPC];
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      sc[e] = rstd * gm[e];
+      sh[e] = bt[e] - mean * sc[e];
+    }
+    float dzs[NR][EPC];
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       const int p = r0 + j * rpi;
@@ -834,8 +844,14 @@ __global__ __launch_bounds__(NT) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]
       for (int e = 0; e < EPC; ++e) {
         float g = gv[e];
         if (b.dthresh) g = drop_keep((uint64_t)pix * C + c0 + e, dseed, b.dthresh) ? g * b.dscale : 0.f;
-        float xh;
-        const float dz = gn_dz(x[e], g, mean, rstd, gm[e], bt[e], xh, b.silu);
+        float dz = g;
+        if (b.silu) {
+          const float z = fmaf(x[e], sc[e], sh[e]);
+          const float sg = sigmoid_f(z);
+          dz = g * sg * (1.f + z * (1.f - sg));
+        }
+        dzs[j][e] = dz;
+        const float xh = (x[e] - mean) * rstd;
         a1[e] += dz;
         a2[e] = fmaf(dz, xh, a2[e]);
       }
@@ -875,33 +891,18 @@ __global__ __launch_bounds__(NT) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]
     // gn_bwd_final's per-channel coefficients (same expressions)
     const int gl = gt - g0;
     const float ku = -rstd * rstd * sm[gl][1], kw = -rstd * sm[gl][0];
-    float sc[EPC], sh[EPC], sum[EPC];
+    float sum[EPC];
 #pragma unroll
-    for (int e = 0; e < EPC; ++e) {
-      sc[e] = rstd * gm[e];
-      sh[e] = bt[e] - mean * sc[e];
-      sum[e] = 0.f;
-    }
+    for (int e = 0; e < EPC; ++e) sum[e] = 0.f;
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       const int p = r0 + j * rpi;
       if (!(active && p < HW)) break;
       const int pix = n * HW + p;
-      float x[EPC], gv[EPC], o[EPC];
+      float x[EPC], o[EPC];
       Chunk<T>::unpack(bx[j], x);
-      Chunk<T>::unpack(bg[j], gv);
 #pragma unroll
-      for (int e = 0; e < EPC; ++e) {
-        float gg = gv[e];
-        if (b.dthresh) gg = drop_keep((uint64_t)pix * C + c0 + e, dseed, b.dthresh) ? gg * b.dscale : 0.f;
-        float dz = gg;
-        if (b.silu) {
-          const float z = fmaf(x[e], sc[e], sh[e]);
-          const float sg = sigmoid_f(z);
-          dz = gg * sg * (1.f + z * (1.f - sg));
-        }
-        o[e] = fmaf(sc[e], dz, fmaf(ku, x[e] - mean, kw));
-      }
+      for (int e = 0; e < EPC; ++e) o[e] = fmaf(sc[e], dzs[j][e], fmaf(ku, x[e] - mean, kw));
       if (acc) {
         float prev[EPC];
         Chunk<T>::unpack(bp[j], prev);
