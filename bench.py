@@ -46,9 +46,9 @@ CIFAR = dict(image_size=(32, 32), in_channels=3, model_channels=128, out_channel
              attention_resolutions=(16, 8), dropout=0.1, channel_mult=(1, 2, 2, 2), use_attention=True)
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense, MI355X_MICROARCH.md
 TRAIN_GFLOP_PER_IMG = 37.890     # fwd + bwd, = 3 x 12.632 forward
-PMC_FILE = "r5_pmc_roofline_conv.json"          # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of the roofline conv
-ROOFLINE_CSV = "r5_roofline_kernel_stats.csv"   # rocprofv3 --kernel-trace --stats of `bench.py --roofline-only`
-DIT_PMC_FILE = "r5_pmc_dit_loop.json"           # rocprofv3 --pmc over `bench.py --dit-only --no-train`
+PMC_FILE = "r6_pmc_roofline_conv.json"          # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of the roofline conv
+ROOFLINE_CSV = "r6_roofline_kernel_stats.csv"   # rocprofv3 --kernel-trace --stats of `bench.py --roofline-only`
+DIT_PMC_FILE = "r6_pmc_dit_loop.json"           # rocprofv3 --pmc over `bench.py --dit-only --no-train`
 
 
 def log(*a):
