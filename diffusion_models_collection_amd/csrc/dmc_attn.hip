@@ -81,14 +81,20 @@ DMC_DEV void stage_tile(const AttnK& a, const char* base, int ld, int n, int r0,
 // zero. Every thread issues all its loads before its first LDS store (one global round trip); rows that
 // are not needed load row 0 of the image (always valid) and are zeroed, so no load sits behind a branch.
 template <typename T, int HDP>
-DMC_DEV void stage_rows2(const AttnK& a, const char* bA, int ldA, int cA, const char* bB, int ldB, int cB, int n,
-                         int h0, int HG, int Lp, char* A, char* B) {
-  constexpr int KPL = TT<T>::KPL;
-  constexpr int CPR = HDP / KPL;
-  constexpr int PITCH = HDP * sizeof(T) + 16;
-  constexpr int PER = kResRows * CPR / 512;
+struct StageRegs {
+  static constexpr int PER = kResRows * (HDP / TT<T>::KPL) / 512;
   v4i va[PER], vb[PER];
   bool ok[PER];
+};
+template <typename T, int HDP>
+DMC_DEV void stage_rows2_issue(const AttnK& a, const char* bA, int ldA, int cA, const char* bB, int ldB, int cB, int n,
+                               int h0, int HG, int Lp, StageRegs<T, HDP>& st) {
+  constexpr int KPL = TT<T>::KPL;
+  constexpr int CPR = HDP / KPL;
+  constexpr int PER = StageRegs<T, HDP>::PER;
+  v4i* const va = st.va;
+  v4i* const vb = st.vb;
+  bool* const ok = st.ok;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int i = threadIdx.x + j * 512;
@@ -100,6 +106,15 @@ DMC_DEV void stage_rows2(const AttnK& a, const char* bA, int ldA, int cA, const 
     va[j] = *(const v4i*)(bA + (row * ldA + cA + off) * sizeof(T));
     vb[j] = *(const v4i*)(bB + (row * ldB + cB + off) * sizeof(T));
   }
+}
+template <typename T, int HDP>
+DMC_DEV void stage_rows2_store(StageRegs<T, HDP>& st, char* A, char* B) {
+  constexpr int CPR = HDP / TT<T>::KPL;
+  constexpr int PITCH = HDP * sizeof(T) + 16;
+  constexpr int PER = StageRegs<T, HDP>::PER;
+  v4i* const va = st.va;
+  v4i* const vb = st.vb;
+  bool* const ok = st.ok;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int i = threadIdx.x + j * 512;
@@ -108,6 +123,13 @@ DMC_DEV void stage_rows2(const AttnK& a, const char* bA, int ldA, int cA, const 
     *(v4i*)(A + r * PITCH + c * 16) = va[j];
     *(v4i*)(B + r * PITCH + c * 16) = vb[j];
   }
+}
+template <typename T, int HDP>
+DMC_DEV void stage_rows2(const AttnK& a, const char* bA, int ldA, int cA, const char* bB, int ldB, int cB, int n,
+                         int h0, int HG, int Lp, char* A, char* B) {
+  StageRegs<T, HDP> st;
+  stage_rows2_issue<T, HDP>(a, bA, ldA, cA, bB, ldB, cB, n, h0, HG, Lp, st);
+  stage_rows2_store<T, HDP>(st, A, B);
 }
 
 // A operand = transposed LDS tile (rows = tokens kc-chunk, cols = d tile dt), with the token order of
@@ -219,6 +241,41 @@ DMC_DEV void fwd_store(const AttnK& a, int n, int hh, int q, float m, float lsum
 
 // dQ: delta = rowsum(dO * O) of the lane's query (also published for dK/dV). All 2*HDP/KPL loads are
 // issued before the first use (clamped addresses, dropped values past hd), not one round trip per chunk.
+template <typename T, int HDP>
+struct DeltaRegs {
+  v4i vo[HDP / TT<T>::KPL], vd[HDP / TT<T>::KPL];
+};
+template <typename T, int HDP>
+DMC_DEV void delta_issue(const AttnK& a, int n, int hh, int q, DeltaRegs<T, HDP>& dr) {
+  constexpr int KPL = TT<T>::KPL;
+  constexpr int NCH = HDP / KPL;
+  const size_t row = (size_t)(n * a.L + (q < a.L ? q : 0)) * a.ld_o + hh * a.hd;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int d0 = i * KPL < a.hd ? i * KPL : 0;
+    dr.vo[i] = *(const v4i*)(a.o + (row + d0) * sizeof(T));
+    dr.vd[i] = *(const v4i*)(a.dout + (row + d0) * sizeof(T));
+  }
+}
+template <typename T, int HDP>
+DMC_DEV float delta_sum(const AttnK& a, const DeltaRegs<T, HDP>& dr) {
+  constexpr int KPL = TT<T>::KPL;
+  constexpr int NCH = HDP / KPL;
+  const v4i* const vo = dr.vo;
+  const v4i* const vd = dr.vd;
+  float dl = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    if (i * KPL < a.hd) {
+      float fo[KPL], fd[KPL];
+      Chunk<T>::unpack(vo[i], fo);
+      Chunk<T>::unpack(vd[i], fd);
+#pragma unroll
+      for (int e = 0; e < KPL; ++e) dl = fmaf(fo[e], fd[e], dl);
+    }
+  }
+  return dl;
+}
 template <typename T, int HDP>
 DMC_DEV float dq_delta(const AttnK& a, int n, int hh, int q) {
   constexpr int KPL = TT<T>::KPL;
@@ -469,16 +526,27 @@ __global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnK a, int HG, int 
   const int groups = (a.heads + HG - 1) / HG;
   const int n = blockIdx.x / groups, h0 = (blockIdx.x - n * groups) * HG;
   const int C = a.heads * a.hd;
+  const int tph = (a.L + 15) / 16;
+  // a wave's (at most two: HG * Lp <= 256 rows) 16-query tiles: their Q fragments are loaded with the K / V
+  // staging loads, in the same round trip (round 6)
+  v4i qf2[2][DC];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int tile = wave + 8 * i, g = tile / tph;
+    if (tile < HG * tph && h0 + g < a.heads)
+      load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, (tile - g * tph) * 16 + r, (h0 + g) * a.hd, qf2[i]);
+  }
   stage_rows2<T, HDP>(a, a.qkv, a.ld_qkv, C, a.qkv, a.ld_qkv, 2 * C, n, h0, HG, Lp, sK, sV);
   __syncthreads();
   const uint32_t seed = attn_seed(a);
-  const int tph = (a.L + 15) / 16;
-  for (int tile = wave; tile < HG * tph; tile += 8) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int tile = wave + 8 * i;
+    if (tile >= HG * tph) break;
     const int g = tile / tph, hh = h0 + g;
     if (hh >= a.heads) break;   // wave-uniform; later tiles belong to later heads
     const int q = (tile - g * tph) * 16 + r;
-    v4i qf[DC];
-    load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, q, hh * a.hd, qf);
+    const v4i* const qf = qf2[i];
     float m = -INFINITY, lsum = 0.f;
     v4f o[DT];
 #pragma unroll
@@ -498,26 +566,55 @@ __global__ __launch_bounds__(512) void attn_dq_res_kernel(AttnK a, int HG, int L
   constexpr int DT = HDP / 16;
   constexpr int PITCH = HDP * sizeof(T) + 16;
   __shared__ __attribute__((aligned(16))) char lds[2 * kResRows * PITCH];
+  __shared__ float sDl[kResRows];
   char* const sK = lds;
   char* const sV = lds + kResRows * PITCH;
   const int wave = threadIdx.x >> 6, r = threadIdx.x & 15;
   const int groups = (a.heads + HG - 1) / HG;
   const int n = blockIdx.x / groups, h0 = (blockIdx.x - n * groups) * HG;
   const int C = a.heads * a.hd;
-  stage_rows2<T, HDP>(a, a.qkv, a.ld_qkv, C, a.qkv, a.ld_qkv, 2 * C, n, h0, HG, Lp, sK, sV);
+  const int tph = (a.L + 15) / 16;
+  // round 6: delta = rowsum(dO * O) of the block's rows by one thread each (dq_delta's arithmetic), its loads in
+  // the K / V staging round trip, instead of 16 dependent loads per lane at the head of every tile; the first
+  // tile's Q / dO fragments ride along too
+  v4i qf0[DC], df0[DC];
+  {
+    const int g = wave / tph;
+    if (wave < HG * tph && h0 + g < a.heads) {
+      const int q = (wave - g * tph) * 16 + r;
+      load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, q, (h0 + g) * a.hd, qf0);
+      load_tok_frags<T, DC>(a, a.dout, a.ld_o, n, q, (h0 + g) * a.hd, df0);
+    }
+  }
+  StageRegs<T, HDP> st;
+  stage_rows2_issue<T, HDP>(a, a.qkv, a.ld_qkv, C, a.qkv, a.ld_qkv, 2 * C, n, h0, HG, Lp, st);
+  const int rg = threadIdx.x / Lp, rtok = threadIdx.x - rg * Lp;
+  const bool rok = threadIdx.x < kResRows && rg < HG && h0 + rg < a.heads && rtok < a.L;
+  DeltaRegs<T, HDP> dr;
+  if (rok) delta_issue<T, HDP>(a, n, h0 + rg, rtok, dr);
+  stage_rows2_store<T, HDP>(st, sK, sV);
+  if (threadIdx.x < kResRows) {
+    const float dl = rok ? delta_sum<T, HDP>(a, dr) : 0.f;
+    sDl[threadIdx.x] = dl;
+    if (rok) a.delta_out[((size_t)n * a.heads + h0 + rg) * a.L + rtok] = dl;
+  }
   __syncthreads();
   const uint32_t seed = attn_seed(a);
-  const int tph = (a.L + 15) / 16;
   for (int tile = wave; tile < HG * tph; tile += 8) {
     const int g = tile / tph, hh = h0 + g;
     if (hh >= a.heads) break;
     const int q = (tile - g * tph) * 16 + r;
     const size_t nh = (size_t)n * a.heads + hh;
     v4i qf[DC], df[DC];
-    load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, q, hh * a.hd, qf);
-    load_tok_frags<T, DC>(a, a.dout, a.ld_o, n, q, hh * a.hd, df);
+    if (tile == wave) {
+#pragma unroll
+      for (int dc = 0; dc < DC; ++dc) { qf[dc] = qf0[dc]; df[dc] = df0[dc]; }
+    } else {
+      load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, q, hh * a.hd, qf);
+      load_tok_frags<T, DC>(a, a.dout, a.ld_o, n, q, hh * a.hd, df);
+    }
     const float lse2 = q < a.L ? a.lse[nh * a.L + q] * kLog2e : 0.f;
-    const float dl = dq_delta<T, HDP>(a, n, hh, q);
+    const float dl = q < a.L ? sDl[g * Lp + q] : 0.f;
     v4f dq[DT];
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) dq[dt] = v4f{0.f, 0.f, 0.f, 0.f};
@@ -543,24 +640,42 @@ __global__ __launch_bounds__(512) void attn_dkdv_res_kernel(AttnK a, int HG, int
   const int groups = (a.heads + HG - 1) / HG;
   const int n = blockIdx.x / groups, h0 = (blockIdx.x - n * groups) * HG;
   const int C = a.heads * a.hd;
-  stage_rows2<T, HDP>(a, a.qkv, a.ld_qkv, 0, a.dout, a.ld_o, 0, n, h0, HG, Lp, sQ, sD);
+  const int tph = (a.L + 15) / 16;
+  // round 6: the first tile's K / V fragments and the rows' lse / delta are loaded in the Q / dO staging round trip
+  v4i kf0[DC], vf0[DC];
+  {
+    const int g = wave / tph;
+    if (wave < HG * tph && h0 + g < a.heads) {
+      const int key = (wave - g * tph) * 16 + r;
+      load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, key, C + (h0 + g) * a.hd, kf0);
+      load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, key, 2 * C + (h0 + g) * a.hd, vf0);
+    }
+  }
+  StageRegs<T, HDP> st;
+  stage_rows2_issue<T, HDP>(a, a.qkv, a.ld_qkv, 0, a.dout, a.ld_o, 0, n, h0, HG, Lp, st);
   const uint32_t seed = attn_seed(a);
+  float lv = INFINITY, dv_ = 0.f;
   if (threadIdx.x < kResRows) {
     const int g = threadIdx.x / Lp, tok = threadIdx.x - g * Lp;
     const bool ok = g < HG && h0 + g < a.heads && tok < a.L;
     const size_t idx = ((size_t)n * a.heads + h0 + g) * a.L + tok;
-    sL[threadIdx.x] = ok ? a.lse[idx] * kLog2e : INFINITY;
-    sDl[threadIdx.x] = ok ? a.delta[idx] : 0.f;
+    if (ok) { lv = a.lse[idx] * kLog2e; dv_ = a.delta[idx]; }
   }
+  stage_rows2_store<T, HDP>(st, sQ, sD);
+  if (threadIdx.x < kResRows) { sL[threadIdx.x] = lv; sDl[threadIdx.x] = dv_; }
   __syncthreads();
-  const int tph = (a.L + 15) / 16;
   for (int tile = wave; tile < HG * tph; tile += 8) {
     const int g = tile / tph, hh = h0 + g;
     if (hh >= a.heads) break;
     const int key = (tile - g * tph) * 16 + r;
     v4i kf[DC], vf[DC];
-    load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, key, C + hh * a.hd, kf);
-    load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, key, 2 * C + hh * a.hd, vf);
+    if (tile == wave) {
+#pragma unroll
+      for (int dc = 0; dc < DC; ++dc) { kf[dc] = kf0[dc]; vf[dc] = vf0[dc]; }
+    } else {
+      load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, key, C + hh * a.hd, kf);
+      load_tok_frags<T, DC>(a, a.qkv, a.ld_qkv, n, key, 2 * C + hh * a.hd, vf);
+    }
     v4f dk[DT], dv[DT];
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) { dk[dt] = v4f{0.f, 0.f, 0.f, 0.f}; dv[dt] = v4f{0.f, 0.f, 0.f, 0.f}; }
