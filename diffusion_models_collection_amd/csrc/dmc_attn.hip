@@ -42,6 +42,11 @@ struct AttnK {
   uint32_t dseed, dthresh; float dscale; const uint32_t* dseed_base;
 };
 
+// 2^x as the bare v_exp_f32 (round 6): exp2f wraps it in a denormal-range rescale (compare, two selects, ldexp per
+// call), a third of the softmax's VALU work. Identical for x >= -126; below, the hardware result (a denormal or 0) is
+// < 2^-126 relative to the row maximum's term 1 -- nothing an fp32 row sum can hold.
+DMC_DEV float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 DMC_DEV uint32_t attn_seed(const AttnK& a) { return a.dthresh ? a.dseed + (a.dseed_base ? *a.dseed_base : 0u) : 0u; }
 DMC_DEV float attn_keep(const AttnK& a, uint32_t seed, size_t idx) {
   return drop_keep(idx, seed, a.dthresh) ? a.dscale : 0.f;
@@ -183,27 +188,35 @@ DMC_DEV void fwd_keys(const AttnK& a, const char* sK, const char* sV, int k0, co
   const int h = (threadIdx.x & 63) >> 4;
   float p[4][4];
   float mt = -INFINITY;
+  const bool full = k0 + 64 <= a.L;   // wave-uniform: only the last key tile of a ragged L needs the key mask
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     v4f s = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int dc = 0; dc < DC; ++dc) s = mma16<T>(s, lds_frag_rows(sK, PITCH, 16 * t, dc * 64), qf[dc]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int key = k0 + 16 * t + 4 * h + i;
-      p[t][i] = key < a.L ? s[i] * sl2 : -INFINITY;
-      mt = fmaxf(mt, p[t][i]);
-    }
+    for (int i = 0; i < 4; ++i) p[t][i] = s[i] * sl2;
   }
+  if (!full) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (k0 + 16 * t + 4 * h + i >= a.L) p[t][i] = -INFINITY;
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) mt = fmaxf(mt, p[t][i]);
   mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
   mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
   const float mn = fmaxf(m, mt);
-  const float alpha = exp2f(m - mn);
+  const float alpha = ex2(m - mn);
   float rs = 0.f;
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { p[t][i] = exp2f(p[t][i] - mn); rs += p[t][i]; }
+    for (int i = 0; i < 4; ++i) { p[t][i] = ex2(p[t][i] - mn); rs += p[t][i]; }
   rs += __shfl_xor(rs, 16, 64);
   rs += __shfl_xor(rs, 32, 64);
   lsum = lsum * alpha + rs;
@@ -315,6 +328,7 @@ DMC_DEV void dq_keys(const AttnK& a, const char* sK, const char* sV, int k0, con
   constexpr int PITCH = HDP * sizeof(T) + 16;
   const int h = (threadIdx.x & 63) >> 4;
   float ds[4][4];
+  const bool full = k0 + 64 <= a.L;   // wave-uniform
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
@@ -326,7 +340,8 @@ DMC_DEV void dq_keys(const AttnK& a, const char* sK, const char* sV, int k0, con
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int key = k0 + 16 * t + 4 * h + i;
-      const float pv = key < a.L ? exp2f(s[i] * sl2 - lse2) : 0.f;
+      float pv = ex2(s[i] * sl2 - lse2);
+      if (!full && key >= a.L) pv = 0.f;
       // with dropout O = (P*M) V: dP = (dO V^T) * M, and delta = rowsum(dO * O) still equals rowsum(P * dP)
       const float dpv = a.dthresh ? dp[i] * attn_keep(a, seed, mrow + (size_t)key) : dp[i];
       ds[t][i] = pv * (dpv - dl);
@@ -376,7 +391,7 @@ DMC_DEV void dkdv_queries(const AttnK& a, const char* sQ, const char* sD, const 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int qi = 16 * t + 4 * h + i;   // query (row) within the tile
-      const float pv = exp2f(s[i] * sl2 - sL[qi]);
+      const float pv = ex2(s[i] * sl2 - sL[qi]);
       if (a.dthresh) {   // ibase = index of (tile query 0, this key): query qi adds qi * L
         const float mk = attn_keep(a, seed, ibase + (size_t)qi * a.L);
         p[t][i] = pv * mk;

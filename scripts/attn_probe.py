@@ -28,11 +28,13 @@ def timeit(fn, iters=50):
     return e0.elapsed_time(e1) / iters * 1e3
 
 
-def run(save):
+def run(save, only=0):
     from diffusion_models_collection_amd import kernels as K
     dt, dev = torch.bfloat16, "cuda"
     out = {}
     for (N, L, heads, hd) in SHAPES:
+        if only and L != only:
+            continue
         C = heads * hd
         g = torch.Generator(device="cpu").manual_seed(L)
         qkv = torch.randn(N, L, 3 * C, generator=g).to(dt).to(dev)
@@ -68,5 +70,6 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--save")
     ap.add_argument("--compare", nargs=2)
+    ap.add_argument("--L", type=int, default=0, help="only this sequence length")
     a = ap.parse_args()
-    compare(*a.compare) if a.compare else run(a.save)
+    compare(*a.compare) if a.compare else run(a.save, a.L)
