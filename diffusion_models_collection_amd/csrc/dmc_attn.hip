@@ -177,7 +177,7 @@ DMC_DEV void store_d4(char* base, size_t idx, const float* v) {
 // tile; sK/sV/sQ/sD point at that tile's first row, which is row k0 / q0 of the sequence.
 
 // Forward: online-softmax update of (m, lsum, o) with keys [k0, k0+64).
-template <typename T, int HDP>
+template <typename T, int HDP, bool DROP = true>
 DMC_DEV void fwd_keys(const AttnK& a, const char* sK, const char* sV, int k0, const v4i* qf, float sl2, float& m,
                       float& lsum, v4f* o, size_t mrow = 0, uint32_t seed = 0) {
   constexpr int KPL = TT<T>::KPL;
@@ -221,7 +221,7 @@ DMC_DEV void fwd_keys(const AttnK& a, const char* sK, const char* sV, int k0, co
   rs += __shfl_xor(rs, 32, 64);
   lsum = lsum * alpha + rs;
   m = mn;
-  if (a.dthresh) {   // dropout on the probabilities that multiply V (the row sum above is of the undropped P)
+  if (DROP && a.dthresh) {   // dropout on the probabilities that multiply V (the row sum above is of the undropped P)
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -318,7 +318,7 @@ DMC_DEV float dq_delta(const AttnK& a, int n, int hh, int q) {
 }
 
 // dQ += dS K over keys [k0, k0+64), P recomputed from the log-sum-exp, dS = P (dP - delta)
-template <typename T, int HDP>
+template <typename T, int HDP, bool DROP = true>
 DMC_DEV void dq_keys(const AttnK& a, const char* sK, const char* sV, int k0, const v4i* qf, const v4i* df, float sl2,
                      float lse2, float dl, v4f* dq, size_t mrow = 0, uint32_t seed = 0) {
   constexpr int KPL = TT<T>::KPL;
@@ -343,7 +343,7 @@ DMC_DEV void dq_keys(const AttnK& a, const char* sK, const char* sV, int k0, con
       float pv = ex2(s[i] * sl2 - lse2);
       if (!full && key >= a.L) pv = 0.f;
       // with dropout O = (P*M) V: dP = (dO V^T) * M, and delta = rowsum(dO * O) still equals rowsum(P * dP)
-      const float dpv = a.dthresh ? dp[i] * attn_keep(a, seed, mrow + (size_t)key) : dp[i];
+      const float dpv = DROP && a.dthresh ? dp[i] * attn_keep(a, seed, mrow + (size_t)key) : dp[i];
       ds[t][i] = pv * (dpv - dl);
     }
   }
@@ -369,7 +369,7 @@ DMC_DEV void dq_store(const AttnK& a, int n, int hh, int q, const v4f* dq) {
 }
 
 // dK/dV of the lane's key over queries [q0, q0+64): sL = log2-scaled lse (+inf past L -> P = 0), sDl = delta
-template <typename T, int HDP>
+template <typename T, int HDP, bool DROP = true>
 DMC_DEV void dkdv_queries(const AttnK& a, const char* sQ, const char* sD, const float* sL, const float* sDl,
                           const v4i* kf, const v4i* vf, float sl2, v4f* dk, v4f* dv, size_t ibase = 0,
                           uint32_t seed = 0) {
@@ -392,7 +392,7 @@ DMC_DEV void dkdv_queries(const AttnK& a, const char* sQ, const char* sD, const 
     for (int i = 0; i < 4; ++i) {
       const int qi = 16 * t + 4 * h + i;   // query (row) within the tile
       const float pv = ex2(s[i] * sl2 - sL[qi]);
-      if (a.dthresh) {   // ibase = index of (tile query 0, this key): query qi adds qi * L
+      if (DROP && a.dthresh) {   // ibase = index of (tile query 0, this key): query qi adds qi * L
         const float mk = attn_keep(a, seed, ibase + (size_t)qi * a.L);
         p[t][i] = pv * mk;
         ds[t][i] = pv * (dp[i] * mk - sDl[qi]);
@@ -529,7 +529,7 @@ __global__ __launch_bounds__(256) void attn_dkdv_kernel(AttnK a) {
 // ------------------------------------------------------------------------------------------------
 // Resident kernels: grid N * heads/HG blocks of 8 waves; a block's 16-row tiles are head-major
 // (tile -> head g = tile / tiles_per_head) and dealt to the waves round-robin.
-template <typename T, int HDP>
+template <typename T, int HDP, bool DROP>
 __global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnK a, int HG, int Lp) {
   constexpr int DC = HDP / (4 * TT<T>::KPL);
   constexpr int DT = HDP / 16;
@@ -569,13 +569,13 @@ __global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnK a, int HG, int 
     const size_t base = (size_t)g * Lp * PITCH;
     const size_t mrow = (((size_t)n * a.heads + hh) * a.L + q) * a.L;
     for (int k0 = 0; k0 < a.L; k0 += 64)
-      fwd_keys<T, HDP>(a, sK + base + k0 * PITCH, sV + base + k0 * PITCH, k0, qf, a.scale * kLog2e, m, lsum, o, mrow,
-                       seed);
+      fwd_keys<T, HDP, DROP>(a, sK + base + k0 * PITCH, sV + base + k0 * PITCH, k0, qf, a.scale * kLog2e, m, lsum, o,
+                             mrow, seed);
     fwd_store<T, HDP>(a, n, hh, q, m, lsum, o);
   }
 }
 
-template <typename T, int HDP>
+template <typename T, int HDP, bool DROP>
 __global__ __launch_bounds__(512) void attn_dq_res_kernel(AttnK a, int HG, int Lp) {
   constexpr int DC = HDP / (4 * TT<T>::KPL);
   constexpr int DT = HDP / 16;
@@ -635,13 +635,13 @@ __global__ __launch_bounds__(512) void attn_dq_res_kernel(AttnK a, int HG, int L
     for (int dt = 0; dt < DT; ++dt) dq[dt] = v4f{0.f, 0.f, 0.f, 0.f};
     const size_t base = (size_t)g * Lp * PITCH;
     for (int k0 = 0; k0 < a.L; k0 += 64)
-      dq_keys<T, HDP>(a, sK + base + k0 * PITCH, sV + base + k0 * PITCH, k0, qf, df, a.scale * kLog2e, lse2, dl, dq,
-                      (nh * a.L + q) * a.L, seed);
+      dq_keys<T, HDP, DROP>(a, sK + base + k0 * PITCH, sV + base + k0 * PITCH, k0, qf, df, a.scale * kLog2e, lse2, dl,
+                            dq, (nh * a.L + q) * a.L, seed);
     dq_store<T, HDP>(a, n, hh, q, dq);
   }
 }
 
-template <typename T, int HDP>
+template <typename T, int HDP, bool DROP>
 __global__ __launch_bounds__(512) void attn_dkdv_res_kernel(AttnK a, int HG, int Lp) {
   constexpr int DC = HDP / (4 * TT<T>::KPL);
   constexpr int DT = HDP / 16;
@@ -697,8 +697,8 @@ __global__ __launch_bounds__(512) void attn_dkdv_res_kernel(AttnK a, int HG, int
     const int row0 = g * Lp;
     const size_t nhl = ((size_t)n * a.heads + hh) * a.L;
     for (int q0 = 0; q0 < a.L; q0 += 64)
-      dkdv_queries<T, HDP>(a, sQ + (size_t)(row0 + q0) * PITCH, sD + (size_t)(row0 + q0) * PITCH, sL + row0 + q0,
-                           sDl + row0 + q0, kf, vf, a.scale * kLog2e, dk, dv, (nhl + q0) * a.L + key, seed);
+      dkdv_queries<T, HDP, DROP>(a, sQ + (size_t)(row0 + q0) * PITCH, sD + (size_t)(row0 + q0) * PITCH, sL + row0 + q0,
+                                 sDl + row0 + q0, kf, vf, a.scale * kLog2e, dk, dv, (nhl + q0) * a.L + key, seed);
     dkdv_store<T, HDP>(a, n, hh, key, dk, dv);
   }
 }
@@ -724,12 +724,21 @@ int launch_all(bool fwd, AttnK a, float* delta, hipStream_t s) {
   if (!fwd) { a.delta = delta; a.delta_out = delta; }
   if (hg > 0) {
     const int blocks = a.N * dmc::cdiv(a.heads, hg);
+    // DROP is a kernel parameter: without dropout the tile bodies have no per-element branches (which also split
+    // the MFMA / VALU schedule into basic blocks) and the register allocation is that path's alone
+    const bool drop = a.dthresh != 0;
     if (fwd) {
-      attn_fwd_res_kernel<T, HDP><<<blocks, 512, 0, s>>>(a, hg, Lp);
+      if (drop) attn_fwd_res_kernel<T, HDP, true><<<blocks, 512, 0, s>>>(a, hg, Lp);
+      else attn_fwd_res_kernel<T, HDP, false><<<blocks, 512, 0, s>>>(a, hg, Lp);
       return dmc::check_launch("dmc_attn_fwd");
     }
-    attn_dq_res_kernel<T, HDP><<<blocks, 512, 0, s>>>(a, hg, Lp);
-    attn_dkdv_res_kernel<T, HDP><<<blocks, 512, 0, s>>>(a, hg, Lp);
+    if (drop) {
+      attn_dq_res_kernel<T, HDP, true><<<blocks, 512, 0, s>>>(a, hg, Lp);
+      attn_dkdv_res_kernel<T, HDP, true><<<blocks, 512, 0, s>>>(a, hg, Lp);
+    } else {
+      attn_dq_res_kernel<T, HDP, false><<<blocks, 512, 0, s>>>(a, hg, Lp);
+      attn_dkdv_res_kernel<T, HDP, false><<<blocks, 512, 0, s>>>(a, hg, Lp);
+    }
     return dmc::check_launch("dmc_attn_bwd");
   }
   dim3 g(dmc::cdiv(a.L, 64), a.N * a.heads);
