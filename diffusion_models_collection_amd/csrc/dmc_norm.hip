@@ -563,7 +563,8 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float* in, int R, in
 // by the backward (weight gradients read `a` directly, dropout masks never stored).
 // Grid (N, pixel splits); a thread owns one 16-byte channel chunk column (its scale/shift stay in
 // registers) and walks pixels of one sample, so each wave streams whole contiguous rows.
-template <typename T>
+// MODE (round 6): bit 0 SiLU, bit 1 dropout -- compile-time, so the element loop has no per-element uniform branches
+template <typename T, int MODE>
 __global__ __launch_bounds__(256) void gn_apply_kernel(Src2 s, int HW, const float* scale, const float* shift,
                                                        int silu, uint32_t seed0, const uint32_t* seed_base,
                                                        uint32_t thresh, float dscale, char* out, int ldo, int splits) {
@@ -601,8 +602,8 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(Src2 s, int HW, const flo
 #pragma unroll
       for (int e = 0; e < EPC; ++e) {
         float v = fmaf(f[e], sc[e], sh[e]);
-        if (silu) v = silu_f(v);
-        if (thresh) v = drop_keep((uint64_t)pix * C + c0 + e, seed, thresh) ? v * dscale : 0.f;
+        if (MODE & 1) v = silu_f(v);
+        if (MODE & 2) v = drop_keep((uint64_t)pix * C + c0 + e, seed, thresh) ? v * dscale : 0.f;
         f[e] = v;
       }
       *(v4i*)(out + ((size_t)pix * ldo + c0) * sizeof(T)) = Chunk<T>::pack(f);
@@ -770,7 +771,8 @@ __global__ __launch_bounds__(256) void gn_bwd_apply(GnBwd b, const float* cf, ch
 // two. The per-(n, c) pixel sums of the stored dx (bias / time-embedding gradients) are reduced in-block and
 // written directly; dgamma / dbeta and the per-c sums are column sums over n (gn_bwd_finish_kernel).
 // (two samples per block, the second one's rows loaded with the first's, measured slower: round 4, -3 %)
-template <int NR, int NT>
+// MODE (round 6): bit 0 SiLU, bit 1 dropout, compile-time (no per-element uniform branches in pass 1)
+template <int NR, int NT, int MODE>
 __global__ __launch_bounds__(NT) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]*/, char* dx1, char* dx2, int ld1,
                                                      int ld2, int acc1, int acc2, float* sums /*[N][C]*/,
                                                      float* out_nc, int ld_nc) {
@@ -843,9 +845,9 @@ __global__ __launch_bounds__(NT) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]
 #pragma unroll
       for (int e = 0; e < EPC; ++e) {
         float g = gv[e];
-        if (b.dthresh) g = drop_keep((uint64_t)pix * C + c0 + e, dseed, b.dthresh) ? g * b.dscale : 0.f;
+        if (MODE & 2) g = drop_keep((uint64_t)pix * C + c0 + e, dseed, b.dthresh) ? g * b.dscale : 0.f;
         float dz = g;
-        if (b.silu) {
+        if (MODE & 1) {
           const float z = fmaf(x[e], sc[e], sh[e]);
           const float sg = sigmoid_f(z);
           dz = g * sg * (1.f + z * (1.f - sg));
@@ -1139,16 +1141,22 @@ int gn_silu_bwd_impl(int dtype, const void* g, int ld_g, const void* x1, const v
       if (defer) A = A_keep;
       float* ssum = want_sums ? (defer && sums_keep ? sums_keep : sums) : nullptr;
       const dim3 gf(N, S);
+      const int mode = (silu ? 1 : 0) | (drop_thresh ? 2 : 0);
+#define DMC_GNBF2(NR_, M_) do { \
+        if (NT == 512) gn_bwd_fused<NR_, 512, M_><<<gf, 512, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
+                                                               accumulate1, accumulate2, ssum, dx_sum_nc, ld_sum_nc); \
+        else gn_bwd_fused<NR_, 1024, M_><<<gf, 1024, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
+                                                         accumulate1, accumulate2, ssum, dx_sum_nc, ld_sum_nc); \
+      } while (0)
 #define DMC_GNBF(NR_) do { \
-        if (NT == 512) gn_bwd_fused<NR_, 512><<<gf, 512, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
-                                                           accumulate1, accumulate2, ssum, dx_sum_nc, ld_sum_nc); \
-        else gn_bwd_fused<NR_, 1024><<<gf, 1024, 0, s>>>(b, A, (char*)dx1, (char*)dx2, ld_dx1, ld_dx2, \
-                                                     accumulate1, accumulate2, ssum, dx_sum_nc, ld_sum_nc); \
+        if (mode == 0) DMC_GNBF2(NR_, 0); else if (mode == 1) DMC_GNBF2(NR_, 1); \
+        else if (mode == 2) DMC_GNBF2(NR_, 2); else DMC_GNBF2(NR_, 3); \
       } while (0)
       if (nr <= 1) DMC_GNBF(1);
       else if (nr <= 2) DMC_GNBF(2);
       else DMC_GNBF(4);
 #undef DMC_GNBF
+#undef DMC_GNBF2
       if (defer) {
         if (deferred) *deferred = 1;
         return dmc::check_launch("dmc_gn_silu_bwd");
@@ -1303,11 +1311,17 @@ extern "C" int dmc_gn_apply(int dtype, const void* x1, const void* x2, int N, in
   hipStream_t s = dmc::as_stream(stream);
   Src2 src{(const char*)x1, (const char*)x2, C1, C2, ld1, ld2};
   dim3 g(N, splits);
-  if (dtype == DMC_F32)
-    gn_apply_kernel<float><<<g, 256, 0, s>>>(src, HW, scale, shift, silu, drop_seed, drop_seed_base, drop_thresh, drop_scale,
-                                             (char*)out, ld_out, splits);
-  else
-    gn_apply_kernel<bf16_t><<<g, 256, 0, s>>>(src, HW, scale, shift, silu, drop_seed, drop_seed_base, drop_thresh, drop_scale,
-                                              (char*)out, ld_out, splits);
+  const int mode = (silu ? 1 : 0) | (drop_thresh ? 2 : 0);
+#define DMC_GNA(T_, M_)                                                                                          \
+  gn_apply_kernel<T_, M_><<<g, 256, 0, s>>>(src, HW, scale, shift, silu, drop_seed, drop_seed_base, drop_thresh, \
+                                            drop_scale, (char*)out, ld_out, splits)
+  if (dtype == DMC_F32) {
+    if (mode == 0) DMC_GNA(float, 0); else if (mode == 1) DMC_GNA(float, 1);
+    else if (mode == 2) DMC_GNA(float, 2); else DMC_GNA(float, 3);
+  } else {
+    if (mode == 0) DMC_GNA(bf16_t, 0); else if (mode == 1) DMC_GNA(bf16_t, 1);
+    else if (mode == 2) DMC_GNA(bf16_t, 2); else DMC_GNA(bf16_t, 3);
+  }
+#undef DMC_GNA
   return dmc::check_launch("dmc_gn_apply");
 }

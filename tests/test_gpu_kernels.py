@@ -1069,8 +1069,11 @@ def test_gn_bwd_with_precomputed_partials(shape, silu, dropout):
                  dg, db, part=pp)
         outs.append((torch.cat([dx1, dx2], -1) if C2 else dx1, dg, db))
     torch.cuda.synchronize()
+    # bf16 dx: the two paths are different kernels (gn_bwd_apply's folded coefficients vs gn_bwd_fused's
+    # sc * dz + ku * (x - mean) + kw, fp32 contraction chosen by the compiler), so last-bit flips of the bf16 rounding
+    # (2^-8 relative each) are expected on a fraction of the elements: 3e-3 in the norm
     for a, b in zip(outs[0], outs[1]):
-        assert rel_err(a.float(), b.float()) < (2e-3 if a.dtype == dt else 1e-5), (rel_err(a.float(), b.float()))
+        assert rel_err(a.float(), b.float()) < (3e-3 if a.dtype == dt else 1e-5), (rel_err(a.float(), b.float()))
 
 
 @pytest.mark.parametrize("case", ["linear", "concat", "ragged", "split_tail"])
