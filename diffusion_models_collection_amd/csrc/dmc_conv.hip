@@ -2041,23 +2041,35 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(const dmc_pack_job* job
     const int KW = J.koff >= 0 ? J.Cin : J.Kc;
     const int kn = min(kPackFwdK, KW - k0);
     const int kv = max(0, min(kn, J.Cin - k0));          // columns backed by the weight (rest: zero padding)
-    const int run = kv * khkw;
-    for (int j0 = tid; j0 < run; j0 += 3 * 256) {       // up to 12 loads in flight per thread
-      float v[kPackFwdCo][3];
+    const int run = kv * khkw;                            // <= 256 * 9
+    {
+      // the whole tile's loads in flight at once (round 6; the three-load rounds were one HBM round trip each:
+      // the pack ran at 3 TB/s)
+      float v[kPackFwdCo][9];
 #pragma unroll
       for (int r = 0; r < kPackFwdCo; ++r)
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {
-          const int j = j0 + u * 256;
+        for (int u = 0; u < 9; ++u) {
+          const int j = tid + u * 256;
           v[r][u] = (r < nco && j < run) ? J.w[((size_t)(co0 + r) * J.Cin + k0) * khkw + j] : 0.f;
         }
 #pragma unroll
       for (int r = 0; r < kPackFwdCo; ++r)
 #pragma unroll
-        for (int u = 0; u < 3; ++u)
-          if (r < nco && j0 + u * 256 < run) sw[r * kPackFwdK * 9 + j0 + u * 256] = v[r][u];
+        for (int u = 0; u < 9; ++u)
+          if (r < nco && tid + u * 256 < run) sw[r * kPackFwdK * 9 + tid + u * 256] = v[r][u];
     }
     __syncthreads();
+    if (!f32 && ((J.Kc | koff | k0 | kn) & 1) == 0) {   // bf16 pairs: one 4-byte store per two columns (round 6)
+      for (int r = 0; r < nco; ++r)
+        for (int t = 0; t < khkw; ++t)
+          for (int k = 2 * tid; k < kn; k += 512) {
+            const float v0 = k < kv ? sw[r * kPackFwdK * 9 + k * khkw + t] : 0.f;
+            const float v1 = k + 1 < kv ? sw[r * kPackFwdK * 9 + (k + 1) * khkw + t] : 0.f;
+            *(uint32_t*)((bf16_t*)J.dst + ((long)(co0 + r) * khkw + t) * J.Kc + koff + k0 + k) = f2bf2(v0, v1);
+          }
+      return;
+    }
     for (int r = 0; r < nco; ++r)
       for (int t = 0; t < khkw; ++t)
         for (int k = tid; k < kn; k += 256)
@@ -2070,29 +2082,27 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(const dmc_pack_job* job
   const int cn = min(kPackDgC, J.Cin - c0), con = min(kPackDgCo, KW - co0);
   const int cov = max(0, min(con, J.Cout - co0));           // columns backed by the weight
   const int run = cn * khkw;                                // <= 16 * 9 = 144 = 64 * 3 - 48
-  for (int r0 = wv; r0 < cov; r0 += 16) {                  // wave -> rows r0, r0+4, r0+8, r0+12; lane -> column
-    float v[4][3];
+  {
+    // wave -> rows wv, wv + 4, ..., lane -> column; all 16 rows per wave in flight at once (round 6)
+    float v[16][3];
 #pragma unroll
-    for (int a2 = 0; a2 < 4; ++a2)
+    for (int a2 = 0; a2 < 16; ++a2)
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
-        const int r = r0 + 4 * a2, j = ln + 64 * u;
+        const int r = wv + 4 * a2, j = ln + 64 * u;
         v[a2][u] = (r < cov && j < run) ? J.w[((size_t)(co0 + r) * J.Cin + c0) * khkw + j] : 0.f;
       }
 #pragma unroll
-    for (int a2 = 0; a2 < 4; ++a2)
+    for (int a2 = 0; a2 < 16; ++a2)
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
-        const int r = r0 + 4 * a2, j = ln + 64 * u;
+        const int r = wv + 4 * a2, j = ln + 64 * u;
         if (r < cov && j < run) sw[r * kPackDgP + j] = v[a2][u];
       }
   }
   __syncthreads();
   const int ntaps = J.mode == DMC_PACK_UPDGRAD ? 16 : khkw;
-  const int co = ln;                                        // con <= 64 columns, one per lane
-  for (int q = wv; q < cn * ntaps; q += 4) {
-    const int c = q / ntaps, t = q - c * ntaps;             // wave-uniform
-    if (co >= con) continue;
+  auto value = [&](int co, int c, int t) {   // packed value of column co (output channel co0 + co), row (c, t)
     float v = 0.f;
     if (co < cov) {
       const float* wp = sw + co * kPackDgP + c * khkw;
@@ -2112,7 +2122,24 @@ __global__ __launch_bounds__(256) void pack_tiles_kernel(const dmc_pack_job* job
         }
       }
     }
-    store(((long)(c0 + c) * ntaps + t) * J.Kc + koff + co0 + co, v);
+    return v;
+  };
+  if (!f32 && ((J.Kc | koff | co0 | con) & 1) == 0) {
+    // bf16 pairs (round 6): a half-wave per row (c, t), a lane per two columns, one 4-byte store
+    const int cp = 2 * (ln & 31);
+    for (int q = 2 * wv + (ln >> 5); q < cn * ntaps; q += 8) {
+      const int c = q / ntaps, t = q - c * ntaps;
+      if (cp >= con) continue;
+      *(uint32_t*)((bf16_t*)J.dst + ((long)(c0 + c) * ntaps + t) * J.Kc + koff + co0 + cp) =
+          f2bf2(value(cp, c, t), value(cp + 1, c, t));
+    }
+    return;
+  }
+  const int co = ln;                                        // con <= 64 columns, one per lane
+  for (int q = wv; q < cn * ntaps; q += 4) {
+    const int c = q / ntaps, t = q - c * ntaps;             // wave-uniform
+    if (co >= con) continue;
+    store(((long)(c0 + c) * ntaps + t) * J.Kc + koff + co0 + co, value(co, c, t));
   }
 }
 
