@@ -546,7 +546,7 @@ DMC_DEV void xcd_tile(int NB, int& mb, int& nb) {
 // counts (no LDS staging, no block barrier: the LDS-staged epilogue of the 2-blocks-per-CU halo conv runs with
 // both blocks of a CU in lockstep, so its staging and barriers were exposed). Same statistics as tile_epilogue8 up
 // to the fp32 summation order.
-DMC_DEV bool reg_epi_ok(const ConvK& a) {
+__host__ __device__ inline bool reg_epi_ok(const ConvK& a) {
   // DMC_REG_EPI: 1 = where the tile also emits GroupNorm partials (the LDS-staged form reduces them across the waves
   // through LDS behind a second barrier; without partials it is the faster one in isolation: 52.5 vs 57.1 us on the
   // 32x32 conv with bias + time embedding + residual, kernel trace), 2 = every eligible tile, 3 = every eligible
@@ -1806,11 +1806,16 @@ __global__ __launch_bounds__(256) void conv3x3_nout_kernel(ConvK a, int R, int n
 // weights), three steps in all. Wave w owns output channels [32w, 32w+32) of the 128-channel tile over its 128
 // pixels; the tile goes through the shared LDS epilogue (16-byte NHWC stores, bias / time embedding, the
 // GroupNorm partials of the stored output).
+// REG (round 6, when reg_epi_ok): the waves split the tile 2 x 2 (64 pixels x 64 channels each, the halo conv's
+// layout) and the epilogue runs from the accumulators (reg_epilogue), so the block holds only its 5 KB halo in LDS
+// instead of the 76 KB fp32 epilogue tile: many blocks per CU instead of two, and no LDS round trip of the tile.
+template <bool REG>
 __global__ __launch_bounds__(256) void conv3x3_nin_kernel(ConvK a, int R, int nimg) {
   using T = bf16_t;
   constexpr int BM = 128, BN = 128, EP = BN * 4 + 16;
   constexpr int HALO = 320;                        // >= nimg * (R + 2) * (OW + 2) for every halo2_plan geometry
-  constexpr int LDS_BYTES = BM * EP + 4 * 2 * 16 * 64 > HALO * 16 ? BM * EP + 4 * 2 * 16 * 64 : HALO * 16;
+  constexpr int LDS_EPI = BM * EP + 4 * 2 * 16 * 64;
+  constexpr int LDS_BYTES = !REG && LDS_EPI > HALO * 16 ? LDS_EPI : HALO * 16;
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1829,6 +1834,49 @@ __global__ __launch_bounds__(256) void conv3x3_nin_kernel(ConvK a, int R, int ni
     *(v4i*)(lds + h * 16) = v;
   }
   const int fr = lane & 15, fh = lane >> 4;
+  if constexpr (REG) {
+    const int wm = wave % 2, wn = wave / 2;
+    v4i fa[3][4];
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = n0 + wn * 64 + 16 * i + fr, tap = 4 * s + fh;
+        const bool ok = co < a.Cout && tap < 9;
+        v4i w = *(const v4i*)(a.w + ((size_t)(ok ? co : 0) * 9 * a.Kc + (size_t)(ok ? tap : 0) * a.Kc) * 2);
+        fa[s][i] = ok ? w : v4i{0, 0, 0, 0};
+      }
+    int hb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = wm * 64 + j * 16 + fr;
+      const int img = m / (R * OW), rem = m - img * (R * OW);
+      const int rr = rem / OW, col = rem - rr * OW;
+      hb[j] = img * segpix + (rr + 1) * HW + col + 1;
+    }
+    int dl[3];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int t = 4 * s + fh < 9 ? 4 * s + fh : 0, ty = t / 3, tx = t - ty * 3;
+      dl[s] = (a.tdy0 + a.tsy * ty) * HW + (a.tdx0 + a.tsx * tx);
+    }
+    __syncthreads();
+    v4f acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const v4i fb = *(const v4i*)(lds + (hb[j] + dl[s]) * 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][j] = mma16<T>(acc[i][j], fa[s][i], fb);
+      }
+    reg_epilogue(a, acc, m0, n0, wm, wn);
+    return;
+  }
   // weights: rows co = n0 + 32 wave + 16 i + fr; the k32 step s covers taps 4s .. 4s+3, lane group fh takes tap 4s+fh
   v4i fa[3][2];
 #pragma unroll
@@ -2340,7 +2388,8 @@ int launch_fwd(ConvK k, void* ws, size_t ws_bytes, hipStream_t s) {
   if (!dmc::opt(dmc::OPT_NO_NARROW) && sizeof(T) == 2) {
     int R, nimg;
     if (k.C2 == 0 && k.C1 <= EPC && k.Cout >= 16 && nin_plan(k, &R, &nimg)) {
-      conv3x3_nin_kernel<<<dim3(k.M / 128, k.Cout / 128), 256, 0, s>>>(k, R, nimg);
+      if (reg_epi_ok(k)) conv3x3_nin_kernel<true><<<dim3(k.M / 128, k.Cout / 128), 256, 0, s>>>(k, R, nimg);
+      else conv3x3_nin_kernel<false><<<dim3(k.M / 128, k.Cout / 128), 256, 0, s>>>(k, R, nimg);
       return dmc::check_launch("dmc_conv2d");
     }
     const int hp = k.Cout <= 8 ? nout_plan(k, &R, &nimg) : 0;
