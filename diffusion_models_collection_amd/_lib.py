@@ -110,7 +110,7 @@ def _load():
                                               _c_int, _c_int, _c_int, _c_p, _c_p, _c_p, _c_int, _c_u32, _c_p, _c_u32,
                                               _c_f, _c_p, _c_p, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p, _c_p,
                                               _c_int, _c_p, _c_p, _c_p, _c_p, _c_p, ctypes.POINTER(ctypes.c_int),
-                                              _c_p]),
+                                              _c_p, _c_int, _c_p]),
         "dmc_colsum_batch": (_c_int, [ctypes.POINTER(ColsumJob), _c_int, _c_p]),
         "dmc_channel_sum_workspace": (_c_size, [_c_int, _c_int, _c_int]),
         "dmc_channel_sum": (_c_int, [_c_int, _c_p, _c_int, _c_int, _c_int, _c_int, _c_p, _c_int, _c_p, _c_f, _c_p,

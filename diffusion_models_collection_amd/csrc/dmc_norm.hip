@@ -280,6 +280,7 @@ struct GnBwd {
   uint32_t dseed, dthresh; float dscale;
   const uint32_t* dseed_base;   // device word added to dseed when not NULL
   int silu;
+  const char* add1; int ld_add1;   // gn_bwd_fused: an extra operand added into dx1 (round 6), NULL = none
 };
 
 
@@ -888,6 +889,14 @@ __global__ __launch_bounds__(NT) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]
         if (active && p < HW) bp[j] = *(const v4i*)(dst + ((size_t)(n * HW + p) * ldd + cd) * sizeof(T));
       }
     }
+    v4i ba[NR];
+    if (b.add1) {   // the extra operand (single source: channel c0 of add1), read while the group sums finish
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        const int p = r0 + j * rpi;
+        if (active && p < HW) ba[j] = *(const v4i*)(b.add1 + ((size_t)(n * HW + p) * b.ld_add1 + c0) * sizeof(T));
+      }
+    }
     __syncthreads();
     if (!active && !sums) return;
     // gn_bwd_final's per-channel coefficients (same expressions)
@@ -910,6 +919,12 @@ __global__ __launch_bounds__(NT) void gn_bwd_fused(GnBwd b, float* A /*[n][C][2]
         Chunk<T>::unpack(bp[j], prev);
 #pragma unroll
         for (int e = 0; e < EPC; ++e) o[e] += prev[e];
+      }
+      if (b.add1) {
+        float ad[EPC];
+        Chunk<T>::unpack(ba[j], ad);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) o[e] += ad[e];
       }
       const v4i packed = Chunk<T>::pack(o);
       *(v4i*)(dst + ((size_t)pix * ldd + cd) * sizeof(T)) = packed;
@@ -1090,13 +1105,33 @@ extern "C" int dmc_gn_finalize(const float* part1, int C1, const float* part2, i
 }
 
 namespace {
+// dst[pix][c] += src[pix][c] for c < C (16-byte chunks): dmc_gn_silu_bwd_deferred's extra operand when the one-pass
+// kernel does not take the call
+template <typename T>
+__global__ __launch_bounds__(256) void add_rows_kernel(char* dst, int ldd, const char* src, int lds, long P, int C) {
+  constexpr int EPC = TT<T>::KPL;
+  const int cpr = C / EPC;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < P * cpr; i += (long)gridDim.x * 256) {
+    const long pix = i / cpr;
+    const int c = (int)(i - pix * cpr) * EPC;
+    v4i* d = (v4i*)(dst + ((size_t)pix * ldd + c) * sizeof(T));
+    float a[EPC], b[EPC];
+    Chunk<T>::unpack(*d, a);
+    Chunk<T>::unpack(*(const v4i*)(src + ((size_t)pix * lds + c) * sizeof(T)), b);
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) a[e] += b[e];
+    *d = Chunk<T>::pack(a);
+  }
+}
+
 int gn_silu_bwd_impl(int dtype, const void* g, int ld_g, const void* x1, const void* x2, int N, int HW, int C1,
                      int C2, int ld1, int ld2, int G, const float* mean_rstd, const float* gamma,
                      const float* beta, int silu, uint32_t drop_seed, const uint32_t* drop_seed_base,
                      uint32_t drop_thresh, float drop_scale, void* dx1,
                      void* dx2, int ld_dx1, int ld_dx2, int accumulate1, int accumulate2, float* dgamma,
                      float* dbeta, float* dx_sum_nc, int ld_sum_nc, float* dx_sum_c, const float* part,
-                     void* workspace, void* stream, float* A_keep, float* sums_keep, int* deferred) {
+                     void* workspace, void* stream, float* A_keep, float* sums_keep, int* deferred,
+                     const void* add1 = nullptr, int ld_add1 = 0) {
   if (deferred) *deferred = 0;
   const int epc = dtype == DMC_F32 ? 4 : 8;
   const int C = C1 + C2;
@@ -1112,6 +1147,9 @@ int gn_silu_bwd_impl(int dtype, const void* g, int ld_g, const void* x1, const v
   b.mr = mean_rstd; b.gamma = gamma; b.beta = beta;
   b.dseed = drop_seed; b.dthresh = drop_thresh; b.dscale = drop_scale; b.dseed_base = drop_seed_base;
   b.silu = silu;
+  b.add1 = nullptr; b.ld_add1 = 0;
+  DMC_REQUIRE(!add1 || (C2 == 0 && accumulate1 && ld_add1 % epc == 0 && !dx_sum_nc && !dx_sum_c),
+              "gn_bwd: the extra operand needs a single accumulated source and no dx pixel sums");
   float* partial = (float*)workspace;
   float* A = partial + (size_t)N * b.splits * C * 2;
   float* cf = A + (size_t)N * C * 2;
@@ -1139,6 +1177,7 @@ int gn_silu_bwd_impl(int dtype, const void* g, int ld_g, const void* x1, const v
       // deferred column sums: A and the per-(n, c) sums go to the caller's buffers, the finish is its batch
       const bool defer = A_keep && (!dx_sum_c || sums_keep);
       if (defer) A = A_keep;
+      b.add1 = (const char*)add1; b.ld_add1 = ld_add1;
       float* ssum = want_sums ? (defer && sums_keep ? sums_keep : sums) : nullptr;
       const dim3 gf(N, S);
       const int mode = (silu ? 1 : 0) | (drop_thresh ? 2 : 0);
@@ -1165,6 +1204,14 @@ int gn_silu_bwd_impl(int dtype, const void* g, int ld_g, const void* x1, const v
       gn_bwd_finish_kernel<<<nb, 1024, 0, s>>>(A, ssum, N, C, dbeta, dgamma, dx_sum_c);
       return dmc::check_launch("dmc_gn_silu_bwd");
     }
+  }
+  if (add1) {
+    // the other kernels: the extra operand is added into dx1 first, then accumulated into -- the order of a separate
+    // add before the call (bitwise the former executor's result, e.g. in the fp32 parity mode)
+    const long P = (long)N * HW;
+    const int blocks = (int)std::min<long>((P * (C1 / epc) + 255) / 256, 4096);
+    if (dtype == DMC_F32) add_rows_kernel<float><<<blocks, 256, 0, s>>>((char*)dx1, ld_dx1, (const char*)add1, ld_add1, P, C1);
+    else add_rows_kernel<bf16_t><<<blocks, 256, 0, s>>>((char*)dx1, ld_dx1, (const char*)add1, ld_add1, P, C1);
   }
   if (part) {
     // the per-(64-pixel segment, channel) sums came from the input-gradient conv's epilogue (dmc_gn_bwd_epi):
@@ -1233,12 +1280,12 @@ extern "C" int dmc_gn_silu_bwd_deferred(int dtype, const void* g, int ld_g, cons
                                         void* dx1, void* dx2, int ld_dx1, int ld_dx2, int accumulate1, int accumulate2,
                                         float* dgamma, float* dbeta, float* dx_sum_nc, int ld_sum_nc, float* dx_sum_c,
                                         const float* part, void* workspace, float* A_keep, float* sums_keep,
-                                        int* deferred, void* stream) {
+                                        int* deferred, const void* add1, int ld_add1, void* stream) {
   DMC_REQUIRE(A_keep && deferred && (!dx_sum_c || sums_keep), "gn_silu_bwd_deferred: keep buffers / flag");
   return gn_silu_bwd_impl(dtype, g, ld_g, x1, x2, N, HW, C1, C2, ld1, ld2, G, mean_rstd, gamma, beta, silu, drop_seed,
                           drop_seed_base, drop_thresh, drop_scale, dx1, dx2, ld_dx1, ld_dx2, accumulate1, accumulate2,
                           dgamma, dbeta, dx_sum_nc, ld_sum_nc, dx_sum_c, part, workspace, stream, A_keep, sums_keep,
-                          deferred);
+                          deferred, add1, ld_add1);
 }
 
 extern "C" int dmc_colsum_batch(const dmc_colsum_job* jobs, int njobs, void* stream) {

@@ -346,10 +346,12 @@ def gn_apply(dtype, x1, x2, N, HW, C1, C2, ld1, ld2, scale, shift, silu=True, dr
 
 
 def gn_bwd(dtype, g, ld_g, x1, x2, N, HW, C1, C2, ld1, ld2, G, mr, gamma, beta, silu, drop, dx1, dx2, ld_dx1,
-           ld_dx2, acc1, acc2, dgamma, dbeta, dx_sum_nc=None, ld_sum_nc=0, dx_sum_c=None, part=None, defer=None):
+           ld_dx2, acc1, acc2, dgamma, dbeta, dx_sum_nc=None, ld_sum_nc=0, dx_sum_c=None, part=None, defer=None,
+           add1=None, ld_add1=0):
     """GroupNorm(+SiLU+dropout) backward; optionally also the per-(n,c) / per-c pixel sums of dx (the bias and
     time-embedding gradients of the layer that produced x), fused into the dx pass. part: (sum dz, sum dz*xhat)
-    partials from an earlier pass ([N*HW/64][C][2]), skipping the reduction."""
+    partials from an earlier pass ([N*HW/64][C][2]), skipping the reduction. add1: a second operand added into dx1
+    (single source, no pixel sums; folded into the one-pass kernel's dx pass on the deferred path)."""
     ws = SCRATCH.get(LIB.dmc_gn_workspace(N, C1 + C2, G, HW), g.device)
     seed, base, thresh, scale = drop_args(drop)
     if defer is not None:
@@ -362,7 +364,7 @@ def gn_bwd(dtype, g, ld_g, x1, x2, N, HW, C1, C2, ld1, ld2, G, mr, gamma, beta, 
             L.dtype_code(dtype), ptr(g), ld_g, ptr(x1), ptr(x2), N, HW, C1, C2, ld1, ld2, G, ptr(mr), ptr(gamma),
             ptr(beta), int(silu), seed, base, thresh, scale, ptr(dx1), ptr(dx2), ld_dx1, ld_dx2, int(acc1), int(acc2),
             ptr(dgamma), ptr(dbeta), ptr(dx_sum_nc), ld_sum_nc, ptr(dx_sum_c), ptr(part), ptr(ws), ptr(a_keep),
-            ptr(s_keep), ctypes.byref(flag), L.stream()), "dmc_gn_silu_bwd_deferred")
+            ptr(s_keep), ctypes.byref(flag), ptr(add1), int(ld_add1), L.stream()), "dmc_gn_silu_bwd_deferred")
         if flag.value:
             defer.append((a_keep, N, C, 2 * C, 2, dbeta, dgamma))
             if s_keep is not None:
@@ -372,6 +374,8 @@ def gn_bwd(dtype, g, ld_g, x1, x2, N, HW, C1, C2, ld1, ld2, G, mr, gamma, beta, 
                               ptr(gamma), ptr(beta), int(silu), seed, base, thresh, scale, ptr(dx1), ptr(dx2), ld_dx1,
                               ld_dx2, int(acc1), int(acc2), ptr(dgamma), ptr(dbeta), ptr(dx_sum_nc), ld_sum_nc,
                               ptr(dx_sum_c), ptr(part), ptr(ws), L.stream()), "dmc_gn_silu_bwd")
+    if add1 is not None:   # the immediate entry point has no extra operand: a separate add
+        add_(dtype, dx1, add1)
 
 
 def colsum_batch(jobs):

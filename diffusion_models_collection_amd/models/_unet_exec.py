@@ -808,6 +808,7 @@ class UNetExecutor(ExecCore):
         gn1, conv1, gn2, conv2 = rb.conv1[0], rb.conv1[2], rb.conv2[0], rb.conv2[3]
         dout = out.grad
         HW = H * W
+        short_add = None   # an identity-shortcut gradient left for the GN1 backward to add (below)
         # conv2 (weight, bias) and its input gradient; a2 = dropout(SiLU(GN2(h1))) was kept from forward
         self._wgrad([a2], dout, Cout, K.TAPS3, H, W, Cout, gv(conv2.weight), dbias=gv(conv2.bias))
         g2 = torch.empty(N, H, W, Cout, dtype=dt, device=dout.device)
@@ -835,6 +836,10 @@ class UNetExecutor(ExecCore):
         else:
             if a.grad is None:
                 a.grad = dout          # identity shortcut: alias (dout is dead after this block)
+            elif len(srcs) == 1:
+                # a.grad already holds a skip connection's gradient: the identity-shortcut gradient is added by the
+                # GroupNorm backward below, which accumulates into a.grad anyway (round 6: one HBM pass fewer)
+                short_add = dout
             else:
                 K.add_(dt, a.grad, dout)
         # GN2 + SiLU + dropout backward -> dh1, with its pixel sums fused in: per (n, c) -> the time-embedding
@@ -859,7 +864,7 @@ class UNetExecutor(ExecCore):
             b2, acc2, ld2 = None, 0, 0
         self._gn_bwd(dt, g1, C1 + C2, a.t, srcs[1].t if len(srcs) > 1 else None, N, HW, C1, C2, a.t.shape[-1], ld2,
                  gn1.num_groups, st1[2], gn1.weight, gn1.bias, True, None, b1, b2, a.t.shape[-1], ld2, acc1, acc2,
-                 gv(gn1.weight), gv(gn1.bias))
+                 gv(gn1.weight), gv(gn1.bias), add1=short_add, ld_add1=Cout if short_add is not None else 0)
 
     def _gn_bwd(self, *a, **kw):
         """K.gn_bwd with its parameter column sums (dgamma / dbeta / the bias sums) deferred to one batched launch

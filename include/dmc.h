@@ -214,14 +214,18 @@ int dmc_gn_silu_bwd(int dtype, const void* g, int ld_g, const void* x1, const vo
 /* dmc_gn_silu_bwd with its column sums deferred: when the one-pass kernel takes the call (*deferred = 1), the
  * per-(n, c) sums A = (sum dz, sum dz*xhat) go to A_keep ([N][C][2]) and the per-(n, c) dx pixel sums to sums_keep
  * ([N][C], needed when dx_sum_c is set), and dgamma / dbeta / dx_sum_c are NOT written: the caller adds them to a
- * dmc_colsum_batch (the column sums over n). Otherwise (*deferred = 0) the call is dmc_gn_silu_bwd. */
+ * dmc_colsum_batch (the column sums over n). Otherwise (*deferred = 0) the call is dmc_gn_silu_bwd.
+ * add1 (may be NULL; single source, accumulate1 set, no dx pixel sums): a second operand [pix][ld_add1] added too --
+ * dx1 += dx + add1: a ResBlock's identity-shortcut gradient folded into the GroupNorm backward that writes the block
+ * input's gradient (models/unet.py:64, round 6); in the one-pass kernel's dx pass (one bf16 rounding), otherwise
+ * as an add into dx1 before the accumulation. */
 int dmc_gn_silu_bwd_deferred(int dtype, const void* g, int ld_g, const void* x1, const void* x2, int N, int HW,
                              int C1, int C2, int ld1, int ld2, int G, const float* mean_rstd, const float* gamma,
                              const float* beta, int silu, uint32_t drop_seed, const uint32_t* drop_seed_base,
                              uint32_t drop_thresh, float drop_scale, void* dx1, void* dx2, int ld_dx1, int ld_dx2,
                              int accumulate1, int accumulate2, float* dgamma, float* dbeta, float* dx_sum_nc,
                              int ld_sum_nc, float* dx_sum_c, const float* part, void* workspace, float* A_keep,
-                             float* sums_keep, int* deferred, void* stream);
+                             float* sums_keep, int* deferred, const void* add1, int ld_add1, void* stream);
 
 /* Column sums of up to 56 fp32 matrices in one launch: out0[c] = scale * sum_r in[r*ld + c*stride], out1 likewise
  * at +1 (may be NULL) -- the deferred GroupNorm-backward parameter sums (bitwise the immediate ones). */

@@ -577,6 +577,53 @@ def test_groupnorm_backward_fused_one_pass(shape, dmc_opt):
     assert rel_err(res[(4, False)][0], dxk) > 1e-2
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(128, 32, 32, 128), (128, 8, 8, 256), (16, 8, 8, 128)])
+def test_gn_bwd_extra_operand(shape, dt):
+    """dmc_gn_silu_bwd_deferred(add1=...): the identity-shortcut gradient added into the accumulated dx1 by the
+    GroupNorm backward (round 6) vs the same call followed by a separate add (the executor's former order). bf16 on
+    the one-pass kernel: one rounding instead of two, so within bf16 last-bit flips; fp32 / small batches take the
+    other kernels plus the add launch, which is the separate add: bitwise."""
+    L, K = _lib()
+    torch.manual_seed(17)
+    N, H, W, C = shape
+    G, HW = 8, H * W
+    x = (torch.randn(N, H, W, C) * 1.3 + 0.4).to(dt).to(DEV)
+    g = torch.randn(N, H, W, C).to(dt).to(DEV)
+    add = torch.randn(N, H, W, C).to(dt).to(DEV)
+    prev = torch.randn(N, H, W, C).to(dt).to(DEV)
+    gamma, beta = (torch.rand(C) + 0.5).to(DEV), torch.randn(C).to(DEV)
+    _, _, mr = K.gn_stats(dt, x, None, N, HW, C, 0, C, 0, G, 1e-5, gamma, beta)
+    drop = (5, 1 << 29, 1.0 / 0.875)
+    outs = []
+    for fold in (False, True):
+        dx = prev.clone()
+        if not fold:
+            K.add_(dt, dx, add)
+        dg, db = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        jobs = []
+        K.gn_bwd(dt, g, C, x, None, N, HW, C, 0, C, 0, G, mr, gamma, beta, True, drop, dx, None, C, 0, 1, 0, dg, db,
+                 defer=jobs, add1=add if fold else None, ld_add1=C if fold else 0)
+        K.colsum_batch(jobs)
+        torch.cuda.synchronize()
+        outs.append((dx.float(), dg, db))
+    (a, dga, dba), (b, dgb, dbb) = outs
+    assert torch.equal(dga, dgb) and torch.equal(dba, dbb)
+    fused = dt == torch.bfloat16 and N >= 64
+    if fused:
+        # reference: the GroupNorm gradient alone (no accumulation), summed with prev and add in fp32
+        alone = torch.empty_like(prev)
+        K.gn_bwd(dt, g, C, x, None, N, HW, C, 0, C, 0, G, mr, gamma, beta, True, drop, alone, None, C, 0, 0, 0,
+                 torch.empty(C, device=DEV), torch.empty(C, device=DEV))
+        torch.cuda.synchronize()
+        ref = prev.float() + add.float() + alone.float()
+        # one bf16 rounding of the three-term sum instead of two: no further from the fp32 sum than the separate add
+        assert rel_err(b, ref) <= rel_err(a, ref) * 1.02, (rel_err(b, ref), rel_err(a, ref))
+        assert rel_err(b, a) < 1e-2, rel_err(b, a)
+    else:
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("shape", [(128, 32, 32, 128), (128, 8, 8, 256), (64, 4, 4, 512)])
 def test_gn_bwd_deferred_column_sums_bitwise(shape):
     """dmc_gn_silu_bwd_deferred + dmc_colsum_batch (the parameter column sums of several GroupNorm backwards in one
