@@ -982,6 +982,11 @@ __global__ __launch_bounds__(256, NS <= 2 ? 2 : 1) void gemm1x1_persist_kernel(C
       __builtin_amdgcn_sched_barrier(0);
       const int t = t_begin + s / kst, mb = t / NB, nb = t - mb * NB;
       const int m0 = mb * BM, n0 = nb * BN;
+      // split output (round 6: the 1x1 input gradient into the two sources of a concat, y1 | y2 at Csplit, a
+      // multiple of 128 so that a tile lies on one side)
+      const bool second = n0 >= a.Csplit;
+      char* const ybase = second ? a.y2 : a.y1;
+      const int ldy = second ? a.ldy2 : a.ldy1, cbase = second ? a.Csplit : 0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int co = n0 + wn * 64 + i * 16 + fh * 4;
@@ -998,7 +1003,7 @@ __global__ __launch_bounds__(256, NS <= 2 ? 2 : 1) void gemm1x1_persist_kernel(C
           v2i o;
           o[0] = (int)f2bf2(v[0], v[1]);
           o[1] = (int)f2bf2(v[2], v[3]);
-          *(v2i*)(a.y1 + ((size_t)px * a.ldy1 + co) * 2) = o;
+          *(v2i*)(ybase + ((size_t)px * ldy + co - cbase) * 2) = o;
           acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
         }
       }
@@ -2371,9 +2376,11 @@ int gemm1x1_plan(const ConvK& k) {
   if (k.C1 % 64 || k.C2 % 64 || k.Kc != k.C1 + k.C2 || k.x1_bytes == 0 || (k.C2 && k.x2_bytes == 0) || k.w_bytes == 0)
     return 0;
   if (k.addvec || (k.resid && (k.ld_res & 3)) || k.silu_pre || k.gst || k.gsk ||
-      k.act != DMC_ACT_NONE || k.sk || k.Csplit != k.Cout || k.out_f32 || k.out_nchw || (k.ldy1 & 3) || k.M % 128 ||
+      k.act != DMC_ACT_NONE || k.sk || k.out_f32 || k.out_nchw || (k.ldy1 & 3) || k.M % 128 ||
       k.Cout % 128 || k.Cout > 1024)
     return 0;
+  // a split output: whole 128-channel tiles on each side, no residual (the accumulate form is single-output)
+  if (k.Csplit != k.Cout && (k.Csplit % 128 || (k.ldy2 & 3) || !k.y2 || k.resid)) return 0;
   const long ntiles = (long)(k.M / 128) * (k.Cout / 128);
   if (ntiles < 128) return 0;
   const long blocks = 512;   // the 2-slot ring, two blocks per CU (the 4-slot one-block form: +1 % only, round 4)

@@ -1073,6 +1073,37 @@ def test_gemm1x1_persistent_residual_bitwise(N, H, C1, Cout, inplace, dmc_opt):
     assert rel_err(outs[0].float().reshape(-1, Cout), ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,Cin,C1,C2", [(64, 32, 128, 128, 128), (64, 32, 128, 256, 128), (128, 16, 256, 256, 256),
+                                          (32, 32, 128, 192, 64)])
+def test_gemm1x1_persistent_split_output_bitwise(N, H, Cin, C1, C2, dmc_opt):
+    """Round 6: the persistent 1x1 GEMM writing a split output (the 1x1 shortcut's input gradient into the two
+    sources of a concat, models/unet.py:70 on the up path: y1 = channels [0, Csplit), y2 = the rest) is BITWISE the
+    per-tile LDS-DMA kernel (DMC_GEMM1X1=0). (32, 32, 128, 192, 64): a split that is not a multiple of 128 keeps the
+    per-tile kernel on both arms."""
+    from diffusion_models_collection_amd import _lib as L, kernels as K
+    gen = torch.Generator().manual_seed(N + H + C1 + C2)
+    dt = torch.bfloat16
+    Cout = C1 + C2
+    x1 = torch.randn(N, H, H, Cin, generator=gen).to(dt).to(DEV)
+    w = (torch.randn(Cout, Cin, 1, 1, generator=gen) * 0.05).to(DEV)
+    Kc = L.kc_for(Cin, dt)
+    wp = K.pack_weight(L.PACK_FWD, dt, w, Kc)
+    outs = []
+    for on in (1, 0):
+        dmc_opt("DMC_GEMM1X1", on)
+        y1 = torch.full((N, H, H, C1), 7.0, device=DEV, dtype=dt)
+        y2 = torch.full((N, H, H, C2), 7.0, device=DEV, dtype=dt)
+        d = K.make_desc(dt, N, H, H, Cin, 0, Cin, 0, Kc, H, H, Cout, K.TAPS1)
+        K.set_epilogue(d, ldy1=C1, ldy2=C2, Csplit=C1)
+        K.conv(d, x1, None, wp, y1, y2)
+        outs.append((y1, y2))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    ref = x1.float().reshape(-1, Cin) @ w.view(Cout, -1).to(dt).float().t()
+    got = torch.cat([outs[0][0], outs[0][1]], -1).float().reshape(-1, Cout)
+    assert rel_err(got, ref) < 1e-2
+
+
 @pytest.mark.parametrize("shape", [(32, 32, 32, 256, 0), (64, 16, 16, 128, 128)])
 @pytest.mark.parametrize("silu,dropout", [(True, False), (True, True), (False, False)])
 def test_gn_bwd_with_precomputed_partials(shape, silu, dropout):
